@@ -1,0 +1,178 @@
+"""ctypes loader for libalgodsp_hip.so (the C ABI declared in include/algodsp.h).
+
+The product path is the HIP library only: if it cannot be loaded, or no
+gfx950 device is visible, every create call raises -- there is no CPU
+fallback anywhere in this package.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import pathlib
+
+import numpy as np
+
+_HERE = pathlib.Path(__file__).resolve().parent
+LIB_PATH = _HERE.parent / "libalgodsp_hip.so"
+HEADER_PATH = _HERE.parent.parent / "include" / "algodsp.h"
+
+# status codes (include/algodsp.h)
+AD_OK = 0
+AD_ERR_EMPTY_INPUT = 1
+AD_ERR_EMPTY_KERNEL = 2
+AD_ERR_LENGTH_MISMATCH = 3
+AD_ERR_INVALID_BLOCK_SIZE = 4
+AD_ERR_INVALID_BLOCK_ORDER = 5
+AD_ERR_EMPTY_IMPULSE_RESPONSE = 6
+AD_ERR_STAGE_INDEX_OUT_OF_RANGE = 7
+AD_ERR_INVALID_ARGUMENT = 8
+AD_ERR_DEVICE = 100
+AD_ERR_NO_DEVICE = 101
+AD_ERR_INTERNAL = 102
+
+
+class ADError(Exception):
+    """Error returned through the C ABI; `code` is the AD_* status."""
+
+    code = None
+
+    def __init__(self, code: int, msg: str = ""):
+        super().__init__(f"[{code}] {msg}")
+        self.code = code
+
+
+class ErrEmptyInput(ADError):
+    pass
+
+
+class ErrEmptyKernel(ADError):
+    pass
+
+
+class ErrLengthMismatch(ADError):
+    pass
+
+
+class ErrInvalidBlockSize(ADError):
+    pass
+
+
+class ErrInvalidBlockOrder(ADError):
+    pass
+
+
+class ErrEmptyImpulseResponse(ADError):
+    pass
+
+
+class ErrStageIndexOutOfRange(ADError):
+    pass
+
+
+class ErrInvalidArgument(ADError):
+    pass
+
+
+class ErrDevice(ADError):
+    pass
+
+
+_BY_CODE = {
+    AD_ERR_EMPTY_INPUT: ErrEmptyInput,
+    AD_ERR_EMPTY_KERNEL: ErrEmptyKernel,
+    AD_ERR_LENGTH_MISMATCH: ErrLengthMismatch,
+    AD_ERR_INVALID_BLOCK_SIZE: ErrInvalidBlockSize,
+    AD_ERR_INVALID_BLOCK_ORDER: ErrInvalidBlockOrder,
+    AD_ERR_EMPTY_IMPULSE_RESPONSE: ErrEmptyImpulseResponse,
+    AD_ERR_STAGE_INDEX_OUT_OF_RANGE: ErrStageIndexOutOfRange,
+    AD_ERR_INVALID_ARGUMENT: ErrInvalidArgument,
+}
+
+_lib = None
+
+c_double_p = C.POINTER(C.c_double)
+c_int64_p = C.POINTER(C.c_int64)
+
+
+def lib() -> C.CDLL:
+    """Loads (once) and returns the HIP library; raises if it is missing."""
+    global _lib
+    if _lib is None:
+        path = os.environ.get("ALGODSP_LIB", str(LIB_PATH))
+        if not pathlib.Path(path).exists():
+            raise ImportError(f"libalgodsp_hip.so not built at {path}; run `make -C algo-dsp_amd`")
+        _lib = C.CDLL(path)
+        _declare(_lib)
+    return _lib
+
+
+def _declare(L: C.CDLL) -> None:
+    vp = C.c_void_p
+    i64 = C.c_int64
+    sig = {
+        "ad_last_error": (C.c_char_p, []),
+        "ad_version": (C.c_int, []),
+        "ad_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+        "ad_conv_stream_ols_create": (C.c_int, [c_double_p, i64, i64, C.c_int, C.POINTER(vp)]),
+        "ad_conv_stream_ola_create": (C.c_int, [c_double_p, i64, i64, C.c_int, C.POINTER(vp)]),
+        "ad_conv_process_block": (C.c_int, [vp, c_double_p, i64, c_double_p, i64]),
+        "ad_conv_ols_create": (C.c_int, [c_double_p, i64, i64, C.c_int, C.POINTER(vp)]),
+        "ad_conv_ola_create": (C.c_int, [c_double_p, i64, i64, C.c_int, C.POINTER(vp)]),
+        "ad_conv_process": (C.c_int, [vp, c_double_p, i64, c_double_p, i64]),
+        "ad_conv_partitioned_create": (C.c_int, [c_double_p, i64, C.c_int, C.c_int, C.c_int, C.POINTER(vp)]),
+        "ad_conv_partitioned_process_block": (C.c_int, [vp, c_double_p, i64, c_double_p, i64]),
+        "ad_conv_stage_count": (C.c_int, [vp]),
+        "ad_conv_stage_info": (C.c_int, [vp, C.c_int, c_int64_p, c_int64_p]),
+        "ad_conv_reset": (C.c_int, [vp]),
+        "ad_conv_block_size": (i64, [vp]),
+        "ad_conv_kernel_len": (i64, [vp]),
+        "ad_conv_fft_size": (i64, [vp]),
+        "ad_conv_step_size": (i64, [vp]),
+        "ad_conv_latency": (i64, [vp]),
+        "ad_conv_destroy": (None, [vp]),
+        "ad_conv_direct": (C.c_int, [c_double_p, i64, c_double_p, i64, c_double_p, C.c_int]),
+        "ad_conv_direct_circular": (C.c_int, [c_double_p, i64, c_double_p, i64, c_double_p, C.c_int]),
+        "ad_conv_convolve": (C.c_int, [c_double_p, i64, c_double_p, i64, C.c_int, c_double_p, i64, c_int64_p,
+                                       C.c_int]),
+        "ad_conv_multi_create": (C.c_int, [c_double_p, C.c_int, i64, i64, C.c_int, C.POINTER(C.c_int32), i64,
+                                           C.c_int, C.POINTER(vp)]),
+        "ad_conv_multi_process_device": (C.c_int, [vp, vp, i64, i64, vp, i64, i64, vp]),
+        "ad_conv_mixdown_device": (C.c_int, [vp, C.c_int, i64, i64, vp, vp]),
+        "ad_conv_profile_enable": (C.c_int, [vp, C.c_int]),
+        "ad_conv_profile_read": (C.c_int, [vp, c_double_p, c_int64_p, c_double_p]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+
+
+def check(rc: int) -> None:
+    if rc == AD_OK:
+        return
+    msg = lib().ad_last_error().decode("utf-8", "replace")
+    raise _BY_CODE.get(rc, ErrDevice if rc >= 100 else ADError)(rc, msg)
+
+
+def f64(a) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(a, dtype=np.float64))
+
+
+def ptr(a: np.ndarray):
+    if a.size == 0:
+        return C.cast(C.c_void_p(0), c_double_p)
+    return a.ctypes.data_as(c_double_p)
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    lib().ad_device_count(C.byref(n))
+    return n.value
+
+
+def exported_symbols() -> list[str]:
+    """Every ad_* symbol declared in include/algodsp.h."""
+    import re
+
+    text = HEADER_PATH.read_text()
+    return sorted(set(re.findall(r"\b(ad_[a-z0-9_]+)\s*\(", text)))

@@ -1,0 +1,600 @@
+// C ABI of dsp/conv (include/algodsp.h) on top of the UPOLS engine and the
+// time-domain kernels.  Host logic here mirrors the reference constructors'
+// validation and size selection; all sample arithmetic runs on the GPU.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <deque>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "ad_common.hpp"
+#include "conv_kernels.hpp"
+#include "upols_engine.hpp"
+
+using namespace adsp;
+
+namespace {
+
+enum class Kind { StreamOLS, StreamOLA, BatchOLS, BatchOLA, Partitioned, Multi };
+
+struct StageDesc {
+  int64_t part_size;
+  int64_t count;
+  int64_t start;
+};
+
+// partitionIR (dsp/conv/partitioned.go:269-332) restated: host-side stage
+// planning that StageCount/StageInfo report.
+int trunc_log2(int64_t n) {  // partitioned.go:186-199
+  if (n <= 0) return 0;
+  int r = 0;
+  while (n > 1) {
+    n >>= 1;
+    ++r;
+  }
+  return r;
+}
+int64_t bit_count_to_bits(int n) { return (int64_t(2) << n) - 1; }  // partitioned.go:202-204
+
+std::vector<StageDesc> partition_ir(int64_t kernel_len_padded, int min_order, int max_order) {
+  const int64_t min_block = int64_t(1) << min_order;
+  int max_ir = trunc_log2(kernel_len_padded + min_block) - 1;
+  int64_t res = kernel_len_padded - (bit_count_to_bits(max_ir) - bit_count_to_bits(min_order - 1));
+  if (res > 0 && ((res >> max_ir) & 1) == 0 && max_ir > min_order) --max_ir;
+  if (max_ir > max_order) max_ir = max_order;
+  res = kernel_len_padded - (bit_count_to_bits(max_ir) - bit_count_to_bits(min_order - 1));
+  std::vector<StageDesc> st;
+  int64_t start = 0;
+  for (int order = min_order; order < max_ir; ++order) {
+    const int64_t count = 1 + ((res >> order) & 1);
+    st.push_back({int64_t(1) << order, count, start});
+    start += count << order;
+    res -= (count - 1) << order;
+  }
+  int64_t count = 1;
+  if (max_ir > 0) count = std::max<int64_t>(1, 1 + res / (int64_t(1) << max_ir));
+  st.push_back({int64_t(1) << max_ir, count, start});
+  return st;
+}
+
+int pick_device(int device) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) AD_FAIL(AD_ERR_NO_DEVICE, "no HIP device available");
+  if (device < 0 || device >= n) AD_FAIL(AD_ERR_NO_DEVICE, "device index out of range");
+  return device;
+}
+
+int64_t largest_pow2_divisor(int64_t v, int64_t cap) {
+  int64_t l = 1;
+  while ((v % (l * 2)) == 0 && l * 2 <= cap) l *= 2;
+  return l;
+}
+
+}  // namespace
+
+struct ad_conv {
+  Kind kind;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int64_t K = 0;
+  int64_t conv_len = 0;    // taps actually convolved (partitioned: stage coverage)
+  int64_t block_size = 0;  // streaming block / OLA block
+  int64_t fft_size = 0;    // reported FFTSize()
+  int64_t step_size = 0;   // OverlapSave.StepSize()
+  int64_t latency = 0;     // partitioned
+  std::vector<StageDesc> stages;
+
+  std::unique_ptr<Upols> eng;  // FFT path
+  int64_t hop = 0;
+
+  // time-domain streaming path (hop too small for the FFT engine)
+  bool direct_stream = false;
+  DevBuf<double> hdev;
+  DevBuf<double> sbuf[2];
+  int cur = 0;
+
+  // staging
+  DevBuf<double> din, dout;
+
+  // partitioned FIFO state
+  std::vector<double> pending;   // input samples not yet convolved (< hop)
+  std::deque<double> ylin;       // convolved samples not yet emitted
+  int64_t emitted = 0;           // output samples emitted so far
+  int64_t ylin_base = 0;         // linear-conv index of ylin.front()
+
+  ~ad_conv() {
+    eng.reset();
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+};
+
+namespace {
+
+ad_conv* new_handle(Kind k, int device) {
+  auto* h = new ad_conv();
+  h->kind = k;
+  h->device = device;
+  DeviceScope ds(device);
+  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete h;
+    AD_FAIL(AD_ERR_DEVICE, "hipStreamCreate failed");
+  }
+  return h;
+}
+
+// zero-latency streaming convolution state for `hop` sized chunks
+void setup_stream_engine(ad_conv* h, const double* kernel, int64_t K, int64_t B, int64_t hop_cap) {
+  const int64_t hop = largest_pow2_divisor(B, hop_cap);
+  h->hop = hop;
+  h->conv_len = K;
+  if (hop >= 16) {
+    const int jc = (int)std::max<int64_t>(1, std::min<int64_t>(B / hop, 256));
+    h->eng.reset(new Upols(h->device, kernel, 1, K, (int)hop, 1, nullptr, jc, h->stream));
+  } else {
+    h->direct_stream = true;
+    h->hdev.alloc((size_t)K);
+    AD_HIP(hipMemcpyAsync(h->hdev.p, kernel, K * sizeof(double), hipMemcpyHostToDevice, h->stream));
+  }
+}
+
+void stream_reset(ad_conv* h) {
+  if (h->eng) h->eng->reset_stream(h->stream);
+  for (auto& b : h->sbuf)
+    if (b.p) AD_HIP(hipMemsetAsync(b.p, 0, b.n * sizeof(double), h->stream));
+  h->pending.clear();
+  h->ylin.clear();
+  h->emitted = 0;
+  h->ylin_base = 0;
+  AD_HIP(hipStreamSynchronize(h->stream));
+}
+
+// Convolves n new samples (host) with the running history; n must be a
+// multiple of the hop on the FFT path.  Writes n linear-conv samples to out.
+void stream_convolve(ad_conv* h, const double* in, int64_t n, double* out) {
+  if (n == 0) return;
+  hipStream_t s = h->stream;
+  if (h->direct_stream) {
+    const int64_t K = h->conv_len;
+    const size_t need = (size_t)(K - 1 + n);
+    DevBuf<double>& curb = h->sbuf[h->cur];
+    DevBuf<double>& nxt = h->sbuf[h->cur ^ 1];
+    if (curb.n < need) {
+      // grow, keeping the K-1 history at the front
+      DevBuf<double> tmp;
+      tmp.alloc(need);
+      AD_HIP(hipMemsetAsync(tmp.p, 0, need * sizeof(double), s));
+      if (curb.p && K > 1) AD_HIP(hipMemcpyAsync(tmp.p, curb.p, (K - 1) * sizeof(double), hipMemcpyDeviceToDevice, s));
+      AD_HIP(hipStreamSynchronize(s));
+      std::swap(curb.p, tmp.p);
+      std::swap(curb.n, tmp.n);
+    }
+    nxt.reserve(need);
+    AD_HIP(hipMemcpyAsync(curb.p + (K - 1), in, n * sizeof(double), hipMemcpyHostToDevice, s));
+    h->dout.reserve((size_t)n);
+    launch_stream_direct(h->hdev.p, K, curb.p, n, h->dout.p, s);
+    AD_HIP(hipGetLastError());
+    if (K > 1) AD_HIP(hipMemcpyAsync(nxt.p, curb.p + n, (K - 1) * sizeof(double), hipMemcpyDeviceToDevice, s));
+    h->cur ^= 1;
+    AD_HIP(hipMemcpyAsync(out, h->dout.p, n * sizeof(double), hipMemcpyDeviceToHost, s));
+    AD_HIP(hipStreamSynchronize(s));
+    return;
+  }
+  h->din.reserve((size_t)n);
+  h->dout.reserve((size_t)n);
+  AD_HIP(hipMemcpyAsync(h->din.p, in, n * sizeof(double), hipMemcpyHostToDevice, s));
+  h->eng->run(h->din.p, n, n, h->dout.p, n, n, /*use_hist=*/true, s);
+  h->eng->save_history(h->din.p, n, n, s);
+  AD_HIP(hipMemcpyAsync(out, h->dout.p, n * sizeof(double), hipMemcpyDeviceToHost, s));
+  AD_HIP(hipStreamSynchronize(s));
+}
+
+// Offline full convolution of one channel with the handle's kernel.
+void batch_convolve(ad_conv* h, const double* in, int64_t n, double* out, int64_t out_len) {
+  hipStream_t s = h->stream;
+  h->din.reserve((size_t)n);
+  h->dout.reserve((size_t)out_len);
+  AD_HIP(hipMemcpyAsync(h->din.p, in, n * sizeof(double), hipMemcpyHostToDevice, s));
+  h->eng->begin_offline(s);
+  h->eng->run(h->din.p, n, n, h->dout.p, out_len, out_len, /*use_hist=*/false, s);
+  AD_HIP(hipMemcpyAsync(out, h->dout.p, out_len * sizeof(double), hipMemcpyDeviceToHost, s));
+  AD_HIP(hipStreamSynchronize(s));
+}
+
+int64_t batch_hop(int64_t K) {
+  int64_t l = next_pow2(std::max<int64_t>(K, 256));
+  return std::min<int64_t>(l, 4096);
+}
+
+void make_batch_engine(ad_conv* h, const double* kernel, int64_t K) {
+  h->hop = batch_hop(K);
+  h->eng.reset(new Upols(h->device, kernel, 1, K, (int)h->hop, 1, nullptr, 64, h->stream));
+}
+
+template <class Fn>
+int create_guarded(ad_conv** out, Fn&& fn) {
+  if (out) *out = nullptr;
+  ad_conv* h = nullptr;
+  const int rc = guard([&] { h = fn(); });
+  if (rc != AD_OK) {
+    delete h;
+    return rc;
+  }
+  if (out) *out = h;
+  return AD_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+// --- streaming ------------------------------------------------------------
+
+static int stream_create(Kind kind, const double* kernel, int64_t K, int64_t B, int device, ad_conv** out) {
+  // NewStreamingOverlapSaveT streaming_overlap_save.go:45-84 /
+  // NewStreamingOverlapAddT streaming_overlap_add.go:43-83
+  return create_guarded(out, [&]() -> ad_conv* {
+    if (K <= 0 || !kernel) AD_FAIL(AD_ERR_EMPTY_KERNEL, "conv: empty kernel");
+    if (B <= 0) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "conv: blockSize must be positive, got " + std::to_string(B));
+    const int dev = pick_device(device);
+    DeviceScope ds(dev);
+    std::unique_ptr<ad_conv> h(new_handle(kind, dev));
+    h->K = K;
+    h->block_size = B;
+    h->fft_size = next_pow2(B + K - 1);
+    setup_stream_engine(h.get(), kernel, K, B, 4096);
+    stream_reset(h.get());
+    return h.release();
+  });
+}
+
+int ad_conv_stream_ols_create(const double* kernel, int64_t kernel_len, int64_t block_size, int device,
+                              ad_conv** out) {
+  return stream_create(Kind::StreamOLS, kernel, kernel_len, block_size, device, out);
+}
+
+int ad_conv_stream_ola_create(const double* kernel, int64_t kernel_len, int64_t block_size, int device,
+                              ad_conv** out) {
+  return stream_create(Kind::StreamOLA, kernel, kernel_len, block_size, device, out);
+}
+
+int ad_conv_process_block(ad_conv* h, const double* in, int64_t in_len, double* out, int64_t out_len) {
+  return guard([&] {
+    if (!h) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "nil handle");
+    if (h->kind != Kind::StreamOLS && h->kind != Kind::StreamOLA)
+      AD_FAIL(AD_ERR_INVALID_ARGUMENT, "ProcessBlockTo on a non-streaming convolver");
+    if (in_len != h->block_size)
+      AD_FAIL(AD_ERR_LENGTH_MISMATCH, "conv: buffer length mismatch: expected " + std::to_string(h->block_size) +
+                                          " input samples, got " + std::to_string(in_len));
+    if (out_len != h->block_size)
+      AD_FAIL(AD_ERR_LENGTH_MISMATCH, "conv: buffer length mismatch: expected " + std::to_string(h->block_size) +
+                                          " output samples, got " + std::to_string(out_len));
+    DeviceScope ds(h->device);
+    stream_convolve(h, in, in_len, out);
+  });
+}
+
+// --- batch ------------------------------------------------------------------
+
+int ad_conv_ols_create(const double* kernel, int64_t K, int64_t fft_size, int device, ad_conv** out) {
+  // NewOverlapSave overlap_save.go:53-107
+  return create_guarded(out, [&]() -> ad_conv* {
+    if (K <= 0 || !kernel) AD_FAIL(AD_ERR_EMPTY_KERNEL, "conv: empty kernel");
+    int64_t n = fft_size;
+    if (n <= 0) n = std::max<int64_t>(next_pow2(2 * K), 256);
+    if (!is_pow2(n))
+      AD_FAIL(AD_ERR_INVALID_BLOCK_SIZE, "conv: invalid block size: fftSize must be power of 2, got " +
+                                             std::to_string(n));
+    if (n < 2 * K) n = next_pow2(2 * K);
+    const int dev = pick_device(device);
+    DeviceScope ds(dev);
+    std::unique_ptr<ad_conv> h(new_handle(Kind::BatchOLS, dev));
+    h->K = K;
+    h->fft_size = n;
+    h->step_size = n - K + 1;
+    make_batch_engine(h.get(), kernel, K);
+    AD_HIP(hipStreamSynchronize(h->stream));
+    return h.release();
+  });
+}
+
+int ad_conv_ola_create(const double* kernel, int64_t K, int64_t block_size, int device, ad_conv** out) {
+  // NewOverlapAdd overlap_add.go:44-89
+  return create_guarded(out, [&]() -> ad_conv* {
+    if (K <= 0 || !kernel) AD_FAIL(AD_ERR_EMPTY_KERNEL, "conv: empty kernel");
+    int64_t b = block_size;
+    if (b <= 0) b = std::max<int64_t>(next_pow2(K), 256);
+    const int dev = pick_device(device);
+    DeviceScope ds(dev);
+    std::unique_ptr<ad_conv> h(new_handle(Kind::BatchOLA, dev));
+    h->K = K;
+    h->block_size = b;
+    h->fft_size = next_pow2(b + K - 1);
+    make_batch_engine(h.get(), kernel, K);
+    AD_HIP(hipStreamSynchronize(h->stream));
+    return h.release();
+  });
+}
+
+int ad_conv_process(ad_conv* h, const double* in, int64_t in_len, double* out, int64_t out_len) {
+  // OverlapSave.Process/ProcessTo overlap_save.go:126-272,
+  // OverlapAdd.Process/ProcessTo overlap_add.go:108-182
+  return guard([&] {
+    if (!h) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "nil handle");
+    if (h->kind != Kind::BatchOLS && h->kind != Kind::BatchOLA)
+      AD_FAIL(AD_ERR_INVALID_ARGUMENT, "Process on a non-batch convolver");
+    const int64_t expected = in_len + h->K - 1;
+    if (out_len != expected)
+      AD_FAIL(AD_ERR_LENGTH_MISMATCH, "conv: buffer length mismatch: expected " + std::to_string(expected) +
+                                          ", got " + std::to_string(out_len));
+    if (in_len <= 0) AD_FAIL(AD_ERR_EMPTY_INPUT, "conv: empty input");
+    DeviceScope ds(h->device);
+    batch_convolve(h, in, in_len, out, out_len);
+  });
+}
+
+// --- partitioned ---------------------------------------------------------------
+
+int ad_conv_partitioned_create(const double* kernel, int64_t K, int min_order, int max_order, int device,
+                               ad_conv** out) {
+  // NewPartitionedConvolutionT partitioned.go:212-266
+  return create_guarded(out, [&]() -> ad_conv* {
+    if (K <= 0 || !kernel) AD_FAIL(AD_ERR_EMPTY_IMPULSE_RESPONSE, "conv: empty impulse response");
+    if (min_order < 1)
+      AD_FAIL(AD_ERR_INVALID_BLOCK_ORDER,
+              "conv: invalid block order: minBlockOrder must be >= 1, got " + std::to_string(min_order));
+    if (max_order < min_order)
+      AD_FAIL(AD_ERR_INVALID_BLOCK_ORDER, "conv: invalid block order: maxBlockOrder (" + std::to_string(max_order) +
+                                              ") must be >= minBlockOrder (" + std::to_string(min_order) + ")");
+    if (min_order > 30) AD_FAIL(AD_ERR_INVALID_BLOCK_ORDER, "conv: invalid block order: minBlockOrder too large");
+    const int dev = pick_device(device);
+    DeviceScope ds(dev);
+    std::unique_ptr<ad_conv> h(new_handle(Kind::Partitioned, dev));
+    const int64_t latency = int64_t(1) << min_order;
+    const int64_t padded = ((K + latency - 1) / latency) * latency;
+    h->K = K;
+    h->latency = latency;
+    h->block_size = latency;
+    h->stages = partition_ir(padded, min_order, max_order);
+    // Effective kernel: the taps the stage layout covers (the reference never
+    // convolves taps beyond the last stage).
+    int64_t cover = 0;
+    for (const auto& s : h->stages) cover = std::max(cover, s.start + s.count * s.part_size);
+    const int64_t keff = std::min<int64_t>(K, cover);
+    h->fft_size = 2 * h->stages.back().part_size;
+    // Zero-latency engine with hop = latency (<= 4096), output delayed by latency.
+    setup_stream_engine(h.get(), kernel, keff, latency, 4096);
+    stream_reset(h.get());
+    return h.release();
+  });
+}
+
+int ad_conv_partitioned_process_block(ad_conv* h, const double* in, int64_t in_len, double* out, int64_t out_len) {
+  // PartitionedConvolutionT.ProcessBlock partitioned.go:348-396
+  return guard([&] {
+    if (!h || h->kind != Kind::Partitioned) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "not a partitioned convolver");
+    if (in_len != out_len)
+      AD_FAIL(AD_ERR_LENGTH_MISMATCH, "conv: buffer length mismatch: input length " + std::to_string(in_len) +
+                                          " != output length " + std::to_string(out_len));
+    if (in_len == 0) return;
+    DeviceScope ds(h->device);
+    // Convolve every complete hop-sized block (all samples on the direct path).
+    h->pending.insert(h->pending.end(), in, in + in_len);
+    const int64_t hop = h->direct_stream ? 1 : h->hop;
+    const int64_t nconv = ((int64_t)h->pending.size() / hop) * hop;
+    if (nconv > 0) {
+      std::vector<double> y((size_t)nconv);
+      stream_convolve(h, h->pending.data(), nconv, y.data());
+      h->ylin.insert(h->ylin.end(), y.begin(), y.end());
+      h->pending.erase(h->pending.begin(), h->pending.begin() + nconv);
+    }
+    // Emit: output sample o is ylin[o - latency] (zero before the latency).
+    for (int64_t i = 0; i < out_len; ++i) {
+      const int64_t o = h->emitted + i;
+      const int64_t src = o - h->latency;
+      if (src < 0) {
+        out[i] = 0.0;
+        continue;
+      }
+      while (h->ylin_base < src) {
+        h->ylin.pop_front();
+        ++h->ylin_base;
+      }
+      out[i] = h->ylin.front();
+    }
+    h->emitted += out_len;
+  });
+}
+
+int ad_conv_stage_count(const ad_conv* h) { return h ? (int)h->stages.size() : 0; }
+
+int ad_conv_stage_info(const ad_conv* h, int index, int64_t* part_size, int64_t* block_count) {
+  // StageInfo partitioned.go:427-436
+  return guard([&] {
+    if (!h) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "nil handle");
+    if (index < 0 || index >= (int)h->stages.size())
+      AD_FAIL(AD_ERR_STAGE_INDEX_OUT_OF_RANGE, "conv: stage index out of range: index " + std::to_string(index) +
+                                                   ", have " + std::to_string(h->stages.size()) + " stages");
+    if (part_size) *part_size = h->stages[index].part_size;
+    if (block_count) *block_count = h->stages[index].count;
+  });
+}
+
+// --- common -------------------------------------------------------------------
+
+int ad_conv_reset(ad_conv* h) {
+  return guard([&] {
+    if (!h) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "nil handle");
+    DeviceScope ds(h->device);
+    stream_reset(h);
+  });
+}
+
+int64_t ad_conv_block_size(const ad_conv* h) { return h ? h->block_size : 0; }
+int64_t ad_conv_kernel_len(const ad_conv* h) { return h ? h->K : 0; }
+int64_t ad_conv_fft_size(const ad_conv* h) { return h ? h->fft_size : 0; }
+int64_t ad_conv_step_size(const ad_conv* h) { return h ? h->step_size : 0; }
+int64_t ad_conv_latency(const ad_conv* h) { return h ? h->latency : 0; }
+
+void ad_conv_destroy(ad_conv* h) {
+  if (!h) return;
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  (void)hipSetDevice(h->device);
+  delete h;
+  (void)hipSetDevice(cur);
+}
+
+// --- one-shot -----------------------------------------------------------------
+
+static void direct_on_device(const double* a, int64_t n, const double* b, int64_t m, double* dst, int device) {
+  const int dev = pick_device(device);
+  DeviceScope ds(dev);
+  DevBuf<double> da, db, dd;
+  da.alloc((size_t)n);
+  db.alloc((size_t)m);
+  dd.alloc((size_t)(n + m - 1));
+  AD_HIP(hipMemcpy(da.p, a, n * sizeof(double), hipMemcpyHostToDevice));
+  AD_HIP(hipMemcpy(db.p, b, m * sizeof(double), hipMemcpyHostToDevice));
+  launch_direct(da.p, n, db.p, m, dd.p, nullptr);
+  AD_HIP(hipGetLastError());
+  AD_HIP(hipMemcpy(dst, dd.p, (n + m - 1) * sizeof(double), hipMemcpyDeviceToHost));
+}
+
+int ad_conv_direct(const double* a, int64_t n, const double* b, int64_t m, double* dst, int device) {
+  // conv.Direct conv.go:76-93
+  return guard([&] {
+    if (n <= 0) AD_FAIL(AD_ERR_EMPTY_INPUT, "conv: empty input");
+    if (m <= 0) AD_FAIL(AD_ERR_EMPTY_KERNEL, "conv: empty kernel");
+    direct_on_device(a, n, b, m, dst, device);
+  });
+}
+
+int ad_conv_direct_circular(const double* a, int64_t n, const double* b, int64_t m, double* dst, int device) {
+  // conv.DirectCircular conv.go:158-173
+  return guard([&] {
+    if (n <= 0 || m <= 0) AD_FAIL(AD_ERR_EMPTY_INPUT, "conv: empty input");
+    if (n != m) AD_FAIL(AD_ERR_LENGTH_MISMATCH, "conv: buffer length mismatch");
+    const int dev = pick_device(device);
+    DeviceScope ds(dev);
+    DevBuf<double> da, db, dd;
+    da.alloc((size_t)n);
+    db.alloc((size_t)n);
+    dd.alloc((size_t)n);
+    AD_HIP(hipMemcpy(da.p, a, n * sizeof(double), hipMemcpyHostToDevice));
+    AD_HIP(hipMemcpy(db.p, b, n * sizeof(double), hipMemcpyHostToDevice));
+    launch_direct_circular(da.p, db.p, n, dd.p, nullptr);
+    AD_HIP(hipGetLastError());
+    AD_HIP(hipMemcpy(dst, dd.p, n * sizeof(double), hipMemcpyDeviceToHost));
+  });
+}
+
+int ad_conv_convolve(const double* a, int64_t n, const double* b, int64_t m, int mode, double* dst, int64_t dst_cap,
+                     int64_t* dst_len, int device) {
+  // conv.Convolve conv.go:194-216 and ConvolveMode/trimToMode :219-247
+  return guard([&] {
+    if (n <= 0) AD_FAIL(AD_ERR_EMPTY_INPUT, "conv: empty input");
+    if (m <= 0) AD_FAIL(AD_ERR_EMPTY_KERNEL, "conv: empty kernel");
+    const double* la = a;
+    const double* lb = b;
+    int64_t ln = n, lm = m;
+    if (lm > ln) {
+      std::swap(la, lb);
+      std::swap(ln, lm);
+    }
+    const int64_t full_len = ln + lm - 1;
+    std::vector<double> full((size_t)full_len);
+    if (lm <= 64) {
+      direct_on_device(la, ln, lb, lm, full.data(), device);
+    } else {
+      // OverlapAddConvolve overlap_add.go:221-253
+      const int dev = pick_device(device);
+      DeviceScope ds(dev);
+      std::unique_ptr<ad_conv> h(new_handle(Kind::BatchOLA, dev));
+      h->K = lm;
+      make_batch_engine(h.get(), lb, lm);
+      batch_convolve(h.get(), la, ln, full.data(), full_len);
+    }
+    int64_t start = 0, len = full_len;
+    if (mode == AD_MODE_SAME) {
+      start = (m - 1) / 2;
+      len = n;
+    } else if (mode == AD_MODE_VALID) {
+      if (n >= m) {
+        start = m - 1;
+        len = n - (m - 1);
+      } else {
+        start = n - 1;
+        len = m - (n - 1);
+      }
+    }
+    if (dst_len) *dst_len = len;
+    if (dst_cap < len) AD_FAIL(AD_ERR_LENGTH_MISMATCH, "dst capacity too small");
+    std::memcpy(dst, full.data() + start, (size_t)len * sizeof(double));
+  });
+}
+
+// --- multi-channel device path ---------------------------------------------------
+
+int ad_conv_multi_create(const double* kernels, int n_ir, int64_t K, int64_t hop, int channels,
+                         const int32_t* ir_index, int64_t max_chunk_blocks, int device, ad_conv** out) {
+  return create_guarded(out, [&]() -> ad_conv* {
+    if (K <= 0 || !kernels || n_ir <= 0) AD_FAIL(AD_ERR_EMPTY_KERNEL, "conv: empty kernel");
+    if (channels <= 0) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "channels must be positive");
+    if (hop <= 0) hop = 4096;
+    if (hop < 16 || hop > 4096 || !is_pow2(hop))
+      AD_FAIL(AD_ERR_INVALID_BLOCK_SIZE, "hop must be a power of two in [16, 4096]");
+    if (max_chunk_blocks <= 0) max_chunk_blocks = 1024;
+    const int dev = pick_device(device);
+    DeviceScope ds(dev);
+    std::unique_ptr<ad_conv> h(new_handle(Kind::Multi, dev));
+    h->K = K;
+    h->hop = hop;
+    h->block_size = hop;
+    h->fft_size = 2 * hop;
+    h->eng.reset(new Upols(dev, kernels, n_ir, K, (int)hop, channels, ir_index, (int)max_chunk_blocks, h->stream));
+    return h.release();
+  });
+}
+
+int ad_conv_multi_process_device(ad_conv* h, const double* d_in, int64_t in_stride, int64_t in_len, double* d_out,
+                                 int64_t out_stride, int64_t out_len, void* stream) {
+  return guard([&] {
+    if (!h || h->kind != Kind::Multi) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "not a multi-channel convolver");
+    if (in_len <= 0) AD_FAIL(AD_ERR_EMPTY_INPUT, "conv: empty input");
+    if (out_len > in_len + h->K - 1 || out_len <= 0)
+      AD_FAIL(AD_ERR_LENGTH_MISMATCH, "conv: buffer length mismatch");
+    DeviceScope ds(h->device);
+    hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : h->stream;
+    h->eng->begin_offline(s);
+    h->eng->run(d_in, in_stride, in_len, d_out, out_stride, out_len, /*use_hist=*/false, s);
+  });
+}
+
+int ad_conv_profile_enable(ad_conv* h, int enable) {
+  return guard([&] {
+    if (!h || !h->eng) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "handle has no FFT engine");
+    h->eng->set_profiling(enable != 0);
+  });
+}
+
+int ad_conv_profile_read(ad_conv* h, double* total_ms, int64_t* launches, double* alg_bytes) {
+  return guard([&] {
+    if (!h || !h->eng) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "handle has no FFT engine");
+    DeviceScope ds(h->device);
+    h->eng->read_profile(total_ms, launches, alg_bytes);
+  });
+}
+
+int ad_conv_mixdown_device(const double* d_chan, int channels, int64_t stride, int64_t len, double* d_mix,
+                           void* stream) {
+  return guard([&] {
+    if (channels <= 0 || len <= 0) AD_FAIL(AD_ERR_EMPTY_INPUT, "empty mixdown");
+    launch_mixdown(d_chan, channels, stride, len, d_mix, reinterpret_cast<hipStream_t>(stream));
+    AD_HIP(hipGetLastError());
+  });
+}
+
+}  // extern "C"

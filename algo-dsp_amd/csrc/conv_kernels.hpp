@@ -1,0 +1,70 @@
+// Argument blocks and launchers of the conv kernels (conv_kernels.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace adsp {
+
+struct RfftArgs {
+  const double* x;      // input samples, channel c at x + c*x_stride (call-relative index)
+  int64_t x_stride;
+  int64_t n;            // valid input samples per channel (beyond: zeros)
+  const double* xhist;  // [C][hist_stride]: the L samples preceding the call (nullable -> zeros)
+  int64_t hist_stride;
+  int64_t s0;           // first output sample of chunk block 0 (call-relative)
+  int jc;               // blocks per channel in this launch
+  int channels;
+  int aligned;          // x and x_stride allow 16-byte pair loads
+  double2* X;           // spectra ring [C][Q][MS]
+  int64_t x_ch_stride;  // Q*MS
+  int Q;
+  int slot0;            // ring slot of block 0
+  int MS;
+  const double2* twM;   // W_M^e, e < M
+  const double2* twN;   // W_{2M}^k, k < M
+};
+
+struct MacArgs {
+  const double2* X;
+  int64_t x_ch_stride;
+  int Q;
+  int slot0;
+  int MS;
+  const double2* H;     // [n_ir][P][MS]
+  int64_t h_ir_stride;  // P*MS
+  const int* ir_index;  // [C] device (nullable -> c % n_ir)
+  int n_ir;
+  double2* Y;           // [C][jc_max][MS]
+  int64_t y_ch_stride;
+  int jc;
+  int R;                // output blocks per wave run
+  int P;                // partitions
+  int M;                // bins 0..M
+};
+
+struct IrfftArgs {
+  const double2* Y;
+  int64_t y_ch_stride;
+  int MS;
+  double* out;
+  int64_t out_stride;
+  int64_t out_len;      // valid output samples per channel (call-relative)
+  int64_t o0;           // output sample of chunk block 0
+  int jc;
+  int channels;
+  int aligned;
+  const double2* twM;
+  const double2* twN;
+};
+
+bool launch_window_rfft(int M, const RfftArgs& a, hipStream_t s);
+bool launch_irfft_store(int M, const IrfftArgs& a, hipStream_t s);
+bool launch_fdl_mac(int PC, const MacArgs& a, int channels, hipStream_t s);
+void launch_direct(const double* a, int64_t n, const double* b, int64_t m, double* dst, hipStream_t s);
+void launch_direct_circular(const double* a, const double* b, int64_t n, double* dst, hipStream_t s);
+void launch_stream_direct(const double* h, int64_t K, const double* buf, int64_t B, double* y, hipStream_t s);
+void launch_mixdown(const double* ch, int channels, int64_t stride, int64_t len, double* mix, hipStream_t s);
+
+}  // namespace adsp

@@ -1,0 +1,250 @@
+// LDS-resident FP64 Stockham FFT building blocks for gfx950 (CDNA4).
+//
+// Replaces the third-party `github.com/cwbudde/algo-fft v0.6.10` complex128
+// plans the reference calls from dsp/conv/streaming.go:57-98 (fftEngine) and
+// overlap_{add,save}.go (NewPlan64). Semantics kept: forward transform is
+// unnormalised (exp(-2*pi*i*k*n/N)), the inverse carries the 1/N factor
+// (overlap_add.go:138-160 uses real(IFFT(.)) as the convolution result).
+//
+// Design (MI355X-first, not a translation of the Go code):
+//   * one M-point complex FFT is done by M/16 threads, each holding 16
+//     complex128 values in VGPRs; passes are radix-16 (first pass may be
+//     radix 2/4/8), so M = 4096 takes three passes and two LDS exchanges;
+//   * the LDS image is interleaved double2 padded by one element per 16
+//     (pad(i) = i + i/16) so the stride-R butterfly writes of a Stockham
+//     pass hit distinct 16-B slots of the 256-B bank row (ds_write_b128);
+//   * a 256-thread workgroup carries 4096/M independent FFTs, so every size
+//     from 16 to 4096 points keeps the same 69.6 KiB LDS footprint
+//     (two workgroups per CU);
+//   * butterfly twiddles come from one W_M table read once per butterfly and
+//     powered by complex multiplies in registers (FP64 sincos is far too
+//     expensive on the VALU).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+namespace adsp {
+
+struct cplx {
+  double x, y;
+};
+
+__device__ __forceinline__ double2 c_add(double2 a, double2 b) { return make_double2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ double2 c_sub(double2 a, double2 b) { return make_double2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ double2 c_mul(double2 a, double2 b) {
+  return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__device__ __forceinline__ double2 c_conj(double2 a) { return make_double2(a.x, -a.y); }
+__device__ __forceinline__ double2 c_scale(double2 a, double s) { return make_double2(a.x * s, a.y * s); }
+
+// cos(2*pi*k/16), k = 0..15
+__device__ constexpr double kCos16[16] = {
+    1.0,
+    0.92387953251128675613,
+    0.70710678118654752440,
+    0.38268343236508977173,
+    0.0,
+    -0.38268343236508977173,
+    -0.70710678118654752440,
+    -0.92387953251128675613,
+    -1.0,
+    -0.92387953251128675613,
+    -0.70710678118654752440,
+    -0.38268343236508977173,
+    0.0,
+    0.38268343236508977173,
+    0.70710678118654752440,
+    0.92387953251128675613,
+};
+
+// a * W16^E with W16 = exp(-2*pi*i/16) for the forward direction (conjugate
+// for the inverse). Trivial rotations are special-cased so no multiply by an
+// exact 0/1 is ever issued.
+template <int E, bool FWD>
+__device__ __forceinline__ double2 tw16(double2 a) {
+  constexpr int e = E & 15;
+  constexpr double R2 = 0.70710678118654752440;
+  if constexpr (e == 0) {
+    return a;
+  } else if constexpr (e == 4) {
+    return FWD ? make_double2(a.y, -a.x) : make_double2(-a.y, a.x);
+  } else if constexpr (e == 8) {
+    return make_double2(-a.x, -a.y);
+  } else if constexpr (e == 12) {
+    return FWD ? make_double2(-a.y, a.x) : make_double2(a.y, -a.x);
+  } else if constexpr (e == 2) {
+    return FWD ? make_double2((a.x + a.y) * R2, (a.y - a.x) * R2) : make_double2((a.x - a.y) * R2, (a.y + a.x) * R2);
+  } else if constexpr (e == 6) {
+    return FWD ? make_double2((a.y - a.x) * R2, -(a.x + a.y) * R2) : make_double2(-(a.x + a.y) * R2, (a.x - a.y) * R2);
+  } else if constexpr (e == 10) {
+    return FWD ? make_double2(-(a.x + a.y) * R2, (a.x - a.y) * R2) : make_double2((a.y - a.x) * R2, -(a.x + a.y) * R2);
+  } else if constexpr (e == 14) {
+    return FWD ? make_double2((a.x - a.y) * R2, (a.y + a.x) * R2) : make_double2((a.x + a.y) * R2, (a.y - a.x) * R2);
+  } else {
+    constexpr double c = kCos16[e];
+    constexpr double s0 = kCos16[(e + 12) & 15];  // sin(2*pi*e/16)
+    constexpr double s = FWD ? -s0 : s0;
+    return make_double2(a.x * c - a.y * s, a.x * s + a.y * c);
+  }
+}
+
+// In-register DFT of R = 1,2,4,8,16 points, natural order in and out.
+// Radix-2 decimation in time, fully unrolled at compile time.
+template <int R, bool FWD>
+struct Dft {
+  template <int I = 0>
+  __device__ static __forceinline__ void combine(double2* v, const double2* e, const double2* o) {
+    if constexpr (I < R / 2) {
+      const double2 t = tw16<I*(16 / R), FWD>(o[I]);
+      v[I] = c_add(e[I], t);
+      v[I + R / 2] = c_sub(e[I], t);
+      combine<I + 1>(v, e, o);
+    }
+  }
+  __device__ static __forceinline__ void run(double2* v) {
+    double2 e[R / 2], o[R / 2];
+#pragma unroll
+    for (int i = 0; i < R / 2; ++i) {
+      e[i] = v[2 * i];
+      o[i] = v[2 * i + 1];
+    }
+    Dft<R / 2, FWD>::run(e);
+    Dft<R / 2, FWD>::run(o);
+    combine(v, e, o);
+  }
+};
+template <bool FWD>
+struct Dft<1, FWD> {
+  __device__ static __forceinline__ void run(double2*) {}
+};
+
+// ---------------------------------------------------------------------------
+// Mixed-radix Stockham plan for M = 2^m, 16 <= M <= 4096.
+// Passes: first radix R0 = M / 16^(passes-1) in {2,4,8,16}, then radix 16.
+// ---------------------------------------------------------------------------
+__host__ __device__ constexpr int ilog2c(int v) { return v <= 1 ? 0 : 1 + ilog2c(v >> 1); }
+template <int M>
+struct FftPlan {
+  static_assert(M >= 16 && M <= 4096 && (M & (M - 1)) == 0, "FFT size must be a power of two in [16, 4096]");
+  static constexpr int LOG = ilog2c(M);
+  static constexpr int NPASS = (LOG + 3) / 4;
+  static constexpr int R0 = 1 << (LOG - 4 * (NPASS - 1));
+  static constexpr int T = M / 16;          // threads per FFT
+  static constexpr int F = 256 / T;         // FFTs per 256-thread workgroup
+  static constexpr int MP = M + M / 16;     // padded LDS elements per FFT
+  static constexpr int radix(int p) { return p == 0 ? R0 : 16; }
+  static constexpr int ns(int p) { return p == 0 ? 1 : R0 * (1 << (4 * (p - 1))); }
+};
+
+__device__ __forceinline__ int lds_pad(int i) { return i + (i >> 4); }
+
+// Twiddle multiply for butterfly jb of a pass with stride NS and radix R:
+// v[r] *= W_{NS*R}^{(jb mod NS) * r} = W_M^{e*r}, e = (jb mod NS) * M/(NS*R).
+template <int M, int R, int NS, bool FWD>
+__device__ __forceinline__ void apply_twiddles(double2* v, int jb, const double2* __restrict__ twM) {
+  if constexpr (NS > 1) {
+    const int e = (jb & (NS - 1)) * (M / (NS * R));
+    double2 w = twM[e];
+    if (!FWD) w = c_conj(w);
+    double2 wr = w;
+#pragma unroll
+    for (int r = 1; r < R; ++r) {
+      v[r] = c_mul(v[r], wr);
+      if (r + 1 < R) wr = c_mul(wr, w);
+    }
+  }
+}
+
+// One in-register pass on the thread's 16 values (16/R butterflies of radix R),
+// followed by the Stockham store into the LDS image of this FFT.
+template <int M, int P, bool FWD>
+__device__ __forceinline__ void pass_compute_store(double2* v, int tid, double2* lds, const double2* __restrict__ twM) {
+  using Plan = FftPlan<M>;
+  constexpr int R = Plan::radix(P);
+  constexpr int NS = Plan::ns(P);
+  constexpr int NB = 16 / R;
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const int jb = tid + b * Plan::T;
+    apply_twiddles<M, R, NS, FWD>(v + b * R, jb, twM);
+    Dft<R, FWD>::run(v + b * R);
+  }
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const int jb = tid + b * Plan::T;
+    const int base = (jb / NS) * NS * R + (jb & (NS - 1));
+#pragma unroll
+    for (int r = 0; r < R; ++r) lds[lds_pad(base + r * NS)] = v[b * R + r];
+  }
+}
+
+// Load the thread's 16 values of pass P from the LDS image.
+template <int M, int P>
+__device__ __forceinline__ void pass_load(double2* v, int tid, const double2* lds) {
+  using Plan = FftPlan<M>;
+  constexpr int R = Plan::radix(P);
+  constexpr int NB = 16 / R;
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const int jb = tid + b * Plan::T;
+#pragma unroll
+    for (int r = 0; r < R; ++r) v[b * R + r] = lds[lds_pad(jb + r * (M / R))];
+  }
+}
+
+// Index (in the natural-order input) of value slot s of the thread for pass 0.
+template <int M>
+__device__ __forceinline__ int pass0_index(int tid, int s) {
+  using Plan = FftPlan<M>;
+  constexpr int R = Plan::R0;
+  const int b = s / R, r = s % R;
+  return tid + b * Plan::T + r * (M / R);
+}
+
+// Runs passes [1, NPASS-1) (the middle passes) after pass 0 has been stored:
+// barrier, load, compute, barrier, store.  Leaves the last pass's input in v
+// (already loaded), ready for the caller's final pass handling.
+template <int M, bool FWD, int P = 1>
+__device__ __forceinline__ void run_middle_passes(double2* v, int tid, double2* lds, const double2* __restrict__ twM) {
+  using Plan = FftPlan<M>;
+  if constexpr (P < Plan::NPASS) {
+    __syncthreads();
+    pass_load<M, P>(v, tid, lds);
+    if constexpr (P + 1 < Plan::NPASS) {
+      __syncthreads();
+      pass_compute_store<M, P, FWD>(v, tid, lds, twM);
+      run_middle_passes<M, FWD, P + 1>(v, tid, lds, twM);
+    }
+  }
+}
+
+// Computes the last pass in registers (twiddles + DFT) without storing.
+// After this, slot r of the thread holds output index tid + r*T (R = 16).
+template <int M, bool FWD>
+__device__ __forceinline__ void last_pass_compute(double2* v, int tid, const double2* __restrict__ twM) {
+  using Plan = FftPlan<M>;
+  constexpr int P = Plan::NPASS - 1;
+  constexpr int R = Plan::radix(P);
+  constexpr int NS = Plan::ns(P);
+  constexpr int NB = 16 / R;
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const int jb = tid + b * Plan::T;
+    apply_twiddles<M, R, NS, FWD>(v + b * R, jb, twM);
+    Dft<R, FWD>::run(v + b * R);
+  }
+}
+
+// Output index held by slot s after last_pass_compute.
+template <int M>
+__device__ __forceinline__ int last_pass_index(int tid, int s) {
+  using Plan = FftPlan<M>;
+  constexpr int P = Plan::NPASS - 1;
+  constexpr int R = Plan::radix(P);
+  constexpr int NS = Plan::ns(P);
+  const int b = s / R, r = s % R;
+  const int jb = tid + b * Plan::T;
+  return (jb / NS) * NS * R + (jb & (NS - 1)) + r * NS;
+}
+
+}  // namespace adsp

@@ -1,0 +1,260 @@
+// Host runtime of the UPOLS convolution engine.  See upols_engine.hpp and the
+// data-flow comment at the top of conv_kernels.hip.
+#include "upols_engine.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+
+#include "conv_kernels.hpp"
+
+namespace adsp {
+
+namespace {
+
+int env_int(const char* name, int dflt) {
+  const char* v = std::getenv(name);
+  if (!v || !*v) return dflt;
+  return std::atoi(v);
+}
+
+int pick_pc(int P) {
+  // partitions held in VGPRs per wave: the smallest power of two >= P, capped
+  if (P <= 1) return 1;
+  if (P <= 2) return 2;
+  if (P <= 4) return 4;
+  if (P <= 8) return 8;
+  if (P <= 16) return 16;
+  return env_int("AD_MAC_PC_MAX", 32) >= 32 ? 32 : 16;
+}
+
+}  // namespace
+
+Upols::Upols(int device, const double* kernels, int n_ir, int64_t K, int L, int C, const int32_t* ir_map, int jc_max,
+             hipStream_t stream)
+    : K_(K), L_(L), C_(C), n_ir_(n_ir), jc_max_(jc_max), stream_(stream) {
+  if (L < 16 || L > 4096 || !is_pow2(L)) AD_FAIL(AD_ERR_INTERNAL, "UPOLS hop must be a power of two in [16, 4096]");
+  if (n_ir < 1 || C < 1 || K < 1 || jc_max < 1) AD_FAIL(AD_ERR_INTERNAL, "UPOLS: bad geometry");
+  M_ = L;
+  MS_ = M_ + 8;
+  P_ = (int)((K + L - 1) / L);
+  PC_ = pick_pc(P_);
+  Q_ = jc_max_ + P_ + PC_ + 1;
+  R_ = std::max(1, env_int("AD_MAC_R", 128));
+
+  // Twiddle tables, computed in long double on the host.
+  std::vector<double2> tw(2 * (size_t)M_);
+  const long double two_pi = 6.283185307179586476925286766559005768L;
+  for (int e = 0; e < M_; ++e) {
+    const long double a = -two_pi * (long double)e / (long double)M_;
+    tw[e] = make_double2((double)cosl(a), (double)sinl(a));
+    const long double b = -two_pi * (long double)e / (long double)(2 * M_);
+    tw[M_ + e] = make_double2((double)cosl(b), (double)sinl(b));
+  }
+  tw_.alloc(tw.size());
+  AD_HIP(hipMemcpyAsync(tw_.p, tw.data(), tw.size() * sizeof(double2), hipMemcpyHostToDevice, stream_));
+
+  // IR partitions [n_ir*P][L], zero padded, then their spectra via K1.
+  const int64_t nparts = (int64_t)n_ir_ * P_;
+  std::vector<double> parts((size_t)(nparts * L_), 0.0);
+  for (int r = 0; r < n_ir_; ++r)
+    for (int p = 0; p < P_; ++p) {
+      const int64_t start = (int64_t)p * L_;
+      const int64_t cnt = std::min<int64_t>(L_, K_ - start);
+      std::memcpy(&parts[(size_t)(((int64_t)r * P_ + p) * L_)], kernels + (int64_t)r * K_ + start,
+                  (size_t)cnt * sizeof(double));
+    }
+  DevBuf<double> dparts;
+  dparts.alloc(parts.size());
+  AD_HIP(hipMemcpyAsync(dparts.p, parts.data(), parts.size() * sizeof(double), hipMemcpyHostToDevice, stream_));
+  H_.alloc((size_t)nparts * MS_);
+  AD_HIP(hipMemsetAsync(H_.p, 0, H_.n * sizeof(double2), stream_));
+  RfftArgs a{};
+  a.x = dparts.p;
+  a.x_stride = L_;
+  a.n = L_;
+  a.xhist = nullptr;
+  a.hist_stride = 0;
+  a.s0 = L_;
+  a.jc = 1;
+  a.channels = (int)nparts;
+  a.aligned = 1;
+  a.X = H_.p;
+  a.x_ch_stride = MS_;
+  a.Q = 1;
+  a.slot0 = 0;
+  a.MS = MS_;
+  a.twM = tw_.p;
+  a.twN = tw_.p + M_;
+  if (!launch_window_rfft(M_, a, stream_)) AD_FAIL(AD_ERR_INTERNAL, "unsupported FFT size");
+  AD_HIP(hipGetLastError());
+
+  X_.alloc((size_t)C_ * Q_ * MS_);
+  Y_.alloc((size_t)C_ * jc_max_ * MS_);
+  hist_.alloc((size_t)C_ * L_);
+  std::vector<int> irm(C_);
+  for (int c = 0; c < C_; ++c) irm[c] = ir_map ? ir_map[c] : (c % n_ir_);
+  for (int c = 0; c < C_; ++c)
+    if (irm[c] < 0 || irm[c] >= n_ir_) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "ir_index out of range");
+  irmap_.alloc(C_);
+  AD_HIP(hipMemcpyAsync(irmap_.p, irm.data(), C_ * sizeof(int), hipMemcpyHostToDevice, stream_));
+  reset_stream(stream_);
+  // dparts must outlive the K1 launch that reads it
+  AD_HIP(hipStreamSynchronize(stream_));
+}
+
+Upols::~Upols() {
+  for (auto& r : prof_recs_) {
+    (void)hipEventDestroy(r.start);
+    (void)hipEventDestroy(r.stop);
+  }
+  for (auto e : event_pool_) (void)hipEventDestroy(e);
+}
+
+hipEvent_t Upols::take_event() {
+  if (!event_pool_.empty()) {
+    hipEvent_t e = event_pool_.back();
+    event_pool_.pop_back();
+    return e;
+  }
+  hipEvent_t e;
+  AD_HIP(hipEventCreate(&e));
+  return e;
+}
+
+void Upols::prof_begin(hipStream_t s, hipEvent_t* e) {
+  *e = nullptr;
+  if (!prof_) return;
+  *e = take_event();
+  AD_HIP(hipEventRecord(*e, s));
+}
+
+void Upols::prof_end(hipStream_t s, hipEvent_t e0, int kernel, double bytes) {
+  if (!prof_ || !e0) return;
+  hipEvent_t e1 = take_event();
+  AD_HIP(hipEventRecord(e1, s));
+  prof_recs_.push_back({e0, e1, kernel, bytes});
+}
+
+void Upols::set_profiling(bool on) { prof_ = on; }
+
+void Upols::read_profile(double* ms, int64_t* launches, double* alg_bytes) {
+  for (auto& r : prof_recs_) {
+    AD_HIP(hipEventSynchronize(r.stop));
+    float t = 0.f;
+    AD_HIP(hipEventElapsedTime(&t, r.start, r.stop));
+    acc_ms_[r.kernel] += t;
+    acc_n_[r.kernel] += 1;
+    acc_bytes_[r.kernel] += r.bytes;
+    event_pool_.push_back(r.start);
+    event_pool_.push_back(r.stop);
+  }
+  prof_recs_.clear();
+  for (int k = 0; k < kKernels; ++k) {
+    if (ms) ms[k] = acc_ms_[k];
+    if (launches) launches[k] = acc_n_[k];
+    if (alg_bytes) alg_bytes[k] = acc_bytes_[k];
+    acc_ms_[k] = 0;
+    acc_n_[k] = 0;
+    acc_bytes_[k] = 0;
+  }
+}
+
+void Upols::reset_stream(hipStream_t s) {
+  AD_HIP(hipMemsetAsync(X_.p, 0, X_.n * sizeof(double2), s));
+  AD_HIP(hipMemsetAsync(hist_.p, 0, hist_.n * sizeof(double), s));
+  g_next_ = 0;
+}
+
+void Upols::begin_offline(hipStream_t s) {
+  // blocks with logical index in [-(P+PC), 0) are read as history: zero them.
+  g_next_ = 0;
+  const int nz = P_ + PC_;
+  const size_t pitch = (size_t)Q_ * MS_ * sizeof(double2);
+  AD_HIP(hipMemset2DAsync(X_.p + (size_t)(Q_ - nz) * MS_, pitch, 0, (size_t)nz * MS_ * sizeof(double2), C_, s));
+}
+
+void Upols::run(const double* d_in, int64_t in_stride, int64_t n, double* d_out, int64_t out_stride, int64_t out_len,
+                bool use_hist, hipStream_t s) {
+  if (out_len <= 0) return;
+  const int64_t J = (out_len + L_ - 1) / L_;
+  const int in_aligned = ((reinterpret_cast<uintptr_t>(d_in) & 15) == 0) && (in_stride % 2 == 0);
+  const int out_aligned = ((reinterpret_cast<uintptr_t>(d_out) & 15) == 0) && (out_stride % 2 == 0);
+  for (int64_t cs = 0; cs < J; cs += jc_max_) {
+    const int jc = (int)std::min<int64_t>(jc_max_, J - cs);
+    const int slot0 = (int)(g_next_ % Q_);
+
+    RfftArgs a{};
+    a.x = d_in;
+    a.x_stride = in_stride;
+    a.n = n;
+    a.xhist = use_hist ? hist_.p : nullptr;
+    a.hist_stride = L_;
+    a.s0 = cs * L_;
+    a.jc = jc;
+    a.channels = C_;
+    a.aligned = in_aligned;
+    a.X = X_.p;
+    a.x_ch_stride = (int64_t)Q_ * MS_;
+    a.Q = Q_;
+    a.slot0 = slot0;
+    a.MS = MS_;
+    a.twM = tw_.p;
+    a.twN = tw_.p + M_;
+    // algorithmic bytes per launch: unique input samples in,
+    // M+1 complex128 bins out, per (channel, block)
+    const double blocks = (double)C_ * jc;
+    hipEvent_t e0;
+    prof_begin(s, &e0);
+    launch_window_rfft(M_, a, s);
+    prof_end(s, e0, 0, blocks * ((double)L_ * 8 + (double)(M_ + 1) * 16));
+
+    MacArgs m{};
+    m.X = X_.p;
+    m.x_ch_stride = (int64_t)Q_ * MS_;
+    m.Q = Q_;
+    m.slot0 = slot0;
+    m.MS = MS_;
+    m.H = H_.p;
+    m.h_ir_stride = (int64_t)P_ * MS_;
+    m.ir_index = irmap_.p;
+    m.n_ir = n_ir_;
+    m.Y = Y_.p;
+    m.y_ch_stride = (int64_t)jc_max_ * MS_;
+    m.jc = jc;
+    m.R = std::min(R_, jc);
+    m.P = P_;
+    m.M = M_;
+    prof_begin(s, &e0);
+    launch_fdl_mac(PC_, m, C_, s);
+    prof_end(s, e0, 1, blocks * (double)(M_ + 1) * 32 + (double)n_ir_ * P_ * (M_ + 1) * 16);
+
+    IrfftArgs b{};
+    b.Y = Y_.p;
+    b.y_ch_stride = (int64_t)jc_max_ * MS_;
+    b.MS = MS_;
+    b.out = d_out;
+    b.out_stride = out_stride;
+    b.out_len = out_len;
+    b.o0 = cs * L_;
+    b.jc = jc;
+    b.channels = C_;
+    b.aligned = out_aligned;
+    b.twM = tw_.p;
+    b.twN = tw_.p + M_;
+    prof_begin(s, &e0);
+    launch_irfft_store(M_, b, s);
+    prof_end(s, e0, 2, blocks * ((double)(M_ + 1) * 16 + (double)L_ * 8));
+    AD_HIP(hipGetLastError());
+    g_next_ += jc;
+  }
+}
+
+void Upols::save_history(const double* d_in, int64_t in_stride, int64_t n, hipStream_t s) {
+  if (n < L_) AD_FAIL(AD_ERR_INTERNAL, "streaming call shorter than the hop");
+  AD_HIP(hipMemcpy2DAsync(hist_.p, (size_t)L_ * sizeof(double), d_in + (n - L_), (size_t)in_stride * sizeof(double),
+                          (size_t)L_ * sizeof(double), C_, hipMemcpyDeviceToDevice, s));
+}
+
+}  // namespace adsp

@@ -1,0 +1,79 @@
+// Uniformly partitioned overlap-save engine (host runtime around the HIP
+// kernels of conv_kernels.hip).  One engine owns the IR spectra of n_ir
+// impulse responses, the per-channel frequency-domain delay line (X ring),
+// the per-chunk product spectra (Y) and the input history for streaming.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <vector>
+
+#include "ad_common.hpp"
+
+namespace adsp {
+
+class Upols {
+ public:
+  // kernels: host [n_ir][K].  L: hop (power of two, 16..4096).  C: channels.
+  // ir_map: host [C] IR index per channel (nullable: c % n_ir).
+  // jc_max: blocks per channel per internal chunk.
+  Upols(int device, const double* kernels, int n_ir, int64_t K, int L, int C, const int32_t* ir_map, int jc_max,
+        hipStream_t stream);
+  ~Upols();
+
+  int hop() const { return L_; }
+  int partitions() const { return P_; }
+  int channels() const { return C_; }
+  int64_t kernel_len() const { return K_; }
+  hipStream_t stream() const { return stream_; }
+
+  // Streaming state: zero the delay line and input history.
+  void reset_stream(hipStream_t s);
+  // Offline call start: only the delay-line slots preceding block 0 are zeroed.
+  void begin_offline(hipStream_t s);
+
+  // Runs ceil(out_len/L) blocks for all channels.  d_in: [C][in_stride],
+  // n valid samples.  d_out: [C][out_stride], out_len samples written.
+  // use_hist: the L samples before the call come from the streaming history.
+  void run(const double* d_in, int64_t in_stride, int64_t n, double* d_out, int64_t out_stride, int64_t out_len,
+           bool use_hist, hipStream_t s);
+  // Saves the last L input samples of the call into the streaming history.
+  void save_history(const double* d_in, int64_t in_stride, int64_t n, hipStream_t s);
+
+  // Live kernel timing with HIP events on the launch stream (kernel k:
+  // 0 window rFFT, 1 FDL MAC, 2 inverse rFFT + store).  read_profile
+  // synchronises, accumulates and clears the recorded launches.
+  static constexpr int kKernels = 3;
+  void set_profiling(bool on);
+  void read_profile(double* ms, int64_t* launches, double* alg_bytes);
+
+ private:
+  int64_t K_;
+  int L_, M_, MS_, P_, PC_, C_, n_ir_, jc_max_, Q_, R_;
+  int64_t g_next_ = 0;  // logical index of the next spectrum block
+  hipStream_t stream_;
+  DevBuf<double2> tw_;   // [twM (M) | twN (M)]
+  DevBuf<double2> H_;    // [n_ir][P][MS]
+  DevBuf<double2> X_;    // [C][Q][MS]
+  DevBuf<double2> Y_;    // [C][jc_max][MS]
+  DevBuf<double> hist_;  // [C][L]
+  DevBuf<int> irmap_;    // [C]
+
+  struct ProfRec {
+    hipEvent_t start, stop;
+    int kernel;
+    double bytes;
+  };
+  bool prof_ = false;
+  std::vector<ProfRec> prof_recs_;
+  std::vector<hipEvent_t> event_pool_;
+  double acc_ms_[kKernels] = {0, 0, 0};
+  int64_t acc_n_[kKernels] = {0, 0, 0};
+  double acc_bytes_[kKernels] = {0, 0, 0};
+  hipEvent_t take_event();
+  void prof_begin(hipStream_t s, hipEvent_t* e);
+  void prof_end(hipStream_t s, hipEvent_t e0, int kernel, double bytes);
+};
+
+}  // namespace adsp

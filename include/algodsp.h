@@ -1,0 +1,150 @@
+/*
+ * algodsp.h — C ABI of the MI355X-native block-DSP engine (libalgodsp_hip.so).
+ *
+ * This is the drop-in boundary for the sample-buffer hot path of
+ * github.com/cwbudde/algo-dsp (pure Go, reference snapshot 2026-03-06).  Every
+ * entry point names the reference API it replaces as `file:line` relative to
+ * the reference repository root.  A cgo binding for each is shown in
+ * INTEGRATION.md.
+ *
+ * Conventions
+ *  - plain pointers + int64 sizes only; no C++/torch types cross the boundary;
+ *  - every fallible call returns an int status (AD_OK = 0); the sentinel codes
+ *    mirror the reference's `errors.Is` targets so the Go side can map them
+ *    back (conv.go:41-46, partitioned.go:11-15);
+ *  - host-pointer calls copy in and out inside the call (cgo forbids C from
+ *    retaining Go pointers); `*_device` calls take device pointers and a HIP
+ *    stream (`void*`, NULL = the library's per-handle stream) and are
+ *    asynchronous with respect to the host;
+ *  - a handle is single-caller, like the reference types (no internal locks);
+ *  - ad_last_error() returns a thread-local description of the last failure.
+ *  - there is no CPU fallback: with no usable GPU the create calls fail with
+ *    AD_ERR_NO_DEVICE.
+ */
+#ifndef ALGODSP_H_
+#define ALGODSP_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ------------------------------------------------------ */
+#define AD_OK 0
+#define AD_ERR_EMPTY_INPUT 1              /* conv.ErrEmptyInput        conv.go:42 */
+#define AD_ERR_EMPTY_KERNEL 2             /* conv.ErrEmptyKernel       conv.go:43 */
+#define AD_ERR_LENGTH_MISMATCH 3          /* conv.ErrLengthMismatch    conv.go:44 */
+#define AD_ERR_INVALID_BLOCK_SIZE 4       /* conv.ErrInvalidBlockSize  conv.go:45 */
+#define AD_ERR_INVALID_BLOCK_ORDER 5      /* conv.ErrInvalidBlockOrder partitioned.go:12 */
+#define AD_ERR_EMPTY_IMPULSE_RESPONSE 6   /* conv.ErrEmptyImpulseResponse partitioned.go:13 */
+#define AD_ERR_STAGE_INDEX_OUT_OF_RANGE 7 /* conv.ErrStageIndexOutOfRange partitioned.go:14 */
+#define AD_ERR_INVALID_ARGUMENT 8         /* non-sentinel fmt.Errorf validation errors,
+                                             e.g. streaming_overlap_save.go:50-52 */
+#define AD_ERR_DEVICE 100                 /* HIP runtime failure */
+#define AD_ERR_NO_DEVICE 101              /* no usable gfx950 device */
+#define AD_ERR_INTERNAL 102
+
+/* conv.Mode (conv.go:57-69) */
+#define AD_MODE_FULL 0
+#define AD_MODE_SAME 1
+#define AD_MODE_VALID 2
+
+const char* ad_last_error(void);
+int ad_version(void);
+/* Number of visible HIP devices (0 when none). */
+int ad_device_count(int* count);
+
+/* ======================================================================== */
+/* dsp/conv                                                                 */
+/* ======================================================================== */
+
+typedef struct ad_conv ad_conv;
+
+/* ---- conv.StreamingConvolverT (streaming.go:27-49) ----------------------
+ * NewStreamingOverlapSave(kernel, blockSize)   streaming_overlap_save.go:88
+ * NewStreamingOverlapAdd(kernel, blockSize)    streaming_overlap_add.go:87
+ * Both are zero-latency: out = linear convolution of the stream, block by
+ * block.  FFTSize() reports the reference's nextPow2(blockSize+K-1).      */
+int ad_conv_stream_ols_create(const double* kernel, int64_t kernel_len, int64_t block_size, int device,
+                              ad_conv** out);
+int ad_conv_stream_ola_create(const double* kernel, int64_t kernel_len, int64_t block_size, int device,
+                              ad_conv** out);
+/* ProcessBlockTo(output, input)  streaming_overlap_save.go:152-164,
+ * streaming_overlap_add.go:154-168.  in_len/out_len must equal BlockSize()
+ * (AD_ERR_LENGTH_MISMATCH otherwise).  in and out may alias.              */
+int ad_conv_process_block(ad_conv* h, const double* in, int64_t in_len, double* out, int64_t out_len);
+
+/* ---- batch conv.OverlapSave / conv.OverlapAdd ---------------------------
+ * NewOverlapSave(kernel, fftSize)  overlap_save.go:53-107 (fftSize<=0: auto,
+ *   non-power-of-two: AD_ERR_INVALID_BLOCK_SIZE, < 2K: silently raised)
+ * NewOverlapAdd(kernel, blockSize) overlap_add.go:44-89 (blockSize<=0: auto)
+ * Process/ProcessTo: out_len must be in_len + K - 1 (overlap_save.go:126-272,
+ *   overlap_add.go:108-182); empty input -> AD_ERR_EMPTY_INPUT.           */
+int ad_conv_ols_create(const double* kernel, int64_t kernel_len, int64_t fft_size, int device, ad_conv** out);
+int ad_conv_ola_create(const double* kernel, int64_t kernel_len, int64_t block_size, int device, ad_conv** out);
+int ad_conv_process(ad_conv* h, const double* in, int64_t in_len, double* out, int64_t out_len);
+
+/* ---- conv.PartitionedConvolutionT (partitioned.go:27-436) ---------------
+ * Output is the linear convolution delayed by Latency() = 2^minBlockOrder.
+ * ProcessBlock(input, output) accepts any length (in_len must equal out_len).
+ * Stage layout (StageCount/StageInfo) follows partitionIR (:269-332).     */
+int ad_conv_partitioned_create(const double* kernel, int64_t kernel_len, int min_block_order, int max_block_order,
+                               int device, ad_conv** out);
+int ad_conv_partitioned_process_block(ad_conv* h, const double* in, int64_t in_len, double* out, int64_t out_len);
+int ad_conv_stage_count(const ad_conv* h);
+int ad_conv_stage_info(const ad_conv* h, int index, int64_t* part_size, int64_t* block_count);
+
+/* ---- common handle API -------------------------------------------------- */
+int ad_conv_reset(ad_conv* h);   /* Reset(): clears history/tail/FDL state */
+int64_t ad_conv_block_size(const ad_conv* h);
+int64_t ad_conv_kernel_len(const ad_conv* h);
+int64_t ad_conv_fft_size(const ad_conv* h);
+int64_t ad_conv_step_size(const ad_conv* h); /* OverlapSave.StepSize (overlap_save.go:115) */
+int64_t ad_conv_latency(const ad_conv* h);   /* PartitionedConvolution.Latency (partitioned.go:410) */
+void ad_conv_destroy(ad_conv* h);
+
+/* ---- one-shot functions ------------------------------------------------- */
+/* conv.Direct / DirectTo (conv.go:76-154): bit-exact input-stationary
+ * scatter-add order.  dst has n+m-1 elements.                             */
+int ad_conv_direct(const double* a, int64_t n, const double* b, int64_t m, double* dst, int device);
+/* conv.DirectCircular (conv.go:158-189): n == m, dst has n elements.      */
+int ad_conv_direct_circular(const double* a, int64_t n, const double* b, int64_t m, double* dst, int device);
+/* conv.Convolve / ConvolveMode (conv.go:194-247).  dst_cap is the capacity
+ * of dst; *dst_len receives the result length.                            */
+int ad_conv_convolve(const double* a, int64_t n, const double* b, int64_t m, int mode, double* dst, int64_t dst_cap,
+                     int64_t* dst_len, int device);
+
+/* ---- multi-channel device-resident engine (offline / many-channel path) --
+ * Uniformly partitioned overlap-save with a frequency-domain delay line.
+ * kernels: n_ir impulse responses of kernel_len taps each, row-major.
+ * hop: partition/hop length (power of two, 16..4096); 0 = auto (4096).
+ * channels: number of channels processed per call; ir_index[c] selects the
+ *   IR of channel c (NULL: c % n_ir).
+ * max_chunk_blocks: blocks per channel per internal chunk (0 = auto).     */
+int ad_conv_multi_create(const double* kernels, int n_ir, int64_t kernel_len, int64_t hop, int channels,
+                         const int32_t* ir_index, int64_t max_chunk_blocks, int device, ad_conv** out);
+/* Full linear convolution of every channel (ModeFull semantics per channel):
+ * d_in  [channels][in_stride] (first in_len used),
+ * d_out [channels][out_stride] (first out_len written; out_len <= in_len+K-1).
+ * Device pointers; asynchronous on `stream` (NULL = handle stream).       */
+int ad_conv_multi_process_device(ad_conv* h, const double* d_in, int64_t in_stride, int64_t in_len, double* d_out,
+                                 int64_t out_stride, int64_t out_len, void* stream);
+/* Live kernel timing (HIP events recorded around every launch on the launch
+ * stream) for the FFT engine of a handle.  Kernel index: 0 window rFFT,
+ * 1 frequency-domain delay-line MAC, 2 inverse rFFT + overlap-save store.
+ * read() synchronises and returns, per kernel, the summed duration (ms),
+ * the launch count and the algorithmic bytes those launches moved
+ * (DESIGN.md), then clears the counters.  Arrays have 3 entries.          */
+int ad_conv_profile_enable(ad_conv* h, int enable);
+int ad_conv_profile_read(ad_conv* h, double* total_ms, int64_t* launches, double* alg_bytes);
+/* Stereo mixdown of a channel group (build-defined):
+ * d_mix[0][t] = sum of even channels, d_mix[1][t] = sum of odd channels. */
+int ad_conv_mixdown_device(const double* d_chan, int channels, int64_t stride, int64_t len, double* d_mix,
+                           void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ALGODSP_H_ */

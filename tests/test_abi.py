@@ -1,0 +1,69 @@
+"""C-ABI surface checks that need no GPU: the library loads, exports every
+symbol include/algodsp.h declares, and fails loudly (no CPU fallback) when
+no device is present."""
+import ctypes as C
+import subprocess
+
+import numpy as np
+import pytest
+
+from algodsp import _lib, conv
+
+
+def test_library_exports_every_declared_symbol():
+    L = _lib.lib()
+    syms = _lib.exported_symbols()
+    assert len(syms) >= 20
+    missing = [s for s in syms if not hasattr(L, s)]
+    assert not missing, missing
+    nm = subprocess.run(["nm", "-D", "--defined-only", str(_lib.LIB_PATH)], capture_output=True, text=True).stdout
+    exported = {line.split()[-1] for line in nm.splitlines() if " T " in line}
+    assert set(syms) <= exported
+
+
+def test_header_declares_every_exported_symbol():
+    nm = subprocess.run(["nm", "-D", "--defined-only", str(_lib.LIB_PATH)], capture_output=True, text=True).stdout
+    exported = {line.split()[-1] for line in nm.splitlines() if " T " in line and line.split()[-1].startswith("ad_")}
+    assert exported <= set(_lib.exported_symbols())
+
+
+def test_version_and_last_error():
+    L = _lib.lib()
+    assert L.ad_version() >= 1
+    assert isinstance(L.ad_last_error(), bytes)
+
+
+def _no_gpu():
+    return _lib.device_count() == 0
+
+
+@pytest.mark.skipif(not _no_gpu(), reason="a GPU is visible; covered by the gpu tests")
+def test_no_cpu_fallback_without_device():
+    with pytest.raises(_lib.ADError) as e:
+        conv.NewStreamingOverlapSave([1.0, 0.5], 4)
+    assert e.value.code == _lib.AD_ERR_NO_DEVICE
+    with pytest.raises(_lib.ADError) as e:
+        conv.Direct([1.0, 2.0], [1.0])
+    assert e.value.code == _lib.AD_ERR_NO_DEVICE
+
+
+def test_validation_errors_precede_device_use():
+    """Reference sentinel errors are reported before any device work."""
+    with pytest.raises(conv.ErrEmptyKernel):
+        conv.NewStreamingOverlapSave([], 4)
+    with pytest.raises(conv.ErrInvalidArgument):
+        conv.NewStreamingOverlapSave([1.0], 0)
+    with pytest.raises(conv.ErrEmptyKernel):
+        conv.NewOverlapSave([], 0)
+    with pytest.raises(conv.ErrInvalidBlockSize):
+        conv.NewOverlapSave(np.ones(10), 300)
+    with pytest.raises(conv.ErrEmptyImpulseResponse):
+        conv.NewPartitionedConvolution([], 7, 13)
+    with pytest.raises(conv.ErrInvalidBlockOrder):
+        conv.NewPartitionedConvolution([1.0], 0, 13)
+    with pytest.raises(conv.ErrInvalidBlockOrder):
+        conv.NewPartitionedConvolution([1.0], 8, 7)
+    with pytest.raises(conv.ErrEmptyInput):
+        conv.Direct([], [1.0])
+    with pytest.raises(conv.ErrEmptyKernel):
+        conv.Direct([1.0], [])

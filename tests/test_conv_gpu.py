@@ -1,0 +1,271 @@
+"""GPU parity of dsp/conv through the HIP C ABI against the CPU oracle.
+
+Tolerances (BASELINE.json north_star): direct convolution is compared
+bit-exactly (same operation order, no FMA); FFT paths must be within
+1e-7 RMS of the oracle (we also assert a much tighter max-abs bound).
+"""
+import json
+import math
+import pathlib
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+from algodsp import conv, irlib, signals
+
+pytestmark = pytest.mark.gpu
+
+KATS = json.loads((pathlib.Path(__file__).parent / "golden" / "reference_kats.json").read_text())
+FFT_RMS_TOL = 1e-7  # north_star: <= 1e-7 RMS for FFT convolution
+
+
+def rms(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    assert a.shape == b.shape
+    return float(np.sqrt(np.mean((a - b) ** 2))) if a.size else 0.0
+
+
+# ------------------------------------------------------------------ Direct
+@pytest.mark.parametrize("case", KATS["direct"], ids=lambda c: c["source"])
+def test_direct_kat(gpu, case):
+    np.testing.assert_allclose(conv.Direct(case["a"], case["b"]), case["expected"], atol=case["tol"], rtol=0)
+
+
+@pytest.mark.parametrize("n,m", [(1, 1), (7, 3), (100, 15), (100, 16), (48000, 256), (300, 1000), (5, 64)])
+def test_direct_bit_exact(gpu, n, m):
+    a = signals.white_noise(n, 100 + n)
+    b = signals.white_noise(m, 200 + m)
+    got = conv.Direct(a, b)
+    want = O.direct(a, b)
+    assert np.array_equal(got, want), float(np.max(np.abs(got - want)))
+
+
+def test_direct_circular(gpu):
+    c = KATS["direct_circular"][0]
+    np.testing.assert_allclose(conv.DirectCircular(c["a"], c["b"]), c["expected"], atol=1e-10)
+    a, b = signals.white_noise(257, 1), signals.white_noise(257, 2)
+    assert np.array_equal(conv.DirectCircular(a, b), O.direct_circular(a, b))
+    with pytest.raises(conv.ErrLengthMismatch):
+        conv.DirectCircular([1, 2, 3], [1, 2])
+
+
+@pytest.mark.parametrize("m", [5, 64, 65, 300, 5000])
+@pytest.mark.parametrize("mode", [conv.ModeFull, conv.ModeSame, conv.ModeValid])
+def test_convolve_mode(gpu, m, mode):
+    a = signals.make_test_signal(3000)
+    b = signals.make_test_kernel(m)
+    got = conv.ConvolveMode(a, b, mode)
+    want = O.convolve_mode(a, b, mode)
+    assert got.shape == want.shape
+    if m <= 64:
+        assert np.array_equal(got, want)
+    else:
+        assert rms(got, want) < FFT_RMS_TOL and np.max(np.abs(got - want)) < 1e-9
+
+
+def test_convolve_commutative_swap(gpu):
+    a, b = signals.white_noise(50, 1), signals.white_noise(400, 2)
+    np.testing.assert_allclose(conv.Convolve(a, b), conv.Convolve(b, a), atol=1e-10)
+
+
+# --------------------------------------------------------------- streaming
+def test_streaming_ols_impulse_kat(gpu):
+    c = KATS["streaming_ols_impulse"]
+    s = conv.NewStreamingOverlapSave(c["kernel"], c["block_size"])
+    np.testing.assert_allclose(s.ProcessBlock(c["blocks"][0]), c["expected_first"], atol=c["tol"])
+    assert s.BlockSize() == 4 and s.KernelLen() == 3 and s.FFTSize() == 8
+
+
+@pytest.mark.parametrize("ola", [False, True])
+@pytest.mark.parametrize("K,B,nb", [(4, 8, 4), (3, 4, 3), (5, 3, 4), (100, 64, 5), (1000, 4096, 3), (16384, 4096, 6),
+                                    (2048, 256, 12), (4097, 512, 10), (300, 1000, 3), (20000, 16384, 3)])
+def test_streaming_matches_oracle(gpu, ola, K, B, nb):
+    h = signals.make_test_kernel(K) if K > 1 else np.ones(1)
+    x = signals.white_noise(B * nb, K + B)
+    ctor = conv.NewStreamingOverlapAdd if ola else conv.NewStreamingOverlapSave
+    g = ctor(h, B)
+    o = O.Streaming(h, B, ola=ola)
+    assert g.FFTSize() == o.fft_size()
+    got, want = [], []
+    for i in range(nb):
+        blk = x[i * B:(i + 1) * B]
+        out = np.empty(B)
+        g.ProcessBlockTo(out, blk)
+        got.append(out)
+        want.append(o.process_block(blk))
+    got, want = np.concatenate(got), np.concatenate(want)
+    assert rms(got, want) < FFT_RMS_TOL
+    assert np.max(np.abs(got - want)) < 1e-9 * max(1.0, math.sqrt(K) / 8)
+
+
+def test_streaming_reset_and_errors(gpu):
+    h = signals.make_test_kernel(257)
+    s = conv.NewStreamingOverlapSave(h, 256)
+    x = signals.white_noise(512, 3)
+    first = s.ProcessBlock(x[:256])
+    s.ProcessBlock(x[256:])
+    s.Reset()
+    np.testing.assert_allclose(s.ProcessBlock(x[:256]), first, atol=1e-13)
+    with pytest.raises(conv.ErrLengthMismatch):
+        s.ProcessBlock(x[:100])
+    with pytest.raises(conv.ErrLengthMismatch):
+        s.ProcessBlockTo(np.empty(100), x[:256])
+
+
+def test_streaming_in_place(gpu):
+    h = signals.make_test_kernel(64)
+    s = conv.NewStreamingOverlapSave(h, 128)
+    o = O.Streaming(h, 128)
+    x = signals.white_noise(128, 4)
+    buf = x.copy()
+    s.ProcessBlockTo(buf, buf)  # aliasing allowed
+    assert rms(buf, o.process_block(x)) < 1e-12
+
+
+# ------------------------------------------------------------------- batch
+@pytest.mark.parametrize("K,n", [(1, 10), (3, 10), (64, 1000), (257, 4096), (4096, 4096), (5000, 20000),
+                                 (16384, 50000), (131072, 70000)])
+def test_batch_ols_ola(gpu, K, n):
+    h = signals.make_test_kernel(K) if K > 1 else np.ones(1)
+    x = signals.white_noise(n, K)
+    ols = conv.NewOverlapSave(h, 0)
+    ola = conv.NewOverlapAdd(h, 0)
+    o_ols = O.OverlapSave(h, 0)
+    o_ola = O.OverlapAdd(h, 0)
+    assert ols.FFTSize() == o_ols.fft_size() and ols.StepSize() == o_ols.step_size()
+    assert ola.FFTSize() == o_ola.fft_size() and ola.BlockSize() == o_ola.block_size()
+    want = o_ols.process(x)
+    got = ols.Process(x)
+    assert rms(got, want) < FFT_RMS_TOL and np.max(np.abs(got - want)) < 1e-8
+    got2 = ola.Process(x)
+    assert rms(got2, o_ola.process(x)) < FFT_RMS_TOL
+    # ProcessTo + reuse of the same handle
+    out = np.empty(n + K - 1)
+    ols.ProcessTo(out, x)
+    assert np.array_equal(out, got)
+    with pytest.raises(conv.ErrLengthMismatch):
+        ols.ProcessTo(np.empty(n), x)
+    with pytest.raises(conv.ErrEmptyInput):
+        ols.Process(np.empty(0))
+
+
+# -------------------------------------------------------------- partitioned
+@pytest.mark.parametrize("K,lo,hi", [(64, 4, 10), (256, 5, 12), (1024, 6, 13), (8192, 6, 13), (3, 2, 5), (1, 4, 12),
+                                     (95432, 7, 13), (5000, 13, 13), (700, 3, 6)])
+def test_partitioned_matches_oracle(gpu, K, lo, hi):
+    h = signals.make_impulse_kernel(K)
+    lat = 1 << lo
+    n = max(4 * lat, min(3 * K, 60000))
+    x = signals.white_noise(n, K + lo)
+    g = conv.NewPartitionedConvolution(h, lo, hi)
+    o = O.Partitioned(h, lo, hi)
+    assert g.Latency() == o.latency() == lat
+    assert g.StageCount() == o.stage_count()
+    assert [g.StageInfo(i) for i in range(g.StageCount())] == [o.stage_info(i) for i in range(o.stage_count())]
+    sizes = [lat + 3, 1, 2 * lat, lat - 1 if lat > 1 else 1, 5 * lat + 7]
+    pos, step, got, want = 0, 0, [], []
+    while pos < n:
+        m = min(sizes[step % len(sizes)], n - pos)
+        blk = x[pos:pos + m]
+        out = np.empty(m)
+        g.ProcessBlock(blk, out)
+        got.append(out)
+        want.append(o.process_block(blk))
+        pos += m
+        step += 1
+    got, want = np.concatenate(got), np.concatenate(want)
+    assert rms(got, want) < FFT_RMS_TOL
+    assert np.max(np.abs(got - want)) < 1e-9
+    with pytest.raises(conv.ErrStageIndexOutOfRange):
+        g.StageInfo(g.StageCount())
+    with pytest.raises(conv.ErrLengthMismatch):
+        g.ProcessBlock(x[:10], np.empty(9))
+
+
+def test_partitioned_dirac(gpu):
+    c = KATS["partitioned_dirac"]
+    x = signals.white_noise(c["signal_len"], 3)
+    g = conv.NewPartitionedConvolution(c["kernel"], c["min_order"], c["max_order"])
+    lat = 1 << c["min_order"]
+    xin = np.concatenate([x, np.zeros(lat)])
+    out = np.empty(xin.size)
+    g.ProcessBlock(xin, out)
+    np.testing.assert_allclose(out[lat:], x, atol=c["tol"])
+    g.Reset()
+    out2 = np.empty(xin.size)
+    g.ProcessBlock(xin, out2)
+    np.testing.assert_allclose(out2, out, atol=1e-14)
+
+
+# ---------------------------------------------------- multi-channel engine
+def _multi_run(kernels, x, hop=4096, chunk=0, ir_index=None, out_len=None):
+    import torch
+
+    C_, n = x.shape
+    K = kernels.shape[1]
+    out_len = out_len or n + K - 1
+    eng = conv.MultiChannelConvolver(kernels, hop=hop, channels=C_, ir_index=ir_index, chunk_blocks=chunk)
+    dx = torch.from_numpy(x).cuda()
+    dy = torch.zeros((C_, out_len), dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()
+    eng.process_device(dx.data_ptr(), n, n, dy.data_ptr(), out_len, out_len)
+    torch.cuda.synchronize()
+    return dy.cpu().numpy(), eng
+
+
+def test_multi_stereo_large_church_vs_oracle(gpu):
+    """Config 3 shape (stereo x 131072-tap Large Church) at an oracle-sized length."""
+    ir = irlib.large_church()
+    n = 1 << 16
+    x = np.stack([signals.white_noise(n, 0x5EED + c) for c in range(2)])
+    y, _ = _multi_run(ir, x, chunk=7)
+    for c in range(2):
+        want = O.OverlapSave(ir[c], 0).process(x[c])
+        assert rms(y[c], want) < FFT_RMS_TOL
+        assert np.max(np.abs(y[c] - want)) < 1e-9
+
+
+@pytest.mark.parametrize("hop", [16, 256, 1024, 4096])
+def test_multi_hops_and_ir_map(gpu, hop):
+    K = 3000
+    irs = np.stack([signals.make_test_kernel(K), signals.white_noise(K, 7), signals.make_impulse_kernel(K)])
+    C_ = 5
+    n = 20000
+    x = np.stack([signals.white_noise(n, c) for c in range(C_)])
+    ir_index = [2, 0, 1, 1, 0]
+    y, _ = _multi_run(irs, x, hop=hop, chunk=3, ir_index=ir_index)
+    for c in range(C_):
+        want = O.direct_ld(x[c], irs[ir_index[c]])
+        assert rms(y[c], want) < 1e-10
+
+
+def test_multi_full_size_spot_check(gpu):
+    """Full config-3 length (2 x 2^24): size-independent check of random output
+    samples against exact dot products (y[t] = sum_k h[k] x[t-k])."""
+    ir = irlib.large_church()
+    n = 1 << 24
+    x = np.stack([signals.white_noise(n, 0x5EED + c) for c in range(2)])
+    y, _ = _multi_run(ir, x, out_len=n)
+    rng = np.random.default_rng(1)
+    K = ir.shape[1]
+    for c in range(2):
+        ts = np.concatenate([[0, 1, K - 2, K - 1, K, n - 1], rng.integers(0, n, 40)])
+        hr = ir[c][::-1]
+        for t in ts:
+            lo = max(0, t - K + 1)
+            seg = x[c][lo:t + 1]
+            ref = float(np.dot(hr[K - seg.size:], seg))
+            assert abs(y[c][t] - ref) < 1e-9, (c, t, y[c][t], ref)
+
+
+def test_mixdown(gpu):
+    import torch
+
+    x = torch.from_numpy(np.stack([signals.white_noise(1000, c) for c in range(6)])).cuda()
+    mix = torch.zeros((2, 1000), dtype=torch.float64, device="cuda")
+    conv.mixdown_device(x.data_ptr(), 6, 1000, 1000, mix.data_ptr())
+    torch.cuda.synchronize()
+    xn = x.cpu().numpy()
+    np.testing.assert_allclose(mix.cpu().numpy()[0], xn[0] + xn[2] + xn[4], atol=1e-15)
+    np.testing.assert_allclose(mix.cpu().numpy()[1], xn[1] + xn[3] + xn[5], atol=1e-15)
