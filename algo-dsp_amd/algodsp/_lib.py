@@ -98,6 +98,16 @@ def lib() -> C.CDLL:
     """Loads (once) and returns the HIP library; raises if it is missing."""
     global _lib
     if _lib is None:
+        # PyTorch-ROCm bundles its own libamdhip64 (SONAME libamdhip64.so.7) and
+        # refers to it by the unversioned name, so if our library pulled in
+        # /opt/rocm's copy first the process would end up with two HIP/HSA
+        # runtimes and torch would see no GPU.  Importing torch first makes the
+        # dynamic linker bind our NEEDED libamdhip64.so.7 to torch's runtime:
+        # one runtime, shared device pointers and streams.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         path = os.environ.get("ALGODSP_LIB", str(LIB_PATH))
         if not pathlib.Path(path).exists():
             raise ImportError(f"libalgodsp_hip.so not built at {path}; run `make -C algo-dsp_amd`")

@@ -205,7 +205,7 @@ void batch_convolve(ad_conv* h, const double* in, int64_t n, double* out, int64_
 
 int64_t batch_hop(int64_t K) {
   int64_t l = next_pow2(std::max<int64_t>(K, 256));
-  return std::min<int64_t>(l, 4096);
+  return std::min<int64_t>(l, 8192);
 }
 
 void make_batch_engine(ad_conv* h, const double* kernel, int64_t K) {
@@ -244,7 +244,7 @@ static int stream_create(Kind kind, const double* kernel, int64_t K, int64_t B, 
     h->K = K;
     h->block_size = B;
     h->fft_size = next_pow2(B + K - 1);
-    setup_stream_engine(h.get(), kernel, K, B, 4096);
+    setup_stream_engine(h.get(), kernel, K, B, 8192);
     stream_reset(h.get());
     return h.release();
   });
@@ -364,8 +364,8 @@ int ad_conv_partitioned_create(const double* kernel, int64_t K, int min_order, i
     for (const auto& s : h->stages) cover = std::max(cover, s.start + s.count * s.part_size);
     const int64_t keff = std::min<int64_t>(K, cover);
     h->fft_size = 2 * h->stages.back().part_size;
-    // Zero-latency engine with hop = latency (<= 4096), output delayed by latency.
-    setup_stream_engine(h.get(), kernel, keff, latency, 4096);
+    // Zero-latency engine with hop = latency (<= 8192), output delayed by latency.
+    setup_stream_engine(h.get(), kernel, keff, latency, 8192);
     stream_reset(h.get());
     return h.release();
   });
@@ -544,8 +544,8 @@ int ad_conv_multi_create(const double* kernels, int n_ir, int64_t K, int64_t hop
     if (K <= 0 || !kernels || n_ir <= 0) AD_FAIL(AD_ERR_EMPTY_KERNEL, "conv: empty kernel");
     if (channels <= 0) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "channels must be positive");
     if (hop <= 0) hop = 4096;
-    if (hop < 16 || hop > 4096 || !is_pow2(hop))
-      AD_FAIL(AD_ERR_INVALID_BLOCK_SIZE, "hop must be a power of two in [16, 4096]");
+    if (hop < 16 || hop > 8192 || !is_pow2(hop))
+      AD_FAIL(AD_ERR_INVALID_BLOCK_SIZE, "hop must be a power of two in [16, 8192]");
     if (max_chunk_blocks <= 0) max_chunk_blocks = 1024;
     const int dev = pick_device(device);
     DeviceScope ds(dev);

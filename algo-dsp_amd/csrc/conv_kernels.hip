@@ -25,11 +25,22 @@
 
 namespace adsp {
 
+// Workgroups are dealt round-robin over the 8 XCDs (b % 8 share one L2).
+// Remap the hardware index so each XCD owns a contiguous run of logical
+// indices: neighbouring blocks (which share input samples / X rows) then run
+// on the same XCD at about the same time.  Bijective for any grid size; a
+// different placement changes speed only, never results.
+__device__ __forceinline__ int xcd_remap(int b, int G) {
+  const int xcd = b & 7, r = b >> 3;
+  const int q = G >> 3, rem = G & 7;
+  return (xcd < rem) ? xcd * (q + 1) + r : rem * (q + 1) + (xcd - rem) * q + r;
+}
+
 // ---------------------------------------------------------------------------
 // K1: forward real FFT of one overlap-save window per (channel, block).
 // ---------------------------------------------------------------------------
 template <int M>
-__global__ __launch_bounds__(256) void k_window_rfft(RfftArgs a) {
+__global__ __launch_bounds__(FftPlan<M>::BLOCK) void k_window_rfft(RfftArgs a) {
   using Plan = FftPlan<M>;
   constexpr int T = Plan::T;
   constexpr int L = M;
@@ -37,7 +48,7 @@ __global__ __launch_bounds__(256) void k_window_rfft(RfftArgs a) {
 
   const int f = threadIdx.x / T;
   const int tid = threadIdx.x % T;
-  const int64_t e = (int64_t)blockIdx.x * Plan::F + f;
+  const int64_t e = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * Plan::F + f;
   const bool active = e < (int64_t)a.channels * a.jc;
   const int c = active ? (int)(e / a.jc) : 0;
   const int j = active ? (int)(e % a.jc) : 0;
@@ -102,7 +113,7 @@ __global__ __launch_bounds__(256) void k_window_rfft(RfftArgs a) {
 // discard of the first N-L circular outputs), store to y.
 // ---------------------------------------------------------------------------
 template <int M>
-__global__ __launch_bounds__(256) void k_irfft_store(IrfftArgs a) {
+__global__ __launch_bounds__(FftPlan<M>::BLOCK) void k_irfft_store(IrfftArgs a) {
   using Plan = FftPlan<M>;
   constexpr int T = Plan::T;
   constexpr int L = M;
@@ -110,7 +121,7 @@ __global__ __launch_bounds__(256) void k_irfft_store(IrfftArgs a) {
 
   const int f = threadIdx.x / T;
   const int tid = threadIdx.x % T;
-  const int64_t e = (int64_t)blockIdx.x * Plan::F + f;
+  const int64_t e = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * Plan::F + f;
   const bool active = e < (int64_t)a.channels * a.jc;
   const int c = active ? (int)(e / a.jc) : 0;
   const int j = active ? (int)(e % a.jc) : 0;
@@ -166,13 +177,96 @@ __global__ __launch_bounds__(256) void k_irfft_store(IrfftArgs a) {
 // slots are compile-time indices (the unrolled u/q loops), so the kernel
 // reads each spectrum once and writes each output once.  P > PC is handled
 // by sweeping partition chunks, read-modify-writing Y.
+//
+// Blocks with logical index < 0 (before the stream/signal start) read as
+// zeros without touching memory, so an offline call needs no memset.  The
+// warm-up group (the PC-1 spectra before the run) issues only the products
+// that reach outputs of the run: every FMA issued is a useful one.
+// 1-D grid, XCD-remapped so the runs of one bin group (which re-read each
+// other's warm-up rows) share an L2.
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ void cmac(double2& s, const double2 x, const double2 h) {
+  s.x = fma(x.x, h.x, s.x);
+  s.x = fma(-x.y, h.y, s.x);
+  s.y = fma(x.x, h.y, s.y);
+  s.y = fma(x.y, h.x, s.y);
+}
+
+// Ring cursor over the X spectra of one lane's bin (wave-uniform state).
+struct MacCursor {
+  int64_t lx;  // logical spectrum index (< 0: before the signal, reads zero)
+  int slot;    // ring slot of lx
+  int Q;
+  __device__ __forceinline__ double2 load(const double2* Xc, int MS) const {
+    return (lx >= 0) ? Xc[(int64_t)slot * MS] : make_double2(0.0, 0.0);
+  }
+  __device__ __forceinline__ void advance() {
+    ++lx;
+    slot = (slot + 1 == Q) ? 0 : slot + 1;
+  }
+};
+
+// Compile-time unrolled iteration bodies: template recursion keeps every
+// accumulator / H index a constant so the arrays stay in VGPRs.
+template <int PC, int U>
+struct MacWarm {
+  template <int Q = PC - U>
+  __device__ static __forceinline__ void macs(double2 (&acc)[PC], const double2 (&h)[PC], const double2 x) {
+    if constexpr (Q < PC) {
+      cmac(acc[(U + Q) % PC], x, h[Q]);
+      macs<Q + 1>(acc, h, x);
+    }
+  }
+  __device__ static __forceinline__ void run(double2 (&acc)[PC], const double2 (&h)[PC], const double2* Xc, int MS,
+                                             MacCursor& cur) {
+    if constexpr (U < PC) {
+      const double2 x = cur.load(Xc, MS);
+      macs(acc, h, x);
+      cur.advance();
+      MacWarm<PC, U + 1>::run(acc, h, Xc, MS, cur);
+    }
+  }
+};
+
+template <int PC, int U>
+struct MacMain {
+  template <int Q = 0>
+  __device__ static __forceinline__ void macs(double2 (&acc)[PC], const double2 (&h)[PC], const double2 x) {
+    if constexpr (Q < PC) {
+      cmac(acc[(U + Q) % PC], x, h[Q]);
+      macs<Q + 1>(acc, h, x);
+    }
+  }
+  __device__ static __forceinline__ void run(double2 (&acc)[PC], const double2 (&h)[PC], const double2* Xc,
+                                             double2* Yc, int MS, MacCursor& cur, int i, int j1, bool first) {
+    if constexpr (U < PC) {
+      if (i + U >= j1) return;  // wave-uniform
+      const double2 x = cur.load(Xc, MS);
+      macs(acc, h, x);
+      double2* yp = Yc + (int64_t)(i + U) * MS;
+      if (first) {
+        *yp = acc[U];
+      } else {
+        const double2 o = *yp;
+        *yp = make_double2(o.x + acc[U].x, o.y + acc[U].y);
+      }
+      acc[U] = make_double2(0.0, 0.0);
+      cur.advance();
+      MacMain<PC, U + 1>::run(acc, h, Xc, Yc, MS, cur, i, j1, first);
+    }
+  }
+};
+
 template <int PC>
 __global__ __launch_bounds__(64) void k_fdl_mac(MacArgs a) {
-  const int k = blockIdx.x * 64 + threadIdx.x;
+  const int lg = xcd_remap(blockIdx.x, gridDim.x);
+  const int ry = lg % a.ny;
+  const int t = lg / a.ny;
+  const int bx = t % a.nx;
+  const int c = t / a.nx;
+  const int k = bx * 64 + threadIdx.x;
   if (k > a.M) return;
-  const int c = blockIdx.z;
-  const int j0 = blockIdx.y * a.R;
+  const int j0 = ry * a.R;
   const int j1 = min(j0 + a.R, a.jc);
   const int ir = a.ir_index ? a.ir_index[c] : (c % a.n_ir);
   const double2* Hc = a.H + (int64_t)ir * a.h_ir_stride + k;
@@ -182,42 +276,22 @@ __global__ __launch_bounds__(64) void k_fdl_mac(MacArgs a) {
   for (int p0 = 0; p0 < a.P; p0 += PC) {
     double2 h[PC];
 #pragma unroll
-    for (int q = 0; q < PC; ++q) {
-      h[q] = (p0 + q < a.P) ? Hc[(int64_t)(p0 + q) * a.MS] : make_double2(0.0, 0.0);
-    }
+    for (int q = 0; q < PC; ++q) h[q] = (p0 + q < a.P) ? Hc[(int64_t)(p0 + q) * a.MS] : make_double2(0.0, 0.0);
     double2 acc[PC];
 #pragma unroll
     for (int q = 0; q < PC; ++q) acc[q] = make_double2(0.0, 0.0);
 
-    int i = j0 - PC;
-    // ring slot of logical block (slot0 + i - p0), kept in [0, Q)
-    int slot = (int)(((int64_t)a.slot0 + i - p0) % a.Q);
-    if (slot < 0) slot += a.Q;
-    for (; i < j1; i += PC) {
-#pragma unroll
-      for (int u = 0; u < PC; ++u) {
-        const double2 x = Xc[(int64_t)slot * a.MS];
-        slot = (slot + 1 == a.Q) ? 0 : slot + 1;
-#pragma unroll
-        for (int q = 0; q < PC; ++q) {
-          double2& s = acc[(u + q) % PC];
-          s.x = fma(x.x, h[q].x, s.x);
-          s.x = fma(-x.y, h[q].y, s.x);
-          s.y = fma(x.x, h[q].y, s.y);
-          s.y = fma(x.y, h[q].x, s.y);
-        }
-        const int jo = i + u;
-        if (jo >= j0 && jo < j1) {
-          double2* yp = Yc + (int64_t)jo * a.MS;
-          if (p0 == 0) {
-            *yp = acc[u];
-          } else {
-            const double2 o = *yp;
-            *yp = make_double2(o.x + acc[u].x, o.y + acc[u].y);
-          }
-        }
-        acc[u] = make_double2(0.0, 0.0);
-      }
+    // logical spectrum index of iteration u of the warm-up group (u = 0..PC-1)
+    MacCursor cur;
+    cur.lx = a.g0 + j0 - PC - p0;
+    cur.slot = (int)(((cur.lx % a.Q) + a.Q) % a.Q);
+    cur.Q = a.Q;
+    // --- warm-up: X[j0-PC+u] only feeds outputs >= j0 through q >= PC-u
+    cur.advance();
+    MacWarm<PC, 1>::run(acc, h, Xc, a.MS, cur);
+    // --- run: outputs j0 .. j1-1, slot (o - j0) % PC
+    for (int i = j0; i < j1; i += PC) {
+      MacMain<PC, 0>::run(acc, h, Xc, Yc, a.MS, cur, i, j1, p0 == 0);
     }
   }
 }
@@ -294,14 +368,14 @@ static void launch_rfft_m(const RfftArgs& a, hipStream_t s) {
   using Plan = FftPlan<M>;
   const int64_t ffts = (int64_t)a.channels * a.jc;
   const int64_t grid = (ffts + Plan::F - 1) / Plan::F;
-  hipLaunchKernelGGL(k_window_rfft<M>, dim3((unsigned)grid), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_window_rfft<M>, dim3((unsigned)grid), dim3(Plan::BLOCK), 0, s, a);
 }
 template <int M>
 static void launch_irfft_m(const IrfftArgs& a, hipStream_t s) {
   using Plan = FftPlan<M>;
   const int64_t ffts = (int64_t)a.channels * a.jc;
   const int64_t grid = (ffts + Plan::F - 1) / Plan::F;
-  hipLaunchKernelGGL(k_irfft_store<M>, dim3((unsigned)grid), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_irfft_store<M>, dim3((unsigned)grid), dim3(Plan::BLOCK), 0, s, a);
 }
 
 #define AD_DISPATCH_M(M_, FN, ...) \
@@ -315,6 +389,7 @@ static void launch_irfft_m(const IrfftArgs& a, hipStream_t s) {
     case 1024: FN<1024>(__VA_ARGS__); break; \
     case 2048: FN<2048>(__VA_ARGS__); break; \
     case 4096: FN<4096>(__VA_ARGS__); break; \
+    case 8192: FN<8192>(__VA_ARGS__); break; \
     default: return false;                   \
   }
 
@@ -330,9 +405,12 @@ bool launch_irfft_store(int M, const IrfftArgs& a, hipStream_t s) {
   return true;
 }
 
-bool launch_fdl_mac(int PC, const MacArgs& a, int channels, hipStream_t s) {
-  if (channels <= 0 || a.jc <= 0) return true;
-  dim3 grid((unsigned)((a.M + 1 + 63) / 64), (unsigned)((a.jc + a.R - 1) / a.R), (unsigned)channels);
+bool launch_fdl_mac(int PC, const MacArgs& in, int channels, hipStream_t s) {
+  if (channels <= 0 || in.jc <= 0) return true;
+  MacArgs a = in;
+  a.nx = (a.M + 1 + 63) / 64;
+  a.ny = (a.jc + a.R - 1) / a.R;
+  dim3 grid((unsigned)((int64_t)channels * a.nx * a.ny));
   switch (PC) {
     case 1: hipLaunchKernelGGL(k_fdl_mac<1>, grid, dim3(64), 0, s, a); break;
     case 2: hipLaunchKernelGGL(k_fdl_mac<2>, grid, dim3(64), 0, s, a); break;

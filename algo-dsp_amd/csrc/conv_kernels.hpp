@@ -30,7 +30,8 @@ struct MacArgs {
   const double2* X;
   int64_t x_ch_stride;
   int Q;
-  int slot0;
+  int64_t g0;           // logical spectrum index of chunk block 0 (< 0: zeros)
+  int nx, ny;           // bin groups of 64, output runs (set by the launcher)
   int MS;
   const double2* H;     // [n_ir][P][MS]
   int64_t h_ir_stride;  // P*MS

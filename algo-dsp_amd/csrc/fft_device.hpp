@@ -125,13 +125,14 @@ struct Dft<1, FWD> {
 __host__ __device__ constexpr int ilog2c(int v) { return v <= 1 ? 0 : 1 + ilog2c(v >> 1); }
 template <int M>
 struct FftPlan {
-  static_assert(M >= 16 && M <= 4096 && (M & (M - 1)) == 0, "FFT size must be a power of two in [16, 4096]");
+  static_assert(M >= 16 && M <= 8192 && (M & (M - 1)) == 0, "FFT size must be a power of two in [16, 8192]");
   static constexpr int LOG = ilog2c(M);
   static constexpr int NPASS = (LOG + 3) / 4;
   static constexpr int R0 = 1 << (LOG - 4 * (NPASS - 1));
-  static constexpr int T = M / 16;          // threads per FFT
-  static constexpr int F = 256 / T;         // FFTs per 256-thread workgroup
-  static constexpr int MP = M + M / 16;     // padded LDS elements per FFT
+  static constexpr int T = M / 16;                 // threads per FFT
+  static constexpr int BLOCK = T > 256 ? T : 256;  // workgroup size
+  static constexpr int F = BLOCK / T;              // FFTs per workgroup
+  static constexpr int MP = M + M / 16;            // padded LDS elements per FFT
   static constexpr int radix(int p) { return p == 0 ? R0 : 16; }
   static constexpr int ns(int p) { return p == 0 ? 1 : R0 * (1 << (4 * (p - 1))); }
 };

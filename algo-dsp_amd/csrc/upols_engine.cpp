@@ -34,7 +34,7 @@ int pick_pc(int P) {
 Upols::Upols(int device, const double* kernels, int n_ir, int64_t K, int L, int C, const int32_t* ir_map, int jc_max,
              hipStream_t stream)
     : K_(K), L_(L), C_(C), n_ir_(n_ir), jc_max_(jc_max), stream_(stream) {
-  if (L < 16 || L > 4096 || !is_pow2(L)) AD_FAIL(AD_ERR_INTERNAL, "UPOLS hop must be a power of two in [16, 4096]");
+  if (L < 16 || L > 8192 || !is_pow2(L)) AD_FAIL(AD_ERR_INTERNAL, "UPOLS hop must be a power of two in [16, 8192]");
   if (n_ir < 1 || C < 1 || K < 1 || jc_max < 1) AD_FAIL(AD_ERR_INTERNAL, "UPOLS: bad geometry");
   M_ = L;
   MS_ = M_ + 8;
@@ -167,12 +167,10 @@ void Upols::reset_stream(hipStream_t s) {
   g_next_ = 0;
 }
 
-void Upols::begin_offline(hipStream_t s) {
-  // blocks with logical index in [-(P+PC), 0) are read as history: zero them.
+void Upols::begin_offline(hipStream_t) {
+  // Spectra with logical index < 0 read as zeros inside k_fdl_mac, so a new
+  // signal only restarts the logical block counter (no memset).
   g_next_ = 0;
-  const int nz = P_ + PC_;
-  const size_t pitch = (size_t)Q_ * MS_ * sizeof(double2);
-  AD_HIP(hipMemset2DAsync(X_.p + (size_t)(Q_ - nz) * MS_, pitch, 0, (size_t)nz * MS_ * sizeof(double2), C_, s));
 }
 
 void Upols::run(const double* d_in, int64_t in_stride, int64_t n, double* d_out, int64_t out_stride, int64_t out_len,
@@ -181,8 +179,11 @@ void Upols::run(const double* d_in, int64_t in_stride, int64_t n, double* d_out,
   const int64_t J = (out_len + L_ - 1) / L_;
   const int in_aligned = ((reinterpret_cast<uintptr_t>(d_in) & 15) == 0) && (in_stride % 2 == 0);
   const int out_aligned = ((reinterpret_cast<uintptr_t>(d_out) & 15) == 0) && (out_stride % 2 == 0);
-  for (int64_t cs = 0; cs < J; cs += jc_max_) {
-    const int jc = (int)std::min<int64_t>(jc_max_, J - cs);
+  // balanced chunks of at most jc_max blocks (no tiny tail launch)
+  const int64_t nchunks = (J + jc_max_ - 1) / jc_max_;
+  const int64_t jc_even = (J + nchunks - 1) / nchunks;
+  for (int64_t cs = 0; cs < J; cs += jc_even) {
+    const int jc = (int)std::min<int64_t>(jc_even, J - cs);
     const int slot0 = (int)(g_next_ % Q_);
 
     RfftArgs a{};
@@ -214,7 +215,7 @@ void Upols::run(const double* d_in, int64_t in_stride, int64_t n, double* d_out,
     m.X = X_.p;
     m.x_ch_stride = (int64_t)Q_ * MS_;
     m.Q = Q_;
-    m.slot0 = slot0;
+    m.g0 = g_next_;
     m.MS = MS_;
     m.H = H_.p;
     m.h_ir_stride = (int64_t)P_ * MS_;

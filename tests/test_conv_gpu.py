@@ -145,7 +145,7 @@ def test_batch_ols_ola(gpu, K, n):
     ols.ProcessTo(out, x)
     assert np.array_equal(out, got)
     with pytest.raises(conv.ErrLengthMismatch):
-        ols.ProcessTo(np.empty(n), x)
+        ols.ProcessTo(np.empty(n + K), x)
     with pytest.raises(conv.ErrEmptyInput):
         ols.Process(np.empty(0))
 
