@@ -225,9 +225,9 @@ class MultiChannelConvolver(_Handle):
     def process_device(self, d_in: int, in_stride: int, in_len: int, d_out: int, out_stride: int, out_len: int,
                        stream: int = 0) -> None:
         check(lib().ad_conv_multi_process_device(self._h, C.c_void_p(d_in), in_stride, in_len, C.c_void_p(d_out),
-                                                 out_stride, out_len, C.c_void_p(stream) if stream else None))
+                                                 out_stride, out_len, C.c_void_p(stream)))
 
 
 def mixdown_device(d_chan: int, channels: int, stride: int, length: int, d_mix: int, stream: int = 0) -> None:
     check(lib().ad_conv_mixdown_device(C.c_void_p(d_chan), channels, stride, length, C.c_void_p(d_mix),
-                                       C.c_void_p(stream) if stream else None))
+                                       C.c_void_p(stream)))

@@ -130,7 +130,7 @@ void setup_stream_engine(ad_conv* h, const double* kernel, int64_t K, int64_t B,
   const int64_t hop = largest_pow2_divisor(B, hop_cap);
   h->hop = hop;
   h->conv_len = K;
-  if (hop >= 16) {
+  if (hop >= 64) {
     const int jc = (int)std::max<int64_t>(1, std::min<int64_t>(B / hop, 256));
     h->eng.reset(new Upols(h->device, kernel, 1, K, (int)hop, 1, nullptr, jc, h->stream));
   } else {
@@ -544,8 +544,8 @@ int ad_conv_multi_create(const double* kernels, int n_ir, int64_t K, int64_t hop
     if (K <= 0 || !kernels || n_ir <= 0) AD_FAIL(AD_ERR_EMPTY_KERNEL, "conv: empty kernel");
     if (channels <= 0) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "channels must be positive");
     if (hop <= 0) hop = 4096;
-    if (hop < 16 || hop > 8192 || !is_pow2(hop))
-      AD_FAIL(AD_ERR_INVALID_BLOCK_SIZE, "hop must be a power of two in [16, 8192]");
+    if (hop < 64 || hop > 8192 || !is_pow2(hop))
+      AD_FAIL(AD_ERR_INVALID_BLOCK_SIZE, "hop must be a power of two in [64, 8192]");
     if (max_chunk_blocks <= 0) max_chunk_blocks = 1024;
     const int dev = pick_device(device);
     DeviceScope ds(dev);
@@ -567,7 +567,7 @@ int ad_conv_multi_process_device(ad_conv* h, const double* d_in, int64_t in_stri
     if (out_len > in_len + h->K - 1 || out_len <= 0)
       AD_FAIL(AD_ERR_LENGTH_MISMATCH, "conv: buffer length mismatch");
     DeviceScope ds(h->device);
-    hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : h->stream;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);  // NULL = the default (null) stream
     h->eng->begin_offline(s);
     h->eng->run(d_in, in_stride, in_len, d_out, out_stride, out_len, /*use_hist=*/false, s);
   });

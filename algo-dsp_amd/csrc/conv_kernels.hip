@@ -12,13 +12,18 @@
 //
 // UPOLS data flow for hop L (= M, a power of two), real FFT size N = 2L:
 //   K1 k_window_rfft : X[c][g] = rFFT_N( x[(g-1)L .. (g+1)L) )   -> M+1 bins
-//   K2 k_fdl_mac     : Y[c][j] = sum_p X[c][j-p] * H[ir(c)][p]   (per bin)
+//   K2 k_fdl_mac     : Y[c][j] = sum_p X[c][j-p] * H[ir(c)][p]   (per bin),
+//                      folded to the half-length spectrum Z[c][j] (M bins)
 //   K3 k_irfft_store : y[c][jL .. (j+1)L) = last L of irFFT_N(Y[c][j])
+// K1/K3 live in fft_kernels.hip, K2 and the time-domain forms here.
 // H[p] = rFFT_N( h[pL .. (p+1)L) zero-padded ) is built by K1 at create time.
 // X lives in a per-channel ring of Q blocks (frequency-domain delay line); the
 // bins dimension is padded to MS = M + 8 complex128 so every row starts on a
 // 128-byte line.
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
 
 #include "conv_kernels.hpp"
 #include "fft_device.hpp"
@@ -34,138 +39,6 @@ __device__ __forceinline__ int xcd_remap(int b, int G) {
   const int xcd = b & 7, r = b >> 3;
   const int q = G >> 3, rem = G & 7;
   return (xcd < rem) ? xcd * (q + 1) + r : rem * (q + 1) + (xcd - rem) * q + r;
-}
-
-// ---------------------------------------------------------------------------
-// K1: forward real FFT of one overlap-save window per (channel, block).
-// ---------------------------------------------------------------------------
-template <int M>
-__global__ __launch_bounds__(FftPlan<M>::BLOCK) void k_window_rfft(RfftArgs a) {
-  using Plan = FftPlan<M>;
-  constexpr int T = Plan::T;
-  constexpr int L = M;
-  __shared__ __attribute__((aligned(16))) double2 lds_all[Plan::F * Plan::MP];
-
-  const int f = threadIdx.x / T;
-  const int tid = threadIdx.x % T;
-  const int64_t e = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * Plan::F + f;
-  const bool active = e < (int64_t)a.channels * a.jc;
-  const int c = active ? (int)(e / a.jc) : 0;
-  const int j = active ? (int)(e % a.jc) : 0;
-  double2* lds = lds_all + f * Plan::MP;
-
-  const double* xc = a.x + (int64_t)c * a.x_stride;
-  const double* hc = a.xhist ? a.xhist + (int64_t)c * a.hist_stride : nullptr;
-  const int64_t t0 = a.s0 + (int64_t)j * L - L;  // first sample of the 2L window
-
-  double2 v[16];
-#pragma unroll
-  for (int s = 0; s < 16; ++s) {
-    const int m = pass0_index<M>(tid, s);
-    const int64_t t = t0 + 2 * m;
-    double2 z;
-    if (active && t >= 0 && t + 1 < a.n && a.aligned) {
-      z = *reinterpret_cast<const double2*>(xc + t);
-    } else if (!active) {
-      z = make_double2(0.0, 0.0);
-    } else {
-      double r0, r1;
-      r0 = (t < 0) ? (hc ? hc[L + t] : 0.0) : (t < a.n ? xc[t] : 0.0);
-      r1 = (t + 1 < 0) ? (hc ? hc[L + t + 1] : 0.0) : (t + 1 < a.n ? xc[t + 1] : 0.0);
-      z = make_double2(r0, r1);
-    }
-    v[s] = z;
-  }
-
-  if constexpr (Plan::NPASS > 1) {
-    pass_compute_store<M, 0, true>(v, tid, lds, a.twM);
-    run_middle_passes<M, true>(v, tid, lds, a.twM);
-  }
-  last_pass_compute<M, true>(v, tid, a.twM);
-
-  // Exchange through LDS so each thread sees Z[k] and Z[M-k].
-  __syncthreads();
-#pragma unroll
-  for (int s = 0; s < 16; ++s) lds[lds_pad(last_pass_index<M>(tid, s))] = v[s];
-  __syncthreads();
-  if (!active) return;
-
-  double2* Xo = a.X + (int64_t)c * a.x_ch_stride + (int64_t)((a.slot0 + j) % a.Q) * a.MS;
-#pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    const int k = tid + q * T;
-    const double2 A = lds[lds_pad(k)];
-    if (k == 0) {
-      Xo[0] = make_double2(A.x + A.y, 0.0);
-      Xo[M] = make_double2(A.x - A.y, 0.0);
-    } else {
-      const double2 B = c_conj(lds[lds_pad(M - k)]);
-      const double2 fe = c_scale(c_add(A, B), 0.5);
-      const double2 d = c_sub(A, B);
-      const double2 fo = make_double2(0.5 * d.y, -0.5 * d.x);  // -i*(A-B)/2
-      Xo[k] = c_add(fe, c_mul(a.twN[k], fo));
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// K3: inverse real FFT of Y[c][j], keep the last L samples (overlap-save
-// discard of the first N-L circular outputs), store to y.
-// ---------------------------------------------------------------------------
-template <int M>
-__global__ __launch_bounds__(FftPlan<M>::BLOCK) void k_irfft_store(IrfftArgs a) {
-  using Plan = FftPlan<M>;
-  constexpr int T = Plan::T;
-  constexpr int L = M;
-  __shared__ __attribute__((aligned(16))) double2 lds_all[Plan::F * Plan::MP];
-
-  const int f = threadIdx.x / T;
-  const int tid = threadIdx.x % T;
-  const int64_t e = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * Plan::F + f;
-  const bool active = e < (int64_t)a.channels * a.jc;
-  const int c = active ? (int)(e / a.jc) : 0;
-  const int j = active ? (int)(e % a.jc) : 0;
-  double2* lds = lds_all + f * Plan::MP;
-
-  const double2* Yb = a.Y + (int64_t)c * a.y_ch_stride + (int64_t)j * a.MS;
-  const double sc = 0.5 / (double)M;
-  double2 v[16];
-#pragma unroll
-  for (int s = 0; s < 16; ++s) {
-    const int m = pass0_index<M>(tid, s);
-    double2 z = make_double2(0.0, 0.0);
-    if (active) {
-      const double2 A = Yb[m];
-      const double2 B = c_conj(Yb[M - m]);
-      const double2 fe = c_add(A, B);
-      const double2 fo = c_mul(c_sub(A, B), c_conj(a.twN[m]));
-      // Z = (fe + i*fo) / (2M)
-      z = make_double2((fe.x - fo.y) * sc, (fe.y + fo.x) * sc);
-    }
-    v[s] = z;
-  }
-
-  if constexpr (Plan::NPASS > 1) {
-    pass_compute_store<M, 0, false>(v, tid, lds, a.twM);
-    run_middle_passes<M, false>(v, tid, lds, a.twM);
-  }
-  last_pass_compute<M, false>(v, tid, a.twM);
-  if (!active) return;
-
-  double* yc = a.out + (int64_t)c * a.out_stride;
-  const int64_t ob = a.o0 + (int64_t)j * L - M;  // sample of window index 0 minus L
-#pragma unroll
-  for (int s = 0; s < 16; ++s) {
-    const int m = last_pass_index<M>(tid, s);
-    if (m < M / 2) continue;
-    const int64_t o = ob + 2 * m;
-    if (o + 1 < a.out_len && a.aligned) {
-      *reinterpret_cast<double2*>(yc + o) = v[s];
-    } else {
-      if (o < a.out_len) yc[o] = v[s].x;
-      if (o + 1 < a.out_len) yc[o + 1] = v[s].y;
-    }
-  }
 }
 
 // ---------------------------------------------------------------------------
@@ -228,6 +101,41 @@ struct MacWarm {
   }
 };
 
+// Epilogue of one output spectrum of one lane: turns the product spectrum Y
+// into the half-length complex spectrum Z that the inverse real FFT starts
+// from, Z[m] = (Y[m] + conj Y[M-m] + i (Y[m] - conj Y[M-m]) W_2M^-m) / 2M,
+// and stores (or accumulates, for partition chunks after the first) it.
+// Lanes l and l+32 of a pair wave hold mirror bins, so the partner value is
+// one cross-lane swap away; the mirror-free middle bin M/2 has its own wave.
+struct ZEpilogue {
+  double2* zc;     // Z row base of this lane's output index (nullptr: no output)
+  double2 tw;      // conj(W_2M^m) * (0.5 / M)
+  bool paired;     // pair wave (partner in lane ^ 32) vs the self-paired middle bin
+  int MS;
+  __device__ __forceinline__ void store(const double2 y, int64_t j, bool first) const {
+    double2 p;
+    if (paired) {
+      p.x = __shfl_xor(y.x, 32);
+      p.y = __shfl_xor(y.y, 32);
+    } else {
+      p = y;
+    }
+    if (!zc) return;
+    const double2 fe = make_double2(y.x + p.x, y.y - p.y);  // Y + conj(P)
+    const double2 d = make_double2(y.x - p.x, y.y + p.y);   // Y - conj(P)
+    const double2 fo = c_mul(d, tw);
+    const double2 z = make_double2(fe.x * tw_scale - fo.y, fe.y * tw_scale + fo.x);
+    double2* zp = zc + j * MS;
+    if (first) {
+      *zp = z;
+    } else {
+      const double2 o = *zp;
+      *zp = make_double2(o.x + z.x, o.y + z.y);
+    }
+  }
+  double tw_scale;  // 0.5 / M (applied to fe; tw already carries it for fo)
+};
+
 template <int PC, int U>
 struct MacMain {
   template <int Q = 0>
@@ -238,21 +146,16 @@ struct MacMain {
     }
   }
   __device__ static __forceinline__ void run(double2 (&acc)[PC], const double2 (&h)[PC], const double2* Xc,
-                                             double2* Yc, int MS, MacCursor& cur, int i, int j1, bool first) {
+                                             const ZEpilogue& epi, int MS, MacCursor& cur, int i, int j1,
+                                             bool first) {
     if constexpr (U < PC) {
       if (i + U >= j1) return;  // wave-uniform
       const double2 x = cur.load(Xc, MS);
       macs(acc, h, x);
-      double2* yp = Yc + (int64_t)(i + U) * MS;
-      if (first) {
-        *yp = acc[U];
-      } else {
-        const double2 o = *yp;
-        *yp = make_double2(o.x + acc[U].x, o.y + acc[U].y);
-      }
+      epi.store(acc[U], i + U, first);
       acc[U] = make_double2(0.0, 0.0);
       cur.advance();
-      MacMain<PC, U + 1>::run(acc, h, Xc, Yc, MS, cur, i, j1, first);
+      MacMain<PC, U + 1>::run(acc, h, Xc, epi, MS, cur, i, j1, first);
     }
   }
 };
@@ -264,14 +167,33 @@ __global__ __launch_bounds__(64) void k_fdl_mac(MacArgs a) {
   const int t = lg / a.ny;
   const int bx = t % a.nx;
   const int c = t / a.nx;
-  const int k = bx * 64 + threadIdx.x;
-  if (k > a.M) return;
+  const int lane = threadIdx.x;
+  // bin of this lane: pair waves cover [0, M/2) in lanes 0-31 and the mirror
+  // bins (M/2, M] in lanes 32-63; the last wave carries the middle bin M/2.
+  const bool paired = bx < a.M / 64;
+  int k;
+  if (paired) {
+    k = (lane < 32) ? bx * 32 + lane : a.M - (bx * 32 + lane - 32);
+  } else {
+    if (lane != 0) return;
+    k = a.M / 2;
+  }
   const int j0 = ry * a.R;
   const int j1 = min(j0 + a.R, a.jc);
   const int ir = a.ir_index ? a.ir_index[c] : (c % a.n_ir);
   const double2* Hc = a.H + (int64_t)ir * a.h_ir_stride + k;
   const double2* Xc = a.X + (int64_t)c * a.x_ch_stride + k;
-  double2* Yc = a.Y + (int64_t)c * a.y_ch_stride + k;
+  ZEpilogue epi;
+  epi.paired = paired;
+  epi.MS = a.MS;
+  epi.tw_scale = 0.5 / (double)a.M;
+  if (k < a.M) {
+    epi.zc = a.Y + (int64_t)c * a.y_ch_stride + k;
+    epi.tw = c_scale(c_conj(a.twN[k]), epi.tw_scale);
+  } else {
+    epi.zc = nullptr;  // the Nyquist lane only feeds its partner (bin 0)
+    epi.tw = make_double2(0.0, 0.0);
+  }
 
   for (int p0 = 0; p0 < a.P; p0 += PC) {
     double2 h[PC];
@@ -291,7 +213,7 @@ __global__ __launch_bounds__(64) void k_fdl_mac(MacArgs a) {
     MacWarm<PC, 1>::run(acc, h, Xc, a.MS, cur);
     // --- run: outputs j0 .. j1-1, slot (o - j0) % PC
     for (int i = j0; i < j1; i += PC) {
-      MacMain<PC, 0>::run(acc, h, Xc, Yc, a.MS, cur, i, j1, p0 == 0);
+      MacMain<PC, 0>::run(acc, h, Xc, epi, a.MS, cur, i, j1, p0 == 0);
     }
   }
 }
@@ -363,52 +285,11 @@ __global__ __launch_bounds__(256) void k_mixdown(const double* __restrict__ ch, 
 // ---------------------------------------------------------------------------
 // Launchers
 // ---------------------------------------------------------------------------
-template <int M>
-static void launch_rfft_m(const RfftArgs& a, hipStream_t s) {
-  using Plan = FftPlan<M>;
-  const int64_t ffts = (int64_t)a.channels * a.jc;
-  const int64_t grid = (ffts + Plan::F - 1) / Plan::F;
-  hipLaunchKernelGGL(k_window_rfft<M>, dim3((unsigned)grid), dim3(Plan::BLOCK), 0, s, a);
-}
-template <int M>
-static void launch_irfft_m(const IrfftArgs& a, hipStream_t s) {
-  using Plan = FftPlan<M>;
-  const int64_t ffts = (int64_t)a.channels * a.jc;
-  const int64_t grid = (ffts + Plan::F - 1) / Plan::F;
-  hipLaunchKernelGGL(k_irfft_store<M>, dim3((unsigned)grid), dim3(Plan::BLOCK), 0, s, a);
-}
-
-#define AD_DISPATCH_M(M_, FN, ...) \
-  switch (M_) {                    \
-    case 16: FN<16>(__VA_ARGS__); break;     \
-    case 32: FN<32>(__VA_ARGS__); break;     \
-    case 64: FN<64>(__VA_ARGS__); break;     \
-    case 128: FN<128>(__VA_ARGS__); break;   \
-    case 256: FN<256>(__VA_ARGS__); break;   \
-    case 512: FN<512>(__VA_ARGS__); break;   \
-    case 1024: FN<1024>(__VA_ARGS__); break; \
-    case 2048: FN<2048>(__VA_ARGS__); break; \
-    case 4096: FN<4096>(__VA_ARGS__); break; \
-    case 8192: FN<8192>(__VA_ARGS__); break; \
-    default: return false;                   \
-  }
-
-bool launch_window_rfft(int M, const RfftArgs& a, hipStream_t s) {
-  if (a.channels <= 0 || a.jc <= 0) return true;
-  AD_DISPATCH_M(M, launch_rfft_m, a, s);
-  return true;
-}
-
-bool launch_irfft_store(int M, const IrfftArgs& a, hipStream_t s) {
-  if (a.channels <= 0 || a.jc <= 0) return true;
-  AD_DISPATCH_M(M, launch_irfft_m, a, s);
-  return true;
-}
-
 bool launch_fdl_mac(int PC, const MacArgs& in, int channels, hipStream_t s) {
   if (channels <= 0 || in.jc <= 0) return true;
   MacArgs a = in;
-  a.nx = (a.M + 1 + 63) / 64;
+  if (a.M < 64) return false;  // pair waves need M/2 >= 32 bins
+  a.nx = a.M / 64 + 1;         // pair waves + the middle-bin wave
   a.ny = (a.jc + a.R - 1) / a.R;
   dim3 grid((unsigned)((int64_t)channels * a.nx * a.ny));
   switch (PC) {

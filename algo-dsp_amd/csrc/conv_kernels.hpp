@@ -37,8 +37,9 @@ struct MacArgs {
   int64_t h_ir_stride;  // P*MS
   const int* ir_index;  // [C] device (nullable -> c % n_ir)
   int n_ir;
-  double2* Y;           // [C][jc_max][MS]
+  double2* Y;           // Z output [C][jc_max][MS] (half-length spectra for the inverse rFFT)
   int64_t y_ch_stride;
+  const double2* twN;   // W_{2M}^k, k < M
   int jc;
   int R;                // output blocks per wave run
   int P;                // partitions

@@ -7,9 +7,9 @@
 // (overlap_add.go:138-160 uses real(IFFT(.)) as the convolution result).
 //
 // Design (MI355X-first, not a translation of the Go code):
-//   * one M-point complex FFT is done by M/16 threads, each holding 16
-//     complex128 values in VGPRs; passes are radix-16 (first pass may be
-//     radix 2/4/8), so M = 4096 takes three passes and two LDS exchanges;
+//   * one M-point complex FFT is done by M/V threads, each holding V = 8 or
+//     16 complex128 values in VGPRs; passes are radix-V (the first pass may
+//     be radix 2/4/8), so M = 4096 at V = 16 takes three passes;
 //   * the LDS image is interleaved double2 padded by one element per 16
 //     (pad(i) = i + i/16) so the stride-R butterfly writes of a Stockham
 //     pass hit distinct 16-B slots of the 256-B bank row (ds_write_b128);
@@ -119,22 +119,25 @@ struct Dft<1, FWD> {
 };
 
 // ---------------------------------------------------------------------------
-// Mixed-radix Stockham plan for M = 2^m, 16 <= M <= 4096.
-// Passes: first radix R0 = M / 16^(passes-1) in {2,4,8,16}, then radix 16.
+// Mixed-radix Stockham plan for M = 2^m, 16 <= M <= 8192, V values per thread
+// (V = 16: radix-16 passes; V = 8: radix-8 passes, half the VGPRs per lane and
+// twice the threads).  Passes: first radix R0 = M / V^(passes-1), then radix V.
 // ---------------------------------------------------------------------------
 __host__ __device__ constexpr int ilog2c(int v) { return v <= 1 ? 0 : 1 + ilog2c(v >> 1); }
-template <int M>
+template <int M, int V = 16>
 struct FftPlan {
   static_assert(M >= 16 && M <= 8192 && (M & (M - 1)) == 0, "FFT size must be a power of two in [16, 8192]");
+  static_assert(V == 8 || V == 16, "8 or 16 values per thread");
+  static constexpr int LOGV = ilog2c(V);
   static constexpr int LOG = ilog2c(M);
-  static constexpr int NPASS = (LOG + 3) / 4;
-  static constexpr int R0 = 1 << (LOG - 4 * (NPASS - 1));
-  static constexpr int T = M / 16;                 // threads per FFT
+  static constexpr int NPASS = (LOG + LOGV - 1) / LOGV;
+  static constexpr int R0 = 1 << (LOG - LOGV * (NPASS - 1));
+  static constexpr int T = M / V;                  // threads per FFT
   static constexpr int BLOCK = T > 256 ? T : 256;  // workgroup size
   static constexpr int F = BLOCK / T;              // FFTs per workgroup
   static constexpr int MP = M + M / 16;            // padded LDS elements per FFT
-  static constexpr int radix(int p) { return p == 0 ? R0 : 16; }
-  static constexpr int ns(int p) { return p == 0 ? 1 : R0 * (1 << (4 * (p - 1))); }
+  static constexpr int radix(int p) { return p == 0 ? R0 : V; }
+  static constexpr int ns(int p) { return p == 0 ? 1 : R0 * (1 << (LOGV * (p - 1))); }
 };
 
 __device__ __forceinline__ int lds_pad(int i) { return i + (i >> 4); }
@@ -156,14 +159,14 @@ __device__ __forceinline__ void apply_twiddles(double2* v, int jb, const double2
   }
 }
 
-// One in-register pass on the thread's 16 values (16/R butterflies of radix R),
+// One in-register pass on the thread's V values (V/R butterflies of radix R),
 // followed by the Stockham store into the LDS image of this FFT.
-template <int M, int P, bool FWD>
+template <int M, int V, int P, bool FWD>
 __device__ __forceinline__ void pass_compute_store(double2* v, int tid, double2* lds, const double2* __restrict__ twM) {
-  using Plan = FftPlan<M>;
+  using Plan = FftPlan<M, V>;
   constexpr int R = Plan::radix(P);
   constexpr int NS = Plan::ns(P);
-  constexpr int NB = 16 / R;
+  constexpr int NB = V / R;
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
     const int jb = tid + b * Plan::T;
@@ -179,12 +182,12 @@ __device__ __forceinline__ void pass_compute_store(double2* v, int tid, double2*
   }
 }
 
-// Load the thread's 16 values of pass P from the LDS image.
-template <int M, int P>
+// Load the thread's V values of pass P from the LDS image.
+template <int M, int V, int P>
 __device__ __forceinline__ void pass_load(double2* v, int tid, const double2* lds) {
-  using Plan = FftPlan<M>;
+  using Plan = FftPlan<M, V>;
   constexpr int R = Plan::radix(P);
-  constexpr int NB = 16 / R;
+  constexpr int NB = V / R;
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
     const int jb = tid + b * Plan::T;
@@ -194,9 +197,9 @@ __device__ __forceinline__ void pass_load(double2* v, int tid, const double2* ld
 }
 
 // Index (in the natural-order input) of value slot s of the thread for pass 0.
-template <int M>
+template <int M, int V = 16>
 __device__ __forceinline__ int pass0_index(int tid, int s) {
-  using Plan = FftPlan<M>;
+  using Plan = FftPlan<M, V>;
   constexpr int R = Plan::R0;
   const int b = s / R, r = s % R;
   return tid + b * Plan::T + r * (M / R);
@@ -205,29 +208,28 @@ __device__ __forceinline__ int pass0_index(int tid, int s) {
 // Runs passes [1, NPASS-1) (the middle passes) after pass 0 has been stored:
 // barrier, load, compute, barrier, store.  Leaves the last pass's input in v
 // (already loaded), ready for the caller's final pass handling.
-template <int M, bool FWD, int P = 1>
+template <int M, int V, bool FWD, int P = 1>
 __device__ __forceinline__ void run_middle_passes(double2* v, int tid, double2* lds, const double2* __restrict__ twM) {
-  using Plan = FftPlan<M>;
+  using Plan = FftPlan<M, V>;
   if constexpr (P < Plan::NPASS) {
     __syncthreads();
-    pass_load<M, P>(v, tid, lds);
+    pass_load<M, V, P>(v, tid, lds);
     if constexpr (P + 1 < Plan::NPASS) {
       __syncthreads();
-      pass_compute_store<M, P, FWD>(v, tid, lds, twM);
-      run_middle_passes<M, FWD, P + 1>(v, tid, lds, twM);
+      pass_compute_store<M, V, P, FWD>(v, tid, lds, twM);
+      run_middle_passes<M, V, FWD, P + 1>(v, tid, lds, twM);
     }
   }
 }
 
 // Computes the last pass in registers (twiddles + DFT) without storing.
-// After this, slot r of the thread holds output index tid + r*T (R = 16).
-template <int M, bool FWD>
+template <int M, int V, bool FWD>
 __device__ __forceinline__ void last_pass_compute(double2* v, int tid, const double2* __restrict__ twM) {
-  using Plan = FftPlan<M>;
+  using Plan = FftPlan<M, V>;
   constexpr int P = Plan::NPASS - 1;
   constexpr int R = Plan::radix(P);
   constexpr int NS = Plan::ns(P);
-  constexpr int NB = 16 / R;
+  constexpr int NB = V / R;
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
     const int jb = tid + b * Plan::T;
@@ -237,9 +239,9 @@ __device__ __forceinline__ void last_pass_compute(double2* v, int tid, const dou
 }
 
 // Output index held by slot s after last_pass_compute.
-template <int M>
+template <int M, int V = 16>
 __device__ __forceinline__ int last_pass_index(int tid, int s) {
-  using Plan = FftPlan<M>;
+  using Plan = FftPlan<M, V>;
   constexpr int P = Plan::NPASS - 1;
   constexpr int R = Plan::radix(P);
   constexpr int NS = Plan::ns(P);

@@ -34,7 +34,7 @@ int pick_pc(int P) {
 Upols::Upols(int device, const double* kernels, int n_ir, int64_t K, int L, int C, const int32_t* ir_map, int jc_max,
              hipStream_t stream)
     : K_(K), L_(L), C_(C), n_ir_(n_ir), jc_max_(jc_max), stream_(stream) {
-  if (L < 16 || L > 8192 || !is_pow2(L)) AD_FAIL(AD_ERR_INTERNAL, "UPOLS hop must be a power of two in [16, 8192]");
+  if (L < 64 || L > 8192 || !is_pow2(L)) AD_FAIL(AD_ERR_INTERNAL, "UPOLS hop must be a power of two in [64, 8192]");
   if (n_ir < 1 || C < 1 || K < 1 || jc_max < 1) AD_FAIL(AD_ERR_INTERNAL, "UPOLS: bad geometry");
   M_ = L;
   MS_ = M_ + 8;
@@ -137,7 +137,15 @@ void Upols::prof_end(hipStream_t s, hipEvent_t e0, int kernel, double bytes) {
   prof_recs_.push_back({e0, e1, kernel, bytes});
 }
 
-void Upols::set_profiling(bool on) { prof_ = on; }
+void Upols::set_profiling(bool on) {
+  prof_ = on;
+  // pre-create events so recording inside a timed region never pays hipEventCreate
+  while (on && event_pool_.size() < 512) {
+    hipEvent_t e;
+    AD_HIP(hipEventCreate(&e));
+    event_pool_.push_back(e);
+  }
+}
 
 void Upols::read_profile(double* ms, int64_t* launches, double* alg_bytes) {
   for (auto& r : prof_recs_) {
@@ -227,6 +235,7 @@ void Upols::run(const double* d_in, int64_t in_stride, int64_t n, double* d_out,
     m.R = std::min(R_, jc);
     m.P = P_;
     m.M = M_;
+    m.twN = tw_.p + M_;
     prof_begin(s, &e0);
     launch_fdl_mac(PC_, m, C_, s);
     prof_end(s, e0, 1, blocks * (double)(M_ + 1) * 32 + (double)n_ir_ * P_ * (M_ + 1) * 16);

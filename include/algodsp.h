@@ -14,7 +14,7 @@
  *    back (conv.go:41-46, partitioned.go:11-15);
  *  - host-pointer calls copy in and out inside the call (cgo forbids C from
  *    retaining Go pointers); `*_device` calls take device pointers and a HIP
- *    stream (`void*`, NULL = the library's per-handle stream) and are
+ *    stream (`void*`, NULL = the HIP default stream, as in the HIP API) and are
  *    asynchronous with respect to the host;
  *  - a handle is single-caller, like the reference types (no internal locks);
  *  - ad_last_error() returns a thread-local description of the last failure.
@@ -118,7 +118,7 @@ int ad_conv_convolve(const double* a, int64_t n, const double* b, int64_t m, int
 /* ---- multi-channel device-resident engine (offline / many-channel path) --
  * Uniformly partitioned overlap-save with a frequency-domain delay line.
  * kernels: n_ir impulse responses of kernel_len taps each, row-major.
- * hop: partition/hop length (power of two, 16..8192); 0 = auto (4096).
+ * hop: partition/hop length (power of two, 64..8192); 0 = auto (4096).
  * channels: number of channels processed per call; ir_index[c] selects the
  *   IR of channel c (NULL: c % n_ir).
  * max_chunk_blocks: blocks per channel per internal chunk (0 = auto).     */
@@ -127,7 +127,7 @@ int ad_conv_multi_create(const double* kernels, int n_ir, int64_t kernel_len, in
 /* Full linear convolution of every channel (ModeFull semantics per channel):
  * d_in  [channels][in_stride] (first in_len used),
  * d_out [channels][out_stride] (first out_len written; out_len <= in_len+K-1).
- * Device pointers; asynchronous on `stream` (NULL = handle stream).       */
+ * Device pointers; asynchronous on `stream` (NULL = default stream).      */
 int ad_conv_multi_process_device(ad_conv* h, const double* d_in, int64_t in_stride, int64_t in_len, double* d_out,
                                  int64_t out_stride, int64_t out_len, void* stream);
 /* Live kernel timing (HIP events recorded around every launch on the launch

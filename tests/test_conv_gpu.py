@@ -226,7 +226,7 @@ def test_multi_stereo_large_church_vs_oracle(gpu):
         assert np.max(np.abs(y[c] - want)) < 1e-9
 
 
-@pytest.mark.parametrize("hop", [16, 256, 1024, 4096])
+@pytest.mark.parametrize("hop", [64, 128, 256, 1024, 4096, 8192])
 def test_multi_hops_and_ir_map(gpu, hop):
     K = 3000
     irs = np.stack([signals.make_test_kernel(K), signals.white_noise(K, 7), signals.make_impulse_kernel(K)])
