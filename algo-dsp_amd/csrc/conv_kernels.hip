@@ -51,10 +51,10 @@ __device__ __forceinline__ int xcd_remap(int b, int G) {
 // reads each spectrum once and writes each output once.  P > PC is handled
 // by sweeping partition chunks, read-modify-writing Y.
 //
-// Blocks with logical index < 0 (before the stream/signal start) read as
-// zeros without touching memory, so an offline call needs no memset.  The
-// warm-up group (the PC-1 spectra before the run) issues only the products
-// that reach outputs of the run: every FMA issued is a useful one.
+// Blocks with logical index < 0 (before the stream/signal start) read the
+// ring's zero row, so an offline call needs no memset.  The warm-up group
+// (the PC-1 spectra before the run) issues only the products that reach
+// outputs of the run: every FMA issued is a useful one.
 // 1-D grid, XCD-remapped so the runs of one bin group (which re-read each
 // other's warm-up rows) share an L2.
 // ---------------------------------------------------------------------------
@@ -65,22 +65,24 @@ __device__ __forceinline__ void cmac(double2& s, const double2 x, const double2 
   s.y = fma(x.y, h.x, s.y);
 }
 
-// Ring cursor over the X spectra of one lane's bin (wave-uniform state).
-struct MacCursor {
-  int64_t lx;  // logical spectrum index (< 0: before the signal, reads zero)
-  int slot;    // ring slot of lx
-  int Q;
-  __device__ __forceinline__ double2 load(const double2* Xc, int MS) const {
-    return (lx >= 0) ? Xc[(int64_t)slot * MS] : make_double2(0.0, 0.0);
+// Loads xg[U0..U1) of a group of PC consecutive spectra whose first logical
+// index is lx0 (ring slot s0).  Branch-free: spectra before the signal start
+// (logical index < 0) read the ring's zero row (slot Q), and spectra past the
+// run read stale ring rows whose products only reach outputs that are never
+// stored, so every load is a plain, hoistable global load.
+template <int PC, int U0, int U1>
+__device__ __forceinline__ void load_span(double2 (&xg)[PC], const double2* __restrict__ Xc, int Q, int MS,
+                                          int64_t lx0, int s0) {
+#pragma unroll
+  for (int u = U0; u < U1; ++u) {
+    int sl = s0 + u;
+    if (sl >= Q) sl -= Q;
+    const int row = (lx0 + u >= 0) ? sl : Q;
+    xg[u] = Xc[(int64_t)row * MS];
   }
-  __device__ __forceinline__ void advance() {
-    ++lx;
-    slot = (slot + 1 == Q) ? 0 : slot + 1;
-  }
-};
+}
 
-// Compile-time unrolled iteration bodies: template recursion keeps every
-// accumulator / H index a constant so the arrays stay in VGPRs.
+// Warm-up products: X[j0-PC+u] only reaches outputs >= j0 through q >= PC-u.
 template <int PC, int U>
 struct MacWarm {
   template <int Q = PC - U>
@@ -90,13 +92,10 @@ struct MacWarm {
       macs<Q + 1>(acc, h, x);
     }
   }
-  __device__ static __forceinline__ void run(double2 (&acc)[PC], const double2 (&h)[PC], const double2* Xc, int MS,
-                                             MacCursor& cur) {
+  __device__ static __forceinline__ void run(double2 (&acc)[PC], const double2 (&h)[PC], const double2 (&xg)[PC]) {
     if constexpr (U < PC) {
-      const double2 x = cur.load(Xc, MS);
-      macs(acc, h, x);
-      cur.advance();
-      MacWarm<PC, U + 1>::run(acc, h, Xc, MS, cur);
+      macs(acc, h, xg[U]);
+      MacWarm<PC, U + 1>::run(acc, h, xg);
     }
   }
 };
@@ -136,8 +135,10 @@ struct ZEpilogue {
   double tw_scale;  // 0.5 / M (applied to fe; tw already carries it for fo)
 };
 
-template <int PC, int U>
-struct MacMain {
+// Iterations U..UE-1 of a run group: PC products per spectrum into the
+// rotating accumulators, then the finished output (slot U) is stored.
+template <int PC, int U, int UE>
+struct MacSpan {
   template <int Q = 0>
   __device__ static __forceinline__ void macs(double2 (&acc)[PC], const double2 (&h)[PC], const double2 x) {
     if constexpr (Q < PC) {
@@ -145,17 +146,13 @@ struct MacMain {
       macs<Q + 1>(acc, h, x);
     }
   }
-  __device__ static __forceinline__ void run(double2 (&acc)[PC], const double2 (&h)[PC], const double2* Xc,
-                                             const ZEpilogue& epi, int MS, MacCursor& cur, int i, int j1,
-                                             bool first) {
-    if constexpr (U < PC) {
-      if (i + U >= j1) return;  // wave-uniform
-      const double2 x = cur.load(Xc, MS);
-      macs(acc, h, x);
-      epi.store(acc[U], i + U, first);
+  __device__ static __forceinline__ void run(double2 (&acc)[PC], const double2 (&h)[PC], const double2 (&xg)[PC],
+                                             const ZEpilogue& epi, int i, int j1, bool first) {
+    if constexpr (U < UE) {
+      macs(acc, h, xg[U]);
+      if (i + U < j1) epi.store(acc[U], i + U, first);  // wave-uniform
       acc[U] = make_double2(0.0, 0.0);
-      cur.advance();
-      MacMain<PC, U + 1>::run(acc, h, Xc, epi, MS, cur, i, j1, first);
+      MacSpan<PC, U + 1, UE>::run(acc, h, xg, epi, i, j1, first);
     }
   }
 };
@@ -203,17 +200,28 @@ __global__ __launch_bounds__(64) void k_fdl_mac(MacArgs a) {
 #pragma unroll
     for (int q = 0; q < PC; ++q) acc[q] = make_double2(0.0, 0.0);
 
-    // logical spectrum index of iteration u of the warm-up group (u = 0..PC-1)
-    MacCursor cur;
-    cur.lx = a.g0 + j0 - PC - p0;
-    cur.slot = (int)(((cur.lx % a.Q) + a.Q) % a.Q);
-    cur.Q = a.Q;
-    // --- warm-up: X[j0-PC+u] only feeds outputs >= j0 through q >= PC-u
-    cur.advance();
-    MacWarm<PC, 1>::run(acc, h, Xc, a.MS, cur);
-    // --- run: outputs j0 .. j1-1, slot (o - j0) % PC
+    constexpr int HH = PC / 2 > 0 ? PC / 2 : 1;
+    double2 xg[PC];
+    // --- warm-up group: spectra j0-PC .. j0-1 (slot u = 0 feeds nothing)
+    int64_t lx = a.g0 + j0 - PC - p0;
+    int sl = (int)(((lx % a.Q) + a.Q) % a.Q);
+    load_span<PC, 1, PC>(xg, Xc, a.Q, a.MS, lx, sl);
+    MacWarm<PC, 1>::run(acc, h, xg);
+    lx += PC;
+    sl += PC;
+    if (sl >= a.Q) sl -= a.Q;
+    // --- run groups, software pipelined: the second half of a group is
+    // loaded when the group starts, the next group's first half while the
+    // second half computes.
+    load_span<PC, 0, HH>(xg, Xc, a.Q, a.MS, lx, sl);
     for (int i = j0; i < j1; i += PC) {
-      MacMain<PC, 0>::run(acc, h, Xc, epi, a.MS, cur, i, j1, p0 == 0);
+      load_span<PC, HH, PC>(xg, Xc, a.Q, a.MS, lx, sl);
+      MacSpan<PC, 0, HH>::run(acc, h, xg, epi, i, j1, p0 == 0);
+      lx += PC;
+      sl += PC;
+      if (sl >= a.Q) sl -= a.Q;
+      if (i + PC < j1) load_span<PC, 0, HH>(xg, Xc, a.Q, a.MS, lx, sl);
+      MacSpan<PC, HH, PC>::run(acc, h, xg, epi, i, j1, p0 == 0);
     }
   }
 }

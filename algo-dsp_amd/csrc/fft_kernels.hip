@@ -228,9 +228,14 @@ __global__ __launch_bounds__((FftPlan<M, V>::BLOCK)) void k_window_rfft_p(RfftAr
       }
     }
     if (e > e0) __syncthreads();  // the previous item's LDS reads are done
-    fft_run<M, V, true>(v, tid, lds, a.twM);
+    // Opaque copy of tid: keeps the ~80 loop-invariant LDS/twiddle addresses
+    // from being hoisted out of the item loop and pinned in VGPRs for its
+    // whole length (they are cheap to recompute per item).
+    int tid_i = tid;
+    asm volatile("" : "+v"(tid_i));
+    fft_run<M, V, true>(v, tid_i, lds, a.twM);
     double2* Xo = a.X + (int64_t)c * a.x_ch_stride + (int64_t)((a.slot0 + j) % a.Q) * a.MS;
-    rfft_post_store<M, V>(v, tid, lds, Xo, a.twN, true);
+    rfft_post_store<M, V>(v, tid_i, lds, Xo, a.twN, true);
   }
 }
 
@@ -269,8 +274,10 @@ __global__ __launch_bounds__((FftPlan<M, V>::BLOCK)) void k_irfft_store_p(IrfftA
       for (int s = 0; s < V; ++s) nz[s] = Zn[pass0_index<M, V>(tid, s)];
     }
     if (e > e0) __syncthreads();  // the previous item's LDS reads are done
-    fft_run<M, V, false>(v, tid, lds, a.twM);
-    irfft_store_out<M, V>(v, tid, a.out + (int64_t)c * a.out_stride, a.o0 + (int64_t)j * L - M, a.out_len,
+    int tid_i = tid;  // opaque per item (see k_window_rfft_p)
+    asm volatile("" : "+v"(tid_i));
+    fft_run<M, V, false>(v, tid_i, lds, a.twM);
+    irfft_store_out<M, V>(v, tid_i, a.out + (int64_t)c * a.out_stride, a.o0 + (int64_t)j * L - M, a.out_len,
                           a.aligned);
     c = cn;
     j = jn;

@@ -90,7 +90,7 @@ Upols::Upols(int device, const double* kernels, int n_ir, int64_t K, int L, int 
   if (!launch_window_rfft(M_, a, stream_)) AD_FAIL(AD_ERR_INTERNAL, "unsupported FFT size");
   AD_HIP(hipGetLastError());
 
-  X_.alloc((size_t)C_ * Q_ * MS_);
+  X_.alloc((size_t)C_ * (Q_ + 1) * MS_);  // Q ring rows + one zero row per channel
   Y_.alloc((size_t)C_ * jc_max_ * MS_);
   hist_.alloc((size_t)C_ * L_);
   std::vector<int> irm(C_);
@@ -205,7 +205,7 @@ void Upols::run(const double* d_in, int64_t in_stride, int64_t n, double* d_out,
     a.channels = C_;
     a.aligned = in_aligned;
     a.X = X_.p;
-    a.x_ch_stride = (int64_t)Q_ * MS_;
+    a.x_ch_stride = (int64_t)(Q_ + 1) * MS_;
     a.Q = Q_;
     a.slot0 = slot0;
     a.MS = MS_;
@@ -221,7 +221,7 @@ void Upols::run(const double* d_in, int64_t in_stride, int64_t n, double* d_out,
 
     MacArgs m{};
     m.X = X_.p;
-    m.x_ch_stride = (int64_t)Q_ * MS_;
+    m.x_ch_stride = (int64_t)(Q_ + 1) * MS_;
     m.Q = Q_;
     m.g0 = g_next_;
     m.MS = MS_;
