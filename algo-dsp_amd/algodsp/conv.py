@@ -192,7 +192,7 @@ def Convolve(a, b) -> np.ndarray:
 class MultiChannelConvolver(_Handle):
     """Device-resident many-channel UPOLS engine (offline path; include/algodsp.h)."""
 
-    def __init__(self, kernels, hop: int = 4096, channels: int = 1, ir_index=None, chunk_blocks: int = 0,
+    def __init__(self, kernels, hop: int = 0, channels: int = 1, ir_index=None, chunk_blocks: int = 0,
                  device: int = DEVICE):
         k = f64(kernels)
         if k.ndim == 1:

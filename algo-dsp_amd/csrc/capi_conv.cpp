@@ -543,10 +543,15 @@ int ad_conv_multi_create(const double* kernels, int n_ir, int64_t K, int64_t hop
   return create_guarded(out, [&]() -> ad_conv* {
     if (K <= 0 || !kernels || n_ir <= 0) AD_FAIL(AD_ERR_EMPTY_KERNEL, "conv: empty kernel");
     if (channels <= 0) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "channels must be positive");
-    if (hop <= 0) hop = 4096;
+    if (hop <= 0) hop = batch_hop(K);
     if (hop < 64 || hop > 8192 || !is_pow2(hop))
       AD_FAIL(AD_ERR_INVALID_BLOCK_SIZE, "hop must be a power of two in [64, 8192]");
-    if (max_chunk_blocks <= 0) max_chunk_blocks = 1024;
+    if (max_chunk_blocks <= 0) {
+      // X ring + Z scratch cost ~32 B per (channel, block, bin): give the
+      // chunked offline path an ~8 GiB working set, 64..4096 blocks per chunk
+      const int64_t budget = (int64_t)8 << 30;
+      max_chunk_blocks = std::max<int64_t>(64, std::min<int64_t>(4096, budget / ((int64_t)channels * hop * 32)));
+    }
     const int dev = pick_device(device);
     DeviceScope ds(dev);
     std::unique_ptr<ad_conv> h(new_handle(Kind::Multi, dev));

@@ -11,12 +11,14 @@
 //   DirectTo / directToSIMD                 dsp/conv/conv.go:97-154
 //
 // UPOLS data flow for hop L (= M, a power of two), real FFT size N = 2L:
-//   K1 k_window_rfft : X[c][g] = rFFT_N( x[(g-1)L .. (g+1)L) )   -> M+1 bins
-//   K2 k_fdl_mac     : Y[c][j] = sum_p X[c][j-p] * H[ir(c)][p]   (per bin),
+//   K1 k_window_rfft : Zr[c][g] = packed FFT_M of x[(g-1)L .. (g+1)L)  (M values)
+//   K2 k_fdl_mac     : X = separate(Zr) (bins 0..M, on load),
+//                      Y[c][j] = sum_p X[c][j-p] * H[ir(c)][p]   (per bin),
 //                      folded to the half-length spectrum Z[c][j] (M bins)
 //   K3 k_irfft_store : y[c][jL .. (j+1)L) = last L of irFFT_N(Y[c][j])
 // K1/K3 live in fft_kernels.hip, K2 and the time-domain forms here.
-// H[p] = rFFT_N( h[pL .. (p+1)L) zero-padded ) is built by K1 at create time.
+// H[p] (packed spectra of h[pL .. (p+1)L) zero-padded) is built by K1 at
+// create time and separated like X.
 // X lives in a per-channel ring of Q blocks (frequency-domain delay line); the
 // bins dimension is padded to MS = M + 8 complex128 so every row starts on a
 // 128-byte line.
@@ -44,17 +46,30 @@ __device__ __forceinline__ int xcd_remap(int b, int G) {
 // ---------------------------------------------------------------------------
 // K2: frequency-domain delay-line multiply-accumulate.
 //   Y[c][j][k] = sum_{p<P} X[c][g0+j-p][k] * H[ir(c)][p][k]
-// One lane per bin k; a wave owns 64 consecutive bins of one channel and a
-// run of R output blocks.  PC partitions' spectra sit in VGPRs; the X stream
-// is read once per run and every X value feeds PC rotating accumulators whose
-// slots are compile-time indices (the unrolled u/q loops), so the kernel
-// reads each spectrum once and writes each output once.  P > PC is handled
-// by sweeping partition chunks, read-modify-writing Y.
+// Bin-stationary: a lane owns one bin k for a run of R output blocks, keeps
+// PC partitions' spectra in VGPRs and feeds every X value it loads into PC
+// rotating accumulators whose slots are compile-time indices (unrolled u/q
+// loops), so X is read once per run and every output written once.
+//
+// Wave layout (NH = 2, P > 1): lane = ph*32 + mi*16 + l.
+//   ph  partition half: lanes 32-63 take partitions [PC, 2PC) of the chunk,
+//       reading the X stream PC rows earlier; the halves' sums meet in one
+//       v_permlane32_swap before the store (only ph = 0 stores);
+//   mi  mirror: bins 16bx + l (mi = 0) and M - (16bx + l) (mi = 1), so the
+//       conj(Zr[M-k]) that separates K1's packed spectrum, and the Y[M-m]
+//       that folds the output for K3, are one v_permlane16_swap away.
+// Halving the partitions per lane halves the VGPRs (h, accumulators and the
+// X group), which doubles the waves per SIMD and the loads in flight: K2 is
+// bound by HBM latency x loads in flight, not by its FP64 FMAs.
+// NH = 1 (P = 1): lane = mi*32 + l, 32 bin pairs per wave.
+// The last wave (bx = M/(32/NH*2)) carries the self-mirrored middle bin M/2.
+// P > NH*PC is handled by one launch per partition chunk, the later ones
+// read-modify-writing Z (FIRST = false).
 //
 // Blocks with logical index < 0 (before the stream/signal start) read the
 // ring's zero row, so an offline call needs no memset.  The warm-up group
 // (the PC-1 spectra before the run) issues only the products that reach
-// outputs of the run: every FMA issued is a useful one.
+// outputs of the run.
 // 1-D grid, XCD-remapped so the runs of one bin group (which re-read each
 // other's warm-up rows) share an L2.
 // ---------------------------------------------------------------------------
@@ -65,163 +80,241 @@ __device__ __forceinline__ void cmac(double2& s, const double2 x, const double2 
   s.y = fma(x.y, h.x, s.y);
 }
 
-// Loads xg[U0..U1) of a group of PC consecutive spectra whose first logical
-// index is lx0 (ring slot s0).  Branch-free: spectra before the signal start
-// (logical index < 0) read the ring's zero row (slot Q), and spectra past the
-// run read stale ring rows whose products only reach outputs that are never
-// stored, so every load is a plain, hoistable global load.
-template <int PC, int U0, int U1>
-__device__ __forceinline__ void load_span(double2 (&xg)[PC], const double2* __restrict__ Xc, int Q, int MS,
-                                          int64_t lx0, int s0) {
-#pragma unroll
-  for (int u = U0; u < U1; ++u) {
-    int sl = s0 + u;
+// Ring-slot walker over this lane's X stream.  Branch-free: spectra before
+// the signal start (logical index < 0) read the ring's zero row (slot Q), and
+// spectra past the run read stale ring rows whose products only reach
+// outputs that are never stored, so every load is a plain global load.
+struct XStream {
+  const double2* Xc;
+  int Q, MS;
+  int64_t lx;  // logical index of row 0 of the current group (wave-uniform, ph = 0)
+  int sl;      // its ring slot (wave-uniform)
+  int dph;     // row offset of the ph = 1 half (-PC)
+  bool ph;
+  __device__ __forceinline__ int slot(int off) const {  // wave-uniform
+    int s = sl + off;
+    if (s >= Q) s -= Q;
+    if (s < 0) s += Q;
+    return (lx + off >= 0) ? s : Q;
+  }
+  __device__ __forceinline__ double2 load(int off) const {  // row lx + off (+ dph for ph = 1)
+    const int r0 = slot(off), r1 = slot(off + dph);
+    const int row = ph ? r1 : r0;
+    return Xc[(int64_t)row * MS];
+  }
+  template <int PC>
+  __device__ __forceinline__ void advance() {
+    lx += PC;
+    sl += PC;
     if (sl >= Q) sl -= Q;
-    const int row = (lx0 + u >= 0) ? sl : Q;
-    xg[u] = Xc[(int64_t)row * MS];
-  }
-}
-
-// Warm-up products: X[j0-PC+u] only reaches outputs >= j0 through q >= PC-u.
-template <int PC, int U>
-struct MacWarm {
-  template <int Q = PC - U>
-  __device__ static __forceinline__ void macs(double2 (&acc)[PC], const double2 (&h)[PC], const double2 x) {
-    if constexpr (Q < PC) {
-      cmac(acc[(U + Q) % PC], x, h[Q]);
-      macs<Q + 1>(acc, h, x);
-    }
-  }
-  __device__ static __forceinline__ void run(double2 (&acc)[PC], const double2 (&h)[PC], const double2 (&xg)[PC]) {
-    if constexpr (U < PC) {
-      macs(acc, h, xg[U]);
-      MacWarm<PC, U + 1>::run(acc, h, xg);
-    }
   }
 };
 
-// Epilogue of one output spectrum of one lane: turns the product spectrum Y
-// into the half-length complex spectrum Z that the inverse real FFT starts
-// from, Z[m] = (Y[m] + conj Y[M-m] + i (Y[m] - conj Y[M-m]) W_2M^-m) / 2M,
-// and stores (or accumulates, for partition chunks after the first) it.
-// Lanes l and l+32 of a pair wave hold mirror bins, so the partner value is
-// one cross-lane swap away; the mirror-free middle bin M/2 has its own wave.
+// Lane-pair exchange with v_permlane{32,16}_swap (no LDS round trip; all 64
+// lanes active).  For a lane pair (lower, upper) = (bit clear, bit set) of
+// lane bit 5 (B32) or bit 4, xpair returns u, v with
+//   lower lane: u = own value, v = partner's;  upper lane: u = partner's, v = own.
+// Consumers use only u + v, u - v and a per-lane sign s = +1 (lower) / -1
+// (upper) folded into constants, so no select is needed after the swap.
+template <bool B32>
+__device__ __forceinline__ void xpair(double a, double& u, double& v) {
+  const int lo = __double2loint(a), hi = __double2hiint(a);
+  if constexpr (B32) {
+    const auto r = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto t = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    u = __hiloint2double(t[0], r[0]);
+    v = __hiloint2double(t[1], r[1]);
+  } else {
+    const auto r = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto t = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    u = __hiloint2double(t[0], r[0]);
+    v = __hiloint2double(t[1], r[1]);
+  }
+  asm volatile("" : "+v"(u), "+v"(v));  // materialise here: keeps the swap's temporaries short-lived
+}
+template <bool B32>
+__device__ __forceinline__ void xpair(double2 a, double2& u, double2& v) {
+  xpair<B32>(a.x, u.x, v.x);
+  xpair<B32>(a.y, u.y, v.y);
+}
+
+// Separation of K1's raw packed spectrum into the real-signal spectrum (x2):
+//   X'[k] = (A + B) - i W_2M^k (A - B),  A = Zr[k], B = conj Zr[M-k]   (= 2 X[k])
+// with A, conj(B) the mirror pair (u, v) of xpair:
+//   X'.x = (u.x + v.x) + W.x (u.y + v.y) + s W.y (u.x - v.x)
+//   X'.y = s (u.y - v.y) + W.y (u.y + v.y) - s W.x (u.x - v.x)
+// The middle-bin wave holds M/2 in every lane, so its "mirror" lane holds the
+// same bin and the formula needs no special case.  The factor 2 of X' and of
+// H' is taken out in the Z epilogue's scale.
+template <int NH>
+struct Unpack {
+  double2 tw;   // W_2M^k (k = M: -1)
+  double2 stw;  // s * tw
+  double s;     // +1 lower mirror lane, -1 upper
+  __device__ __forceinline__ double2 operator()(const double2 a) const {
+    double2 u, v;
+    xpair<NH == 1>(a, u, v);
+    const double sx = u.x + v.x, dx = u.x - v.x, sy = u.y + v.y, dy = u.y - v.y;
+    return make_double2(fma(stw.y, dx, fma(tw.x, sy, sx)), fma(-stw.x, dx, fma(tw.y, sy, s * dy)));
+  }
+};
+
+// Epilogue of one output spectrum of one lane: adds the other partition
+// half's sum (NH = 2), then turns the product spectrum Y into the
+// half-length complex spectrum Z that the inverse real FFT starts from,
+// Z[m] = (Y[m] + conj Y[M-m] + i (Y[m] - conj Y[M-m]) W_2M^-m) / 2M
+// (Y here is 4x the product spectrum: see Unpack), and stores (or
+// accumulates, for partition chunks after the first) it.  With (u, v) the
+// mirror pair of Y, t = conj(W_2M^m) * S and S = 1/8M:
+//   Z.x = (u.x + v.x) S - s t.y (u.x - v.x) - t.x (u.y + v.y)
+//   Z.y = s S (u.y - v.y) + s t.x (u.x - v.x) - t.y (u.y + v.y)
+template <int NH>
 struct ZEpilogue {
-  double2* zc;     // Z row base of this lane's output index (nullptr: no output)
-  double2 tw;      // conj(W_2M^m) * (0.5 / M)
-  bool paired;     // pair wave (partner in lane ^ 32) vs the self-paired middle bin
-  int MS;
-  __device__ __forceinline__ void store(const double2 y, int64_t j, bool first) const {
-    double2 p;
-    if (paired) {
-      p.x = __shfl_xor(y.x, 32);
-      p.y = __shfl_xor(y.y, 32);
-    } else {
-      p = y;
+  double2* zc;      // Z row base of this lane's bin (bin M: the row's padding column M)
+  int64_t jstride;  // MS
+  double2 tw;       // t = conj(W_2M^m) * S
+  double2 stw;      // s * t
+  double S, sS;     // 1/8M, s/8M
+  // Unconditional (branch-free) store: rows past the run land in the spare
+  // rows after jc_max (or in rows >= jc that K3 never reads), so the wave's
+  // vmcnt bookkeeping stays exact across the group loop.  Lanes that carry
+  // the same bin (the two partition halves; every lane of the middle-bin
+  // wave) hold bit-identical z (a + b == b + a) and store it to the same
+  // address in the same instruction; bin M stores into padding column M.
+  template <bool FIRST>
+  __device__ __forceinline__ void store(double2 y, int64_t j) const {
+    if constexpr (NH == 2) {
+      double2 a, b;
+      xpair<true>(y, a, b);
+      y = make_double2(a.x + b.x, a.y + b.y);
     }
-    if (!zc) return;
-    const double2 fe = make_double2(y.x + p.x, y.y - p.y);  // Y + conj(P)
-    const double2 d = make_double2(y.x - p.x, y.y + p.y);   // Y - conj(P)
-    const double2 fo = c_mul(d, tw);
-    const double2 z = make_double2(fe.x * tw_scale - fo.y, fe.y * tw_scale + fo.x);
-    double2* zp = zc + j * MS;
-    if (first) {
+    double2 u, v;
+    xpair<NH == 1>(y, u, v);
+    const double sx = u.x + v.x, dx = u.x - v.x, sy = u.y + v.y, dy = u.y - v.y;
+    const double2 z = make_double2(fma(-tw.x, sy, fma(-stw.y, dx, sx * S)), fma(-tw.y, sy, fma(stw.x, dx, sS * dy)));
+    double2* zp = zc + j * jstride;
+    if constexpr (FIRST) {
       *zp = z;
     } else {
       const double2 o = *zp;
       *zp = make_double2(o.x + z.x, o.y + z.y);
     }
   }
-  double tw_scale;  // 0.5 / M (applied to fe; tw already carries it for fo)
 };
 
-// Iterations U..UE-1 of a run group: PC products per spectrum into the
-// rotating accumulators, then the finished output (slot U) is stored.
-template <int PC, int U, int UE>
-struct MacSpan {
-  template <int Q = 0>
+// Row U of a group of PC rows: the X value prefetched D rows earlier is
+// separated and fed to the rotating accumulators, and row U + D is
+// prefetched into the freed ring entry (xb[U % D]; PC % D == 0 keeps the
+// index compile-time across groups).  WARM: the group before the run, whose
+// row U only reaches outputs of the run through partitions q >= PC - U.
+// Otherwise the finished output (slot U) is stored (outputs past the run
+// land in rows nobody reads; see ZEpilogue).
+template <int PC, int D, int U, bool WARM>
+struct Row {
+  template <int Q>
   __device__ static __forceinline__ void macs(double2 (&acc)[PC], const double2 (&h)[PC], const double2 x) {
     if constexpr (Q < PC) {
       cmac(acc[(U + Q) % PC], x, h[Q]);
       macs<Q + 1>(acc, h, x);
     }
   }
-  __device__ static __forceinline__ void run(double2 (&acc)[PC], const double2 (&h)[PC], const double2 (&xg)[PC],
-                                             const ZEpilogue& epi, int i, int j1, bool first) {
-    if constexpr (U < UE) {
-      macs(acc, h, xg[U]);
-      if (i + U < j1) epi.store(acc[U], i + U, first);  // wave-uniform
-      acc[U] = make_double2(0.0, 0.0);
-      MacSpan<PC, U + 1, UE>::run(acc, h, xg, epi, i, j1, first);
+  template <bool FIRST, class UP, class EPI>
+  __device__ static __forceinline__ void run(double2 (&acc)[PC], const double2 (&h)[PC], double2 (&xb)[D],
+                                             const XStream& st, const UP& up, const EPI& epi, int i) {
+    if constexpr (U < PC) {
+      const double2 x = up(xb[U % D]);
+      xb[U % D] = st.load(U + D);
+      if constexpr (WARM) {
+        macs<PC - U>(acc, h, x);
+      } else {
+        macs<0>(acc, h, x);
+        epi.template store<FIRST>(acc[U], i + U);
+        acc[U] = make_double2(0.0, 0.0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      Row<PC, D, U + 1, WARM>::template run<FIRST>(acc, h, xb, st, up, epi, i);
     }
   }
 };
 
+// Occupancy target (waves per SIMD): the scheduler otherwise hoists loads
+// for ILP at the cost of occupancy, and K2 wants loads in flight per CU.
+template <int PC, int NH>
+struct MacOcc {
+  static constexpr int W = PC <= 4 ? 4 : (PC == 8 ? 3 : 2);
+};
+// X prefetch depth (rows in flight per lane).
 template <int PC>
-__global__ __launch_bounds__(64) void k_fdl_mac(MacArgs a) {
+struct MacDepth {
+  static constexpr int D = PC < 4 ? PC : 4;
+};
+
+template <int PC, int NH, bool FIRST>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MacOcc<PC, NH>::W))) void k_fdl_mac(MacArgs a) {
+  constexpr int BW = 32 / NH;  // bin pairs per wave
   const int lg = xcd_remap(blockIdx.x, gridDim.x);
   const int ry = lg % a.ny;
   const int t = lg / a.ny;
   const int bx = t % a.nx;
   const int c = t / a.nx;
   const int lane = threadIdx.x;
-  // bin of this lane: pair waves cover [0, M/2) in lanes 0-31 and the mirror
-  // bins (M/2, M] in lanes 32-63; the last wave carries the middle bin M/2.
-  const bool paired = bx < a.M / 64;
-  int k;
-  if (paired) {
-    k = (lane < 32) ? bx * 32 + lane : a.M - (bx * 32 + lane - 32);
-  } else {
-    if (lane != 0) return;
-    k = a.M / 2;
-  }
+  const bool ph = NH == 2 && lane >= 32;
+  const bool mi = NH == 2 ? ((lane >> 4) & 1) : (lane >> 5);
+  const int l = lane & (BW - 1);
+  // pair waves: bins [0, M/2) (mi = 0) and their mirrors (M/2, M] (mi = 1);
+  // the last wave: the middle bin M/2 in every lane, stored by lane 0.
+  const bool paired = bx < a.M / (2 * BW);
+  const int k = paired ? (mi ? a.M - (bx * BW + l) : bx * BW + l) : a.M / 2;
   const int j0 = ry * a.R;
   const int j1 = min(j0 + a.R, a.jc);
   const int ir = a.ir_index ? a.ir_index[c] : (c % a.n_ir);
-  const double2* Hc = a.H + (int64_t)ir * a.h_ir_stride + k;
-  const double2* Xc = a.X + (int64_t)c * a.x_ch_stride + k;
-  ZEpilogue epi;
-  epi.paired = paired;
-  epi.MS = a.MS;
-  epi.tw_scale = 0.5 / (double)a.M;
-  if (k < a.M) {
-    epi.zc = a.Y + (int64_t)c * a.y_ch_stride + k;
-    epi.tw = c_scale(c_conj(a.twN[k]), epi.tw_scale);
-  } else {
-    epi.zc = nullptr;  // the Nyquist lane only feeds its partner (bin 0)
-    epi.tw = make_double2(0.0, 0.0);
-  }
+  const int kz = k & (a.M - 1);  // raw spectrum index: bin M reads Zr[0]
+  const double2* Hc = a.H + (int64_t)ir * a.h_ir_stride + kz;
+  const double2* Xc = a.X + (int64_t)c * a.x_ch_stride + kz;
+  const double sgn = mi ? -1.0 : 1.0;
+  Unpack<NH> up;
+  up.s = sgn;
+  up.tw = (k < a.M) ? a.twN[k] : make_double2(-1.0, 0.0);
+  up.stw = c_scale(up.tw, sgn);
+  ZEpilogue<NH> epi;
+  epi.S = 0.125 / (double)a.M;
+  epi.sS = sgn * epi.S;
+  epi.zc = a.Y + (int64_t)c * a.y_ch_stride + k;  // k = M: padding column
+  epi.jstride = a.MS;
+  epi.tw = (k < a.M) ? c_scale(c_conj(a.twN[k]), epi.S) : make_double2(0.0, 0.0);
+  epi.stw = c_scale(epi.tw, sgn);
 
-  for (int p0 = 0; p0 < a.P; p0 += PC) {
+  {
+    const int pb = a.p0 + (ph ? PC : 0);  // this lane's first partition
     double2 h[PC];
 #pragma unroll
-    for (int q = 0; q < PC; ++q) h[q] = (p0 + q < a.P) ? Hc[(int64_t)(p0 + q) * a.MS] : make_double2(0.0, 0.0);
+    for (int q = 0; q < PC; ++q) {
+      const double2 hv = Hc[(int64_t)min(pb + q, a.P - 1) * a.MS];
+      h[q] = up(hv);
+      if (pb + q >= a.P) h[q] = make_double2(0.0, 0.0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
     double2 acc[PC];
 #pragma unroll
     for (int q = 0; q < PC; ++q) acc[q] = make_double2(0.0, 0.0);
 
-    constexpr int HH = PC / 2 > 0 ? PC / 2 : 1;
-    double2 xg[PC];
-    // --- warm-up group: spectra j0-PC .. j0-1 (slot u = 0 feeds nothing)
-    int64_t lx = a.g0 + j0 - PC - p0;
-    int sl = (int)(((lx % a.Q) + a.Q) % a.Q);
-    load_span<PC, 1, PC>(xg, Xc, a.Q, a.MS, lx, sl);
-    MacWarm<PC, 1>::run(acc, h, xg);
-    lx += PC;
-    sl += PC;
-    if (sl >= a.Q) sl -= a.Q;
-    // --- run groups, software pipelined: the second half of a group is
-    // loaded when the group starts, the next group's first half while the
-    // second half computes.
-    load_span<PC, 0, HH>(xg, Xc, a.Q, a.MS, lx, sl);
+    constexpr int D = MacDepth<PC>::D;
+    XStream st;
+    st.Xc = Xc;
+    st.Q = a.Q;
+    st.MS = a.MS;
+    st.lx = a.g0 + j0 - PC - a.p0;  // row 0 of the warm-up group (feeds nothing), ph = 0
+    st.sl = (int)(((st.lx % a.Q) + a.Q) % a.Q);
+    st.dph = -PC;
+    st.ph = ph;
+    double2 xb[D];
+#pragma unroll
+    for (int d = 1; d <= D; ++d) xb[d % D] = st.load(d);
+    Row<PC, D, 1, true>::template run<FIRST>(acc, h, xb, st, up, epi, j0);
+    st.advance<PC>();
     for (int i = j0; i < j1; i += PC) {
-      load_span<PC, HH, PC>(xg, Xc, a.Q, a.MS, lx, sl);
-      MacSpan<PC, 0, HH>::run(acc, h, xg, epi, i, j1, p0 == 0);
-      lx += PC;
-      sl += PC;
-      if (sl >= a.Q) sl -= a.Q;
-      if (i + PC < j1) load_span<PC, 0, HH>(xg, Xc, a.Q, a.MS, lx, sl);
-      MacSpan<PC, HH, PC>::run(acc, h, xg, epi, i, j1, p0 == 0);
+      Row<PC, D, 0, false>::template run<FIRST>(acc, h, xb, st, up, epi, i);
+      st.advance<PC>();
     }
   }
 }
@@ -293,20 +386,47 @@ __global__ __launch_bounds__(256) void k_mixdown(const double* __restrict__ ch, 
 // ---------------------------------------------------------------------------
 // Launchers
 // ---------------------------------------------------------------------------
-bool launch_fdl_mac(int PC, const MacArgs& in, int channels, hipStream_t s) {
+namespace {
+template <int PC, int NH>
+void mac_go(const MacArgs& a, dim3 grid, hipStream_t s) {
+  MacArgs c = a;
+  for (c.p0 = 0; c.p0 < a.P; c.p0 += NH * PC) {
+    if (c.p0 == 0)
+      hipLaunchKernelGGL((k_fdl_mac<PC, NH, true>), grid, dim3(64), 0, s, c);
+    else
+      hipLaunchKernelGGL((k_fdl_mac<PC, NH, false>), grid, dim3(64), 0, s, c);
+  }
+}
+}  // namespace
+
+bool launch_fdl_mac(int PC, int NH, const MacArgs& in, int channels, hipStream_t s) {
   if (channels <= 0 || in.jc <= 0) return true;
   MacArgs a = in;
-  if (a.M < 64) return false;  // pair waves need M/2 >= 32 bins
-  a.nx = a.M / 64 + 1;         // pair waves + the middle-bin wave
+  const int BW = 32 / NH;
+  if (a.M < 2 * BW) return false;  // a pair wave needs M/2 >= BW bins
+  a.nx = a.M / (2 * BW) + 1;        // pair waves + the middle-bin wave
+  // runs must be whole groups of PC (<= 16) outputs so the overshoot of a run
+  // never lands in the next run's rows
+  if (a.jc > a.R) a.R = (a.R + 15) / 16 * 16;
   a.ny = (a.jc + a.R - 1) / a.R;
-  dim3 grid((unsigned)((int64_t)channels * a.nx * a.ny));
+  const dim3 grid((unsigned)((int64_t)channels * a.nx * a.ny));
+  if (NH == 1) {
+    switch (PC) {
+      case 1: mac_go<1, 1>(a, grid, s); break;
+      case 2: mac_go<2, 1>(a, grid, s); break;
+      case 4: mac_go<4, 1>(a, grid, s); break;
+      case 8: mac_go<8, 1>(a, grid, s); break;
+      case 16: mac_go<16, 1>(a, grid, s); break;
+      default: return false;
+    }
+    return true;
+  }
   switch (PC) {
-    case 1: hipLaunchKernelGGL(k_fdl_mac<1>, grid, dim3(64), 0, s, a); break;
-    case 2: hipLaunchKernelGGL(k_fdl_mac<2>, grid, dim3(64), 0, s, a); break;
-    case 4: hipLaunchKernelGGL(k_fdl_mac<4>, grid, dim3(64), 0, s, a); break;
-    case 8: hipLaunchKernelGGL(k_fdl_mac<8>, grid, dim3(64), 0, s, a); break;
-    case 16: hipLaunchKernelGGL(k_fdl_mac<16>, grid, dim3(64), 0, s, a); break;
-    case 32: hipLaunchKernelGGL(k_fdl_mac<32>, grid, dim3(64), 0, s, a); break;
+    case 1: mac_go<1, 2>(a, grid, s); break;
+    case 2: mac_go<2, 2>(a, grid, s); break;
+    case 4: mac_go<4, 2>(a, grid, s); break;
+    case 8: mac_go<8, 2>(a, grid, s); break;
+    case 16: mac_go<16, 2>(a, grid, s); break;
     default: return false;
   }
   return true;

@@ -31,13 +31,15 @@ struct MacArgs {
   int64_t x_ch_stride;
   int Q;
   int64_t g0;           // logical spectrum index of chunk block 0 (< 0: zeros)
-  int nx, ny;           // bin groups of 64, output runs (set by the launcher)
+  int nx, ny;           // bin-pair waves, output runs (set by the launcher)
+  int p0;               // first partition of this launch's chunk (set by the launcher)
   int MS;
   const double2* H;     // [n_ir][P][MS]
   int64_t h_ir_stride;  // P*MS
   const int* ir_index;  // [C] device (nullable -> c % n_ir)
   int n_ir;
-  double2* Y;           // Z output [C][jc_max][MS] (half-length spectra for the inverse rFFT)
+  double2* Y;           // Z output [C][jc_max + 16][MS] (half-length spectra for the inverse rFFT;
+                        // rows >= jc_max absorb the last run's overshoot)
   int64_t y_ch_stride;
   const double2* twN;   // W_{2M}^k, k < M
   int jc;
@@ -63,7 +65,7 @@ struct IrfftArgs {
 
 bool launch_window_rfft(int M, const RfftArgs& a, hipStream_t s);
 bool launch_irfft_store(int M, const IrfftArgs& a, hipStream_t s);
-bool launch_fdl_mac(int PC, const MacArgs& a, int channels, hipStream_t s);
+bool launch_fdl_mac(int PC, int NH, const MacArgs& a, int channels, hipStream_t s);
 void launch_direct(const double* a, int64_t n, const double* b, int64_t m, double* dst, hipStream_t s);
 void launch_direct_circular(const double* a, const double* b, int64_t n, double* dst, hipStream_t s);
 void launch_stream_direct(const double* h, int64_t K, const double* buf, int64_t B, double* y, hipStream_t s);

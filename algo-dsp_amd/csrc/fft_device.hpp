@@ -13,9 +13,9 @@
 //   * the LDS image is interleaved double2 padded by one element per 16
 //     (pad(i) = i + i/16) so the stride-R butterfly writes of a Stockham
 //     pass hit distinct 16-B slots of the 256-B bank row (ds_write_b128);
-//   * a 256-thread workgroup carries 4096/M independent FFTs, so every size
-//     from 16 to 4096 points keeps the same 69.6 KiB LDS footprint
-//     (two workgroups per CU);
+//   * a workgroup of max(M/V, 256) threads carries max(1, 256V/M) FFTs
+//     (fft_kernels.hip splits M >= 2048 into two M/2 transforms so that two
+//     workgroups share a CU);
 //   * butterfly twiddles come from one W_M table read once per butterfly and
 //     powered by complex multiplies in registers (FP64 sincos is far too
 //     expensive on the VALU).
@@ -142,13 +142,53 @@ struct FftPlan {
 
 __device__ __forceinline__ int lds_pad(int i) { return i + (i >> 4); }
 
+// Twiddle sources.  TwGlobal reads W_M^e from the HBM table.  TwLds reads it
+// from two small LDS tables, W^e = lo[e mod 2^S] * hi[e >> S] (S = ceil(log2 M / 2),
+// 2^S + M/2^S entries): no global load inside the passes, so the only vector
+// memory traffic of a persistent FFT workgroup is its own prefetch and stores,
+// and waiting on a twiddle never drains them (vmcnt is in-order on gfx950).
+// One extra rounding vs the direct table (~1 ulp), far inside the 1e-7 gate.
+struct TwGlobal {
+  const double2* __restrict__ t;
+  __device__ __forceinline__ double2 operator()(int e) const { return t[e]; }
+};
+template <int M>
+struct TwSplit {
+  static constexpr int S = (ilog2c(M) + 1) / 2;
+  static constexpr int NLO = 1 << S;
+  static constexpr int NHI = M >> S;
+  static constexpr int N = NLO + NHI;  // LDS entries per table
+};
+template <int M>
+struct TwLds {
+  const double2* lo;  // LDS: W^i, i < 2^S
+  const double2* hi;  // LDS: W^(i 2^S), i < M / 2^S
+  __device__ __forceinline__ double2 operator()(int e) const {
+    using Sp = TwSplit<M>;
+    if constexpr (Sp::NHI == 1) return lo[e];
+    const double2 a = lo[e & (Sp::NLO - 1)];
+    const double2 b = hi[e >> Sp::S];
+    return c_mul(a, b);
+  }
+};
+// Fills an LDS table pair from a full W_M table in HBM (all threads of the
+// workgroup take part; the caller barriers before the first use).
+// STRIDE > 1 reads W_M^e as g[e * STRIDE] from a finer table (W_{M*STRIDE}).
+template <int M, int STRIDE = 1>
+__device__ __forceinline__ TwLds<M> tw_lds_fill(double2* ltab, const double2* __restrict__ g, int tid, int nthreads) {
+  using Sp = TwSplit<M>;
+  for (int i = tid; i < Sp::N; i += nthreads)
+    ltab[i] = (i < Sp::NLO) ? g[i * STRIDE] : g[((i - Sp::NLO) << Sp::S) * STRIDE];
+  return TwLds<M>{ltab, ltab + Sp::NLO};
+}
+
 // Twiddle multiply for butterfly jb of a pass with stride NS and radix R:
 // v[r] *= W_{NS*R}^{(jb mod NS) * r} = W_M^{e*r}, e = (jb mod NS) * M/(NS*R).
-template <int M, int R, int NS, bool FWD>
-__device__ __forceinline__ void apply_twiddles(double2* v, int jb, const double2* __restrict__ twM) {
+template <int M, int R, int NS, bool FWD, class TW>
+__device__ __forceinline__ void apply_twiddles(double2* v, int jb, const TW& tw) {
   if constexpr (NS > 1) {
     const int e = (jb & (NS - 1)) * (M / (NS * R));
-    double2 w = twM[e];
+    double2 w = tw(e);
     if (!FWD) w = c_conj(w);
     double2 wr = w;
 #pragma unroll
@@ -161,8 +201,8 @@ __device__ __forceinline__ void apply_twiddles(double2* v, int jb, const double2
 
 // One in-register pass on the thread's V values (V/R butterflies of radix R),
 // followed by the Stockham store into the LDS image of this FFT.
-template <int M, int V, int P, bool FWD>
-__device__ __forceinline__ void pass_compute_store(double2* v, int tid, double2* lds, const double2* __restrict__ twM) {
+template <int M, int V, int P, bool FWD, class TW>
+__device__ __forceinline__ void pass_compute_store(double2* v, int tid, double2* lds, const TW& twM) {
   using Plan = FftPlan<M, V>;
   constexpr int R = Plan::radix(P);
   constexpr int NS = Plan::ns(P);
@@ -170,7 +210,7 @@ __device__ __forceinline__ void pass_compute_store(double2* v, int tid, double2*
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
     const int jb = tid + b * Plan::T;
-    apply_twiddles<M, R, NS, FWD>(v + b * R, jb, twM);
+    apply_twiddles<M, R, NS, FWD, TW>(v + b * R, jb, twM);
     Dft<R, FWD>::run(v + b * R);
   }
 #pragma unroll
@@ -208,23 +248,23 @@ __device__ __forceinline__ int pass0_index(int tid, int s) {
 // Runs passes [1, NPASS-1) (the middle passes) after pass 0 has been stored:
 // barrier, load, compute, barrier, store.  Leaves the last pass's input in v
 // (already loaded), ready for the caller's final pass handling.
-template <int M, int V, bool FWD, int P = 1>
-__device__ __forceinline__ void run_middle_passes(double2* v, int tid, double2* lds, const double2* __restrict__ twM) {
+template <int M, int V, bool FWD, int P = 1, class TW>
+__device__ __forceinline__ void run_middle_passes(double2* v, int tid, double2* lds, const TW& twM) {
   using Plan = FftPlan<M, V>;
   if constexpr (P < Plan::NPASS) {
     __syncthreads();
     pass_load<M, V, P>(v, tid, lds);
     if constexpr (P + 1 < Plan::NPASS) {
       __syncthreads();
-      pass_compute_store<M, V, P, FWD>(v, tid, lds, twM);
-      run_middle_passes<M, V, FWD, P + 1>(v, tid, lds, twM);
+      pass_compute_store<M, V, P, FWD, TW>(v, tid, lds, twM);
+      run_middle_passes<M, V, FWD, P + 1, TW>(v, tid, lds, twM);
     }
   }
 }
 
 // Computes the last pass in registers (twiddles + DFT) without storing.
-template <int M, int V, bool FWD>
-__device__ __forceinline__ void last_pass_compute(double2* v, int tid, const double2* __restrict__ twM) {
+template <int M, int V, bool FWD, class TW>
+__device__ __forceinline__ void last_pass_compute(double2* v, int tid, const TW& twM) {
   using Plan = FftPlan<M, V>;
   constexpr int P = Plan::NPASS - 1;
   constexpr int R = Plan::radix(P);
@@ -233,7 +273,7 @@ __device__ __forceinline__ void last_pass_compute(double2* v, int tid, const dou
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
     const int jb = tid + b * Plan::T;
-    apply_twiddles<M, R, NS, FWD>(v + b * R, jb, twM);
+    apply_twiddles<M, R, NS, FWD, TW>(v + b * R, jb, twM);
     Dft<R, FWD>::run(v + b * R);
   }
 }

@@ -19,14 +19,19 @@ int env_int(const char* name, int dflt) {
   return std::atoi(v);
 }
 
-int pick_pc(int P) {
-  // partitions held in VGPRs per wave: the smallest power of two >= P, capped
+// K2 lane layout: NH = 2 splits the partitions over two lane halves (half
+// the VGPRs per lane, twice the waves); NH = 1 keeps all of a chunk's
+// partitions in one lane.  PC = partitions per lane: the smallest power of
+// two >= P/NH, capped at 16 (larger P: one launch per chunk of NH*16).
+int pick_nh(int P) {
   if (P <= 1) return 1;
-  if (P <= 2) return 2;
-  if (P <= 4) return 4;
-  if (P <= 8) return 8;
-  if (P <= 16) return 16;
-  return env_int("AD_MAC_PC_MAX", 32) >= 32 ? 32 : 16;
+  return env_int("AD_MAC_NH", 1) == 2 ? 2 : 1;
+}
+int pick_pc(int P, int NH) {
+  const int per = (P + NH - 1) / NH;
+  int pc = 1;
+  while (pc < per && pc < 16) pc *= 2;
+  return pc;
 }
 
 }  // namespace
@@ -39,9 +44,10 @@ Upols::Upols(int device, const double* kernels, int n_ir, int64_t K, int L, int 
   M_ = L;
   MS_ = M_ + 8;
   P_ = (int)((K + L - 1) / L);
-  PC_ = pick_pc(P_);
-  Q_ = jc_max_ + P_ + PC_ + 1;
-  R_ = std::max(1, env_int("AD_MAC_R", 128));
+  NH_ = pick_nh(P_);
+  PC_ = pick_pc(P_, NH_);
+  Q_ = jc_max_ + P_ + 2 * PC_ + 1;
+  R_ = std::max(1, env_int("AD_MAC_R", 64));
 
   // Twiddle tables, computed in long double on the host.
   std::vector<double2> tw(2 * (size_t)M_);
@@ -91,7 +97,8 @@ Upols::Upols(int device, const double* kernels, int n_ir, int64_t K, int L, int 
   AD_HIP(hipGetLastError());
 
   X_.alloc((size_t)C_ * (Q_ + 1) * MS_);  // Q ring rows + one zero row per channel
-  Y_.alloc((size_t)C_ * jc_max_ * MS_);
+  // Z rows: jc_max outputs + 16 rows of run overshoot (k_fdl_mac)
+  Y_.alloc((size_t)C_ * (jc_max_ + 16) * MS_);
   hist_.alloc((size_t)C_ * L_);
   std::vector<int> irm(C_);
   for (int c = 0; c < C_; ++c) irm[c] = ir_map ? ir_map[c] : (c % n_ir_);
@@ -230,19 +237,19 @@ void Upols::run(const double* d_in, int64_t in_stride, int64_t n, double* d_out,
     m.ir_index = irmap_.p;
     m.n_ir = n_ir_;
     m.Y = Y_.p;
-    m.y_ch_stride = (int64_t)jc_max_ * MS_;
+    m.y_ch_stride = (int64_t)(jc_max_ + 16) * MS_;
     m.jc = jc;
     m.R = std::min(R_, jc);
     m.P = P_;
     m.M = M_;
     m.twN = tw_.p + M_;
     prof_begin(s, &e0);
-    launch_fdl_mac(PC_, m, C_, s);
+    launch_fdl_mac(PC_, NH_, m, C_, s);
     prof_end(s, e0, 1, blocks * (double)(M_ + 1) * 32 + (double)n_ir_ * P_ * (M_ + 1) * 16);
 
     IrfftArgs b{};
     b.Y = Y_.p;
-    b.y_ch_stride = (int64_t)jc_max_ * MS_;
+    b.y_ch_stride = (int64_t)(jc_max_ + 16) * MS_;
     b.MS = MS_;
     b.out = d_out;
     b.out_stride = out_stride;

@@ -50,7 +50,7 @@ class Upols {
 
  private:
   int64_t K_;
-  int L_, M_, MS_, P_, PC_, C_, n_ir_, jc_max_, Q_, R_;
+  int L_, M_, MS_, P_, PC_, NH_, C_, n_ir_, jc_max_, Q_, R_;
   int64_t g_next_ = 0;  // logical index of the next spectrum block
   hipStream_t stream_;
   DevBuf<double2> tw_;   // [twM (M) | twN (M)]

@@ -32,7 +32,7 @@ def parse():
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--samples", type=int, default=1 << 24, help="samples per channel per step")
-    p.add_argument("--hop", type=int, default=4096)
+    p.add_argument("--hop", type=int, default=8192)
     p.add_argument("--chunk", type=int, default=0, help="blocks per channel per engine chunk (0 = auto)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-sample", type=int, default=1 << 24, help="samples of one channel for the CPU leg")

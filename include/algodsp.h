@@ -118,7 +118,7 @@ int ad_conv_convolve(const double* a, int64_t n, const double* b, int64_t m, int
 /* ---- multi-channel device-resident engine (offline / many-channel path) --
  * Uniformly partitioned overlap-save with a frequency-domain delay line.
  * kernels: n_ir impulse responses of kernel_len taps each, row-major.
- * hop: partition/hop length (power of two, 64..8192); 0 = auto (4096).
+ * hop: partition/hop length (power of two, 64..8192); 0 = auto (min(8192, nextpow2(max(K, 256))).
  * channels: number of channels processed per call; ir_index[c] selects the
  *   IR of channel c (NULL: c % n_ir).
  * max_chunk_blocks: blocks per channel per internal chunk (0 = auto).     */
