@@ -88,6 +88,15 @@ _BY_CODE = {
     AD_ERR_INVALID_ARGUMENT: ErrInvalidArgument,
 }
 
+class CompressorConfig(C.Structure):
+    """ad_compressor_config (include/algodsp.h)."""
+
+    _fields_ = [(n, C.c_double) for n in ("sample_rate", "threshold_db", "ratio", "knee_db", "attack_ms",
+                                          "release_ms", "rms_window_ms", "makeup_db", "sidechain_low_cut_hz",
+                                          "sidechain_high_cut_hz")] + \
+               [(n, C.c_int) for n in ("topology", "detector_mode", "feedback_ratio_scale", "auto_makeup")]
+
+
 _lib = None
 
 c_double_p = C.POINTER(C.c_double)
@@ -150,6 +159,26 @@ def _declare(L: C.CDLL) -> None:
         "ad_conv_mixdown_device": (C.c_int, [vp, C.c_int, i64, i64, vp, vp]),
         "ad_conv_profile_enable": (C.c_int, [vp, C.c_int]),
         "ad_conv_profile_read": (C.c_int, [vp, c_double_p, c_int64_p, c_double_p]),
+        "ad_compressor_default_config": (None, [C.POINTER(CompressorConfig), C.c_double]),
+        "ad_fx_chain_create": (C.c_int, [C.c_int, C.c_int, C.POINTER(vp)]),
+        "ad_fx_chain_set_eq": (C.c_int, [vp, c_double_p, C.c_int, C.c_int]),
+        "ad_fx_chain_set_compressor": (C.c_int, [vp, C.POINTER(CompressorConfig)]),
+        "ad_fx_chain_set_freeverb": (C.c_int, [vp, C.c_double, C.c_double, C.c_double, C.c_double, C.c_double]),
+        "ad_fx_chain_disable_freeverb": (C.c_int, [vp]),
+        "ad_fx_chain_reset": (C.c_int, [vp]),
+        "ad_fx_chain_process": (C.c_int, [vp, c_double_p, i64]),
+        "ad_fx_chain_process_device": (C.c_int, [vp, vp, i64, i64, vp]),
+        "ad_fx_chain_compressor_metrics": (C.c_int, [vp, C.c_int, c_double_p, c_double_p, c_double_p]),
+        "ad_fx_chain_eq_state": (C.c_int, [vp, c_double_p, i64]),
+        "ad_fx_chain_destroy": (None, [vp]),
+        "ad_biquad_chain_process": (C.c_int, [c_double_p, c_double_p, C.c_double, c_double_p, C.c_int, C.c_int, i64,
+                                              C.c_int]),
+        "ad_fir_create": (C.c_int, [c_double_p, i64, C.c_int, C.c_int, C.POINTER(vp)]),
+        "ad_fir_process_block": (C.c_int, [vp, c_double_p, i64]),
+        "ad_fir_process_block_to": (C.c_int, [vp, c_double_p, c_double_p, i64]),
+        "ad_fir_process_device": (C.c_int, [vp, vp, i64, vp, i64, i64, vp]),
+        "ad_fir_reset": (C.c_int, [vp]),
+        "ad_fir_destroy": (None, [vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

@@ -1,0 +1,288 @@
+"""Host-side mirror of the reference's per-sample processors on the HIP engine.
+
+Names and argument meaning follow the Go packages so the parity tests read
+like the reference's own tests:
+
+  biquad.Chain / biquad.Section  dsp/filter/biquad/chain.go, section.go
+  dynamics.Compressor            dsp/effects/dynamics/compressor.go
+  reverb.Reverb (Freeverb)       dsp/effects/reverb/reverb.go
+  fir.Filter                     dsp/filter/fir/filter.go
+  effectchain filter -> dyn-compressor -> reverb-freeverb (EffectChain)
+
+Every instance can carry `channels` independent reference instances (one
+lane each on the GPU); buffers are [channels][n] float64 (a 1-D buffer is
+one channel).  All work runs in libalgodsp_hip.so; there is no CPU path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from ._lib import CompressorConfig, check, f64, lib, ptr
+
+DEVICE = 0
+SEC_STRIDE = 6  # {pre_gain, b0, b1, b2, a1, a2}
+
+
+def _as2d(buf, channels: int):
+    if not isinstance(buf, np.ndarray) or buf.dtype != np.float64 or not buf.flags.c_contiguous:
+        raise TypeError("buffer must be a C-contiguous float64 numpy array")
+    b2 = buf.reshape(1, -1) if buf.ndim == 1 else buf
+    if b2.shape[0] != channels:
+        raise ValueError(f"buffer has {b2.shape[0]} channels, processor has {channels}")
+    return b2
+
+
+def section_table(coeffs, gain: float = 1.0) -> np.ndarray:
+    """[sections][5] {b0,b1,b2,a1,a2} (+ chain gain) -> [sections][6] device table."""
+    c = f64(coeffs).reshape(-1, 5)
+    t = np.ones((c.shape[0], SEC_STRIDE))
+    t[:, 1:] = c
+    if c.shape[0]:
+        t[0, 0] = gain
+    return t
+
+
+class _FxChain:
+    def __init__(self, channels: int, device: int):
+        self.channels = int(channels)
+        self._h = C.c_void_p()
+        check(lib().ad_fx_chain_create(self.channels, int(device), C.byref(self._h)))
+
+    def _process(self, buf):
+        b = _as2d(buf, self.channels)
+        check(lib().ad_fx_chain_process(self._h, ptr(b), b.shape[1]))
+
+    def process_device(self, d_buf: int, stride: int, n: int, stream: int | None = None):
+        check(lib().ad_fx_chain_process_device(self._h, C.c_void_p(d_buf), int(stride), int(n),
+                                               C.c_void_p(stream or 0)))
+
+    def Reset(self):
+        check(lib().ad_fx_chain_reset(self._h))
+
+    def close(self):
+        if self._h:
+            lib().ad_fx_chain_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Chain(_FxChain):
+    """biquad.Chain (chain.go:6-138): optional gain, then sections in order."""
+
+    def __init__(self, coeffs, gain: float = 1.0, channels: int = 1, device: int = DEVICE):
+        super().__init__(channels, device)
+        self._coeffs = f64(coeffs).reshape(-1, 5)
+        self._gain = float(gain)
+        self._load()
+
+    def _load(self):
+        t = section_table(self._coeffs, self._gain)
+        check(lib().ad_fx_chain_set_eq(self._h, ptr(t), t.shape[0], 0))
+
+    def NumSections(self) -> int:
+        return self._coeffs.shape[0]
+
+    def Gain(self) -> float:
+        return self._gain
+
+    def SetGain(self, g: float):  # chain.go:89-97
+        self._gain = float(g)
+        self._load()
+
+    def UpdateCoefficients(self, coeffs, gain: float | None = None):  # chain.go:99-115
+        self._coeffs = f64(coeffs).reshape(-1, 5)
+        if gain is not None:
+            self._gain = float(gain)
+        self._load()
+
+    def ProcessBlock(self, buf):  # chain.go:59-70
+        self._process(buf)
+
+    def State(self) -> np.ndarray:  # chain.go:122-130 -> [channels][sections][2]
+        out = np.zeros((self.channels, self.NumSections(), 2))
+        check(lib().ad_fx_chain_eq_state(self._h, ptr(out), out.size))
+        return out
+
+
+def Section(b0, b1, b2, a1, a2, channels: int = 1, device: int = DEVICE) -> Chain:
+    """biquad.Section (section.go:26-155) = a one-section chain with unit gain."""
+    return Chain([[b0, b1, b2, a1, a2]], 1.0, channels, device)
+
+
+class Compressor(_FxChain):
+    """dynamics.Compressor (compressor.go:39-431) on `channels` lanes."""
+
+    def __init__(self, sample_rate: float = 48000.0, channels: int = 1, device: int = DEVICE, **cfg):
+        super().__init__(channels, device)
+        self.cfg = CompressorConfig()
+        lib().ad_compressor_default_config(C.byref(self.cfg), float(sample_rate))
+        for k, v in cfg.items():
+            setattr(self.cfg, k, v)
+        self._apply()
+
+    def _apply(self):
+        check(lib().ad_fx_chain_set_compressor(self._h, C.byref(self.cfg)))
+
+    # setters (compressor.go:130-305)
+    def SetThreshold(self, db):
+        self.cfg.threshold_db = db
+        self._apply()
+
+    def SetRatio(self, r):
+        self.cfg.ratio = r
+        self._apply()
+
+    def SetKnee(self, db):
+        self.cfg.knee_db = db
+        self._apply()
+
+    def SetAttack(self, ms):
+        self.cfg.attack_ms = ms
+        self._apply()
+
+    def SetRelease(self, ms):
+        self.cfg.release_ms = ms
+        self._apply()
+
+    def SetAutoMakeup(self, on: bool):
+        self.cfg.auto_makeup = int(bool(on))
+        self._apply()
+
+    def SetMakeupGain(self, db):
+        self.cfg.makeup_db = db
+        self._apply()
+
+    def ProcessInPlace(self, buf):  # compressor.go:362-366
+        self._process(buf)
+
+    def Metrics(self, channel: int = 0):
+        ip, op, gr = C.c_double(), C.c_double(), C.c_double()
+        check(lib().ad_fx_chain_compressor_metrics(self._h, int(channel), C.byref(ip), C.byref(op), C.byref(gr)))
+        return ip.value, op.value, gr.value
+
+
+class Reverb(_FxChain):
+    """reverb.Reverb (Freeverb, reverb.go:33-235) with NewReverb defaults."""
+
+    def __init__(self, channels: int = 1, device: int = DEVICE):
+        super().__init__(channels, device)
+        self.wet, self.dry, self.room, self.damp, self.gain = 0.22, 1.0, 0.72, 0.45, 0.015
+        self._apply()
+
+    def _apply(self):
+        check(lib().ad_fx_chain_set_freeverb(self._h, self.wet, self.dry, self.room, self.damp, self.gain))
+
+    def SetWet(self, v):
+        self.wet = float(v)
+        self._apply()
+
+    def SetDry(self, v):
+        self.dry = float(v)
+        self._apply()
+
+    def SetRoomSize(self, v):
+        self.room = float(v)
+        self._apply()
+
+    def SetDamp(self, v):
+        self.damp = float(v)
+        self._apply()
+
+    def SetGain(self, v):
+        self.gain = float(v)
+        self._apply()
+
+    def ProcessInPlace(self, buf):  # reverb.go:185-189
+        self._process(buf)
+
+
+class EffectChain(_FxChain):
+    """effectchain `_input -> filter-* -> dyn-compressor -> reverb-freeverb ->
+    _output` for `channels` chains, fused per sample (chain_process.go:11-33).
+
+    eq: list of (coeffs [sections][5], gain) biquad chains (filter nodes, in
+    order); compressor: dict of ad_compressor_config fields or None;
+    freeverb: (wet, dry, room, damp, gain) or None."""
+
+    def __init__(self, channels: int, eq=(), compressor=None, freeverb=None, sample_rate: float = 48000.0,
+                 device: int = DEVICE):
+        super().__init__(channels, device)
+        tabs = [section_table(c, g) for c, g in eq]
+        t = np.concatenate(tabs) if tabs else np.zeros((0, SEC_STRIDE))
+        check(lib().ad_fx_chain_set_eq(self._h, ptr(f64(t)), t.shape[0], 0))
+        if compressor is not None:
+            cfg = CompressorConfig()
+            lib().ad_compressor_default_config(C.byref(cfg), float(sample_rate))
+            for k, v in compressor.items():
+                setattr(cfg, k, v)
+            self.cfg = cfg
+            check(lib().ad_fx_chain_set_compressor(self._h, C.byref(cfg)))
+        if freeverb is not None:
+            check(lib().ad_fx_chain_set_freeverb(self._h, *map(float, freeverb)))
+
+    def Process(self, buf):
+        self._process(buf)
+
+
+class Filter:
+    """fir.Filter (filter.go:11-172) for `channels` lanes sharing the taps."""
+
+    def __init__(self, coeffs, channels: int = 1, device: int = DEVICE):
+        self.coeffs = f64(coeffs).ravel()
+        self.channels = int(channels)
+        self._h = C.c_void_p()
+        check(lib().ad_fir_create(ptr(self.coeffs), self.coeffs.size, self.channels, int(device),
+                                  C.byref(self._h)))
+
+    def ProcessBlock(self, buf):  # :74-114
+        b = _as2d(buf, self.channels)
+        check(lib().ad_fir_process_block(self._h, ptr(b), b.shape[1]))
+
+    def ProcessBlockTo(self, dst, src):  # :119-159
+        d, s = _as2d(dst, self.channels), _as2d(f64(src), self.channels)
+        if d.shape != s.shape:
+            raise ValueError("dst/src length mismatch")
+        check(lib().ad_fir_process_block_to(self._h, ptr(d), ptr(s), s.shape[1]))
+
+    def ProcessSample(self, x: float) -> float:  # :46-69 (one channel)
+        b = np.array([[x]] * self.channels, dtype=np.float64)
+        self.ProcessBlock(b)
+        return float(b[0, 0])
+
+    def process_device(self, d_src: int, src_stride: int, d_dst: int, dst_stride: int, n: int,
+                       stream: int | None = None):
+        check(lib().ad_fir_process_device(self._h, C.c_void_p(d_src), int(src_stride), C.c_void_p(d_dst),
+                                          int(dst_stride), int(n), C.c_void_p(stream or 0)))
+
+    def Reset(self):
+        check(lib().ad_fir_reset(self._h))
+
+    def close(self):
+        if self._h:
+            lib().ad_fir_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def chain_process(coeffs, state, gain, buf):
+    """ad_biquad_chain_process: one-shot Chain.ProcessBlock, state in/out."""
+    c = f64(coeffs).reshape(-1, 5)
+    b = _as2d(buf, buf.shape[0] if buf.ndim == 2 else 1)
+    st = state
+    if not (isinstance(st, np.ndarray) and st.dtype == np.float64 and st.flags.c_contiguous
+            and st.size == b.shape[0] * c.shape[0] * 2):
+        raise TypeError("state must be a C-contiguous float64 array [channels][sections][2]")
+    check(lib().ad_biquad_chain_process(ptr(c), ptr(st), float(gain), ptr(b), b.shape[0], c.shape[0], b.shape[1],
+                                        DEVICE))

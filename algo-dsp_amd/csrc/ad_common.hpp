@@ -86,6 +86,14 @@ struct DevBuf {
   }
 };
 
+// Validates a device index (no CPU fallback: no device is an error).
+inline int pick_device(int device) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) AD_FAIL(AD_ERR_NO_DEVICE, "no HIP device available");
+  if (device < 0 || device >= n) AD_FAIL(AD_ERR_NO_DEVICE, "device index out of range");
+  return device;
+}
+
 // Selects the device for the lifetime of a scope and restores the previous one.
 struct DeviceScope {
   int prev = -1;

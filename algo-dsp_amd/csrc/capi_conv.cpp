@@ -60,13 +60,6 @@ std::vector<StageDesc> partition_ir(int64_t kernel_len_padded, int min_order, in
   return st;
 }
 
-int pick_device(int device) {
-  int n = 0;
-  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) AD_FAIL(AD_ERR_NO_DEVICE, "no HIP device available");
-  if (device < 0 || device >= n) AD_FAIL(AD_ERR_NO_DEVICE, "device index out of range");
-  return device;
-}
-
 int64_t largest_pow2_divisor(int64_t v, int64_t cap) {
   int64_t l = 1;
   while ((v % (l * 2)) == 0 && l * 2 <= cap) l *= 2;

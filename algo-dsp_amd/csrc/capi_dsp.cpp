@@ -1,0 +1,536 @@
+// C ABI of the per-sample processors (biquad chains, Compressor, Freeverb and
+// their fused effect chain) and of the FIR block filter.  Host calls copy in
+// and out inside the call (cgo rule); *_device calls run asynchronously on a
+// caller stream.  See include/algodsp.h for the reference API each replaces.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "ad_common.hpp"
+#include "dsp_kernels.hpp"
+
+using namespace adsp;
+
+namespace {
+
+constexpr double kLog2Of10Div20 = 0.166096404744;  // compressor.go:27 (truncated literal, kept)
+constexpr double kLn2 = 0.693147180559945309417232121458176568;
+constexpr double kPi = 3.14159265358979323846264338327950288;
+
+// dynamicsCore recalculation (core.go:480-540, 600-617), host side.
+CompParams comp_params(const ad_compressor_config& g) {
+  CompParams p{};
+  const double fs = g.sample_rate;
+  double attack = 1.0 - std::exp(-kLn2 / (g.attack_ms * 0.001 * fs));
+  double release = std::exp(-kLn2 / (g.release_ms * 0.001 * fs));
+  if (g.topology == 1 && g.feedback_ratio_scale) {
+    attack = 1.0 - std::exp(-kLn2 / (g.attack_ms * 0.001 * fs * g.ratio));
+    release = std::exp(-kLn2 / (g.release_ms * 0.001 * fs * g.ratio));
+  }
+  p.attack = attack;
+  p.release = release;
+  p.threshold_log2 = g.threshold_db * kLog2Of10Div20;
+  p.knee_width_log2 = g.knee_db * kLog2Of10Div20;
+  p.inv_knee_width_log2 = g.knee_db > 0 ? 1.0 / p.knee_width_log2 : 0.0;
+  p.half_knee = p.knee_width_log2 * 0.5;
+  p.knee_on = g.knee_db > 0;
+  p.cf = 1.0 - 1.0 / g.ratio;
+  if (g.topology == 1 && g.feedback_ratio_scale) p.cf = g.ratio - 1.0;
+  const double makeup_db = g.auto_makeup ? -(g.threshold_db * (1.0 - 1.0 / g.ratio)) : g.makeup_db;
+  p.makeup_lin = std::pow(10.0, makeup_db / 20.0);
+  p.lp_on = g.sidechain_high_cut_hz > 0;
+  p.lp_alpha = p.lp_on ? 1.0 - std::exp(-2.0 * kPi * g.sidechain_high_cut_hz / fs) : 0.0;
+  p.hp_on = g.sidechain_low_cut_hz > 0;
+  p.hp_alpha = p.hp_on ? 1.0 - std::exp(-2.0 * kPi * g.sidechain_low_cut_hz / fs) : 0.0;
+  p.topology_fb = g.topology == 1;
+  p.detector_rms = g.detector_mode == 1;
+  p.rms_n = std::max(1, (int)std::llround(g.rms_window_ms * 0.001 * fs));
+  return p;
+}
+
+void check_comp_config(const ad_compressor_config& g) {
+  // validation of the setters (compressor.go:130-305, core.go validate*)
+  if (!(g.sample_rate > 0) || !std::isfinite(g.sample_rate))
+    AD_FAIL(AD_ERR_INVALID_ARGUMENT, "dynamics: sample rate must be positive and finite");
+  if (!(g.ratio >= 1) || !std::isfinite(g.ratio)) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "dynamics: ratio must be >= 1");
+  if (!(g.knee_db >= 0)) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "dynamics: knee must be >= 0");
+  if (!(g.attack_ms > 0) || !(g.release_ms > 0))
+    AD_FAIL(AD_ERR_INVALID_ARGUMENT, "dynamics: attack/release must be positive");
+  if (!(g.rms_window_ms > 0)) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "dynamics: rms window must be positive");
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// effect chain handle
+// ---------------------------------------------------------------------------
+struct ad_fx_chain {
+  int device = 0, channels = 0, cpad = 0;
+  hipStream_t stream = nullptr;
+  // EQ
+  int nsec = 0;
+  bool eq_uniform = true;
+  std::vector<double> sec_host;  // uniform: [nsec][6]
+  DevBuf<double> sec_dev;        // per-channel: [C][nsec][6]
+  DevBuf<double> eq_state;       // [C][nsec][2]
+  // compressor
+  bool comp_on = false;
+  CompParams cp{};
+  DevBuf<CompChState> cs;
+  DevBuf<double> ring;
+  // Freeverb
+  bool verb_on = false;
+  VerbParams vp{};
+  DevBuf<VerbChState> vs;
+  DevBuf<double> vbuf;
+  // host-call staging
+  DevBuf<double> work;
+
+  ~ad_fx_chain() {
+    if (stream) {
+      (void)hipStreamSynchronize(stream);
+      (void)hipStreamDestroy(stream);
+    }
+  }
+};
+
+namespace {
+
+void fx_reset_comp(ad_fx_chain* h) {
+  if (!h->comp_on) return;
+  std::vector<CompChState> init(h->channels);
+  for (auto& s : init) {  // dynamicsCore.Reset + metrics reset (core.go:572-586)
+    s = CompChState{};
+    s.prev_gain = 1.0;
+    s.gr = 1.0;
+  }
+  AD_HIP(hipMemcpyAsync(h->cs.p, init.data(), init.size() * sizeof(CompChState), hipMemcpyHostToDevice, h->stream));
+  AD_HIP(hipMemsetAsync(h->ring.p, 0, h->ring.n * sizeof(double), h->stream));
+}
+
+void fx_reset_verb(ad_fx_chain* h) {
+  if (!h->verb_on) return;
+  AD_HIP(hipMemsetAsync(h->vs.p, 0, h->vs.n * sizeof(VerbChState), h->stream));
+  AD_HIP(hipMemsetAsync(h->vbuf.p, 0, h->vbuf.n * sizeof(double), h->stream));
+}
+
+void fx_run(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hipStream_t s) {
+  ChainArgs a{};
+  a.buf = d_buf;
+  a.stride = stride;
+  a.n = n;
+  a.channels = h->channels;
+  a.cp = h->cp;
+  a.cs = h->cs.p;
+  a.rms_ring = h->ring.p;
+  a.vp = h->vp;
+  a.vs = h->vs.p;
+  a.vbuf = h->vbuf.p;
+  const int post = (h->comp_on ? 2 : 0) | (h->verb_on ? 4 : 0);
+  // EQ sections in passes of <= kMaxSecPerPass; the last pass fuses the
+  // compressor and Freeverb stages (per-sample fusion is exact, see kernels)
+  int s0 = 0;
+  do {
+    const int ns = std::min(kMaxSecPerPass, h->nsec - s0);
+    a.eq.nsec = ns;
+    a.eq.uniform = h->eq_uniform ? 1 : 0;
+    if (h->eq_uniform) {
+      for (int i = 0; i < ns; ++i)
+        for (int k = 0; k < kSecStride; ++k) a.eq.u[i][k] = h->sec_host[(size_t)(s0 + i) * kSecStride + k];
+      a.eq.sec = nullptr;
+      a.eq.sec_ch_stride = 0;
+    } else {
+      a.eq.sec = h->sec_dev.p + (int64_t)s0 * kSecStride;
+      a.eq.sec_ch_stride = (int64_t)h->nsec * kSecStride;
+    }
+    // state rows of this pass: the kernel indexes [c][ns][2]; keep one
+    // contiguous [C][nsec][2] array by giving each pass its own slab
+    a.eq.state = h->eq_state.p + (int64_t)h->channels * s0 * 2;
+    const bool last = s0 + ns >= h->nsec;
+    const int stages = (ns > 0 ? 1 : 0) | (last ? post : 0);
+    if (stages) launch_chain(stages, a, s);
+    s0 += ns;
+  } while (s0 < h->nsec);
+  AD_HIP(hipGetLastError());
+}
+
+template <class Fn>
+int fx_guard(ad_fx_chain* h, Fn&& fn) {
+  return guard([&] {
+    if (!h) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "null effect-chain handle");
+    DeviceScope ds(h->device);
+    fn();
+  });
+}
+
+}  // namespace
+
+extern "C" {
+
+void ad_compressor_default_config(ad_compressor_config* c, double sample_rate) {
+  // NewCompressor defaults (compressor.go:6-13, 83-98)
+  if (!c) return;
+  std::memset(c, 0, sizeof(*c));
+  c->sample_rate = sample_rate;
+  c->threshold_db = -20.0;
+  c->ratio = 4.0;
+  c->knee_db = 6.0;
+  c->attack_ms = 10.0;
+  c->release_ms = 100.0;
+  c->rms_window_ms = 30.0;
+  c->makeup_db = 0.0;
+  c->auto_makeup = 1;
+  c->feedback_ratio_scale = 1;
+}
+
+int ad_fx_chain_create(int channels, int device, ad_fx_chain** out) {
+  if (out) *out = nullptr;
+  ad_fx_chain* raw = nullptr;
+  const int rc = guard([&] {
+    if (channels <= 0) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "channels must be positive");
+    const int dev = pick_device(device);
+    DeviceScope ds(dev);
+    std::unique_ptr<ad_fx_chain> h(new ad_fx_chain());
+    h->device = dev;
+    h->channels = channels;
+    h->cpad = (channels + 63) / 64 * 64;
+    AD_HIP(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+    raw = h.release();
+  });
+  if (rc == AD_OK && out) *out = raw;
+  return rc;
+}
+
+int ad_fx_chain_set_eq(ad_fx_chain* h, const double* sections, int nsec, int per_channel) {
+  return fx_guard(h, [&] {
+    if (nsec < 0 || (nsec > 0 && !sections)) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "bad EQ section table");
+    AD_HIP(hipStreamSynchronize(h->stream));
+    const bool keep_state = nsec == h->nsec;
+    h->nsec = nsec;
+    h->eq_uniform = !per_channel;
+    if (per_channel) {
+      h->sec_dev.alloc((size_t)h->channels * nsec * kSecStride);
+      if (nsec > 0)
+        AD_HIP(hipMemcpy(h->sec_dev.p, sections, h->sec_dev.n * sizeof(double), hipMemcpyHostToDevice));
+      h->sec_host.clear();
+    } else {
+      h->sec_host.assign(sections, sections + (size_t)nsec * kSecStride);
+    }
+    // Section state survives a coefficient update with the same section
+    // count, like filterRuntime.Configure (runtime_filter_pitch_reverb.go:150-165).
+    if (!keep_state || !h->eq_state.p) {
+      h->eq_state.alloc((size_t)std::max(1, h->channels * nsec * 2));
+      AD_HIP(hipMemset(h->eq_state.p, 0, h->eq_state.n * sizeof(double)));
+    }
+  });
+}
+
+int ad_fx_chain_set_compressor(ad_fx_chain* h, const ad_compressor_config* cfg) {
+  return fx_guard(h, [&] {
+    AD_HIP(hipStreamSynchronize(h->stream));
+    if (!cfg) {
+      h->comp_on = false;
+      return;
+    }
+    check_comp_config(*cfg);
+    const CompParams p = comp_params(*cfg);
+    const bool fresh = !h->comp_on || p.rms_n != h->cp.rms_n;
+    h->cp = p;
+    h->comp_on = true;
+    if (fresh) {
+      h->cs.alloc((size_t)h->channels);
+      h->ring.alloc((size_t)h->channels * p.rms_n);
+      fx_reset_comp(h);
+      AD_HIP(hipStreamSynchronize(h->stream));
+    }
+  });
+}
+
+int ad_fx_chain_set_freeverb(ad_fx_chain* h, double wet, double dry, double room_size, double damp, double gain) {
+  return fx_guard(h, [&] {
+    AD_HIP(hipStreamSynchronize(h->stream));
+    // SetWet/SetDry/SetRoomSize/SetDamp/SetGain (reverb.go:192-220)
+    h->vp.wet = wet;
+    h->vp.dry = dry;
+    h->vp.feedback = room_size;
+    h->vp.damp_a = damp;
+    h->vp.damp_b = 1.0 - damp;
+    h->vp.gain = gain;
+    h->vp.ap_feedback = 0.5;
+    if (!h->verb_on) {
+      h->verb_on = true;
+      h->vs.alloc((size_t)h->channels);
+      h->vbuf.alloc((size_t)kVerbLen * h->cpad);
+      fx_reset_verb(h);
+      AD_HIP(hipStreamSynchronize(h->stream));
+    }
+  });
+}
+
+int ad_fx_chain_disable_freeverb(ad_fx_chain* h) {
+  return fx_guard(h, [&] { h->verb_on = false; });
+}
+
+int ad_fx_chain_reset(ad_fx_chain* h) {
+  return fx_guard(h, [&] {
+    if (h->eq_state.p) AD_HIP(hipMemsetAsync(h->eq_state.p, 0, h->eq_state.n * sizeof(double), h->stream));
+    fx_reset_comp(h);
+    fx_reset_verb(h);
+    AD_HIP(hipStreamSynchronize(h->stream));
+  });
+}
+
+int ad_fx_chain_process(ad_fx_chain* h, double* buf, int64_t n) {
+  return fx_guard(h, [&] {
+    if (n < 0 || (n > 0 && !buf)) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "bad buffer");
+    if (n == 0) return;
+    const size_t bytes = (size_t)h->channels * n * sizeof(double);
+    h->work.reserve((size_t)h->channels * n);
+    AD_HIP(hipMemcpyAsync(h->work.p, buf, bytes, hipMemcpyHostToDevice, h->stream));
+    fx_run(h, h->work.p, n, n, h->stream);
+    AD_HIP(hipMemcpyAsync(buf, h->work.p, bytes, hipMemcpyDeviceToHost, h->stream));
+    AD_HIP(hipStreamSynchronize(h->stream));
+  });
+}
+
+int ad_fx_chain_process_device(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, void* stream) {
+  return fx_guard(h, [&] {
+    if (n < 0 || stride < n) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "bad buffer geometry");
+    fx_run(h, d_buf, stride, n, reinterpret_cast<hipStream_t>(stream));
+  });
+}
+
+int ad_fx_chain_compressor_metrics(ad_fx_chain* h, int channel, double* input_peak, double* output_peak,
+                                   double* gain_reduction) {
+  return fx_guard(h, [&] {
+    if (!h->comp_on) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "compressor stage not configured");
+    if (channel < 0 || channel >= h->channels) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "channel out of range");
+    AD_HIP(hipStreamSynchronize(h->stream));
+    CompChState s{};
+    AD_HIP(hipMemcpy(&s, h->cs.p + channel, sizeof(s), hipMemcpyDeviceToHost));
+    if (input_peak) *input_peak = s.in_peak;
+    if (output_peak) *output_peak = s.out_peak;
+    if (gain_reduction) *gain_reduction = s.gr;
+  });
+}
+
+int ad_fx_chain_eq_state(ad_fx_chain* h, double* state, int64_t cap) {
+  return fx_guard(h, [&] {
+    const int64_t need = (int64_t)h->channels * h->nsec * 2;
+    if (cap < need) AD_FAIL(AD_ERR_LENGTH_MISMATCH, "state buffer too small");
+    AD_HIP(hipStreamSynchronize(h->stream));
+    // device layout: per pass slab [C][ns][2]; return [C][nsec][2]
+    std::vector<double> raw((size_t)need);
+    if (need) AD_HIP(hipMemcpy(raw.data(), h->eq_state.p, need * sizeof(double), hipMemcpyDeviceToHost));
+    for (int s0 = 0; s0 < h->nsec; s0 += kMaxSecPerPass) {
+      const int ns = std::min(kMaxSecPerPass, h->nsec - s0);
+      for (int c = 0; c < h->channels; ++c)
+        for (int i = 0; i < ns; ++i)
+          for (int k = 0; k < 2; ++k)
+            state[((int64_t)c * h->nsec + s0 + i) * 2 + k] =
+                raw[(size_t)h->channels * s0 * 2 + ((size_t)c * ns + i) * 2 + k];
+    }
+  });
+}
+
+void ad_fx_chain_destroy(ad_fx_chain* h) {
+  if (!h) return;
+  (void)guard([&] {
+    DeviceScope ds(h->device);
+    delete h;
+  });
+}
+
+// biquad.Chain.ProcessBlock over `channels` independent chains that share one
+// coefficient set (chain.go:59-70); state [channels][sections][2] in/out.
+int ad_biquad_chain_process(const double* coeffs, double* state, double gain, double* buf, int channels,
+                            int sections, int64_t n, int device) {
+  ad_fx_chain* h = nullptr;
+  int rc = ad_fx_chain_create(channels, device, &h);
+  if (rc != AD_OK) return rc;
+  rc = guard([&] {
+    if (sections < 0 || (sections > 0 && (!coeffs || !state))) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "bad sections");
+    std::vector<double> tab((size_t)sections * kSecStride);
+    for (int s = 0; s < sections; ++s) {
+      tab[(size_t)s * kSecStride] = s == 0 ? gain : 1.0;
+      for (int k = 0; k < 5; ++k) tab[(size_t)s * kSecStride + 1 + k] = coeffs[s * 5 + k];
+    }
+    int r = ad_fx_chain_set_eq(h, tab.data(), sections, 0);
+    if (r != AD_OK) throw Status{r, ad_last_error()};
+    {
+      DeviceScope ds(h->device);
+      // load the caller's state into the pass slabs
+      std::vector<double> raw((size_t)channels * sections * 2);
+      for (int s0 = 0; s0 < sections; s0 += kMaxSecPerPass) {
+        const int ns = std::min(kMaxSecPerPass, sections - s0);
+        for (int c = 0; c < channels; ++c)
+          for (int i = 0; i < ns; ++i)
+            for (int k = 0; k < 2; ++k)
+              raw[(size_t)channels * s0 * 2 + ((size_t)c * ns + i) * 2 + k] =
+                  state[((int64_t)c * sections + s0 + i) * 2 + k];
+      }
+      if (!raw.empty())
+        AD_HIP(hipMemcpy(h->eq_state.p, raw.data(), raw.size() * sizeof(double), hipMemcpyHostToDevice));
+    }
+    r = ad_fx_chain_process(h, buf, n);
+    if (r != AD_OK) throw Status{r, ad_last_error()};
+    r = ad_fx_chain_eq_state(h, state, (int64_t)channels * sections * 2);
+    if (r != AD_OK) throw Status{r, ad_last_error()};
+  });
+  ad_fx_chain_destroy(h);
+  return rc;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// FIR
+// ---------------------------------------------------------------------------
+struct ad_fir {
+  int device = 0, channels = 0;
+  int64_t N = 0, cap = 0;
+  hipStream_t stream = nullptr;
+  DevBuf<double> h;     // [N]
+  DevBuf<double> xbuf;  // [C][N-1 + cap]
+  DevBuf<double> ybuf;  // [C][cap]
+  DevBuf<double> hbuf;  // [C][N-1] history staging (the shift may overlap)
+  ~ad_fir() {
+    if (stream) {
+      (void)hipStreamSynchronize(stream);
+      (void)hipStreamDestroy(stream);
+    }
+  }
+};
+
+namespace {
+
+void fir_reserve(ad_fir* f, int64_t n) {
+  if (n <= f->cap) return;
+  const int64_t hist = f->N - 1;
+  DevBuf<double> nx;
+  nx.alloc((size_t)f->channels * (hist + n));
+  if (hist > 0) {
+    if (f->cap > 0) {
+      AD_HIP(hipMemcpy2DAsync(nx.p, (hist + n) * sizeof(double), f->xbuf.p, (hist + f->cap) * sizeof(double),
+                              hist * sizeof(double), f->channels, hipMemcpyDeviceToDevice, f->stream));
+    } else {
+      AD_HIP(hipMemsetAsync(nx.p, 0, nx.n * sizeof(double), f->stream));
+    }
+  }
+  AD_HIP(hipStreamSynchronize(f->stream));
+  std::swap(f->xbuf.p, nx.p);
+  std::swap(f->xbuf.n, nx.n);
+  f->ybuf.alloc((size_t)f->channels * n);
+  f->cap = n;
+}
+
+// y = FIR(x) for n new samples per channel, device in/out; updates history.
+void fir_run(ad_fir* f, const double* d_src, int64_t src_stride, double* d_dst, int64_t dst_stride, int64_t n,
+             hipStream_t s) {
+  fir_reserve(f, n);
+  const int64_t hist = f->N - 1, xs = hist + f->cap;
+  AD_HIP(hipMemcpy2DAsync(f->xbuf.p + hist, xs * sizeof(double), d_src, src_stride * sizeof(double),
+                          n * sizeof(double), f->channels, hipMemcpyDeviceToDevice, s));
+  FirArgs a{};
+  a.h = f->h.p;
+  a.N = f->N;
+  a.x = f->xbuf.p;
+  a.xstride = xs;
+  a.y = f->ybuf.p;
+  a.ystride = f->cap;
+  a.n = n;
+  a.channels = f->channels;
+  a.reversed = f->N >= 32;
+  launch_fir(a, s);
+  AD_HIP(hipGetLastError());
+  AD_HIP(hipMemcpy2DAsync(d_dst, dst_stride * sizeof(double), f->ybuf.p, f->cap * sizeof(double),
+                          n * sizeof(double), f->channels, hipMemcpyDeviceToDevice, s));
+  if (hist > 0) {  // new history = last N-1 samples of [hist | block]
+    f->hbuf.reserve((size_t)f->channels * hist);
+    AD_HIP(hipMemcpy2DAsync(f->hbuf.p, hist * sizeof(double), f->xbuf.p + n, xs * sizeof(double),
+                            hist * sizeof(double), f->channels, hipMemcpyDeviceToDevice, s));
+    AD_HIP(hipMemcpy2DAsync(f->xbuf.p, xs * sizeof(double), f->hbuf.p, hist * sizeof(double),
+                            hist * sizeof(double), f->channels, hipMemcpyDeviceToDevice, s));
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int ad_fir_create(const double* coeffs, int64_t n_taps, int channels, int device, ad_fir** out) {
+  if (out) *out = nullptr;
+  ad_fir* raw = nullptr;
+  const int rc = guard([&] {
+    if (n_taps < 0 || (n_taps > 0 && !coeffs)) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "bad coefficients");
+    if (channels <= 0) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "channels must be positive");
+    const int dev = pick_device(device);
+    DeviceScope ds(dev);
+    std::unique_ptr<ad_fir> f(new ad_fir());
+    f->device = dev;
+    f->channels = channels;
+    f->N = n_taps;
+    AD_HIP(hipStreamCreateWithFlags(&f->stream, hipStreamNonBlocking));
+    if (n_taps > 0) {
+      f->h.alloc((size_t)n_taps);
+      AD_HIP(hipMemcpy(f->h.p, coeffs, n_taps * sizeof(double), hipMemcpyHostToDevice));
+    }
+    raw = f.release();
+  });
+  if (rc == AD_OK && out) *out = raw;
+  return rc;
+}
+
+int ad_fir_process_block_to(ad_fir* f, double* dst, const double* src, int64_t n) {
+  return guard([&] {
+    if (!f) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "null FIR handle");
+    if (n <= 0) return;
+    if (f->N == 0) {  // filter.go:75-77 / 120-122: no taps -> output untouched
+      return;
+    }
+    DeviceScope ds(f->device);
+    DevBuf<double> io;
+    io.alloc((size_t)f->channels * n);
+    AD_HIP(hipMemcpyAsync(io.p, src, io.n * sizeof(double), hipMemcpyHostToDevice, f->stream));
+    fir_run(f, io.p, n, io.p, n, n, f->stream);
+    AD_HIP(hipMemcpyAsync(dst, io.p, io.n * sizeof(double), hipMemcpyDeviceToHost, f->stream));
+    AD_HIP(hipStreamSynchronize(f->stream));
+  });
+}
+
+int ad_fir_process_block(ad_fir* f, double* buf, int64_t n) { return ad_fir_process_block_to(f, buf, buf, n); }
+
+int ad_fir_process_device(ad_fir* f, const double* d_src, int64_t src_stride, double* d_dst, int64_t dst_stride,
+                          int64_t n, void* stream) {
+  return guard([&] {
+    if (!f) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "null FIR handle");
+    if (n <= 0 || f->N == 0) return;
+    if (src_stride < n || dst_stride < n) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "bad strides");
+    DeviceScope ds(f->device);
+    fir_run(f, d_src, src_stride, d_dst, dst_stride, n, reinterpret_cast<hipStream_t>(stream));
+  });
+}
+
+int ad_fir_reset(ad_fir* f) {
+  return guard([&] {
+    if (!f) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "null FIR handle");
+    DeviceScope ds(f->device);
+    if (f->xbuf.p) AD_HIP(hipMemsetAsync(f->xbuf.p, 0, f->xbuf.n * sizeof(double), f->stream));
+    AD_HIP(hipStreamSynchronize(f->stream));
+  });
+}
+
+void ad_fir_destroy(ad_fir* f) {
+  if (!f) return;
+  (void)guard([&] {
+    DeviceScope ds(f->device);
+    delete f;
+  });
+}
+
+}  // extern "C"

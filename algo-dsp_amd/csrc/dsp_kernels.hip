@@ -1,0 +1,290 @@
+// Per-sample processors of the algo-dsp hot path, hand-written for gfx950:
+//   biquad.Chain / biquad.Section ProcessBlock   dsp/filter/biquad/chain.go:59-70, section.go:56-138
+//   dynamics.Compressor ProcessInPlace            dsp/effects/dynamics/compressor.go:348-366,
+//                                                  core.go:274-400
+//   reverb.Reverb (Freeverb) ProcessInPlace       dsp/effects/reverb/reverb.go:57-189
+//   effectchain filter -> dyn-compressor -> reverb-freeverb, fused per sample
+//                                                  dsp/effectchain/chain_process.go:11-33
+//   fir.Filter ProcessBlock / ProcessBlockTo      dsp/filter/fir/filter.go:46-159
+//
+// The recurrences are serial in time, so the parallel axis is the channel:
+// one lane per channel, state in VGPRs for the whole call, coefficients in
+// SGPRs when they are shared by all channels.  Fusing the chain's stages per
+// sample gives the same result bit for bit as the reference's stage-by-stage
+// block passes (each stage is causal and only sees its predecessor's output
+// of the same sample), and reads/writes each sample once instead of once per
+// stage.  `#pragma clang fp contract(off)`: the reference (amd64, no FMA
+// fusion) rounds every product and sum separately, and so do these kernels,
+// which makes the biquad, Freeverb and FIR (taps < 32) paths bit-exact.
+//
+// Freeverb delay lines are stored position-major, channel-minor
+// ([pos][Cpad]): all channels advance their ring indices in lockstep, so the
+// 12 delay-line reads and 12 writes per sample are 512-byte coalesced wave
+// accesses.  The reads of a chunk of D samples are issued together at the
+// chunk start (a line is rewritten only `size` >= 225 samples after it is
+// read, so a D <= 8 lookahead never reads a stale value).
+#include <hip/hip_runtime.h>
+
+#include "dsp_kernels.hpp"
+
+namespace adsp {
+
+namespace {
+
+constexpr int kCombLen[kVerbCombs] = {1116, 1188, 1277, 1356, 1422, 1491, 1557, 1617};  // reverb.go:12-19
+constexpr int kApLen[kVerbAllpass] = {556, 441, 341, 225};                             // reverb.go:21-24
+constexpr int kVerbD = 4;                                                              // samples per chunk
+
+__host__ __device__ constexpr int comb_off(int i) { return i == 0 ? 0 : comb_off(i - 1) + kCombLen[i - 1]; }
+__host__ __device__ constexpr int ap_off(int i) {
+  return i == 0 ? comb_off(kVerbCombs) : ap_off(i - 1) + kApLen[i - 1];
+}
+static_assert(ap_off(kVerbAllpass) == kVerbLen, "Freeverb delay-line layout");
+
+// Go math.Log2 (frexp split + Log(frac)*(1/Ln2) + exp), core.go via compressor_math.go:8-20.
+__device__ __forceinline__ double go_log2(double x) {
+#pragma clang fp contract(off)
+  int e;
+  const double frac = frexp(x, &e);
+  if (frac == 0.5) return (double)(e - 1);
+  return log(frac) * 1.4426950408889634074 + (double)e;
+}
+
+// dynamicsCore.GainForLevel (core.go:288-329)
+__device__ __forceinline__ double gain_for_level(const CompParams& p, double level) {
+#pragma clang fp contract(off)
+  if (level <= 0.0) return 1.0;
+  const double overshoot = go_log2(level) - p.threshold_log2;
+  if (!p.knee_on) {
+    if (overshoot <= 0.0) return 1.0;
+    return pow(2.0, -overshoot * p.cf);
+  }
+  double eff;
+  if (overshoot < -p.half_knee) return 1.0;
+  if (overshoot > p.half_knee) {
+    eff = overshoot;
+  } else {
+    const double s = overshoot + p.half_knee;
+    eff = s * s * 0.5 * p.inv_knee_width_log2;
+  }
+  return pow(2.0, -eff * p.cf);
+}
+
+// UNI: one section table for every channel, read from the kernel-argument
+// block (scalar loads, SGPR operands); otherwise per-channel tables in HBM.
+template <bool EQ, bool COMP, bool VERB, bool UNI>
+__global__ __launch_bounds__(64) void k_chain(ChainArgs a) {
+#pragma clang fp contract(off)
+  const int c = blockIdx.x * 64 + threadIdx.x;
+  const bool active = c < a.channels;
+  const int cc = active ? c : a.channels - 1;  // inactive lanes shadow the last channel, never store
+  double* xb = a.buf + (int64_t)cc * a.stride;
+
+  // --- EQ state / coefficients (up to kMaxSecPerPass sections per launch)
+  double d0[kMaxSecPerPass], d1[kMaxSecPerPass];
+  const double* sec = a.eq.sec + (int64_t)cc * a.eq.sec_ch_stride;
+  if constexpr (EQ) {
+#pragma unroll
+    for (int s = 0; s < kMaxSecPerPass; ++s) {
+      d0[s] = s < a.eq.nsec ? a.eq.state[((int64_t)cc * a.eq.nsec + s) * 2] : 0.0;
+      d1[s] = s < a.eq.nsec ? a.eq.state[((int64_t)cc * a.eq.nsec + s) * 2 + 1] : 0.0;
+    }
+  }
+  // --- compressor state
+  CompChState cs{};
+  double* ring = nullptr;
+  if constexpr (COMP) {
+    cs = a.cs[cc];
+    ring = a.rms_ring + (int64_t)cc * a.cp.rms_n;
+  }
+  // --- Freeverb state
+  VerbChState vs{};
+  const int cpad = (a.channels + 63) / 64 * 64;
+  if constexpr (VERB) vs = a.vs[cc];
+
+  for (int64_t t0 = 0; t0 < a.n; t0 += kVerbD) {
+    const int nd = (int)min((int64_t)kVerbD, a.n - t0);
+    double x[kVerbD];
+#pragma unroll
+    for (int d = 0; d < kVerbD; ++d) x[d] = d < nd ? xb[t0 + d] : 0.0;
+    double dl[kVerbCombs + kVerbAllpass][kVerbD];
+    if constexpr (VERB) {
+#pragma unroll
+      for (int i = 0; i < kVerbCombs; ++i) {
+        int p = vs.comb_idx[i];
+#pragma unroll
+        for (int d = 0; d < kVerbD; ++d) {
+          dl[i][d] = a.vbuf[(int64_t)(comb_off(i) + p) * cpad + c];
+          if (++p >= kCombLen[i]) p = 0;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < kVerbAllpass; ++i) {
+        int p = vs.ap_idx[i];
+#pragma unroll
+        for (int d = 0; d < kVerbD; ++d) {
+          dl[kVerbCombs + i][d] = a.vbuf[(int64_t)(ap_off(i) + p) * cpad + c];
+          if (++p >= kApLen[i]) p = 0;
+        }
+      }
+    }
+#pragma unroll
+    for (int d = 0; d < kVerbD; ++d) {
+      if (d >= nd) break;
+      double v = x[d];
+      if constexpr (EQ) {
+#pragma unroll
+        for (int s = 0; s < kMaxSecPerPass; ++s) {
+          if (s >= a.eq.nsec) break;
+          const double* q = UNI ? a.eq.u[s] : sec + s * kSecStride;
+          v = v * q[0];                                   // chain gain (1.0 is exact)
+          const double y = q[1] * v + d0[s];              // section.go:47-53
+          d0[s] = q[2] * v - q[4] * y + d1[s];
+          d1[s] = q[3] * v - q[5] * y;
+          v = y;
+        }
+      }
+      if constexpr (COMP) {  // Compressor.ProcessSample (compressor.go:348-359, core.go:274-286)
+        const CompParams& p = a.cp;
+        double src;
+        if (p.topology_fb) {
+          src = cs.prev_abs;
+        } else {
+          double s = v;  // applyPrefilter core.go:390-400
+          if (p.lp_on) {
+            cs.lp += p.lp_alpha * (s - cs.lp);
+            s = cs.lp;
+          }
+          if (p.hp_on) {
+            cs.hp += p.hp_alpha * (s - cs.hp);
+            s = s - cs.hp;
+          }
+          src = fabs(s);
+        }
+        if (p.detector_rms) {  // updateRMS core.go:361-388
+          const double sq = src * src;
+          if (cs.rms_filled == p.rms_n)
+            cs.rms_sum -= ring[cs.rms_index];
+          else
+            cs.rms_filled++;
+          ring[cs.rms_index] = sq;
+          cs.rms_sum += sq;
+          if (++cs.rms_index >= p.rms_n) cs.rms_index = 0;
+          const double mean = cs.rms_sum / (double)p.rms_n;
+          src = mean <= 0.0 ? 0.0 : sqrt(mean);
+        }
+        if (src > cs.env)
+          cs.env += (src - cs.env) * p.attack;
+        else
+          cs.env = src + (cs.env - src) * p.release;
+        const double g = gain_for_level(p, cs.env);
+        const double out = v * g * p.makeup_lin;
+        if (p.topology_fb) {
+          cs.prev_gain = g > 1e-9 ? g : 1e-9;
+          cs.prev_abs = fabs(out);
+        }
+        const double il = fabs(v), ol = fabs(out);  // updateMetrics compressor.go:411-423
+        if (il > cs.in_peak) cs.in_peak = il;
+        if (ol > cs.out_peak) cs.out_peak = ol;
+        if (cs.gr == 1.0 || g < cs.gr) cs.gr = g;
+        v = out;
+      }
+      if constexpr (VERB) {  // Reverb.ProcessSample reverb.go:169-182
+        const VerbParams& p = a.vp;
+        const double in = v;
+        const double xg = p.gain * in;
+        double acc = 0.0;
+#pragma unroll
+        for (int i = 0; i < kVerbCombs; ++i) {  // comb.process reverb.go:101-117
+          const double output = dl[i][d];
+          double fs = output * p.damp_b + vs.filter_store[i] * p.damp_a;
+          if (fabs(fs) < 1e-23) fs = 0.0;
+          vs.filter_store[i] = fs;
+          if (active)
+            a.vbuf[(int64_t)(comb_off(i) + vs.comb_idx[i]) * cpad + c] = xg + fs * p.feedback;
+          if (++vs.comb_idx[i] >= kCombLen[i]) vs.comb_idx[i] = 0;
+          acc += output;
+        }
+#pragma unroll
+        for (int i = 0; i < kVerbAllpass; ++i) {  // allpass.process reverb.go:57-68
+          const double bo = dl[kVerbCombs + i][d];
+          const double output = bo - acc;
+          if (active) a.vbuf[(int64_t)(ap_off(i) + vs.ap_idx[i]) * cpad + c] = acc + bo * p.ap_feedback;
+          if (++vs.ap_idx[i] >= kApLen[i]) vs.ap_idx[i] = 0;
+          acc = output;
+        }
+        v = acc * p.wet + in * p.dry;
+      }
+      x[d] = v;
+    }
+    if (active) {
+#pragma unroll
+      for (int d = 0; d < kVerbD; ++d)
+        if (d < nd) xb[t0 + d] = x[d];
+    }
+  }
+
+  if (!active) return;
+  if constexpr (EQ) {
+#pragma unroll
+    for (int s = 0; s < kMaxSecPerPass; ++s) {
+      if (s >= a.eq.nsec) break;
+      a.eq.state[((int64_t)c * a.eq.nsec + s) * 2] = d0[s];
+      a.eq.state[((int64_t)c * a.eq.nsec + s) * 2 + 1] = d1[s];
+    }
+  }
+  if constexpr (COMP) a.cs[c] = cs;
+  if constexpr (VERB) a.vs[c] = vs;
+}
+
+// fir.Filter block paths (filter.go:64-104 / 109-149).  Output-parallel: one
+// lane per output sample, summing in the reference's term order.
+__global__ __launch_bounds__(256) void k_fir(FirArgs a) {
+#pragma clang fp contract(off)
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int c = blockIdx.y;
+  if (i >= a.n) return;
+  const double* xc = a.x + (int64_t)c * a.xstride + (a.N - 1) + i;  // xc[0] = x[i], xc[-k] = x[i-k]
+  double acc = 0.0;
+  if (a.reversed) {
+    // dot(coeffs, linear[pos+1 .. pos+N]): h[j] pairs with x[i - (N-1) + j]
+    const double* xs = xc - (a.N - 1);
+    for (int64_t j = 0; j < a.N; ++j) acc += a.h[j] * xs[j];
+  } else {
+    // ProcessSample: y += coeffs[k] * delay[pos - k] (filter.go:46-69)
+    for (int64_t k = 0; k < a.N; ++k) acc += a.h[k] * xc[-k];
+  }
+  a.y[(int64_t)c * a.ystride + i] = acc;
+}
+
+}  // namespace
+
+template <bool EQ, bool COMP, bool VERB>
+static void chain_go(const ChainArgs& a, hipStream_t s) {
+  const dim3 grid((unsigned)((a.channels + 63) / 64)), block(64);
+  if (EQ && a.eq.uniform)
+    hipLaunchKernelGGL((k_chain<EQ, COMP, VERB, true>), grid, block, 0, s, a);
+  else
+    hipLaunchKernelGGL((k_chain<EQ, COMP, VERB, false>), grid, block, 0, s, a);
+}
+
+void launch_chain(int stages, const ChainArgs& a, hipStream_t s) {
+  if (a.channels <= 0 || a.n <= 0) return;
+  switch (stages) {
+    case 1: chain_go<true, false, false>(a, s); break;
+    case 2: chain_go<false, true, false>(a, s); break;
+    case 3: chain_go<true, true, false>(a, s); break;
+    case 4: chain_go<false, false, true>(a, s); break;
+    case 5: chain_go<true, false, true>(a, s); break;
+    case 6: chain_go<false, true, true>(a, s); break;
+    case 7: chain_go<true, true, true>(a, s); break;
+    default: break;
+  }
+}
+
+void launch_fir(const FirArgs& a, hipStream_t s) {
+  if (a.channels <= 0 || a.n <= 0) return;
+  hipLaunchKernelGGL(k_fir, dim3((unsigned)((a.n + 255) / 256), (unsigned)a.channels), dim3(256), 0, s, a);
+}
+
+}  // namespace adsp

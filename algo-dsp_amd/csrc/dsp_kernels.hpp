@@ -1,0 +1,85 @@
+// Device-side argument blocks of the per-sample processors (biquad chains,
+// compressor, Freeverb, their fused chain) and of the FIR block filter.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace adsp {
+
+// Biquad sections as they run per sample: x *= pre_gain; DF-II-T section.
+// A biquad.Chain with gain g becomes pre_gain = g on its first section and 1
+// on the others (x * 1.0 == x exactly, so the reference's `gain != 1` skip,
+// chain.go:59-64, is reproduced bit for bit).
+constexpr int kSecStride = 6;  // {pre_gain, b0, b1, b2, a1, a2}
+constexpr int kMaxSecPerPass = 8;
+
+struct EqArgs {
+  const double* sec;  // [channels][nsec][6] (per-channel tables)
+  int64_t sec_ch_stride;
+  double* state;  // [channels][nsec][2]  {d0, d1}
+  int nsec;       // <= kMaxSecPerPass in one launch
+  int uniform;    // 1: every channel uses u[][] (passed by value, SGPR operands)
+  double u[kMaxSecPerPass][kSecStride];
+};
+
+// dynamicsCore parameters, precomputed on the host exactly as
+// recalculateDetectorCoefficients / recalculateGainComputer do
+// (dsp/effects/dynamics/core.go:480-540).
+struct CompParams {
+  double threshold_log2, knee_width_log2, inv_knee_width_log2, half_knee;
+  double cf;  // 1 - 1/ratio, or ratio - 1 (feedback topology with ratio scaling)
+  double makeup_lin;
+  double attack, release;  // already the feedback pair when that topology is scaled
+  double lp_alpha, hp_alpha;
+  int knee_on, topology_fb, detector_rms, lp_on, hp_on, rms_n;
+};
+
+struct CompChState {
+  double env, lp, hp, rms_sum, prev_abs, prev_gain, in_peak, out_peak, gr;
+  int rms_index, rms_filled;
+};
+
+// reverb.Reverb (Freeverb) parameters and per-channel state.
+constexpr int kVerbCombs = 8, kVerbAllpass = 4;
+constexpr int kVerbLen = 1116 + 1188 + 1277 + 1356 + 1422 + 1491 + 1557 + 1617 + 556 + 441 + 341 + 225;  // 12587
+struct VerbParams {
+  double wet, dry, gain, feedback, damp_a, damp_b, ap_feedback;
+};
+struct VerbChState {
+  double filter_store[kVerbCombs];
+  int comb_idx[kVerbCombs];
+  int ap_idx[kVerbAllpass];
+};
+
+struct ChainArgs {
+  double* buf;  // [channels][stride], n samples processed in place
+  int64_t stride, n;
+  int channels;
+  EqArgs eq;
+  CompParams cp;
+  CompChState* cs;  // [channels]
+  double* rms_ring;  // [channels][rms_n]
+  VerbParams vp;
+  VerbChState* vs;  // [channels]
+  double* vbuf;     // [channels][kVerbLen]
+};
+
+// stages: bit 0 EQ, bit 1 compressor, bit 2 Freeverb
+void launch_chain(int stages, const ChainArgs& a, hipStream_t s);
+
+// FIR block filter over [hist (N-1) | block (n)] per channel.
+struct FirArgs {
+  const double* h;  // [N]
+  int64_t N;
+  const double* x;  // [channels][xstride]: N-1 history samples then n new ones
+  int64_t xstride;
+  double* y;  // [channels][ystride]
+  int64_t ystride, n;
+  int channels;
+  int reversed;  // taps >= 32: y[i] = sum_j h[j] x[i-N+1+j]; else sum_k h[k] x[i-k]
+};
+void launch_fir(const FirArgs& a, hipStream_t s);
+
+}  // namespace adsp

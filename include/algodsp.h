@@ -143,6 +143,76 @@ int ad_conv_profile_read(ad_conv* h, double* total_ms, int64_t* launches, double
 int ad_conv_mixdown_device(const double* d_chan, int channels, int64_t stride, int64_t len, double* d_mix,
                            void* stream);
 
+/* ======================================================================== */
+/* dsp/filter, dsp/effects: per-sample processors                           */
+/* ======================================================================== */
+
+/* ---- effect chain: biquad EQ -> Compressor -> Freeverb, per channel ------
+ * One handle runs `channels` independent instances of the reference
+ * processors, each stage optional, fused per sample on the GPU (bit-exact
+ * with running the stages block by block, as effectchain.Chain.Process does,
+ * chain_process.go:11-33).  Buffers are [channels][n] (host) or
+ * [channels][stride] (device), processed in place.
+ *
+ * EQ stage = biquad.Chain(s) (chain.go:6-138, section.go:26-155): a table of
+ * sections {pre_gain, b0, b1, b2, a1, a2}; pre_gain is the Chain gain on a
+ * chain's first section (1.0 otherwise).  per_channel = 0: one table [nsec][6]
+ * for all channels; 1: [channels][nsec][6].  Replaces Chain.ProcessBlock and,
+ * with one section, Section.ProcessBlock (the avx2/generic registry kernels,
+ * registry.go:10-100, compute the same DF-II-T recurrence).
+ * Compressor stage = dynamics.Compressor ProcessInPlace (compressor.go:362-366)
+ * configured by an ad_compressor_config struct, mirroring the setters
+ * (compressor.go:130-305).
+ * Freeverb stage = reverb.Reverb ProcessInPlace (reverb.go:185-189) with
+ * SetWet/SetDry/SetRoomSize/SetDamp/SetGain values (reverb.go:192-220).     */
+typedef struct ad_fx_chain ad_fx_chain;
+typedef struct ad_compressor_config {
+  double sample_rate, threshold_db, ratio, knee_db, attack_ms, release_ms, rms_window_ms, makeup_db;
+  double sidechain_low_cut_hz, sidechain_high_cut_hz; /* <= 0: off */
+  int topology;             /* 0 feed-forward, 1 feedback */
+  int detector_mode;        /* 0 peak, 1 RMS */
+  int feedback_ratio_scale; /* 1: feedback topology scales time constants and ratio */
+  int auto_makeup;          /* 1: makeup = -threshold*(1-1/ratio) */
+} ad_compressor_config;
+/* NewCompressor(sampleRate) defaults (compressor.go:77-127). */
+void ad_compressor_default_config(ad_compressor_config* cfg, double sample_rate);
+
+int ad_fx_chain_create(int channels, int device, ad_fx_chain** out);
+int ad_fx_chain_set_eq(ad_fx_chain* h, const double* sections, int nsec, int per_channel);
+int ad_fx_chain_set_compressor(ad_fx_chain* h, const ad_compressor_config* cfg); /* NULL: stage off */
+int ad_fx_chain_set_freeverb(ad_fx_chain* h, double wet, double dry, double room_size, double damp, double gain);
+int ad_fx_chain_disable_freeverb(ad_fx_chain* h);
+int ad_fx_chain_reset(ad_fx_chain* h); /* Chain/Compressor/Reverb Reset() */
+int ad_fx_chain_process(ad_fx_chain* h, double* buf, int64_t n);
+int ad_fx_chain_process_device(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, void* stream);
+/* Compressor metrics of one channel (updateMetrics compressor.go:411-423):
+ * input peak, output peak, minimum gain (gain reduction, linear). */
+int ad_fx_chain_compressor_metrics(ad_fx_chain* h, int channel, double* input_peak, double* output_peak,
+                                   double* gain_reduction);
+/* EQ section state [channels][nsec][2] {d0, d1} (Chain.State, chain.go:122-130). */
+int ad_fx_chain_eq_state(ad_fx_chain* h, double* state, int64_t cap);
+void ad_fx_chain_destroy(ad_fx_chain* h);
+
+/* One-shot biquad.Chain.ProcessBlock over `channels` chains sharing one
+ * coefficient set coeffs [sections][5] {b0,b1,b2,a1,a2} and gain (chain.go:59-70);
+ * state [channels][sections][2] is read and updated; buf [channels][n]. */
+int ad_biquad_chain_process(const double* coeffs, double* state, double gain, double* buf, int channels,
+                            int sections, int64_t n, int device);
+
+/* ---- fir.Filter (dsp/filter/fir/filter.go:11-172) -------------------------
+ * New(coeffs) for `channels` independent filters sharing the taps.
+ * taps < 32: y[n] = sum_k h[k] x[n-k] (ProcessSample order, :46-69);
+ * taps >= 32: the block path's reversed pairing y[n] = sum_j h[j] x[n-N+1+j]
+ * (linear-buffer dot product, :74-159).  n == 0 taps: output untouched.     */
+typedef struct ad_fir ad_fir;
+int ad_fir_create(const double* coeffs, int64_t n_taps, int channels, int device, ad_fir** out);
+int ad_fir_process_block(ad_fir* f, double* buf, int64_t n);                        /* :74-114 */
+int ad_fir_process_block_to(ad_fir* f, double* dst, const double* src, int64_t n);  /* :119-159 */
+int ad_fir_process_device(ad_fir* f, const double* d_src, int64_t src_stride, double* d_dst, int64_t dst_stride,
+                          int64_t n, void* stream);
+int ad_fir_reset(ad_fir* f); /* :162-172 */
+void ad_fir_destroy(ad_fir* f);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,249 @@
+"""GPU parity of the per-sample processors and the FIR filter through the HIP
+C ABI against the CPU oracle.
+
+Tolerances (BASELINE.json north_star / SURVEY 8(d) parity gates):
+  * biquad chains, Freeverb, FIR with < 32 taps: bit-exact (same operation
+    order, no FMA contraction on either side);
+  * FIR with >= 32 taps: <= 1e-12 RMS (the reference's vecmath.DotProduct
+    summation order is unpinned; both sides sum sequentially, so in practice
+    this is exact too);
+  * Compressor and the fused effect chain: <= 1e-12 RMS (log2/pow come from
+    the GPU's math library vs the host libm: a last-ulp difference in the
+    gain, never more).
+"""
+import json
+import pathlib
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+from algodsp import design, processors as P, signals
+
+pytestmark = pytest.mark.gpu
+
+KATS = json.loads((pathlib.Path(__file__).parent / "golden" / "reference_kats.json").read_text())
+RMS_TOL = 1e-12
+
+
+def rms(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    assert a.shape == b.shape
+    return float(np.sqrt(np.mean((a - b) ** 2))) if a.size else 0.0
+
+
+def stable_sections(k, seed):
+    """k stable biquads (poles inside the unit circle) from a seeded RNG."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(k):
+        r, th = rng.uniform(0.2, 0.97), rng.uniform(0.05, 3.0)
+        a1, a2 = -2 * r * np.cos(th), r * r
+        b = rng.uniform(-1, 1, 3)
+        out.append([b[0], b[1], b[2], a1, a2])
+    return np.array(out)
+
+
+def legacy_signal(n=4096, fs=48000.0):
+    """makeLegacyParitySignal (dsp/effects/dynamics/legacy_parity_test.go:8-40):
+    440 Hz at 0.08 / 0.7 / 0.2, then 880 Hz at 0.9, in four equal segments."""
+    k = np.arange(n, dtype=np.float64)
+    q = n // 4
+    amp = np.where(k < q, 0.08, np.where(k < 2 * q, 0.7, np.where(k < 3 * q, 0.2, 0.9)))
+    f = np.where(k < 3 * q, 440.0, 880.0)
+    return amp * np.sin(2 * np.pi * f * k / fs)
+
+
+# ------------------------------------------------------------------ biquad
+def test_biquad_section_kat(gpu):
+    case = KATS["biquad_dfiit_impulse"]
+    x = np.array(case["input"], dtype=np.float64)
+    s = P.Section(*case["coeffs"])
+    s.ProcessBlock(x)
+    np.testing.assert_allclose(x, case["expected"], atol=case["tol"], rtol=0)
+
+
+def test_biquad_avx2_vector_bit_exact(gpu):
+    case = KATS["biquad_avx2_vector"]
+    x = np.array(case["input"], dtype=np.float64)
+    want, _ = O.biquad_block(case["coeffs"], [0.0, 0.0], x)
+    per_sample = []
+    st = np.zeros(2)
+    for v in x:  # register_test.go: block kernel == ProcessSample loop
+        y, st = O.biquad_sample(case["coeffs"], st, v)
+        per_sample.append(y)
+    s = P.Section(*case["coeffs"])
+    s.ProcessBlock(x)
+    assert np.array_equal(x, want)
+    np.testing.assert_allclose(x, per_sample, atol=case["tol"], rtol=0)
+
+
+@pytest.mark.parametrize("sections,gain", [(1, 1.0), (5, 1.0), (3, 0.5), (8, 1.0), (11, 1.7)])
+def test_chain_bit_exact_multichannel(gpu, sections, gain):
+    coeffs = stable_sections(sections, 10 + sections)
+    C, n = 70, 5003  # two workgroups, ragged last one
+    x = np.stack([signals.white_noise(n, 300 + c) for c in range(C)])
+    gpu_ch = P.Chain(coeffs, gain, channels=C)
+    y = x.copy()
+    gpu_ch.ProcessBlock(np.zeros((C, 0)))  # empty block: no-op
+    a, b = y[:, :2000].copy(), y[:, 2000:].copy()  # state carried across blocks
+    gpu_ch.ProcessBlock(a)
+    gpu_ch.ProcessBlock(b)
+    got = np.concatenate([a, b], axis=1)
+    for c in (0, 33, 69):
+        want, st = O.biquad_chain_block(coeffs.ravel(), np.zeros(2 * sections), gain, x[c])
+        assert np.array_equal(got[c], want), (c, float(np.max(np.abs(got[c] - want))))
+        np.testing.assert_array_equal(gpu_ch.State()[c].ravel(), st)
+
+
+def test_chain_one_shot_state_io(gpu):
+    coeffs = stable_sections(4, 3)
+    x = np.stack([signals.white_noise(777, 9), signals.white_noise(777, 10)])
+    state = np.zeros((2, 4, 2))
+    y1, y2 = x[:, :300].copy(), x[:, 300:].copy()
+    P.chain_process(coeffs, state, 0.8, y1)
+    P.chain_process(coeffs, state, 0.8, y2)
+    got = np.concatenate([y1, y2], axis=1)
+    for c in range(2):
+        want, st = O.biquad_chain_block(coeffs.ravel(), np.zeros(8), 0.8, x[c])
+        assert np.array_equal(got[c], want)
+        np.testing.assert_array_equal(state[c].ravel(), st)
+
+
+def test_chain_reset(gpu):
+    coeffs = stable_sections(2, 5)
+    ch = P.Chain(coeffs)
+    x = signals.white_noise(100, 1)
+    a = x.copy()
+    ch.ProcessBlock(a)
+    ch.Reset()
+    b = x.copy()
+    ch.ProcessBlock(b)
+    assert np.array_equal(a, b)
+
+
+# ------------------------------------------------------------------ compressor
+@pytest.mark.parametrize("cfg", [
+    {},
+    {"knee_db": 0.0},
+    {"detector_mode": 1, "rms_window_ms": 5.0},
+    {"topology": 1},
+    {"topology": 1, "feedback_ratio_scale": 0},
+    {"sidechain_low_cut_hz": 80.0, "sidechain_high_cut_hz": 6000.0},
+    {"auto_makeup": 0, "makeup_db": 6.0, "ratio": 10.0, "threshold_db": -30.0},
+], ids=lambda c: ",".join(f"{k}={v}" for k, v in c.items()) or "defaults")
+def test_compressor_vs_oracle(gpu, cfg):
+    C = 3
+    n = 4096
+    sig = [legacy_signal(n), 0.5 * signals.white_noise(n, 77), legacy_signal(n) * 0.3]
+    x = np.stack(sig)
+    comp = P.Compressor(48000.0, channels=C, **cfg)
+    y = x.copy()
+    a, b = y[:, :1500].copy(), y[:, 1500:].copy()
+    comp.ProcessInPlace(a)
+    comp.ProcessInPlace(b)
+    got = np.concatenate([a, b], axis=1)
+    for c in range(C):
+        oc = O.Compressor(48000.0, **cfg)
+        want = oc.process_in_place(x[c])
+        assert rms(got[c], want) <= RMS_TOL, rms(got[c], want)
+        assert float(np.max(np.abs(got[c] - want))) < 1e-12
+        gm, om = np.array(comp.Metrics(c)), np.array(oc.metrics())
+        np.testing.assert_allclose(gm, om, rtol=1e-13, atol=0)
+
+
+# ------------------------------------------------------------------ Freeverb
+def test_freeverb_bit_exact(gpu):
+    C, n = 65, 6000
+    x = np.stack([np.sin(2 * np.pi * np.arange(n) / 23) * (1 + 0.01 * c) for c in range(C)])
+    x[5] = signals.white_noise(n, 5)
+    rv = P.Reverb(channels=C)
+    y = x.copy()
+    a, b = y[:, :2345].copy(), y[:, 2345:].copy()
+    rv.ProcessInPlace(a)
+    rv.ProcessInPlace(b)
+    got = np.concatenate([a, b], axis=1)
+    for c in (0, 5, 64):
+        want = O.Freeverb().process_in_place(x[c])
+        assert np.array_equal(got[c], want), (c, float(np.max(np.abs(got[c] - want))))
+
+
+def test_freeverb_params(gpu):
+    rv = P.Reverb()
+    rv.SetWet(0.5)
+    rv.SetRoomSize(0.9)
+    rv.SetDamp(0.2)
+    rv.SetDry(0.3)
+    rv.SetGain(0.02)
+    x = signals.white_noise(3000, 8)
+    y = x.copy()
+    rv.ProcessInPlace(y)
+    o = O.Freeverb()
+    o.set(0.5, 0.3, 0.9, 0.2, 0.02)
+    assert np.array_equal(y, o.process_in_place(x))
+
+
+# ------------------------------------------------------------------ effect chain (config 5)
+def test_effect_chain_config5(gpu):
+    fs = 48000.0
+    eq = design.config5_eq(fs)
+    comp_cfg = {"auto_makeup": 0, "makeup_db": 0.0}
+    verb = (0.22, 1.0, 0.72, 0.45, 0.015)
+    C, n = 9, 8192
+    x = np.stack([0.5 * signals.white_noise(n, 0x5EED + c) for c in range(C)])
+    fx = P.EffectChain(C, eq, comp_cfg, verb, fs)
+    y = x.copy()
+    fx.Process(y)
+    for c in (0, 4, 8):
+        v = x[c].copy()
+        for co, g in eq:
+            v, _ = O.biquad_chain_block(np.ravel(co), np.zeros(2 * len(co)), g, v)
+        v = O.Compressor(fs, **comp_cfg).process_in_place(v)
+        o = O.Freeverb()
+        o.set(*verb)
+        v = o.process_in_place(v)
+        assert rms(y[c], v) <= RMS_TOL, rms(y[c], v)
+
+
+# ------------------------------------------------------------------ FIR
+@pytest.mark.parametrize("taps", [1, 5, 31, 32, 64, 257])
+def test_fir_vs_oracle(gpu, taps):
+    h = signals.make_test_kernel(taps)
+    C = 3
+    n = 2500
+    x = np.stack([signals.white_noise(n, 40 + c) for c in range(C)])
+    f = P.Filter(h, channels=C)
+    parts = []
+    for lo, hi in [(0, 7), (7, 1200), (1200, 2500)]:  # blocks shorter and longer than the taps
+        blk = x[:, lo:hi].copy()
+        f.ProcessBlock(blk)
+        parts.append(blk)
+    got = np.concatenate(parts, axis=1)
+    for c in range(C):
+        of = O.Fir(h)
+        want = np.concatenate([of.process_block(x[c, lo:hi]) for lo, hi in [(0, 7), (7, 1200), (1200, 2500)]])
+        if taps < 32:
+            assert np.array_equal(got[c], want)
+        else:
+            assert rms(got[c], want) <= RMS_TOL
+
+
+def test_fir_block_to_and_reset(gpu):
+    h = signals.make_test_kernel(40)
+    x = signals.white_noise(500, 3)
+    f = P.Filter(h)
+    dst = np.zeros_like(x)
+    f.ProcessBlockTo(dst, x)
+    f.Reset()
+    y = x.copy()
+    f.ProcessBlock(y)
+    assert np.array_equal(dst, y)
+    case = KATS["fir_block_vs_sample"]  # filter_test.go:91-134: block == per-sample
+    g = P.Filter(case["coeffs"])
+    vals = [g.ProcessSample(v) for v in case["input"]]
+    of = O.Fir(case["coeffs"])
+    want = [of.process_sample(v) for v in case["input"]]
+    blk = np.array(case["input"], dtype=np.float64)
+    P.Filter(case["coeffs"]).ProcessBlock(blk)
+    np.testing.assert_allclose(vals, want, atol=case["tol"], rtol=0)
+    np.testing.assert_allclose(blk, want, atol=case["tol"], rtol=0)
