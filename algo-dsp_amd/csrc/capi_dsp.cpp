@@ -75,8 +75,7 @@ struct ad_fx_chain {
   // EQ
   int nsec = 0;
   bool eq_uniform = true;
-  std::vector<double> sec_host;  // uniform: [nsec][6]
-  DevBuf<double> sec_dev;        // per-channel: [C][nsec][6]
+  DevBuf<double> sec_dev;  // uniform: [nsec][6]; per-channel: [C][nsec][6]
   DevBuf<double> eq_state;       // [C][nsec][2]
   // compressor
   bool comp_on = false;
@@ -138,16 +137,8 @@ void fx_run(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hipStream_
   do {
     const int ns = std::min(kMaxSecPerPass, h->nsec - s0);
     a.eq.nsec = ns;
-    a.eq.uniform = h->eq_uniform ? 1 : 0;
-    if (h->eq_uniform) {
-      for (int i = 0; i < ns; ++i)
-        for (int k = 0; k < kSecStride; ++k) a.eq.u[i][k] = h->sec_host[(size_t)(s0 + i) * kSecStride + k];
-      a.eq.sec = nullptr;
-      a.eq.sec_ch_stride = 0;
-    } else {
-      a.eq.sec = h->sec_dev.p + (int64_t)s0 * kSecStride;
-      a.eq.sec_ch_stride = (int64_t)h->nsec * kSecStride;
-    }
+    a.eq.sec = h->sec_dev.p ? h->sec_dev.p + (int64_t)s0 * kSecStride : nullptr;
+    a.eq.sec_ch_stride = h->eq_uniform ? 0 : (int64_t)h->nsec * kSecStride;
     // state rows of this pass: the kernel indexes [c][ns][2]; keep one
     // contiguous [C][nsec][2] array by giving each pass its own slab
     a.eq.state = h->eq_state.p + (int64_t)h->channels * s0 * 2;
@@ -213,14 +204,8 @@ int ad_fx_chain_set_eq(ad_fx_chain* h, const double* sections, int nsec, int per
     const bool keep_state = nsec == h->nsec;
     h->nsec = nsec;
     h->eq_uniform = !per_channel;
-    if (per_channel) {
-      h->sec_dev.alloc((size_t)h->channels * nsec * kSecStride);
-      if (nsec > 0)
-        AD_HIP(hipMemcpy(h->sec_dev.p, sections, h->sec_dev.n * sizeof(double), hipMemcpyHostToDevice));
-      h->sec_host.clear();
-    } else {
-      h->sec_host.assign(sections, sections + (size_t)nsec * kSecStride);
-    }
+    h->sec_dev.alloc((size_t)(per_channel ? h->channels : 1) * nsec * kSecStride);
+    if (nsec > 0) AD_HIP(hipMemcpy(h->sec_dev.p, sections, h->sec_dev.n * sizeof(double), hipMemcpyHostToDevice));
     // Section state survives a coefficient update with the same section
     // count, like filterRuntime.Configure (runtime_filter_pitch_reverb.go:150-165).
     if (!keep_state || !h->eq_state.p) {

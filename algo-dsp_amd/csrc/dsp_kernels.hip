@@ -8,8 +8,7 @@
 //   fir.Filter ProcessBlock / ProcessBlockTo      dsp/filter/fir/filter.go:46-159
 //
 // The recurrences are serial in time, so the parallel axis is the channel:
-// one lane per channel, state in VGPRs for the whole call, coefficients in
-// SGPRs when they are shared by all channels.  Fusing the chain's stages per
+// one lane per channel, state and coefficients in VGPRs for the whole call.  Fusing the chain's stages per
 // sample gives the same result bit for bit as the reference's stage-by-stage
 // block passes (each stage is causal and only sees its predecessor's output
 // of the same sample), and reads/writes each sample once instead of once per
@@ -33,7 +32,7 @@ namespace {
 
 constexpr int kCombLen[kVerbCombs] = {1116, 1188, 1277, 1356, 1422, 1491, 1557, 1617};  // reverb.go:12-19
 constexpr int kApLen[kVerbAllpass] = {556, 441, 341, 225};                             // reverb.go:21-24
-constexpr int kVerbD = 4;                                                              // samples per chunk
+constexpr int kVerbD = 2;                                                              // samples per chunk
 
 __host__ __device__ constexpr int comb_off(int i) { return i == 0 ? 0 : comb_off(i - 1) + kCombLen[i - 1]; }
 __host__ __device__ constexpr int ap_off(int i) {
@@ -50,14 +49,15 @@ __device__ __forceinline__ double go_log2(double x) {
   return log(frac) * 1.4426950408889634074 + (double)e;
 }
 
-// dynamicsCore.GainForLevel (core.go:288-329)
+// dynamicsCore.GainForLevel (core.go:288-329).  2^y via exp2 (Go:
+// math.Pow(2, y); both within an ulp).
 __device__ __forceinline__ double gain_for_level(const CompParams& p, double level) {
 #pragma clang fp contract(off)
   if (level <= 0.0) return 1.0;
   const double overshoot = go_log2(level) - p.threshold_log2;
   if (!p.knee_on) {
     if (overshoot <= 0.0) return 1.0;
-    return pow(2.0, -overshoot * p.cf);
+    return exp2(-overshoot * p.cf);
   }
   double eff;
   if (overshoot < -p.half_knee) return 1.0;
@@ -67,12 +67,10 @@ __device__ __forceinline__ double gain_for_level(const CompParams& p, double lev
     const double s = overshoot + p.half_knee;
     eff = s * s * 0.5 * p.inv_knee_width_log2;
   }
-  return pow(2.0, -eff * p.cf);
+  return exp2(-eff * p.cf);
 }
 
-// UNI: one section table for every channel, read from the kernel-argument
-// block (scalar loads, SGPR operands); otherwise per-channel tables in HBM.
-template <bool EQ, bool COMP, bool VERB, bool UNI>
+template <bool EQ, bool COMP, bool VERB>
 __global__ __launch_bounds__(64) void k_chain(ChainArgs a) {
 #pragma clang fp contract(off)
   const int c = blockIdx.x * 64 + threadIdx.x;
@@ -80,14 +78,17 @@ __global__ __launch_bounds__(64) void k_chain(ChainArgs a) {
   const int cc = active ? c : a.channels - 1;  // inactive lanes shadow the last channel, never store
   double* xb = a.buf + (int64_t)cc * a.stride;
 
-  // --- EQ state / coefficients (up to kMaxSecPerPass sections per launch)
-  double d0[kMaxSecPerPass], d1[kMaxSecPerPass];
-  const double* sec = a.eq.sec + (int64_t)cc * a.eq.sec_ch_stride;
+  // --- EQ state / coefficients (up to kMaxSecPerPass sections per launch),
+  // held in VGPRs for the whole call (a shared table has channel stride 0)
+  double d0[kMaxSecPerPass], d1[kMaxSecPerPass], q[kMaxSecPerPass][kSecStride];
   if constexpr (EQ) {
+    const double* sec = a.eq.sec + (int64_t)cc * a.eq.sec_ch_stride;
 #pragma unroll
     for (int s = 0; s < kMaxSecPerPass; ++s) {
       d0[s] = s < a.eq.nsec ? a.eq.state[((int64_t)cc * a.eq.nsec + s) * 2] : 0.0;
       d1[s] = s < a.eq.nsec ? a.eq.state[((int64_t)cc * a.eq.nsec + s) * 2 + 1] : 0.0;
+#pragma unroll
+      for (int k = 0; k < kSecStride; ++k) q[s][k] = s < a.eq.nsec ? sec[s * kSecStride + k] : 0.0;
     }
   }
   // --- compressor state
@@ -102,16 +103,19 @@ __global__ __launch_bounds__(64) void k_chain(ChainArgs a) {
   const int cpad = (a.channels + 63) / 64 * 64;
   if constexpr (VERB) vs = a.vs[cc];
 
-  for (int64_t t0 = 0; t0 < a.n; t0 += kVerbD) {
-    const int nd = (int)min((int64_t)kVerbD, a.n - t0);
-    double x[kVerbD];
+  // Chunks of kVerbD samples, double-buffered: the input samples and the
+  // Freeverb delay-line values of chunk k+1 are loaded (branch-free, clamped)
+  // while chunk k computes.  Fixed ping-pong buffers (A/B) instead of a
+  // loop-carried copy keep the loads in flight across the chunk.
+  auto load_chunk = [&](double (&x)[kVerbD], double (&dl)[kVerbCombs + kVerbAllpass][kVerbD], int64_t t0,
+                        int ahead) {
 #pragma unroll
-    for (int d = 0; d < kVerbD; ++d) x[d] = d < nd ? xb[t0 + d] : 0.0;
-    double dl[kVerbCombs + kVerbAllpass][kVerbD];
+    for (int d = 0; d < kVerbD; ++d) x[d] = xb[min(t0 + d, a.n - 1)];
     if constexpr (VERB) {
 #pragma unroll
       for (int i = 0; i < kVerbCombs; ++i) {
-        int p = vs.comb_idx[i];
+        int p = vs.comb_idx[i] + ahead;
+        if (p >= kCombLen[i]) p -= kCombLen[i];
 #pragma unroll
         for (int d = 0; d < kVerbD; ++d) {
           dl[i][d] = a.vbuf[(int64_t)(comb_off(i) + p) * cpad + c];
@@ -120,7 +124,8 @@ __global__ __launch_bounds__(64) void k_chain(ChainArgs a) {
       }
 #pragma unroll
       for (int i = 0; i < kVerbAllpass; ++i) {
-        int p = vs.ap_idx[i];
+        int p = vs.ap_idx[i] + ahead;
+        if (p >= kApLen[i]) p -= kApLen[i];
 #pragma unroll
         for (int d = 0; d < kVerbD; ++d) {
           dl[kVerbCombs + i][d] = a.vbuf[(int64_t)(ap_off(i) + p) * cpad + c];
@@ -128,6 +133,9 @@ __global__ __launch_bounds__(64) void k_chain(ChainArgs a) {
         }
       }
     }
+  };
+  auto compute_chunk = [&](double (&x)[kVerbD], double (&dl)[kVerbCombs + kVerbAllpass][kVerbD], int64_t t0) {
+    const int nd = (int)min((int64_t)kVerbD, a.n - t0);
 #pragma unroll
     for (int d = 0; d < kVerbD; ++d) {
       if (d >= nd) break;
@@ -136,11 +144,10 @@ __global__ __launch_bounds__(64) void k_chain(ChainArgs a) {
 #pragma unroll
         for (int s = 0; s < kMaxSecPerPass; ++s) {
           if (s >= a.eq.nsec) break;
-          const double* q = UNI ? a.eq.u[s] : sec + s * kSecStride;
-          v = v * q[0];                                   // chain gain (1.0 is exact)
-          const double y = q[1] * v + d0[s];              // section.go:47-53
-          d0[s] = q[2] * v - q[4] * y + d1[s];
-          d1[s] = q[3] * v - q[5] * y;
+          v = v * q[s][0];                                // chain gain (1.0 is exact)
+          const double y = q[s][1] * v + d0[s];           // section.go:47-53
+          d0[s] = q[s][2] * v - q[s][4] * y + d1[s];
+          d1[s] = q[s][3] * v - q[s][5] * y;
           v = y;
         }
       }
@@ -222,6 +229,16 @@ __global__ __launch_bounds__(64) void k_chain(ChainArgs a) {
       for (int d = 0; d < kVerbD; ++d)
         if (d < nd) xb[t0 + d] = x[d];
     }
+    };
+  double xa[kVerbD], xbb[kVerbD];
+  double dla[kVerbCombs + kVerbAllpass][kVerbD], dlb[kVerbCombs + kVerbAllpass][kVerbD];
+  load_chunk(xa, dla, 0, 0);
+  for (int64_t t0 = 0; t0 < a.n; t0 += 2 * kVerbD) {
+    load_chunk(xbb, dlb, t0 + kVerbD, kVerbD);
+    compute_chunk(xa, dla, t0);
+    if (t0 + kVerbD >= a.n) break;
+    load_chunk(xa, dla, t0 + 2 * kVerbD, kVerbD);
+    compute_chunk(xbb, dlb, t0 + kVerbD);
   }
 
   if (!active) return;
@@ -261,11 +278,7 @@ __global__ __launch_bounds__(256) void k_fir(FirArgs a) {
 
 template <bool EQ, bool COMP, bool VERB>
 static void chain_go(const ChainArgs& a, hipStream_t s) {
-  const dim3 grid((unsigned)((a.channels + 63) / 64)), block(64);
-  if (EQ && a.eq.uniform)
-    hipLaunchKernelGGL((k_chain<EQ, COMP, VERB, true>), grid, block, 0, s, a);
-  else
-    hipLaunchKernelGGL((k_chain<EQ, COMP, VERB, false>), grid, block, 0, s, a);
+  hipLaunchKernelGGL((k_chain<EQ, COMP, VERB>), dim3((unsigned)((a.channels + 63) / 64)), dim3(64), 0, s, a);
 }
 
 void launch_chain(int stages, const ChainArgs& a, hipStream_t s) {

@@ -16,12 +16,10 @@ constexpr int kSecStride = 6;  // {pre_gain, b0, b1, b2, a1, a2}
 constexpr int kMaxSecPerPass = 8;
 
 struct EqArgs {
-  const double* sec;  // [channels][nsec][6] (per-channel tables)
-  int64_t sec_ch_stride;
-  double* state;  // [channels][nsec][2]  {d0, d1}
-  int nsec;       // <= kMaxSecPerPass in one launch
-  int uniform;    // 1: every channel uses u[][] (passed by value, SGPR operands)
-  double u[kMaxSecPerPass][kSecStride];
+  const double* sec;      // [channels][nsec][6]; a table shared by all channels has stride 0
+  int64_t sec_ch_stride;  // elements between channels' tables
+  double* state;          // [channels][nsec][2]  {d0, d1}
+  int nsec;               // <= kMaxSecPerPass in one launch
 };
 
 // dynamicsCore parameters, precomputed on the host exactly as

@@ -35,10 +35,14 @@ def parse():
     p.add_argument("--hop", type=int, default=8192)
     p.add_argument("--chunk", type=int, default=0, help="blocks per channel per engine chunk (0 = auto)")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-sample", type=int, default=1 << 24, help="samples of one channel for the CPU leg")
+    p.add_argument("--cpu-sample", type=int, default=1 << 25, help="samples of one channel for the CPU leg")
     p.add_argument("--mixdown", choices=["auto", "on", "off"], default="auto")
     p.add_argument("--kernel-timing", choices=["on", "off"], default="on",
                    help="HIP events around every engine kernel launch inside the timed region")
+    p.add_argument("--channels", type=int, default=2,
+                   help="conv: channels per GPU (IR[c %% 2]); 2 = the stereo config, 8 = config 4's shard")
+    p.add_argument("--workload", choices=["conv", "fx"], default="conv",
+                   help="conv: BASELINE metric (overlap-save conv); fx: config 5 effect chain (256 ch)")
     return p.parse_args()
 
 
@@ -70,6 +74,8 @@ def cpu_baseline(ir, sample_len):
 
 def main():
     args = parse()
+    if args.workload == "fx":
+        return main_fx(args)
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -89,19 +95,23 @@ def main():
     K = ir.shape[1]
     n = args.samples
     out_len = n + K - 1                             # full linear convolution (OverlapSave.Process)
-    x_host = np.stack([signals.white_noise(n, 0x5EED + 2 * rank + c) for c in range(2)])
+    C = args.channels
+    x_host = np.stack([signals.white_noise(n, 0x5EED + C * rank + c) for c in range(C)])
     x = torch.from_numpy(x_host).to(dev)
-    y = torch.empty((2, out_len), dtype=torch.float64, device=dev)
+    y = torch.empty((C, out_len), dtype=torch.float64, device=dev)
+    mix = y if C == 2 else torch.empty((2, out_len), dtype=torch.float64, device=dev)
     del x_host
 
-    eng = conv.MultiChannelConvolver(ir, hop=args.hop, channels=2, chunk_blocks=args.chunk, device=local)
+    eng = conv.MultiChannelConvolver(ir, hop=args.hop, channels=C, chunk_blocks=args.chunk, device=local)
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
 
     def step():
         eng.process_device(x.data_ptr(), n, n, y.data_ptr(), out_len, out_len, sptr)
         if mixdown:
-            dist.reduce(y, dst=0, op=dist.ReduceOp.SUM)
+            if C != 2:  # stereo partial mix of this rank's channel group (even -> L, odd -> R)
+                conv.mixdown_device(y.data_ptr(), C, out_len, out_len, mix.data_ptr(), sptr)
+            dist.reduce(mix, dst=0, op=dist.ReduceOp.SUM)
 
     for _ in range(args.warmup):
         step()
@@ -133,7 +143,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    total_samples = world * 2 * n * args.steps
+    total_samples = world * C * n * args.steps
     value = total_samples / elapsed / 1e6
 
     # dominant kernel + its roofline (algorithmic bytes / mean launch duration)
@@ -153,7 +163,9 @@ def main():
         tfile = ROOT / "profiles" / "pmc_traffic.json"
         if tfile.exists():
             try:
-                traffic = json.loads(tfile.read_text()).get(dom, {}).get("hbm_bytes_per_launch")
+                tab = json.loads(tfile.read_text())
+                key = next((k for k in tab if k == dom or k.startswith(dom)), None)
+                traffic = tab[key]["hbm_bytes_per_launch"] if key else None
             except Exception:
                 traffic = None
         line = {
@@ -171,9 +183,10 @@ def main():
             "data": "synthetic: SplitMix64 white noise (seed 0x5EED+channel) x Large Church IR from web/irs.irlib "
                     "(f16, reference decodeF16), zero padded 95432->131072 taps",
             "config": {
-                "workload": "OverlapSave partitioned conv, stereo, 131072-tap IR, full linear convolution "
-                            f"(2 ch x {n} samples per GPU per step)",
-                "channels_per_gpu": 2,
+                "workload": ("OverlapSave partitioned conv, stereo, 131072-tap IR, full linear convolution "
+                             if C == 2 else f"{C}-channel x 131072-tap IR convolution (IR[c mod 2]) ") +
+                            f"({C} ch x {n} samples per GPU per step)",
+                "channels_per_gpu": C,
                 "samples_per_channel": n,
                 "kernel_taps": K,
                 "hop": args.hop,
@@ -198,6 +211,93 @@ def main():
         }
         if cpu:
             line["speedup_vs_cpu"] = round(value / cpu["value"], 1)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def main_fx(args):
+    """BASELINE config 5: effectchain filter(x5 RBJ) -> dyn-compressor ->
+    reverb-freeverb on 256 channels x 2^20 samples, fused per sample (one
+    lane per channel), buffers resident in HBM.  Replicas only for N > 1."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from algodsp import design, processors, signals
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    fs = 48000.0
+    C = 256
+    n = args.samples if args.samples != (1 << 24) else (1 << 20)
+    eq = design.config5_eq(fs)
+    comp_cfg = {"auto_makeup": 0, "makeup_db": 0.0}  # runtime_dynamics.go:46-54
+    verb = (0.22, 1.0, 0.72, 0.45, 0.015)
+    fx = processors.EffectChain(C, eq, comp_cfg, verb, fs, device=local)
+    x = torch.from_numpy(np.stack([0.5 * signals.white_noise(n, 0x5EED + c) for c in range(C)])).to(dev)
+    sptr = torch.cuda.current_stream(dev).cuda_stream
+
+    def step():
+        fx.process_device(x.data_ptr(), n, n, sptr)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    value = world * C * n * args.steps / elapsed / 1e6
+    if rank == 0:
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            sys.path.insert(0, str(ROOT / "tests"))
+            import oracle_lib as O
+
+            m = 1 << 25
+            v = 0.5 * signals.white_noise(m, 0x5EED)
+            tc = time.perf_counter()
+            for co, g in eq:
+                v, _ = O.biquad_chain_block(np.ravel(co), np.zeros(2 * len(co)), g, v)
+            v = O.Compressor(fs, **comp_cfg).process_in_place(v)
+            o = O.Freeverb()
+            o.set(*verb)
+            o.process_in_place(v)
+            dt = time.perf_counter() - tc
+            cpu = {"value": m / dt / 1e6, "unit": "Msamples/s", "cores": 1, "kind": "port",
+                   "sample": f"1 channel x {m} samples, oracle biquad chains + Compressor + Freeverb; {dt:.2f} s"}
+        line = {
+            "metric": "Msamples/sec, effectchain biquad EQ + Compressor + Freeverb (config 5)",
+            "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic: 0.5 x SplitMix64 white noise, 48 kHz",
+            "config": {"workload": f"effectchain filter x5 (RBJ) -> dyn-compressor -> reverb-freeverb, {C} ch x "
+                                   f"{n} samples per GPU per step, fused per sample",
+                       "channels_per_gpu": C, "samples_per_channel": n,
+                       "parallelism": "replicas" if world > 1 else "single GPU"},
+            "roofline": {"bound": "hbm", "achieved": round(value * 16e6 / 1e9, 3), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(value * 16e6 / 1e9 / HBM_PEAK_GBS, 6), "traffic": None,
+                         "note": "16 B/sample in+out; serial per-channel recurrences: latency-bound, not HBM"},
+            "cpu_baseline": cpu,
+        }
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
