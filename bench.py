@@ -95,14 +95,20 @@ def main():
     K = ir.shape[1]
     n = args.samples
     out_len = n + K - 1                             # full linear convolution (OverlapSave.Process)
+    from algodsp import shard
+
     C = args.channels
-    x_host = np.stack([signals.white_noise(n, 0x5EED + C * rank + c) for c in range(C)])
+    if world > 1 and C % 2:
+        raise SystemExit("--channels must be even for the multi-GPU stereo mixdown")
+    ids = list(shard.channel_group(rank, world, C * world))  # this rank's global channel ids
+    x_host = np.stack([signals.white_noise(n, 0x5EED + c) for c in ids])
     x = torch.from_numpy(x_host).to(dev)
     y = torch.empty((C, out_len), dtype=torch.float64, device=dev)
     mix = y if C == 2 else torch.empty((2, out_len), dtype=torch.float64, device=dev)
     del x_host
 
-    eng = conv.MultiChannelConvolver(ir, hop=args.hop, channels=C, chunk_blocks=args.chunk, device=local)
+    eng = conv.MultiChannelConvolver(ir, hop=args.hop, channels=C, ir_index=shard.ir_index(ids),
+                                     chunk_blocks=args.chunk, device=local)
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
 
@@ -111,7 +117,7 @@ def main():
         if mixdown:
             if C != 2:  # stereo partial mix of this rank's channel group (even -> L, odd -> R)
                 conv.mixdown_device(y.data_ptr(), C, out_len, out_len, mix.data_ptr(), sptr)
-            dist.reduce(mix, dst=0, op=dist.ReduceOp.SUM)
+            shard.reduce_mix(mix, dist)
 
     for _ in range(args.warmup):
         step()

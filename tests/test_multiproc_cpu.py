@@ -1,0 +1,72 @@
+"""World-size-2 `gloo` rehearsal of the multi-GPU path on the CPU (no GPU).
+
+Each rank convolves its own channel group (the oracle stands in for the GPU
+convolution here; the GPU side of the same step is covered by the -m gpu
+tests), builds its stereo partial mix and the ranks sum-reduce to rank 0,
+exactly as bench.py does over RCCL.  Rank 0 compares against the
+single-process mix of all channels.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import oracle_lib as O
+from algodsp import shard, signals
+
+TOTAL_CH, N, K = 6, 3000, 700
+
+
+def _kernels():
+    return [signals.make_test_kernel(K), signals.make_impulse_kernel(K)]
+
+
+def _channel_output(c):
+    x = signals.white_noise(N, 0x5EED + c)
+    return O.OverlapSave(_kernels()[c % 2], 0).process(x)
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ids = list(shard.channel_group(rank, world, TOTAL_CH))
+        y = np.stack([_channel_output(c) for c in ids])
+        mix = torch.from_numpy(shard.stereo_partial_mix(y, ids))
+        shard.reduce_mix(mix, dist)
+        if rank == 0:
+            q.put(mix.numpy())
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_channel_shard_reduce_world2():
+    O.build()
+    port = 29500 + os.getpid() % 1000
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    full = shard.stereo_partial_mix(np.stack([_channel_output(c) for c in range(TOTAL_CH)]), range(TOTAL_CH))
+    np.testing.assert_allclose(got, full, rtol=0, atol=1e-12 * np.max(np.abs(full)))
+
+
+def test_channel_groups_partition():
+    for world in (1, 2, 3, 8):
+        for total in (1, 2, 7, 64):
+            if total < world:
+                continue
+            ids = [c for r in range(world) for c in shard.channel_group(r, world, total)]
+            assert ids == list(range(total))
+    assert list(shard.ir_index(range(5))) == [0, 1, 0, 1, 0]
