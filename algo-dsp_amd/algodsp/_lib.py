@@ -173,6 +173,11 @@ def _declare(L: C.CDLL) -> None:
         "ad_fx_chain_destroy": (None, [vp]),
         "ad_biquad_chain_process": (C.c_int, [c_double_p, c_double_p, C.c_double, c_double_p, C.c_int, C.c_int, i64,
                                               C.c_int]),
+        "ad_conv_reverb_create": (C.c_int, [c_double_p, i64, C.c_int, C.c_int, C.POINTER(vp)]),
+        "ad_conv_reverb_set_wet_dry": (C.c_int, [vp, C.c_double, C.c_double]),
+        "ad_conv_reverb_process_inplace": (C.c_int, [vp, c_double_p, i64]),
+        "ad_decode_f16": (C.c_int, [C.POINTER(C.c_uint16), i64, C.c_int, c_double_p, C.c_int]),
+        "ad_decode_f16_device": (C.c_int, [vp, i64, C.c_int, vp, vp]),
         "ad_fir_create": (C.c_int, [c_double_p, i64, C.c_int, C.c_int, C.POINTER(vp)]),
         "ad_fir_process_block": (C.c_int, [vp, c_double_p, i64]),
         "ad_fir_process_block_to": (C.c_int, [vp, c_double_p, c_double_p, i64]),

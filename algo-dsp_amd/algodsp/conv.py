@@ -158,6 +158,28 @@ def NewPartitionedConvolution(kernel, minBlockOrder: int, maxBlockOrder: int) ->
         _create(lib().ad_conv_partitioned_create, ptr(k), k.size, int(minBlockOrder), int(maxBlockOrder), DEVICE))
 
 
+class ConvolutionReverb(_Handle):
+    """reverb.ConvolutionReverb (dsp/effects/reverb/convolution.go:16-95):
+    block = dry*block + wet*PartitionedConvolution(block), latency 2^minBlockOrder."""
+
+    def SetWetDry(self, wet: float, dry: float) -> None:
+        check(lib().ad_conv_reverb_set_wet_dry(self._h, float(wet), float(dry)))
+
+    def ProcessInPlace(self, block: np.ndarray) -> None:
+        if not (isinstance(block, np.ndarray) and block.dtype == np.float64 and block.flags.c_contiguous):
+            raise TypeError("block must be a C-contiguous float64 array")
+        check(lib().ad_conv_reverb_process_inplace(self._h, ptr(block), block.size))
+
+    def Latency(self) -> int:
+        return int(lib().ad_conv_latency(self._h))
+
+
+def NewConvolutionReverb(kernel, minBlockOrder: int) -> ConvolutionReverb:
+    """convolution.go:28-44 (maxBlockOrder fixed at 13, wet = dry = 1)"""
+    k = f64(kernel)
+    return ConvolutionReverb(_create(lib().ad_conv_reverb_create, ptr(k), k.size, int(minBlockOrder), DEVICE))
+
+
 def Direct(a, b) -> np.ndarray:
     """conv.go:76-93"""
     x, y = f64(a), f64(b)

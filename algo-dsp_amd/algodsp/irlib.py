@@ -44,8 +44,24 @@ def _read_string(buf: bytes, pos: int):
     return buf[pos:pos + n].decode("utf-8", "replace"), pos + n
 
 
-def read_irlib(path=DEFAULT_IRLIB):
-    """Returns a list of dicts {name, category, sample_rate, samples[ch][n] (float64)}."""
+def decode_f16_gpu(raw: np.ndarray, channels: int, device: int = 0) -> np.ndarray:
+    """AUDI payload (interleaved f16) -> float64 [channels][frames] on the GPU
+    (ad_decode_f16, bit-exact with decodeF16 incl. its subnormal quirk)."""
+    import ctypes as C
+
+    from ._lib import check, lib
+
+    raw = np.ascontiguousarray(raw, dtype=np.uint16)
+    frames = raw.size // channels
+    out = np.empty((channels, frames), dtype=np.float64)
+    check(lib().ad_decode_f16(raw.ctypes.data_as(C.POINTER(C.c_uint16)), frames, channels,
+                              out.ctypes.data_as(C.POINTER(C.c_double)), device))
+    return out
+
+
+def read_irlib(path=DEFAULT_IRLIB, gpu: bool = False):
+    """Returns a list of dicts {name, category, sample_rate, samples[ch][n] (float64)}.
+    gpu=True decodes the AUDI payloads with the HIP kernel (ad_decode_f16)."""
     buf = pathlib.Path(path).read_bytes()
     if buf[:4] != b"IRLB":
         raise ValueError("irlib: invalid magic")
@@ -68,13 +84,13 @@ def read_irlib(path=DEFAULT_IRLIB):
     out = []
     for off, sr, ch, ln, name, cat in entries:
         try:
-            out.append(_read_chunk(buf, off, ch))
+            out.append(_read_chunk(buf, off, ch, gpu))
         except (ValueError, struct.error):
             continue  # bad chunks are skipped (irlib.go:255-263)
     return out
 
 
-def _read_chunk(buf: bytes, off: int, idx_channels: int):
+def _read_chunk(buf: bytes, off: int, idx_channels: int, gpu: bool = False):
     if buf[off:off + 4] != b"IR--":
         raise ValueError("irlib: expected IR--")
     (chunk_size,) = struct.unpack_from("<Q", buf, off + 4)
@@ -107,8 +123,11 @@ def _read_chunk(buf: bytes, off: int, idx_channels: int):
             ch = meta["channels"] if meta else idx_channels
             frames = raw.size // ch
             if frames:
-                vals = decode_f16(raw[: frames * ch]).astype(np.float64)
-                samples = vals.reshape(frames, ch).T.copy()
+                if gpu:
+                    samples = decode_f16_gpu(raw[: frames * ch], ch)
+                else:
+                    vals = decode_f16(raw[: frames * ch]).astype(np.float64)
+                    samples = vals.reshape(frames, ch).T.copy()
             pos = body + sub
         else:
             pos = body + sub

@@ -78,6 +78,7 @@ struct ad_conv {
   int64_t fft_size = 0;    // reported FFTSize()
   int64_t step_size = 0;   // OverlapSave.StepSize()
   int64_t latency = 0;     // partitioned
+  double wet = 1.0, dry = 1.0;  // ConvolutionReverb mix (reverb/convolution.go:45-58)
   std::vector<StageDesc> stages;
 
   std::unique_ptr<Upols> eng;  // FFT path
@@ -399,6 +400,39 @@ int ad_conv_partitioned_process_block(ad_conv* h, const double* in, int64_t in_l
     }
     h->emitted += out_len;
   });
+}
+
+// --- reverb.ConvolutionReverb (dsp/effects/reverb/convolution.go:16-95) ----------
+
+int ad_conv_reverb_create(const double* kernel, int64_t K, int min_order, int device, ad_conv** out) {
+  // NewConvolutionReverb: partitioned engine with maxBlockOrder 13, wet = dry = 1
+  if (out) *out = nullptr;
+  if (K <= 0 || !kernel) {
+    set_last_error("reverb: empty impulse response kernel");
+    return AD_ERR_EMPTY_IMPULSE_RESPONSE;
+  }
+  return ad_conv_partitioned_create(kernel, K, min_order, 13, device, out);
+}
+
+int ad_conv_reverb_set_wet_dry(ad_conv* h, double wet, double dry) {
+  return guard([&] {
+    if (!h || h->kind != Kind::Partitioned) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "not a convolution reverb");
+    h->wet = wet;
+    h->dry = dry;
+  });
+}
+
+int ad_conv_reverb_process_inplace(ad_conv* h, double* block, int64_t n) {
+  // ProcessInPlace: block[i] = dry*block[i] + wet*reverb(block)[i]  (convolution.go:60-85)
+  if (n <= 0) return AD_OK;
+  std::vector<double> rev((size_t)n);
+  const int rc = ad_conv_partitioned_process_block(h, block, n, rev.data(), n);
+  if (rc != AD_OK) return rc;
+  {
+#pragma clang fp contract(off)
+    for (int64_t i = 0; i < n; ++i) block[i] = h->dry * block[i] + h->wet * rev[(size_t)i];
+  }
+  return AD_OK;
 }
 
 int ad_conv_stage_count(const ad_conv* h) { return h ? (int)h->stages.size() : 0; }

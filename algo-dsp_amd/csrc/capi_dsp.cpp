@@ -519,3 +519,36 @@ void ad_fir_destroy(ad_fir* f) {
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// IRLB f16 decode
+// ---------------------------------------------------------------------------
+extern "C" {
+
+int ad_decode_f16_device(const uint16_t* d_in, int64_t frames, int channels, double* d_out, void* stream) {
+  return guard([&] {
+    if (frames < 0 || channels <= 0) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "bad f16 geometry");
+    launch_decode_f16(d_in, frames, channels, d_out, reinterpret_cast<hipStream_t>(stream));
+    AD_HIP(hipGetLastError());
+  });
+}
+
+int ad_decode_f16(const uint16_t* in, int64_t frames, int channels, double* out, int device) {
+  return guard([&] {
+    if (frames < 0 || channels <= 0) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "bad f16 geometry");
+    if (frames == 0) return;
+    const int dev = pick_device(device);
+    DeviceScope ds(dev);
+    const int64_t n = frames * channels;
+    DevBuf<uint16_t> din;
+    DevBuf<double> dout;
+    din.alloc((size_t)n);
+    dout.alloc((size_t)n);
+    AD_HIP(hipMemcpy(din.p, in, n * sizeof(uint16_t), hipMemcpyHostToDevice));
+    launch_decode_f16(din.p, frames, channels, dout.p, nullptr);
+    AD_HIP(hipGetLastError());
+    AD_HIP(hipMemcpy(out, dout.p, n * sizeof(double), hipMemcpyDeviceToHost));
+  });
+}
+
+}  // extern "C"

@@ -243,13 +243,9 @@ template <int PC, int NH>
 struct MacOcc {
   static constexpr int W = PC <= 4 ? 4 : (PC == 8 ? 3 : 2);
 };
-// X prefetch depth (rows in flight per lane).
-template <int PC>
-struct MacDepth {
-  static constexpr int D = PC < 4 ? PC : 4;
-};
-
-template <int PC, int NH, bool FIRST>
+// X prefetch depth DQ (rows in flight per lane, <= PC so the ring index stays
+// compile-time across groups).
+template <int PC, int NH, bool FIRST, int DQ>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MacOcc<PC, NH>::W))) void k_fdl_mac(MacArgs a) {
   constexpr int BW = 32 / NH;  // bin pairs per wave
   const int lg = xcd_remap(blockIdx.x, gridDim.x);
@@ -298,7 +294,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MacOcc<PC, N
 #pragma unroll
     for (int q = 0; q < PC; ++q) acc[q] = make_double2(0.0, 0.0);
 
-    constexpr int D = MacDepth<PC>::D;
+    constexpr int D = DQ < PC ? DQ : PC;
     XStream st;
     st.Xc = Xc;
     st.Q = a.Q;
@@ -387,15 +383,31 @@ __global__ __launch_bounds__(256) void k_mixdown(const double* __restrict__ ch, 
 // Launchers
 // ---------------------------------------------------------------------------
 namespace {
-template <int PC, int NH>
-void mac_go(const MacArgs& a, dim3 grid, hipStream_t s) {
+int mac_depth() {
+  static const int d = [] {
+    const char* v = std::getenv("AD_MAC_D");
+    return (v && std::atoi(v) == 8) ? 8 : 4;
+  }();
+  return d;
+}
+
+template <int PC, int NH, int DQ>
+void mac_go_d(const MacArgs& a, dim3 grid, hipStream_t s) {
   MacArgs c = a;
   for (c.p0 = 0; c.p0 < a.P; c.p0 += NH * PC) {
     if (c.p0 == 0)
-      hipLaunchKernelGGL((k_fdl_mac<PC, NH, true>), grid, dim3(64), 0, s, c);
+      hipLaunchKernelGGL((k_fdl_mac<PC, NH, true, DQ>), grid, dim3(64), 0, s, c);
     else
-      hipLaunchKernelGGL((k_fdl_mac<PC, NH, false>), grid, dim3(64), 0, s, c);
+      hipLaunchKernelGGL((k_fdl_mac<PC, NH, false, DQ>), grid, dim3(64), 0, s, c);
   }
+}
+
+template <int PC, int NH>
+void mac_go(const MacArgs& a, dim3 grid, hipStream_t s) {
+  if (PC >= 8 && mac_depth() == 8)
+    mac_go_d<PC, NH, 8>(a, grid, s);
+  else
+    mac_go_d<PC, NH, 4>(a, grid, s);
 }
 }  // namespace
 

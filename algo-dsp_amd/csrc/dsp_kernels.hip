@@ -274,7 +274,46 @@ __global__ __launch_bounds__(256) void k_fir(FirArgs a) {
   a.y[(int64_t)c * a.ystride + i] = acc;
 }
 
+// decodeF16 (internal/webdemo/irlib.go:68-97), reference quirk kept: a
+// subnormal is normalised with exponent 127-14-e+1 (one more than IEEE).
+__device__ __forceinline__ float decode_f16(uint32_t h) {
+  const uint32_t sign = (h >> 15) << 31;
+  const uint32_t ex = (h >> 10) & 0x1F;
+  const uint32_t frac = h & 0x3FF;
+  uint32_t bits;
+  if (ex == 0) {
+    if (frac == 0) {
+      bits = sign;
+    } else {
+      const int e = __clz(frac) - 21;  // shifts until bit 10 is set
+      bits = sign | ((uint32_t)(127 - 14 - e + 1) << 23) | (((frac << e) & 0x3FF) << 13);
+    }
+  } else if (ex == 31) {
+    bits = sign | 0x7F800000u | (frac << 13);
+  } else {
+    bits = sign | ((ex + 112) << 23) | (frac << 13);
+  }
+  return __uint_as_float(bits);
+}
+
+// readIRChunk's AUDI loop (irlib.go:414-451): sample i belongs to channel
+// i % ch, frame i / ch; output is channel-major float64.
+__global__ __launch_bounds__(256) void k_decode_f16(const uint16_t* __restrict__ in, int64_t frames, int channels,
+                                                    double* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= frames * channels) return;
+  const int64_t f = i / channels;
+  const int c = (int)(i - f * channels);
+  out[(int64_t)c * frames + f] = (double)decode_f16(in[i]);
+}
+
 }  // namespace
+
+void launch_decode_f16(const uint16_t* in, int64_t frames, int channels, double* out, hipStream_t s) {
+  const int64_t n = frames * channels;
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_decode_f16, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, in, frames, channels, out);
+}
 
 template <bool EQ, bool COMP, bool VERB>
 static void chain_go(const ChainArgs& a, hipStream_t s) {

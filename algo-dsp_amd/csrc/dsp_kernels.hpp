@@ -80,4 +80,7 @@ struct FirArgs {
 };
 void launch_fir(const FirArgs& a, hipStream_t s);
 
+// IRLB f16 decode: in [frames][channels] (interleaved) -> out [channels][frames]
+void launch_decode_f16(const uint16_t* in, int64_t frames, int channels, double* out, hipStream_t s);
+
 }  // namespace adsp

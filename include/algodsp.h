@@ -95,6 +95,15 @@ int ad_conv_partitioned_process_block(ad_conv* h, const double* in, int64_t in_l
 int ad_conv_stage_count(const ad_conv* h);
 int ad_conv_stage_info(const ad_conv* h, int index, int64_t* part_size, int64_t* block_count);
 
+/* ---- reverb.ConvolutionReverb (dsp/effects/reverb/convolution.go:16-95) --
+ * NewConvolutionReverb(kernel, minBlockOrder): partitioned engine with
+ * maxBlockOrder 13, wet = dry = 1, Latency() = 2^minBlockOrder.
+ * ProcessInPlace: block[i] = dry*block[i] + wet*reverb(block)[i] (:60-85).
+ * Reset/Latency/destroy: the common handle API below.                    */
+int ad_conv_reverb_create(const double* kernel, int64_t kernel_len, int min_block_order, int device, ad_conv** out);
+int ad_conv_reverb_set_wet_dry(ad_conv* h, double wet, double dry);
+int ad_conv_reverb_process_inplace(ad_conv* h, double* block, int64_t n);
+
 /* ---- common handle API -------------------------------------------------- */
 int ad_conv_reset(ad_conv* h);   /* Reset(): clears history/tail/FDL state */
 int64_t ad_conv_block_size(const ad_conv* h);
@@ -198,6 +207,13 @@ void ad_fx_chain_destroy(ad_fx_chain* h);
  * state [channels][sections][2] is read and updated; buf [channels][n]. */
 int ad_biquad_chain_process(const double* coeffs, double* state, double gain, double* buf, int channels,
                             int sections, int64_t n, int device);
+
+/* ---- IRLB f16 sample decode (internal/webdemo/irlib.go:68-97, 414-451) ----
+ * AUDI chunk payload (little-endian f16, frames interleaved by channel) ->
+ * float64 [channels][frames], bit-exact with decodeF16 including its
+ * subnormal exponent (every subnormal half decodes to twice its IEEE value). */
+int ad_decode_f16(const uint16_t* in, int64_t frames, int channels, double* out, int device);
+int ad_decode_f16_device(const uint16_t* d_in, int64_t frames, int channels, double* d_out, void* stream);
 
 /* ---- fir.Filter (dsp/filter/fir/filter.go:11-172) -------------------------
  * New(coeffs) for `channels` independent filters sharing the taps.

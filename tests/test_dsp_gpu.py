@@ -247,3 +247,51 @@ def test_fir_block_to_and_reset(gpu):
     P.Filter(case["coeffs"]).ProcessBlock(blk)
     np.testing.assert_allclose(vals, want, atol=case["tol"], rtol=0)
     np.testing.assert_allclose(blk, want, atol=case["tol"], rtol=0)
+
+
+# ------------------------------------------------------------------ IRLB f16 decode (8(f)2)
+def test_decode_f16_all_codes(gpu):
+    from algodsp import irlib
+
+    codes = np.arange(65536, dtype=np.uint16)
+    got = irlib.decode_f16_gpu(codes, 1)[0]
+    want = np.array([O.decode_f16(int(h)) for h in codes], dtype=np.float64)
+    same = (got == want) | (np.isnan(got) & np.isnan(want))
+    assert same.all(), np.flatnonzero(~same)[:10]
+    # subnormal quirk (irlib.go:87): 0x0001 decodes to 2^-23, twice IEEE's 2^-24
+    assert got[1] == 2.0 ** -23
+
+
+def test_irlib_gpu_decode_matches_oracle(gpu):
+    from algodsp import irlib
+
+    data = irlib.DEFAULT_IRLIB.read_bytes()
+    ref = O.irlib_read(data)
+    got = irlib.read_irlib(gpu=True)
+    assert len(got) == len(ref)
+    for g, (name, fs, samples) in zip(got, ref):
+        assert g["name"] == name and g["sample_rate"] == fs
+        assert np.array_equal(g["samples"], samples)
+
+
+# ------------------------------------------------------------------ ConvolutionReverb (a10)
+@pytest.mark.parametrize("min_order", [6, 7])
+def test_convolution_reverb(gpu, min_order):
+    from algodsp import conv
+
+    ir = signals.make_impulse_kernel(3000)
+    rv = conv.NewConvolutionReverb(ir, min_order)
+    assert rv.Latency() == 1 << min_order
+    rv.SetWetDry(0.4, 0.9)
+    x = signals.white_noise(5000, 21)
+    blocks = [(0, 100), (100, 1337), (1337, 5000)]  # variable block lengths (convolution.go:60)
+    parts = []
+    for a, b in blocks:
+        seg = x[a:b].copy()
+        rv.ProcessInPlace(seg)
+        parts.append(seg)
+    got = np.concatenate(parts)
+    pc = O.Partitioned(ir, min_order, 13)
+    wet = np.concatenate([pc.process_block(x[a:b]) for a, b in blocks])
+    want = 0.9 * x + 0.4 * wet
+    assert rms(got, want) <= 1e-7
