@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <memory>
@@ -92,6 +93,13 @@ struct ad_conv {
 
   // staging
   DevBuf<double> din, dout;
+  // pinned host staging for the per-block host-buffer calls: DMA straight
+  // from/to page-locked memory instead of the runtime's pageable bounce path
+  double* pin_in = nullptr;
+  double* pin_out = nullptr;
+  double* pin_in_dev = nullptr;   // device-side addresses of the mapped buffers
+  double* pin_out_dev = nullptr;
+  size_t pin_n = 0;
 
   // partitioned FIFO state
   std::vector<double> pending;   // input samples not yet convolved (< hop)
@@ -101,6 +109,9 @@ struct ad_conv {
 
   ~ad_conv() {
     eng.reset();
+    if (stream) (void)hipStreamSynchronize(stream);
+    if (pin_in) (void)hipHostFree(pin_in);
+    if (pin_out) (void)hipHostFree(pin_out);
     if (stream) (void)hipStreamDestroy(stream);
   }
 };
@@ -121,6 +132,10 @@ ad_conv* new_handle(Kind k, int device) {
 
 // zero-latency streaming convolution state for `hop` sized chunks
 void setup_stream_engine(ad_conv* h, const double* kernel, int64_t K, int64_t B, int64_t hop_cap) {
+  if (const char* v = std::getenv("AD_STREAM_HOP_CAP")) {  // A/B override for sweeps
+    const int64_t c = std::atoll(v);
+    if (c >= 64 && is_pow2(c)) hop_cap = std::min(hop_cap, c);
+  }
   const int64_t hop = largest_pow2_divisor(B, hop_cap);
   h->hop = hop;
   h->conv_len = K;
@@ -176,13 +191,25 @@ void stream_convolve(ad_conv* h, const double* in, int64_t n, double* out) {
     AD_HIP(hipStreamSynchronize(s));
     return;
   }
-  h->din.reserve((size_t)n);
-  h->dout.reserve((size_t)n);
-  AD_HIP(hipMemcpyAsync(h->din.p, in, n * sizeof(double), hipMemcpyHostToDevice, s));
-  h->eng->run(h->din.p, n, n, h->dout.p, n, n, /*use_hist=*/true, s);
-  h->eng->save_history(h->din.p, n, n, s);
-  AD_HIP(hipMemcpyAsync(out, h->dout.p, n * sizeof(double), hipMemcpyDeviceToHost, s));
+  // Zero-copy: the block goes through page-locked host buffers that the GPU
+  // reads (K1) and writes (K3) directly over PCIe, so a block costs three
+  // kernels and one synchronisation, no DMA round trips.  The next call's
+  // history is written by K1 itself (Upols ping-pong history).
+  if (h->pin_n < (size_t)n) {
+    if (h->pin_in) AD_HIP(hipHostFree(h->pin_in));
+    if (h->pin_out) AD_HIP(hipHostFree(h->pin_out));
+    h->pin_in = h->pin_out = nullptr;
+    h->pin_n = 0;
+    AD_HIP(hipHostMalloc(reinterpret_cast<void**>(&h->pin_in), n * sizeof(double), hipHostMallocMapped));
+    AD_HIP(hipHostMalloc(reinterpret_cast<void**>(&h->pin_out), n * sizeof(double), hipHostMallocMapped));
+    AD_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&h->pin_in_dev), h->pin_in, 0));
+    AD_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&h->pin_out_dev), h->pin_out, 0));
+    h->pin_n = (size_t)n;
+  }
+  std::memcpy(h->pin_in, in, n * sizeof(double));
+  h->eng->run(h->pin_in_dev, n, n, h->pin_out_dev, n, n, /*use_hist=*/true, s);
   AD_HIP(hipStreamSynchronize(s));
+  std::memcpy(out, h->pin_out, n * sizeof(double));
 }
 
 // Offline full convolution of one channel with the handle's kernel.

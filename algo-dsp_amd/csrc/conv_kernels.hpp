@@ -12,6 +12,8 @@ struct RfftArgs {
   int64_t x_stride;
   int64_t n;            // valid input samples per channel (beyond: zeros)
   const double* xhist;  // [C][hist_stride]: the L samples preceding the call (nullable -> zeros)
+  double* hist_out;     // [C][hist_stride]: receives the last window's upper half (the next
+                        // call's history) when non-null; must not alias xhist
   int64_t hist_stride;
   int64_t s0;           // first output sample of chunk block 0 (call-relative)
   int jc;               // blocks per channel in this launch

@@ -95,6 +95,17 @@ __global__ __launch_bounds__((FftPlan<M, V>::BLOCK)) void k_window_rfft(RfftArgs
 #pragma unroll
   for (int s = 0; s < V; ++s)
     v[s] = active ? fetch_pair(xc, hc, t0 + 2 * pass0_index<M, V>(tid, s), a.n, L, a.aligned) : make_double2(0, 0);
+  if (active && a.hist_out && j == a.jc - 1) {  // streaming: the next call's history
+    double* ho = a.hist_out + (int64_t)c * a.hist_stride;
+#pragma unroll
+    for (int s = 0; s < V; ++s) {
+      const int w = 2 * pass0_index<M, V>(tid, s);
+      if (w >= L) {
+        ho[w - L] = v[s].x;
+        ho[w - L + 1] = v[s].y;
+      }
+    }
+  }
   fft_run<M, V, true>(v, tid, lds, TwGlobal{a.twM});
   if (!active) return;
   double2* Xo = a.X + (int64_t)c * a.x_ch_stride + (int64_t)((a.slot0 + j) % a.Q) * a.MS;
@@ -180,6 +191,19 @@ __global__ __launch_bounds__((SplitPlan<M>::T)) __attribute__((amdgpu_waves_per_
       const int64_t t = t0 + 4 * pass0_index<M2, V>(tid, s);
       ev[s] = fetch_pair(xc, hc, t, a.n, L, a.aligned);
       ov[s] = fetch_pair(xc, hc, t + 2, a.n, L, a.aligned);
+    }
+  }
+  if (a.hist_out && j == a.jc - 1) {  // streaming: the next call's history
+    double* ho = a.hist_out + (int64_t)c * a.hist_stride;
+#pragma unroll
+    for (int s = 0; s < V; ++s) {
+      const int w = 4 * pass0_index<M2, V>(tid, s);  // window offset of ev[s]
+      if (w >= L) {
+        ho[w - L] = ev[s].x;
+        ho[w - L + 1] = ev[s].y;
+        ho[w - L + 2] = ov[s].x;
+        ho[w - L + 3] = ov[s].y;
+      }
     }
   }
   __syncthreads();  // twiddle tables

@@ -99,7 +99,8 @@ Upols::Upols(int device, const double* kernels, int n_ir, int64_t K, int L, int 
   X_.alloc((size_t)C_ * (Q_ + 1) * MS_);  // Q ring rows + one zero row per channel
   // Z rows: jc_max outputs + 16 rows of run overshoot (k_fdl_mac)
   Y_.alloc((size_t)C_ * (jc_max_ + 16) * MS_);
-  hist_.alloc((size_t)C_ * L_);
+  hist_[0].alloc((size_t)C_ * L_);
+  hist_[1].alloc((size_t)C_ * L_);
   std::vector<int> irm(C_);
   for (int c = 0; c < C_; ++c) irm[c] = ir_map ? ir_map[c] : (c % n_ir_);
   for (int c = 0; c < C_; ++c)
@@ -178,7 +179,9 @@ void Upols::read_profile(double* ms, int64_t* launches, double* alg_bytes) {
 
 void Upols::reset_stream(hipStream_t s) {
   AD_HIP(hipMemsetAsync(X_.p, 0, X_.n * sizeof(double2), s));
-  AD_HIP(hipMemsetAsync(hist_.p, 0, hist_.n * sizeof(double), s));
+  AD_HIP(hipMemsetAsync(hist_[0].p, 0, hist_[0].n * sizeof(double), s));
+  AD_HIP(hipMemsetAsync(hist_[1].p, 0, hist_[1].n * sizeof(double), s));
+  hcur_ = 0;
   g_next_ = 0;
 }
 
@@ -205,7 +208,9 @@ void Upols::run(const double* d_in, int64_t in_stride, int64_t n, double* d_out,
     a.x = d_in;
     a.x_stride = in_stride;
     a.n = n;
-    a.xhist = use_hist ? hist_.p : nullptr;
+    a.xhist = use_hist ? hist_[hcur_].p : nullptr;
+    // the last chunk's last window leaves the next call's history in the other buffer
+    a.hist_out = (use_hist && cs + jc >= J) ? hist_[hcur_ ^ 1].p : nullptr;
     a.hist_stride = L_;
     a.s0 = cs * L_;
     a.jc = jc;
@@ -266,12 +271,11 @@ void Upols::run(const double* d_in, int64_t in_stride, int64_t n, double* d_out,
     AD_HIP(hipGetLastError());
     g_next_ += jc;
   }
+  if (use_hist) hcur_ ^= 1;
 }
 
-void Upols::save_history(const double* d_in, int64_t in_stride, int64_t n, hipStream_t s) {
+void Upols::save_history(const double*, int64_t, int64_t n, hipStream_t) {
   if (n < L_) AD_FAIL(AD_ERR_INTERNAL, "streaming call shorter than the hop");
-  AD_HIP(hipMemcpy2DAsync(hist_.p, (size_t)L_ * sizeof(double), d_in + (n - L_), (size_t)in_stride * sizeof(double),
-                          (size_t)L_ * sizeof(double), C_, hipMemcpyDeviceToDevice, s));
 }
 
 }  // namespace adsp

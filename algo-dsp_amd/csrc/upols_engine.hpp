@@ -39,6 +39,8 @@ class Upols {
   void run(const double* d_in, int64_t in_stride, int64_t n, double* d_out, int64_t out_stride, int64_t out_len,
            bool use_hist, hipStream_t s);
   // Saves the last L input samples of the call into the streaming history.
+  // Streaming calls (use_hist) refresh the history inside K1; kept for API
+  // symmetry, a no-op.
   void save_history(const double* d_in, int64_t in_stride, int64_t n, hipStream_t s);
 
   // Live kernel timing with HIP events on the launch stream (kernel k:
@@ -57,7 +59,8 @@ class Upols {
   DevBuf<double2> H_;    // [n_ir][P][MS]
   DevBuf<double2> X_;    // [C][Q][MS]
   DevBuf<double2> Y_;    // [C][jc_max][MS]
-  DevBuf<double> hist_;  // [C][L]
+  DevBuf<double> hist_[2];  // [C][L] ping-pong: K1 reads one and writes the next call's into the other
+  int hcur_ = 0;
   DevBuf<int> irmap_;    // [C]
 
   struct ProfRec {

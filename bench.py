@@ -41,8 +41,9 @@ def parse():
                    help="HIP events around every engine kernel launch inside the timed region")
     p.add_argument("--channels", type=int, default=2,
                    help="conv: channels per GPU (IR[c %% 2]); 2 = the stereo config, 8 = config 4's shard")
-    p.add_argument("--workload", choices=["conv", "fx"], default="conv",
-                   help="conv: BASELINE metric (overlap-save conv); fx: config 5 effect chain (256 ch)")
+    p.add_argument("--workload", choices=["conv", "fx", "stream"], default="conv",
+                   help="conv: BASELINE metric (overlap-save conv); fx: config 5 effect chain (256 ch); "
+                        "stream: config 2 streaming OLS (mono, 16384 taps, 4096-sample host blocks)")
     return p.parse_args()
 
 
@@ -76,6 +77,8 @@ def main():
     args = parse()
     if args.workload == "fx":
         return main_fx(args)
+    if args.workload == "stream":
+        return main_stream(args)
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -221,6 +224,54 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def main_stream(args):
+    """BASELINE config 2: StreamingOverlapSave(K=16384, B=4096) driven block by
+    block through the host-buffer ABI, as a Go caller would (ProcessBlockTo per
+    block: PCIe in, UPOLS on the GPU, PCIe out, synchronous).  Replicas only."""
+    import numpy as np
+
+    from algodsp import conv, irlib, signals
+
+    ir = irlib.large_church()[0, :16384]
+    B = 4096
+    nblk = max(1, args.samples // B) if args.samples != (1 << 24) else 2048
+    x = signals.white_noise(nblk * B, 0x5EED)
+    y = np.empty_like(x)
+    s = conv.NewStreamingOverlapSave(ir, B)
+    for i in range(min(args.warmup * 8, nblk)):
+        s.ProcessBlockTo(y[i * B:(i + 1) * B], x[i * B:(i + 1) * B])
+    s.Reset()
+    t0 = time.perf_counter()
+    for i in range(nblk):
+        s.ProcessBlockTo(y[i * B:(i + 1) * B], x[i * B:(i + 1) * B])
+    dt = time.perf_counter() - t0
+    cpu = None
+    if not args.no_cpu_baseline:
+        sys.path.insert(0, str(ROOT / "tests"))
+        import oracle_lib as O
+
+        o = O.Streaming(ir, B)
+        m = min(nblk, 256)
+        tc = time.perf_counter()
+        for i in range(m):
+            o.process_block(x[i * B:(i + 1) * B])
+        dtc = time.perf_counter() - tc
+        cpu = {"value": m * B / dtc / 1e6, "unit": "Msamples/s", "cores": 1, "kind": "port",
+               "sample": f"{m} blocks of {B}, oracle StreamingOverlapSave (N=32768); {dtc:.1f} s"}
+    line = {
+        "metric": "Msamples/sec, streaming overlap-save 16384-tap IR, 4096-sample blocks (config 2)",
+        "value": round(nblk * B / dt / 1e6, 3), "unit": "Msamples/s", "n_gpus": 1, "steps": nblk,
+        "warmup": args.warmup, "ms_per_step": round(dt / nblk * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic: SplitMix64 white noise x Large Church L (first 16384 taps)",
+        "config": {"workload": "StreamingOverlapSave mono K=16384 B=4096, host buffers, one block per step",
+                   "block": B, "kernel_taps": 16384},
+        "note": "latency-bound: each block = H2D copy + 3 kernels + D2H copy + sync",
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), flush=True)
 
 
 def main_fx(args):
