@@ -13,6 +13,7 @@
 
 #include "ad_common.hpp"
 #include "conv_kernels.hpp"
+#include "nupols_engine.hpp"
 #include "upols_engine.hpp"
 
 using namespace adsp;
@@ -101,13 +102,17 @@ struct ad_conv {
   double* pin_out_dev = nullptr;
   size_t pin_n = 0;
 
-  // partitioned FIFO state
+  // partitioned: non-uniform multi-stage engine (latency >= 64)
+  std::unique_ptr<Nupols> nup;
+
+  // partitioned FIFO state (latency < 64: time-domain streaming fallback shape)
   std::vector<double> pending;   // input samples not yet convolved (< hop)
   std::deque<double> ylin;       // convolved samples not yet emitted
   int64_t emitted = 0;           // output samples emitted so far
   int64_t ylin_base = 0;         // linear-conv index of ylin.front()
 
   ~ad_conv() {
+    nup.reset();
     eng.reset();
     if (stream) (void)hipStreamSynchronize(stream);
     if (pin_in) (void)hipHostFree(pin_in);
@@ -385,9 +390,18 @@ int ad_conv_partitioned_create(const double* kernel, int64_t K, int min_order, i
     for (const auto& s : h->stages) cover = std::max(cover, s.start + s.count * s.part_size);
     const int64_t keff = std::min<int64_t>(K, cover);
     h->fft_size = 2 * h->stages.back().part_size;
-    // Zero-latency engine with hop = latency (<= 8192), output delayed by latency.
-    setup_stream_engine(h.get(), kernel, keff, latency, 8192);
-    stream_reset(h.get());
+    const char* uni = std::getenv("AD_PC_UNIFORM");
+    if (latency >= 64 && latency <= 8192 && !(uni && *uni == '1')) {
+      // Non-uniform stages: hop lambda for the head of the IR, doubling up to
+      // 2^maxBlockOrder (<= 8192) for the tail (nupols_engine.hpp).
+      const int64_t pmax = std::min<int64_t>(8192, std::max<int64_t>(latency, int64_t(1) << std::min(max_order, 13)));
+      h->conv_len = keff;
+      h->nup.reset(new Nupols(dev, kernel, keff, latency, pmax));
+    } else {
+      // Zero-latency engine with hop = latency (<= 8192), output delayed by latency.
+      setup_stream_engine(h.get(), kernel, keff, latency, 8192);
+      stream_reset(h.get());
+    }
     return h.release();
   });
 }
@@ -401,6 +415,11 @@ int ad_conv_partitioned_process_block(ad_conv* h, const double* in, int64_t in_l
                                           " != output length " + std::to_string(out_len));
     if (in_len == 0) return;
     DeviceScope ds(h->device);
+    if (h->nup) {
+      h->nup->process(in, in_len, out);
+      h->emitted += in_len;
+      return;
+    }
     // Convolve every complete hop-sized block (all samples on the direct path).
     h->pending.insert(h->pending.end(), in, in + in_len);
     const int64_t hop = h->direct_stream ? 1 : h->hop;
@@ -482,6 +501,7 @@ int ad_conv_reset(ad_conv* h) {
   return guard([&] {
     if (!h) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "nil handle");
     DeviceScope ds(h->device);
+    if (h->nup) h->nup->reset();
     stream_reset(h);
   });
 }

@@ -1,0 +1,115 @@
+// Host runtime of the non-uniformly partitioned engine (see nupols_engine.hpp).
+#include "nupols_engine.hpp"
+
+#include <algorithm>
+#include <cstring>
+
+namespace adsp {
+
+Nupols::Nupols(int device, const double* h, int64_t K, int64_t lambda, int64_t p_max)
+    : device_(device), lambda_(lambda) {
+  if (lambda < 64 || !is_pow2(lambda) || p_max < lambda || !is_pow2(p_max) || p_max > 8192)
+    AD_FAIL(AD_ERR_INTERNAL, "Nupols: bad partition sizes");
+  // Stage layout: two partitions per size while the size doubles, the rest
+  // at p_max.  T_{s+1} = T_s + n_s p_s >= p_{s+1} - lambda holds by construction.
+  int64_t T = 0, p = lambda;
+  while (T < K) {
+    int64_t n = 2;
+    if (p >= p_max) n = (K - T + p - 1) / p;
+    Stage s;
+    s.p = p;
+    s.T = T;
+    s.taps = std::min<int64_t>(n * p, K - T);
+    st_.push_back(std::move(s));
+    T += n * p;
+    if (p < p_max) p *= 2;
+  }
+  for (auto& s : st_) {
+    AD_HIP(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+    s.eng.reset(new Upols(device, h + s.T, 1, s.taps, (int)s.p, 1, nullptr, 1, s.stream));
+    AD_HIP(hipHostMalloc(reinterpret_cast<void**>(&s.in_h), s.p * sizeof(double), hipHostMallocMapped));
+    AD_HIP(hipHostMalloc(reinterpret_cast<void**>(&s.out_h), s.p * sizeof(double), hipHostMallocMapped));
+    AD_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&s.in_d), s.in_h, 0));
+    AD_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&s.out_d), s.out_h, 0));
+  }
+  reset();
+}
+
+Nupols::~Nupols() {
+  for (auto& s : st_) {
+    if (s.stream) (void)hipStreamSynchronize(s.stream);
+    s.eng.reset();
+    if (s.in_h) (void)hipHostFree(s.in_h);
+    if (s.out_h) (void)hipHostFree(s.out_h);
+    if (s.stream) (void)hipStreamDestroy(s.stream);
+  }
+}
+
+void Nupols::reset() {
+  for (auto& s : st_) {
+    s.eng->reset_stream(s.stream);
+    s.done = 0;
+  }
+  for (auto& s : st_) AD_HIP(hipStreamSynchronize(s.stream));
+  xin_.clear();
+  xin_base_ = 0;
+  received_ = 0;
+  acc_.clear();
+  acc_base_ = 0;
+  emitted_ = 0;
+}
+
+void Nupols::process(const double* in, int64_t n, double* out) {
+  xin_.insert(xin_.end(), in, in + n);
+  received_ += n;
+  // Rounds: every stage with a complete input block launches one run on its
+  // own stream; one synchronisation per round, then the block outputs are
+  // added into the accumulator at time offset T_s.
+  std::vector<int> due;
+  for (;;) {
+    due.clear();
+    for (int i = 0; i < (int)st_.size(); ++i) {
+      Stage& s = st_[i];
+      if (received_ - s.done < s.p) continue;
+      const int64_t off = s.done - xin_base_;
+      std::copy(xin_.begin() + off, xin_.begin() + off + s.p, s.in_h);
+      s.eng->run(s.in_d, s.p, s.p, s.out_d, s.p, s.p, /*use_hist=*/true, s.stream);
+      due.push_back(i);
+    }
+    if (due.empty()) break;
+    for (int i : due) AD_HIP(hipStreamSynchronize(st_[i].stream));
+    for (int i : due) {
+      Stage& s = st_[i];
+      const int64_t t0 = s.done + s.T;  // absolute output time of the block's first sample
+      const int64_t need = t0 + s.p - acc_base_;
+      if ((int64_t)acc_.size() < need) acc_.resize((size_t)need, 0.0);
+      for (int64_t k = 0; k < s.p; ++k) acc_[(size_t)(t0 - acc_base_ + k)] += s.out_h[k];
+      s.done += s.p;
+    }
+  }
+  // Emit: y[o] = linear conv at o - lambda (complete by the T_s + lambda >= p_s rule).
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t u = emitted_ + i - lambda_;
+    if (u < 0) {
+      out[i] = 0.0;
+      continue;
+    }
+    const int64_t idx = u - acc_base_;
+    out[i] = idx < (int64_t)acc_.size() ? acc_[(size_t)idx] : 0.0;
+  }
+  emitted_ += n;
+  // Drop what no later output or stage needs.
+  const int64_t keep_out = emitted_ - lambda_;
+  while (acc_base_ < keep_out && !acc_.empty()) {
+    acc_.pop_front();
+    ++acc_base_;
+  }
+  int64_t min_done = received_;
+  for (auto& s : st_) min_done = std::min(min_done, s.done);
+  while (xin_base_ < min_done && !xin_.empty()) {
+    xin_.pop_front();
+    ++xin_base_;
+  }
+}
+
+}  // namespace adsp

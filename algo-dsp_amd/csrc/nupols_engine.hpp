@@ -1,0 +1,61 @@
+// Non-uniformly partitioned low-latency convolution engine: the MI355X form
+// of conv.PartitionedConvolutionT's streaming mode (dsp/conv/partitioned.go:
+// 212-436).
+//
+// Output contract (as the reference): y[t] = (h * x)[t - lambda], lambda =
+// 2^minOrder, for any call length.  The taps are split into stages of
+// doubling partition size p_s = lambda, 2 lambda, ..., p_max, each stage a
+// zero-latency UPOLS engine with hop p_s over its own tap segment
+// [T_s, T_s + n_s p_s).  Stage s runs once per p_s input samples and its
+// block output lands at output times offset by T_s; T_s + lambda >= p_s makes
+// every contribution arrive before it is emitted.  Stages run on their own
+// HIP streams (the small kernels of the short stages overlap the long ones),
+// read their input block straight from mapped pinned host memory and write
+// their output there too, so a call costs only the kernels of the stages due
+// plus one synchronisation.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <deque>
+#include <memory>
+#include <vector>
+
+#include "ad_common.hpp"
+#include "upols_engine.hpp"
+
+namespace adsp {
+
+class Nupols {
+ public:
+  // h: host [K] taps (K = the taps the reference convolves), lambda >= 64,
+  // p_max <= 8192 (powers of two).
+  Nupols(int device, const double* h, int64_t K, int64_t lambda, int64_t p_max);
+  ~Nupols();
+
+  void process(const double* in, int64_t n, double* out);
+  void reset();
+  int stage_count() const { return (int)st_.size(); }
+
+ private:
+  struct Stage {
+    int64_t p = 0, T = 0, taps = 0;
+    std::unique_ptr<Upols> eng;
+    hipStream_t stream = nullptr;
+    double *in_h = nullptr, *in_d = nullptr;    // mapped pinned [p]
+    double *out_h = nullptr, *out_d = nullptr;  // mapped pinned [p]
+    int64_t done = 0;                           // input samples consumed
+  };
+  int device_;
+  int64_t lambda_;
+  std::vector<Stage> st_;
+  std::deque<double> xin_;   // input not yet consumed by every stage
+  int64_t xin_base_ = 0;     // absolute time of xin_.front()
+  int64_t received_ = 0;     // input samples received
+  std::deque<double> acc_;   // linear-conv output accumulator
+  int64_t acc_base_ = 0;     // absolute time of acc_.front()
+  int64_t emitted_ = 0;      // output samples emitted
+};
+
+}  // namespace adsp
