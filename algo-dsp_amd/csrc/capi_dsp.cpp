@@ -6,6 +6,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
+#include <cstdio>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -130,6 +132,14 @@ void fx_run(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hipStream_
   a.vp = h->vp;
   a.vs = h->vs.p;
   a.vbuf = h->vbuf.p;
+  if (const char* v = std::getenv("AD_FX_DBG")) a.dbg = std::atoi(v);
+  static DevBuf<unsigned long long> prof;
+  const bool want_prof = std::getenv("AD_FX_PROF") != nullptr;
+  if (want_prof) {
+    prof.reserve((size_t)((h->channels + 63) / 64) * 16);
+    AD_HIP(hipMemsetAsync(prof.p, 0, prof.n * sizeof(unsigned long long), s));
+    a.prof = prof.p;
+  }
   const int post = (h->comp_on ? 2 : 0) | (h->verb_on ? 4 : 0);
   // EQ sections in passes of <= kMaxSecPerPass; the last pass fuses the
   // compressor and Freeverb stages (per-sample fusion is exact, see kernels)
@@ -148,6 +158,14 @@ void fx_run(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hipStream_
     s0 += ns;
   } while (s0 < h->nsec);
   AD_HIP(hipGetLastError());
+  if (want_prof) {
+    std::vector<unsigned long long> v(prof.n);
+    AD_HIP(hipStreamSynchronize(s));
+    AD_HIP(hipMemcpy(v.data(), prof.p, v.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    for (int w = 0; w < 8; ++w)
+      if (v[w * 2 + 1]) fprintf(stderr, "fx-pipe wave %d: busy %llu of %llu ticks (%.1f%%)\n", w, v[w * 2], v[w * 2 + 1],
+                                100.0 * v[w * 2] / v[w * 2 + 1]);
+  }
 }
 
 template <class Fn>

@@ -24,6 +24,8 @@
 // read, so a D <= 8 lookahead never reads a stale value).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "dsp_kernels.hpp"
 
 namespace adsp {
@@ -254,6 +256,332 @@ __global__ __launch_bounds__(64) void k_chain(ChainArgs a) {
   if constexpr (VERB) a.vs[c] = vs;
 }
 
+// ---------------------------------------------------------------------------
+// Wave-pipelined effect chain (EQ -> feed-forward Compressor -> Freeverb).
+// One workgroup of five waves serves 64 channels; each wave runs one stage
+// of every sample and the chunks of kPipeD samples flow through LDS rings:
+//   wave 0  EQ sections + compressor side-chain filters, detector, envelope
+//           (the serial recurrences)          -> v, env
+//   wave 1  gain(env) = 2^(-cf*knee(log2 env - T)), out = v*g*makeup,
+//           metrics (independent per sample given env) -> out
+//   wave 2  Freeverb combs 0-3 (delay-line reads a chunk ahead) -> c0+..+c3
+//   wave 3  Freeverb combs 4-7                                  -> c4..c7
+//   wave 4  comb sum, allpasses, wet/dry mix, store
+// At step k wave w works on chunk k - w; one barrier per step.  Every
+// value is computed with the same operations in the same order as the fused
+// one-wave kernel, so results are identical; the four stages just run on
+// four SIMDs at once instead of one after the other.
+// ---------------------------------------------------------------------------
+constexpr int kPipeD = 8;
+constexpr int kRing = 4;
+
+__global__ __launch_bounds__(320) void k_chain_pipe(ChainArgs a) {
+#pragma clang fp contract(off)
+  __shared__ double ring_v[kRing][kPipeD][64];
+  __shared__ double ring_env[kRing][kPipeD][64];
+  __shared__ double ring_out[kRing][kPipeD][64];
+  __shared__ double ring_acc[kRing][kPipeD][64];     // combs 0-3 partial sum
+  __shared__ double ring_c47[kRing][4][kPipeD][64];  // outputs of combs 4-7
+  const int w = threadIdx.x >> 6;
+  const int l = threadIdx.x & 63;
+  const int c = blockIdx.x * 64 + l;
+  const bool active = c < a.channels;
+  const int cc = active ? c : a.channels - 1;
+  const int cpad = (a.channels + 63) / 64 * 64;
+  double* xb = a.buf + (int64_t)cc * a.stride;
+  const int64_t nch = (a.n + kPipeD - 1) / kPipeD;
+  const CompParams& p = a.cp;
+  const VerbParams& vp = a.vp;
+  unsigned long long t_busy = 0, t_mark = clock64(), t_start = t_mark;
+  // step barrier; with AD_FX_PROF the wave's busy time (excluding the wait) is accumulated
+#define PIPE_SYNC()                                 \
+  do {                                              \
+    if (a.prof) t_busy += clock64() - t_mark;       \
+    __syncthreads();                                \
+    if (a.prof) t_mark = clock64();                 \
+  } while (0)
+
+  if (w == 0) {
+    // ---- EQ + detector
+    double d0[kMaxSecPerPass], d1[kMaxSecPerPass], q[kMaxSecPerPass][kSecStride];
+    const double* sec = a.eq.sec + (int64_t)cc * a.eq.sec_ch_stride;
+#pragma unroll
+    for (int s = 0; s < kMaxSecPerPass; ++s) {
+      d0[s] = s < a.eq.nsec ? a.eq.state[((int64_t)cc * a.eq.nsec + s) * 2] : 0.0;
+      d1[s] = s < a.eq.nsec ? a.eq.state[((int64_t)cc * a.eq.nsec + s) * 2 + 1] : 0.0;
+#pragma unroll
+      for (int k = 0; k < kSecStride; ++k) q[s][k] = s < a.eq.nsec ? sec[s * kSecStride + k] : 0.0;
+    }
+    CompChState cs = a.cs[cc];
+    double* rring = a.rms_ring + (int64_t)cc * p.rms_n;
+    double xn[kPipeD], xn2[kPipeD];  // the next two chunks of input
+#pragma unroll
+    for (int d = 0; d < kPipeD; ++d) {
+      xn[d] = xb[min((int64_t)d, a.n - 1)];
+      xn2[d] = xb[min((int64_t)(kPipeD + d), a.n - 1)];
+    }
+    for (int64_t k = 0; k < nch + 3; ++k) {
+      if (k < nch) {
+        const int r = (int)(k % kRing);
+        const int64_t t0 = k * kPipeD;
+        double x[kPipeD];
+#pragma unroll
+        for (int d = 0; d < kPipeD; ++d) {
+          x[d] = xn[d];
+          xn[d] = xn2[d];
+        }
+#pragma unroll
+        for (int d = 0; d < kPipeD; ++d) xn2[d] = xb[min(t0 + 2 * kPipeD + d, a.n - 1)];
+#pragma unroll
+        for (int d = 0; d < kPipeD; ++d) {
+          const bool real = t0 + d < a.n;  // padding of the last chunk leaves every state untouched
+          double v = x[d];
+#pragma unroll
+          for (int s = 0; s < kMaxSecPerPass; ++s) {
+            if (s >= a.eq.nsec || (a.dbg & 4)) break;
+            v = v * q[s][0];
+            const double y = q[s][1] * v + d0[s];
+            const double n0 = q[s][2] * v - q[s][4] * y + d1[s];
+            const double n1 = q[s][3] * v - q[s][5] * y;
+            d0[s] = real ? n0 : d0[s];
+            d1[s] = real ? n1 : d1[s];
+            v = y;
+          }
+          double sc = v;  // applyPrefilter core.go:390-400
+          if (p.lp_on) {
+            const double nl = cs.lp + p.lp_alpha * (sc - cs.lp);
+            sc = nl;
+            if (real) cs.lp = nl;
+          }
+          if (p.hp_on) {
+            const double nh = cs.hp + p.hp_alpha * (sc - cs.hp);
+            sc = sc - nh;
+            if (real) cs.hp = nh;
+          }
+          double src = fabs(sc);
+          if (p.detector_rms) {  // updateRMS core.go:361-388
+            if (real) {
+              const double sq = src * src;
+              if (cs.rms_filled == p.rms_n)
+                cs.rms_sum -= rring[cs.rms_index];
+              else
+                cs.rms_filled++;
+              rring[cs.rms_index] = sq;
+              cs.rms_sum += sq;
+              if (++cs.rms_index >= p.rms_n) cs.rms_index = 0;
+              const double mean = cs.rms_sum / (double)p.rms_n;
+              src = mean <= 0.0 ? 0.0 : sqrt(mean);
+            }
+          }
+          if (real) {
+            if (src > cs.env)
+              cs.env += (src - cs.env) * p.attack;
+            else
+              cs.env = src + (cs.env - src) * p.release;
+          }
+          ring_v[r][d][l] = v;
+          ring_env[r][d][l] = cs.env;
+        }
+      }
+      PIPE_SYNC();
+    }
+    if (active) {  // each wave stores only the state fields it owns
+#pragma unroll
+      for (int s = 0; s < kMaxSecPerPass; ++s) {
+        if (s >= a.eq.nsec) break;
+        a.eq.state[((int64_t)c * a.eq.nsec + s) * 2] = d0[s];
+        a.eq.state[((int64_t)c * a.eq.nsec + s) * 2 + 1] = d1[s];
+      }
+      CompChState* o = a.cs + c;
+      o->env = cs.env;
+      o->lp = cs.lp;
+      o->hp = cs.hp;
+      o->rms_sum = cs.rms_sum;
+      o->rms_index = cs.rms_index;
+      o->rms_filled = cs.rms_filled;
+    }
+  } else if (w == 1) {
+    // ---- gain + metrics
+    CompChState cs = a.cs[cc];
+    for (int64_t k = 0; k < nch + 3; ++k) {
+      const int64_t my = k - 1;
+      if (my >= 0 && my < nch) {
+        const int r = (int)(my % kRing);
+        const int64_t t0 = my * kPipeD;
+#pragma unroll 4
+        for (int d = 0; d < kPipeD; ++d) {
+          const double v = ring_v[r][d][l];
+          const double g = (a.dbg & 1) ? 1.0 : gain_for_level(p, ring_env[r][d][l]);
+          const double out = v * g * p.makeup_lin;
+          if (t0 + d < a.n) {
+            const double il = fabs(v), ol = fabs(out);
+            if (il > cs.in_peak) cs.in_peak = il;
+            if (ol > cs.out_peak) cs.out_peak = ol;
+            if (cs.gr == 1.0 || g < cs.gr) cs.gr = g;
+          }
+          ring_out[r][d][l] = out;
+        }
+      }
+      PIPE_SYNC();
+    }
+    if (active) {
+      a.cs[c].in_peak = cs.in_peak;
+      a.cs[c].out_peak = cs.out_peak;
+      a.cs[c].gr = cs.gr;
+    }
+  } else if (w == 2 || w == 3) {
+    // ---- combs: wave 2 runs combs 0-3 and passes their running sum, wave 3
+    // runs combs 4-7 and passes each output; the allpass wave finishes the
+    // reference's sequential sum acc = (((c0+c1)+c2)+...)+c7 in order.
+    // Branch-free vmem: lanes past the channel count shadow the last channel
+    // (same state, same input, so identical values to identical addresses),
+    // and padding samples of the last chunk write back the value they read
+    // (a no-op), so every chunk issues the same loads and stores and the
+    // prefetch wait never drains the previous chunk's stores.
+    const int i0 = w == 2 ? 0 : 4;
+    const int col = cc;
+    VerbChState vs = a.vs[cc];
+    int cidx[4];  // write positions (advance on padding too)
+    double fst[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      cidx[i] = vs.comb_idx[i0 + i];
+      fst[i] = vs.filter_store[i0 + i];
+    }
+    auto comb_len = [&](int i) { return w == 2 ? kCombLen[i] : kCombLen[4 + i]; };
+    auto comb_base = [&](int i) { return w == 2 ? comb_off(i) : comb_off(4 + i); };
+    double dn[4][kPipeD], dn2[4][kPipeD];  // the next two chunks (loads get two steps to land)
+    auto prefetch = [&](double (&dl)[4][kPipeD], int ahead) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int len = comb_len(i);
+        int pp = cidx[i] + ahead;
+        if (pp >= len) pp -= len;
+#pragma unroll
+        for (int d = 0; d < kPipeD; ++d) {
+          dl[i][d] = a.vbuf[(int64_t)(comb_base(i) + pp) * cpad + col];
+          if (++pp >= len) pp = 0;
+        }
+      }
+    };
+    prefetch(dn, 0);
+    prefetch(dn2, kPipeD);
+    for (int64_t k = 0; k < nch + 3; ++k) {
+      const int64_t my = k - 2;
+      if (my >= 0 && my < nch) {
+        const int r = (int)(my % kRing);
+        const int64_t t0 = my * kPipeD;
+        double dl[4][kPipeD];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int d = 0; d < kPipeD; ++d) {
+            dl[i][d] = dn[i][d];
+            dn[i][d] = dn2[i][d];
+          }
+        prefetch(dn2, 2 * kPipeD);  // chunk after next (lines rewritten only >= 225 samples later)
+#pragma unroll
+        for (int d = 0; d < kPipeD; ++d) {
+          const double xg = vp.gain * ring_out[r][d][l];
+          const bool real = t0 + d < a.n;
+          double acc = 0.0;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            if (a.dbg & 2) break;
+            const double output = dl[i][d];
+            double fs = output * vp.damp_b + fst[i] * vp.damp_a;
+            if (fabs(fs) < 1e-23) fs = 0.0;
+            fst[i] = real ? fs : fst[i];
+            const double wv = xg + fs * vp.feedback;
+            a.vbuf[(int64_t)(comb_base(i) + cidx[i]) * cpad + col] = real ? wv : output;
+            if (++cidx[i] >= comb_len(i)) cidx[i] = 0;
+            if (w == 2)
+              acc += output;
+            else
+              ring_c47[r][i][d][l] = output;
+          }
+          if (w == 2) ring_acc[r][d][l] = acc;
+        }
+      }
+      PIPE_SYNC();
+    }
+    if (active) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        a.vs[c].filter_store[i0 + i] = fst[i];
+        a.vs[c].comb_idx[i0 + i] = (int)((vs.comb_idx[i0 + i] + a.n) % comb_len(i));
+      }
+    }
+  } else {
+    // ---- allpasses + mix + store (branch-free vmem, as the combs wave)
+    const int col = cc;
+    int ap_idx[kVerbAllpass];
+#pragma unroll
+    for (int i = 0; i < kVerbAllpass; ++i) ap_idx[i] = a.vs[cc].ap_idx[i];
+    const int ap0[kVerbAllpass] = {ap_idx[0], ap_idx[1], ap_idx[2], ap_idx[3]};
+    double dn[kVerbAllpass][kPipeD], dn2[kVerbAllpass][kPipeD];
+    auto prefetch = [&](double (&dl)[kVerbAllpass][kPipeD], int ahead) {
+#pragma unroll
+      for (int i = 0; i < kVerbAllpass; ++i) {
+        int pp = ap_idx[i] + ahead;
+        if (pp >= kApLen[i]) pp -= kApLen[i];
+#pragma unroll
+        for (int d = 0; d < kPipeD; ++d) {
+          dl[i][d] = a.vbuf[(int64_t)(ap_off(i) + pp) * cpad + col];
+          if (++pp >= kApLen[i]) pp = 0;
+        }
+      }
+    };
+    prefetch(dn, 0);
+    prefetch(dn2, kPipeD);
+    for (int64_t k = 0; k < nch + 3; ++k) {
+      const int64_t my = k - 3;
+      if (my >= 0 && my < nch) {
+        const int r = (int)(my % kRing);
+        const int64_t t0 = my * kPipeD;
+        double dl[kVerbAllpass][kPipeD];
+#pragma unroll
+        for (int i = 0; i < kVerbAllpass; ++i)
+#pragma unroll
+          for (int d = 0; d < kPipeD; ++d) {
+            dl[i][d] = dn[i][d];
+            dn[i][d] = dn2[i][d];
+          }
+        prefetch(dn2, 2 * kPipeD);
+        double last = 0.0;
+#pragma unroll
+        for (int d = 0; d < kPipeD; ++d) {
+          double acc = ring_acc[r][d][l];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc += ring_c47[r][i][d][l];
+          const double in = ring_out[r][d][l];
+          const bool real = t0 + d < a.n;
+#pragma unroll
+          for (int i = 0; i < kVerbAllpass; ++i) {
+            const double bo = dl[i][d];
+            const double output = bo - acc;
+            a.vbuf[(int64_t)(ap_off(i) + ap_idx[i]) * cpad + col] = real ? acc + bo * vp.ap_feedback : bo;
+            if (++ap_idx[i] >= kApLen[i]) ap_idx[i] = 0;
+            acc = output;
+          }
+          const double y = acc * vp.wet + in * vp.dry;
+          last = real ? y : last;  // padding rewrites the last real sample with its own value
+          xb[min(t0 + d, a.n - 1)] = last;
+        }
+      }
+      PIPE_SYNC();
+    }
+    if (active) {
+#pragma unroll
+      for (int i = 0; i < kVerbAllpass; ++i) a.vs[c].ap_idx[i] = (int)((ap0[i] + a.n) % kApLen[i]);
+    }
+  }
+  if (a.prof && l == 0) {
+    a.prof[(blockIdx.x * 8 + w) * 2] = t_busy;
+    a.prof[(blockIdx.x * 8 + w) * 2 + 1] = clock64() - t_start;
+  }
+#undef PIPE_SYNC
+}
 // fir.Filter block paths (filter.go:64-104 / 109-149).  Output-parallel: one
 // lane per output sample, summing in the reference's term order.
 __global__ __launch_bounds__(256) void k_fir(FirArgs a) {
@@ -320,8 +648,20 @@ static void chain_go(const ChainArgs& a, hipStream_t s) {
   hipLaunchKernelGGL((k_chain<EQ, COMP, VERB>), dim3((unsigned)((a.channels + 63) / 64)), dim3(64), 0, s, a);
 }
 
+bool chain_pipe_ok(int stages, const ChainArgs& a) {
+  return stages == 7 && !a.cp.topology_fb && a.eq.nsec <= kMaxSecPerPass;
+}
+
 void launch_chain(int stages, const ChainArgs& a, hipStream_t s) {
   if (a.channels <= 0 || a.n <= 0) return;
+  static const bool pipe = [] {
+    const char* v = std::getenv("AD_FX_PIPE");
+    return !(v && *v == '0');
+  }();
+  if (pipe && chain_pipe_ok(stages, a)) {
+    hipLaunchKernelGGL(k_chain_pipe, dim3((unsigned)((a.channels + 63) / 64)), dim3(320), 0, s, a);
+    return;
+  }
   switch (stages) {
     case 1: chain_go<true, false, false>(a, s); break;
     case 2: chain_go<false, true, false>(a, s); break;

@@ -62,6 +62,8 @@ struct ChainArgs {
   VerbParams vp;
   VerbChState* vs;  // [channels]
   double* vbuf;     // [channels][kVerbLen]
+  int dbg;          // diagnostics only (AD_FX_DBG): 1 skip gain math, 2 skip combs, 4 skip EQ+detector
+  unsigned long long* prof;  // diagnostics only (AD_FX_PROF): per wave {busy, total} clock ticks
 };
 
 // stages: bit 0 EQ, bit 1 compressor, bit 2 Freeverb
