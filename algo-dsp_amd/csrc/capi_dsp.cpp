@@ -132,7 +132,6 @@ void fx_run(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hipStream_
   a.vp = h->vp;
   a.vs = h->vs.p;
   a.vbuf = h->vbuf.p;
-  if (const char* v = std::getenv("AD_FX_DBG")) a.dbg = std::atoi(v);
   static DevBuf<unsigned long long> prof;
   const bool want_prof = std::getenv("AD_FX_PROF") != nullptr;
   if (want_prof) {

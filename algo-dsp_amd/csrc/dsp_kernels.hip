@@ -338,7 +338,7 @@ __global__ __launch_bounds__(320) void k_chain_pipe(ChainArgs a) {
           double v = x[d];
 #pragma unroll
           for (int s = 0; s < kMaxSecPerPass; ++s) {
-            if (s >= a.eq.nsec || (a.dbg & 4)) break;
+            if (s >= a.eq.nsec) break;
             v = v * q[s][0];
             const double y = q[s][1] * v + d0[s];
             const double n0 = q[s][2] * v - q[s][4] * y + d1[s];
@@ -411,7 +411,7 @@ __global__ __launch_bounds__(320) void k_chain_pipe(ChainArgs a) {
 #pragma unroll 4
         for (int d = 0; d < kPipeD; ++d) {
           const double v = ring_v[r][d][l];
-          const double g = (a.dbg & 1) ? 1.0 : gain_for_level(p, ring_env[r][d][l]);
+          const double g = gain_for_level(p, ring_env[r][d][l]);
           const double out = v * g * p.makeup_lin;
           if (t0 + d < a.n) {
             const double il = fabs(v), ol = fabs(out);
@@ -450,7 +450,6 @@ __global__ __launch_bounds__(320) void k_chain_pipe(ChainArgs a) {
     }
     auto comb_len = [&](int i) { return w == 2 ? kCombLen[i] : kCombLen[4 + i]; };
     auto comb_base = [&](int i) { return w == 2 ? comb_off(i) : comb_off(4 + i); };
-    double dn[4][kPipeD], dn2[4][kPipeD];  // the next two chunks (loads get two steps to land)
     auto prefetch = [&](double (&dl)[4][kPipeD], int ahead) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -464,46 +463,51 @@ __global__ __launch_bounds__(320) void k_chain_pipe(ChainArgs a) {
         }
       }
     };
-    prefetch(dn, 0);
-    prefetch(dn2, kPipeD);
-    for (int64_t k = 0; k < nch + 3; ++k) {
-      const int64_t my = k - 2;
-      if (my >= 0 && my < nch) {
-        const int r = (int)(my % kRing);
-        const int64_t t0 = my * kPipeD;
-        double dl[4][kPipeD];
+    // Three delay-line buffers in rotation, chunk m in b[m % 3]: the loads
+    // of chunk m+2 are issued while chunk m computes and are first waited on
+    // two steps later.  The step loop is unrolled by three so the rotation is
+    // a compile-time renaming (a runtime copy would wait on them at once).
+    auto step = [&](int64_t my, double (&cur)[4][kPipeD], double (&pre)[4][kPipeD]) {
+      if (my < 0 || my >= nch) return;
+      const int r = (int)(my % kRing);
+      const int64_t t0 = my * kPipeD;
+      prefetch(pre, 2 * kPipeD);  // lines are rewritten only >= 225 samples after they are read
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+      for (int d = 0; d < kPipeD; ++d) {
+        const double xg = vp.gain * ring_out[r][d][l];
+        const bool real = t0 + d < a.n;
+        double acc = 0.0;
 #pragma unroll
-          for (int d = 0; d < kPipeD; ++d) {
-            dl[i][d] = dn[i][d];
-            dn[i][d] = dn2[i][d];
-          }
-        prefetch(dn2, 2 * kPipeD);  // chunk after next (lines rewritten only >= 225 samples later)
-#pragma unroll
-        for (int d = 0; d < kPipeD; ++d) {
-          const double xg = vp.gain * ring_out[r][d][l];
-          const bool real = t0 + d < a.n;
-          double acc = 0.0;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            if (a.dbg & 2) break;
-            const double output = dl[i][d];
-            double fs = output * vp.damp_b + fst[i] * vp.damp_a;
-            if (fabs(fs) < 1e-23) fs = 0.0;
-            fst[i] = real ? fs : fst[i];
-            const double wv = xg + fs * vp.feedback;
-            a.vbuf[(int64_t)(comb_base(i) + cidx[i]) * cpad + col] = real ? wv : output;
-            if (++cidx[i] >= comb_len(i)) cidx[i] = 0;
-            if (w == 2)
-              acc += output;
-            else
-              ring_c47[r][i][d][l] = output;
-          }
-          if (w == 2) ring_acc[r][d][l] = acc;
+        for (int i = 0; i < 4; ++i) {
+          const double output = cur[i][d];
+          double fs = output * vp.damp_b + fst[i] * vp.damp_a;
+          if (fabs(fs) < 1e-23) fs = 0.0;
+          fst[i] = real ? fs : fst[i];
+          const double wv = xg + fs * vp.feedback;
+          a.vbuf[(int64_t)(comb_base(i) + cidx[i]) * cpad + col] = real ? wv : output;
+          if (++cidx[i] >= comb_len(i)) cidx[i] = 0;
+          if (w == 2)
+            acc += output;
+          else
+            ring_c47[r][i][d][l] = output;
         }
+        if (w == 2) ring_acc[r][d][l] = acc;
       }
+    };
+    double b0[4][kPipeD], b1[4][kPipeD], b2[4][kPipeD];
+    prefetch(b0, 0);
+    prefetch(b1, kPipeD);
+    for (int64_t k = 0; k < nch + 3; k += 3) {  // chunk my = k - 2 + j, my % 3 = (1 + j) % 3
+      step(k - 2, b1, b0);
       PIPE_SYNC();
+      if (k + 1 < nch + 3) {
+        step(k - 1, b2, b1);
+        PIPE_SYNC();
+      }
+      if (k + 2 < nch + 3) {
+        step(k, b0, b2);
+        PIPE_SYNC();
+      }
     }
     if (active) {
 #pragma unroll
@@ -519,7 +523,6 @@ __global__ __launch_bounds__(320) void k_chain_pipe(ChainArgs a) {
 #pragma unroll
     for (int i = 0; i < kVerbAllpass; ++i) ap_idx[i] = a.vs[cc].ap_idx[i];
     const int ap0[kVerbAllpass] = {ap_idx[0], ap_idx[1], ap_idx[2], ap_idx[3]};
-    double dn[kVerbAllpass][kPipeD], dn2[kVerbAllpass][kPipeD];
     auto prefetch = [&](double (&dl)[kVerbAllpass][kPipeD], int ahead) {
 #pragma unroll
       for (int i = 0; i < kVerbAllpass; ++i) {
@@ -532,22 +535,11 @@ __global__ __launch_bounds__(320) void k_chain_pipe(ChainArgs a) {
         }
       }
     };
-    prefetch(dn, 0);
-    prefetch(dn2, kPipeD);
-    for (int64_t k = 0; k < nch + 3; ++k) {
-      const int64_t my = k - 3;
-      if (my >= 0 && my < nch) {
-        const int r = (int)(my % kRing);
-        const int64_t t0 = my * kPipeD;
-        double dl[kVerbAllpass][kPipeD];
-#pragma unroll
-        for (int i = 0; i < kVerbAllpass; ++i)
-#pragma unroll
-          for (int d = 0; d < kPipeD; ++d) {
-            dl[i][d] = dn[i][d];
-            dn[i][d] = dn2[i][d];
-          }
-        prefetch(dn2, 2 * kPipeD);
+    auto step = [&](int64_t my, double (&cur)[kVerbAllpass][kPipeD], double (&pre)[kVerbAllpass][kPipeD]) {
+      if (my < 0 || my >= nch) return;
+      const int r = (int)(my % kRing);
+      const int64_t t0 = my * kPipeD;
+      prefetch(pre, 2 * kPipeD);
         double last = 0.0;
 #pragma unroll
         for (int d = 0; d < kPipeD; ++d) {
@@ -558,7 +550,7 @@ __global__ __launch_bounds__(320) void k_chain_pipe(ChainArgs a) {
           const bool real = t0 + d < a.n;
 #pragma unroll
           for (int i = 0; i < kVerbAllpass; ++i) {
-            const double bo = dl[i][d];
+            const double bo = cur[i][d];
             const double output = bo - acc;
             a.vbuf[(int64_t)(ap_off(i) + ap_idx[i]) * cpad + col] = real ? acc + bo * vp.ap_feedback : bo;
             if (++ap_idx[i] >= kApLen[i]) ap_idx[i] = 0;
@@ -568,8 +560,21 @@ __global__ __launch_bounds__(320) void k_chain_pipe(ChainArgs a) {
           last = real ? y : last;  // padding rewrites the last real sample with its own value
           xb[min(t0 + d, a.n - 1)] = last;
         }
-      }
+    };
+    double b0[kVerbAllpass][kPipeD], b1[kVerbAllpass][kPipeD], b2[kVerbAllpass][kPipeD];
+    prefetch(b0, 0);
+    prefetch(b1, kPipeD);
+    for (int64_t k = 0; k < nch + 3; k += 3) {  // chunk my = k - 3 + j, my % 3 = j
+      step(k - 3, b0, b2);
       PIPE_SYNC();
+      if (k + 1 < nch + 3) {
+        step(k - 2, b1, b0);
+        PIPE_SYNC();
+      }
+      if (k + 2 < nch + 3) {
+        step(k - 1, b2, b1);
+        PIPE_SYNC();
+      }
     }
     if (active) {
 #pragma unroll

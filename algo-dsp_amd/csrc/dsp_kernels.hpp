@@ -62,7 +62,6 @@ struct ChainArgs {
   VerbParams vp;
   VerbChState* vs;  // [channels]
   double* vbuf;     // [channels][kVerbLen]
-  int dbg;          // diagnostics only (AD_FX_DBG): 1 skip gain math, 2 skip combs, 4 skip EQ+detector
   unsigned long long* prof;  // diagnostics only (AD_FX_PROF): per wave {busy, total} clock ticks
 };
 
