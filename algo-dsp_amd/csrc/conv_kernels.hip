@@ -275,7 +275,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MacOcc<PC, N
   ZEpilogue<NH> epi;
   epi.S = 0.125 / (double)a.M;
   epi.sS = sgn * epi.S;
-  epi.zc = a.Y + (int64_t)c * a.y_ch_stride + k;  // k = M: padding column
+  // Z rows are stored even bins first, then odd bins (zpos), so K3's split
+  // inverse reads each half with fully contiguous wave loads; bin M (only
+  // a partner, never an output) writes into the padding column M.
+  const int zpos = k < a.M ? ((k & 1) ? (a.M >> 1) + (k >> 1) : (k >> 1)) : a.M;
+  epi.zc = a.Y + (int64_t)c * a.y_ch_stride + zpos;
   epi.jstride = a.MS;
   epi.tw = (k < a.M) ? c_scale(c_conj(a.twN[k]), epi.S) : make_double2(0.0, 0.0);
   epi.stw = c_scale(epi.tw, sgn);

@@ -129,7 +129,10 @@ __global__ __launch_bounds__((FftPlan<M, V>::BLOCK)) void k_irfft_store(IrfftArg
   const double2* Zb = a.Y + (int64_t)c * a.y_ch_stride + (int64_t)j * a.MS;
   double2 v[V];
 #pragma unroll
-  for (int s = 0; s < V; ++s) v[s] = active ? Zb[pass0_index<M, V>(tid, s)] : make_double2(0.0, 0.0);
+  for (int s = 0; s < V; ++s) {
+    const int k = pass0_index<M, V>(tid, s);
+    v[s] = active ? Zb[(k & 1) ? M / 2 + (k >> 1) : (k >> 1)] : make_double2(0.0, 0.0);  // even|odd row layout
+  }
   fft_run<M, V, false>(v, tid, lds, TwGlobal{a.twM});
   if (!active) return;
   irfft_store_out<M, V>(v, tid, a.out + (int64_t)c * a.out_stride, a.o0 + (int64_t)j * L - M, a.out_len, a.aligned);
@@ -142,8 +145,9 @@ __global__ __launch_bounds__((FftPlan<M, V>::BLOCK)) void k_irfft_store(IrfftArg
 //   K1: Zr[k] = E[k] + W_M^k O[k], Zr[k+M/2] = E[k] - W_M^k O[k],
 //       E = FFT(z[2m]), O = FFT(z[2m+1]), z[m] = x[2m] + i x[2m+1];
 //   K3: z[M/2+m] = A[m] - W_M^-m B[m] (only the upper half is kept),
-//       A = IFFT(Z[2k]), B = IFFT(Z[2k+1]).
-// Each thread's E/O (A/B) inputs are 32 contiguous bytes, and its outputs of
+//       A = IFFT(Z[2k]), B = IFFT(Z[2k+1]); k_fdl_mac stores Z rows as
+//       [even bins | odd bins], so A's and B's inputs are contiguous halves.
+// Each thread's E/O inputs are 32 contiguous bytes, and its outputs of
 // both halves are the same last-pass indices, so the radix-2 step needs no
 // exchange.  The LDS image is that of an M/2 transform (69.6 KiB at M = 8192),
 // so two workgroups share a CU and one's HBM phase hides under the other's
@@ -235,9 +239,9 @@ __global__ __launch_bounds__((SplitPlan<M>::T)) __attribute__((amdgpu_waves_per_
   double2 av[V], bv[V];
 #pragma unroll
   for (int s = 0; s < V; ++s) {
-    const double2* p = Zb + 2 * pass0_index<M2, V>(tid, s);
-    av[s] = p[0];
-    bv[s] = p[1];
+    const int k = pass0_index<M2, V>(tid, s);  // Z row = [even bins | odd bins] (k_fdl_mac)
+    av[s] = Zb[k];
+    bv[s] = Zb[M2 + k];
   }
   __syncthreads();  // twiddle tables
   fft_run<M2, V, false>(av, tid, lds, twS);
