@@ -1,0 +1,333 @@
+// Device kernels of the large power-of-two FFT and the pointwise spectral
+// operations of CorrelateFFT / Deconvolve / InverseFilter (see bigfft.hpp).
+#include "bigfft.hpp"
+
+#include <cmath>
+#include <string>
+
+#include "ad_common.hpp"
+#include "fft_device.hpp"
+
+namespace adsp {
+
+// ---------------------------------------------------------------------------
+// One global Stockham pass of radix R (16 <= R <= 4096): F = BLOCK*16/R
+// butterflies per workgroup.
+// ---------------------------------------------------------------------------
+template <int R, bool FWD, bool REALIN, bool REALOUT>
+__global__ __launch_bounds__((FftPlan<R, 16>::BLOCK)) void k_fft_pass(FftPassArgs a) {
+  using Plan = FftPlan<R, 16>;
+  constexpr int V = 16, T = Plan::T, F = Plan::F, BLOCK = Plan::BLOCK, MP = Plan::MP;
+  __shared__ __attribute__((aligned(16))) double2 lds_all[F * MP];
+  const int bt = blockIdx.y;
+  const int64_t nb = a.N / R;  // butterflies
+  const int64_t j0 = (int64_t)blockIdx.x * F;
+
+  // stage in: element r of butterfly j0 + jj is x[j0 + jj + r nb]; jj fastest
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    const int idx = i * BLOCK + (int)threadIdx.x;
+    const int jj = idx % F, r = idx / F;
+    const int64_t j = j0 + jj;
+    double2 v = make_double2(0.0, 0.0);
+    if (j < nb) {
+      const int64_t g = j + (int64_t)r * nb;
+      if constexpr (REALIN) {
+        const double* x = a.xr + bt * a.in_batch;
+        v.x = g < a.n_real ? x[g] : 0.0;
+      } else {
+        v = a.in[bt * a.in_batch + g];
+      }
+    }
+    lds_all[jj * MP + lds_pad(r)] = v;
+  }
+  __syncthreads();
+
+  const int f = threadIdx.x / T, tid = threadIdx.x % T;
+  double2* lds = lds_all + f * MP;
+  const int64_t j = j0 + f;
+  double2 v[V];
+#pragma unroll
+  for (int s = 0; s < V; ++s) v[s] = lds[lds_pad(pass0_index<R, V>(tid, s))];
+  if (a.Ns > 1) {  // pre-twiddle W_{Ns R}^{(j mod Ns) r} = W_N^{(j mod Ns) r N/(Ns R)}
+    const int64_t jm = j & (a.Ns - 1);
+    const int64_t step = a.N / (a.Ns * R);
+    const int64_t mask = ((int64_t)1 << a.S) - 1;
+#pragma unroll
+    for (int s = 0; s < V; ++s) {
+      const int64_t e = jm * pass0_index<R, V>(tid, s) * step;
+      double2 w = c_mul(a.tw_lo[e & mask], a.tw_hi[e >> a.S]);
+      if (!FWD) w = c_conj(w);
+      v[s] = c_mul(v[s], w);
+    }
+  }
+  __syncthreads();
+  fft_run<R, V, FWD>(v, tid, lds, TwGlobal{a.twR});
+  __syncthreads();
+#pragma unroll
+  for (int s = 0; s < V; ++s) lds[lds_pad(last_pass_index<R, V>(tid, s))] = v[s];
+  __syncthreads();
+
+  // stage out: output rr of butterfly j goes to (j/Ns) Ns R + (j mod Ns) + rr Ns
+  const int64_t Ns = a.Ns;
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    const int idx = i * BLOCK + (int)threadIdx.x;
+    int jj, rr;
+    if (Ns == 1) {  // each butterfly's R outputs are contiguous
+      rr = idx % R;
+      jj = idx / R;
+    } else {  // consecutive butterflies are contiguous for a fixed rr
+      jj = idx % F;
+      rr = idx / F;
+    }
+    const int64_t jo = j0 + jj;
+    if (jo >= nb) continue;
+    const double2 val = lds_all[jj * MP + lds_pad(rr)];
+    const int64_t o = (jo & ~(Ns - 1)) * R + (jo & (Ns - 1)) + (int64_t)rr * Ns;
+    if constexpr (REALOUT)
+      a.out_real[bt * a.out_batch + o] = val.x * a.scale;
+    else
+      a.out[bt * a.out_batch + o] = val;
+  }
+}
+
+// Naive DFT for N <= 8 (one thread per output bin).
+__global__ void k_dft_small(FftPassArgs a, int fwd) {
+  const int k = threadIdx.x;
+  const int bt = blockIdx.y;
+  if (k >= a.N) return;
+  double2 acc = make_double2(0.0, 0.0);
+  for (int n = 0; n < a.N; ++n) {
+    double2 x;
+    if (a.xr) {
+      const int64_t g = n;
+      x = make_double2(g < a.n_real ? a.xr[bt * a.in_batch + g] : 0.0, 0.0);
+    } else {
+      x = a.in[bt * a.in_batch + n];
+    }
+    const int e = (int)(((int64_t)n * k) % a.N);
+    double2 w = a.tw_lo[e];  // S covers the whole table for N <= 8
+    if (!fwd) w = c_conj(w);
+    acc = c_add(acc, c_mul(x, w));
+  }
+  if (a.out_real)
+    a.out_real[bt * a.out_batch + k] = acc.x * a.scale;
+  else
+    a.out[bt * a.out_batch + k] = acc;
+}
+
+// ---------------------------------------------------------------------------
+// Host plan
+// ---------------------------------------------------------------------------
+namespace {
+std::vector<double2> twiddles(int64_t N, int64_t count, int64_t stride) {
+  // W_N^(i*stride) = exp(-2 pi i (i*stride)/N), evaluated in long double
+  std::vector<double2> t((size_t)count);
+  const long double two_pi = 6.283185307179586476925286766559005768L;
+  for (int64_t i = 0; i < count; ++i) {
+    const int64_t e = (i * stride) % N;
+    const long double ang = -two_pi * (long double)e / (long double)N;
+    t[(size_t)i] = make_double2((double)cosl(ang), (double)sinl(ang));
+  }
+  return t;
+}
+double2* upload(const std::vector<double2>& v) {
+  double2* p = nullptr;
+  AD_HIP(hipMalloc(reinterpret_cast<void**>(&p), v.size() * sizeof(double2)));
+  AD_HIP(hipMemcpy(p, v.data(), v.size() * sizeof(double2), hipMemcpyHostToDevice));
+  return p;
+}
+
+template <bool FWD, bool RI, bool RO>
+void launch_pass_r(int R, const FftPassArgs& a, int batch, hipStream_t s) {
+  const int64_t nb = a.N / R;
+#define AD_PASS(RR)                                                                                 \
+  case RR: {                                                                                        \
+    using Plan = FftPlan<RR, 16>;                                                                   \
+    const dim3 grid((unsigned)((nb + Plan::F - 1) / Plan::F), (unsigned)batch);                     \
+    hipLaunchKernelGGL((k_fft_pass<RR, FWD, RI, RO>), grid, dim3(Plan::BLOCK), 0, s, a);            \
+    break;                                                                                          \
+  }
+  switch (R) {
+    AD_PASS(16)
+    AD_PASS(32)
+    AD_PASS(64)
+    AD_PASS(128)
+    AD_PASS(256)
+    AD_PASS(512)
+    AD_PASS(1024)
+    AD_PASS(2048)
+    AD_PASS(4096)
+    default:
+      AD_FAIL(AD_ERR_INTERNAL, "BigFft: unsupported radix");
+  }
+#undef AD_PASS
+}
+
+template <bool FWD>
+void launch_pass(int R, bool ri, bool ro, const FftPassArgs& a, int batch, hipStream_t s) {
+  if (ri && ro) return launch_pass_r<FWD, true, true>(R, a, batch, s);
+  if (ri) return launch_pass_r<FWD, true, false>(R, a, batch, s);
+  if (ro) return launch_pass_r<FWD, false, true>(R, a, batch, s);
+  launch_pass_r<FWD, false, false>(R, a, batch, s);
+}
+}  // namespace
+
+BigFft::BigFft(int64_t N) : N_(N) {
+  if (!is_pow2(N) || N > ((int64_t)1 << 27)) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "BigFft: size must be a power of two <= 2^27");
+  int k = 0;
+  while (((int64_t)1 << k) < N) ++k;
+  if (k <= 3) {
+    S_ = k;  // the naive DFT reads W_N^e straight from lo
+  } else if (k <= 12) {
+    radix_.push_back((int)N);
+    S_ = (k + 1) / 2;
+  } else {
+    const int np = (k + 8) / 9;
+    const int base = k / np, extra = k % np;
+    for (int p = 0; p < np; ++p) radix_.push_back(1 << (base + (p < extra ? 1 : 0)));
+    S_ = (k + 1) / 2;
+  }
+  const int64_t nlo = (int64_t)1 << S_;
+  tw_lo_ = upload(twiddles(N, nlo, 1));
+  tw_hi_ = upload(twiddles(N, std::max<int64_t>(1, N >> S_), nlo));
+  for (int R : radix_) twR_.push_back(upload(twiddles(R, R, 1)));
+}
+
+BigFft::~BigFft() {
+  for (double2* p : twR_) (void)hipFree(p);
+  if (tw_lo_) (void)hipFree(tw_lo_);
+  if (tw_hi_) (void)hipFree(tw_hi_);
+}
+
+void BigFft::run(bool forward, const double2* in, const double* xr, int64_t n_real, int64_t in_batch, double2* out,
+                 double* out_real, int64_t out_batch, double scale, int batch, double2* scratch,
+                 hipStream_t s) const {
+  FftPassArgs a{};
+  a.N = N_;
+  a.tw_lo = tw_lo_;
+  a.tw_hi = tw_hi_;
+  a.S = S_;
+  a.scale = scale;
+  if (radix_.empty()) {  // N <= 8
+    a.in = in;
+    a.xr = xr;
+    a.n_real = n_real;
+    a.in_batch = in_batch;
+    a.out = out;
+    a.out_real = out_real;
+    a.out_batch = out_batch;
+    hipLaunchKernelGGL(k_dft_small, dim3(1, (unsigned)batch), dim3(64), 0, s, a, forward ? 1 : 0);
+    AD_HIP(hipGetLastError());
+    return;
+  }
+  // pass p writes the final destination when p is last, else one of two
+  // scratch halves (pass p-1's output is pass p's input)
+  const int P = (int)radix_.size();
+  double2* half[2] = {scratch, scratch + N_ * batch};
+  int64_t Ns = 1;
+  const double2* cur = in;
+  for (int p = 0; p < P; ++p) {
+    const int R = radix_[(size_t)p];
+    const bool first = p == 0, last = p == P - 1;
+    a.in = first ? in : cur;
+    a.xr = first ? xr : nullptr;
+    a.n_real = n_real;
+    a.in_batch = first ? in_batch : N_;
+    a.Ns = Ns;
+    a.twR = twR_[(size_t)p];
+    double2* dst = last ? out : half[p & 1];
+    a.out = dst;
+    a.out_real = last ? out_real : nullptr;
+    a.out_batch = last ? out_batch : N_;
+    const bool ri = first && xr != nullptr;
+    const bool ro = last && out_real != nullptr;
+    if (forward)
+      launch_pass<true>(R, ri, ro, a, batch, s);
+    else
+      launch_pass<false>(R, ri, ro, a, batch, s);
+    AD_HIP(hipGetLastError());
+    cur = dst;
+    Ns *= R;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Pointwise spectral operations, restated in Go complex128 arithmetic:
+// products as (ac - bd, ad + bc), quotients by the Go runtime's
+// complex128div (Smith's algorithm), magnitudes by math.Hypot.
+// ---------------------------------------------------------------------------
+#pragma clang fp contract(off)
+__device__ __forceinline__ double2 go_cmul(double2 a, double2 b) {
+  return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__device__ __forceinline__ double2 go_cdiv(double2 n, double2 m) {
+  double e, f;
+  if (fabs(m.x) >= fabs(m.y)) {
+    const double ratio = m.y / m.x;
+    const double denom = m.x + ratio * m.y;
+    e = (n.x + n.y * ratio) / denom;
+    f = (n.y - n.x * ratio) / denom;
+  } else {
+    const double ratio = m.x / m.y;
+    const double denom = m.y + ratio * m.x;
+    e = (n.x * ratio + n.y) / denom;
+    f = (n.y * ratio - n.x) / denom;
+  }
+  return make_double2(e, f);
+}
+__device__ __forceinline__ double go_hypot(double p, double q) {
+  p = fabs(p);
+  q = fabs(q);
+  if (isinf(p) || isinf(q)) return INFINITY;
+  if (isnan(p) || isnan(q)) return NAN;
+  if (p < q) {
+    const double t = p;
+    p = q;
+    q = t;
+  }
+  if (p == 0) return 0;
+  q = q / p;
+  return p * sqrt(1 + q * q);
+}
+
+__global__ __launch_bounds__(256) void k_spec_op(int op, double2* __restrict__ a, const double2* __restrict__ b,
+                                                 int64_t n, double eps, unsigned long long* bad) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const double2 x = a[i];
+  double2 r;
+  switch (op) {
+    case kSpecCorr:
+      r = go_cmul(x, c_conj(b[i]));
+      break;
+    case kSpecNaive: {
+      const double2 h = b[i];
+      if (go_hypot(h.x, h.y) < 1e-15) atomicMin(bad, (unsigned long long)i);
+      r = go_cdiv(x, h);
+      break;
+    }
+    case kSpecReg: {
+      const double2 h = b[i];
+      const double mag2 = h.x * h.x + h.y * h.y;
+      r = go_cdiv(go_cmul(x, c_conj(h)), make_double2(mag2 + eps, 0.0));
+      break;
+    }
+    default: {  // kSpecInvFilt
+      const double mag2 = x.x * x.x + x.y * x.y;
+      r = go_cdiv(c_conj(x), make_double2(mag2 + eps, 0.0));
+      break;
+    }
+  }
+  a[i] = r;
+}
+
+void launch_spec_op(int op, double2* a, const double2* b, int64_t n, double eps, unsigned long long* bad,
+                    hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_spec_op, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, op, a, b, n, eps, bad);
+  AD_HIP(hipGetLastError());
+}
+
+}  // namespace adsp

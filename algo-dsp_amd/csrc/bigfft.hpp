@@ -1,0 +1,76 @@
+// Power-of-two complex FFTs of any size on the device (spectral row 8(f)3:
+// CorrelateFFT / Deconvolve / InverseFilter, dsp/conv/correlate.go:111-172,
+// deconvolve.go:72-394).  These call algo-fft's NewPlan64(n).Forward/Inverse
+// on one whole zero-padded signal, so the size is nextPow2 of the signal
+// (up to 2^27 here), far past one workgroup's LDS.
+//
+// Global Stockham decomposition N = R_0 R_1 ... R_{P-1}: pass p treats the
+// array as N/R_p butterflies j of radix R_p on elements j + r N/R_p,
+// pre-twiddled by W_{Ns R}^{(j mod Ns) r} (Ns = R_0 .. R_{p-1}), and writes
+// them to (j/Ns) Ns R + (j mod Ns) + r Ns, so the result is in natural order
+// after the last pass (no bit reversal, no transpose pass).  Each radix-R
+// butterfly is an LDS-resident FftPlan<R, 16> transform; a workgroup carries
+// F = 4096/R of them (F consecutive j), staged through LDS in both directions
+// so every global access moves runs of F (or R) contiguous complex128 values.
+// R <= 512 for multi-pass plans keeps F >= 8 (128-byte runs).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <vector>
+
+namespace adsp {
+
+struct FftPassArgs {
+  const double2* in;    // complex input (nullptr when xr is used)
+  const double* xr;     // real input (first pass only), zero past n_real
+  int64_t n_real;
+  int64_t in_batch;     // batch stride (elements) of the input
+  double2* out;         // complex output
+  double* out_real;     // real-part output (last pass only), scaled by `scale`
+  int64_t out_batch;
+  double scale;
+  int64_t N;            // transform size
+  int64_t Ns;           // product of the previous radices
+  const double2* twR;   // W_R^e, e < R (the pass's LDS transform)
+  const double2* tw_lo; // W_N^e, e < 2^S          (pre-twiddles W_N^e = lo[e & (2^S-1)] * hi[e >> S])
+  const double2* tw_hi; // W_N^(e 2^S), e < N/2^S
+  int S;
+};
+
+// Device-resident plan and twiddle tables of one size.
+class BigFft {
+ public:
+  explicit BigFft(int64_t N);
+  ~BigFft();
+  BigFft(const BigFft&) = delete;
+  BigFft& operator=(const BigFft&) = delete;
+
+  int64_t size() const { return N_; }
+  // Forward (inverse: conj twiddles, then *scale on output) transform of
+  // `batch` arrays.  Input: complex `in` or real `xr` (n_real valid values,
+  // zero padded); output: complex `out` or its real part `out_real`.
+  // scratch: N*batch complex; in/out may alias each other and scratch must not.
+  void run(bool forward, const double2* in, const double* xr, int64_t n_real, int64_t in_batch, double2* out,
+           double* out_real, int64_t out_batch, double scale, int batch, double2* scratch, hipStream_t s) const;
+
+ private:
+  int64_t N_;
+  int S_ = 0;
+  std::vector<int> radix_;
+  std::vector<double2*> twR_;  // per pass
+  double2* tw_lo_ = nullptr;
+  double2* tw_hi_ = nullptr;
+};
+
+// Pointwise spectral operations (contraction off: Go complex128 arithmetic).
+// corr:    a[k] = a[k] * conj(b[k])                          (correlate.go:150-156)
+// naive:   a[k] = a[k] / b[k]; first k with |b[k]| < 1e-15 -> *bad (atomicMin) (deconvolve.go:146-154)
+// reg:     a[k] = a[k] * conj(b[k]) / (|b[k]|^2 + eps)       (deconvolve.go:208-213, 298-303)
+// invfilt: a[k] = conj(a[k]) / (|a[k]|^2 + eps)              (deconvolve.go:384-389)
+enum SpecOp { kSpecCorr = 0, kSpecNaive = 1, kSpecReg = 2, kSpecInvFilt = 3 };
+void launch_spec_op(int op, double2* a, const double2* b, int64_t n, double eps, unsigned long long* bad,
+                    hipStream_t s);
+
+}  // namespace adsp

@@ -1,0 +1,218 @@
+// C ABI of the spectral-division / correlation row:
+// CorrelateFFT (dsp/conv/correlate.go:111-172), Deconvolve with its naive,
+// regularised and Wiener methods (deconvolve.go:72-323) and InverseFilter
+// (deconvolve.go:354-394), on the device FFT of bigfft.hip.  Each call copies
+// its host inputs in, runs forward FFTs of the zero-padded real inputs (two
+// transforms in one batched launch per pass), one pointwise kernel, one
+// inverse FFT whose last pass writes the scaled real part, and copies out.
+#pragma clang fp contract(off)  // host-side variance/NSR arithmetic as Go computes it
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <string>
+
+#include "ad_common.hpp"
+#include "bigfft.hpp"
+
+using namespace adsp;
+
+namespace {
+
+// deconvolve.go:326-349 variance (two passes, sequential sums)
+double go_variance(const double* x, int64_t n) {
+  if (n == 0) return 0;
+  double mean = 0;
+  for (int64_t i = 0; i < n; ++i) mean += x[i];
+  mean /= (double)n;
+  double sum = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    const double d = x[i] - mean;
+    sum += d * d;
+  }
+  return sum / (double)n;
+}
+
+// Forward FFTs of `batch` zero-padded real arrays already in xr ([batch][N]).
+struct SpectralRun {
+  int64_t N;
+  BigFft fft;
+  DevBuf<double2> spec, scratch;
+  DevBuf<double> res;
+  explicit SpectralRun(int64_t n) : N(n), fft(n) {}
+  void forward(const double* xr_dev, int batch, hipStream_t s) {
+    spec.alloc((size_t)(N * batch));
+    scratch.alloc((size_t)(2 * N * batch));
+    fft.run(true, nullptr, xr_dev, N, N, spec.p, nullptr, N, 1.0, batch, scratch.p, s);
+  }
+  // inverse of spec[0..N) -> res (real part, 1/N as algo-fft's Inverse)
+  void inverse(hipStream_t s) {
+    res.alloc((size_t)N);
+    fft.run(false, spec.p, nullptr, 0, N, nullptr, res.p, N, 1.0 / (double)N, 1, scratch.p, s);
+  }
+};
+
+// Stages host arrays into one zero-padded [count][N] device buffer.
+void stage_real(DevBuf<double>& buf, int64_t N, const double* const* src, const int64_t* len, int count,
+                hipStream_t s) {
+  buf.alloc((size_t)(N * count));
+  AD_HIP(hipMemsetAsync(buf.p, 0, (size_t)(N * count) * sizeof(double), s));
+  for (int i = 0; i < count; ++i)
+    if (len[i] > 0)
+      AD_HIP(hipMemcpyAsync(buf.p + (int64_t)i * N, src[i], (size_t)len[i] * sizeof(double), hipMemcpyHostToDevice,
+                            s));
+}
+
+}  // namespace
+
+extern "C" {
+
+ad_deconv_options ad_deconv_default_options(void) {
+  // deconvolve.go:57-63 DefaultDeconvOptions
+  ad_deconv_options o;
+  o.method = AD_DECONV_REGULARIZED;
+  o.epsilon = 1e-6;
+  o.noise_variance = 0;
+  o.signal_variance = 0;
+  return o;
+}
+
+int ad_correlate_fft(const double* a, int64_t n, const double* b, int64_t m, double* out, int device) {
+  return guard([&] {
+    if (n <= 0 || m <= 0 || !a || !b) AD_FAIL(AD_ERR_EMPTY_INPUT, "conv: empty input");
+    if (!out) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "null output");
+    DeviceScope ds(pick_device(device));
+    hipStream_t s = nullptr;
+    const int64_t N = next_pow2(n + m - 1);  // correlate.go:119
+    SpectralRun run(N);
+    DevBuf<double> xr;
+    const double* src[2] = {a, b};
+    const int64_t len[2] = {n, m};
+    stage_real(xr, N, src, len, 2, s);
+    run.forward(xr.p, 2, s);
+    launch_spec_op(kSpecCorr, run.spec.p, run.spec.p + N, N, 0.0, nullptr, s);
+    run.inverse(s);
+    // correlate.go:165-171: lags 0..n-1 from the front, -(m-1)..-1 from the back
+    AD_HIP(hipMemcpyAsync(out + (m - 1), run.res.p, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, s));
+    if (m > 1)
+      AD_HIP(hipMemcpyAsync(out, run.res.p + (N - m + 1), (size_t)(m - 1) * sizeof(double), hipMemcpyDeviceToHost,
+                            s));
+    AD_HIP(hipStreamSynchronize(s));
+  });
+}
+
+int ad_correlate_fft_device(const double* a, int64_t n, const double* b, int64_t m, double* out, int device,
+                            void* stream) {
+  return guard([&] {
+    if (n <= 0 || m <= 0 || !a || !b) AD_FAIL(AD_ERR_EMPTY_INPUT, "conv: empty input");
+    if (!out) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "null output");
+    DeviceScope ds(pick_device(device));
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const int64_t N = next_pow2(n + m - 1);
+    SpectralRun run(N);
+    DevBuf<double> xr;
+    xr.alloc((size_t)(2 * N));
+    AD_HIP(hipMemsetAsync(xr.p, 0, (size_t)(2 * N) * sizeof(double), s));
+    AD_HIP(hipMemcpyAsync(xr.p, a, (size_t)n * sizeof(double), hipMemcpyDeviceToDevice, s));
+    AD_HIP(hipMemcpyAsync(xr.p + N, b, (size_t)m * sizeof(double), hipMemcpyDeviceToDevice, s));
+    run.forward(xr.p, 2, s);
+    launch_spec_op(kSpecCorr, run.spec.p, run.spec.p + N, N, 0.0, nullptr, s);
+    run.inverse(s);
+    AD_HIP(hipMemcpyAsync(out + (m - 1), run.res.p, (size_t)n * sizeof(double), hipMemcpyDeviceToDevice, s));
+    if (m > 1)
+      AD_HIP(hipMemcpyAsync(out, run.res.p + (N - m + 1), (size_t)(m - 1) * sizeof(double), hipMemcpyDeviceToDevice,
+                            s));
+    // the temporaries are freed on return: finish the stream's work first
+    AD_HIP(hipStreamSynchronize(s));
+  });
+}
+
+int ad_deconvolve(const double* signal, int64_t n, const double* kernel, int64_t m, const ad_deconv_options* opts,
+                  double* out, int64_t out_cap, int64_t* out_len, int device) {
+  return guard([&] {
+    // deconvolve.go:72-101
+    if (n <= 0 || !signal) AD_FAIL(AD_ERR_EMPTY_INPUT, "conv: empty input");
+    if (m <= 0 || !kernel) AD_FAIL(AD_ERR_EMPTY_KERNEL, "conv: empty kernel");
+    ad_deconv_options o = opts ? *opts : ad_deconv_default_options();
+    int op = kSpecReg;
+    double eps = o.epsilon;
+    switch (o.method) {
+      case AD_DECONV_NAIVE:
+        op = kSpecNaive;
+        break;
+      case AD_DECONV_REGULARIZED:
+        if (eps <= 0) eps = 1e-6;
+        break;
+      case AD_DECONV_WIENER: {  // deconvolve.go:235-262
+        double noise = o.noise_variance, sig = o.signal_variance;
+        if (sig <= 0) sig = go_variance(signal, n);
+        if (noise <= 0) noise = sig * 0.01;
+        double nsr = noise / sig;
+        if (nsr <= 0) nsr = 1e-6;
+        eps = nsr;
+        break;
+      }
+      default:
+        eps = 1e-6;
+        break;
+    }
+    const int64_t N = next_pow2(n);  // deconvolve.go:114,180,264: the SIGNAL length
+    if (m > N) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "conv: kernel longer than the transform (reference indexes out of range)");
+    int64_t olen = n - m + 1;
+    if (olen <= 0) olen = n;
+    if (out_len) *out_len = olen;
+    if (!out || out_cap < olen) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "output capacity too small");
+    DeviceScope ds(pick_device(device));
+    hipStream_t s = nullptr;
+    SpectralRun run(N);
+    DevBuf<double> xr;
+    const double* src[2] = {signal, kernel};
+    const int64_t len[2] = {n, m};
+    stage_real(xr, N, src, len, 2, s);
+    run.forward(xr.p, 2, s);
+    DevBuf<unsigned long long> bad;
+    if (op == kSpecNaive) {
+      bad.alloc(1);
+      AD_HIP(hipMemsetAsync(bad.p, 0xff, sizeof(unsigned long long), s));
+    }
+    launch_spec_op(op, run.spec.p, run.spec.p + N, N, eps, bad.p, s);
+    if (op == kSpecNaive) {
+      unsigned long long first = 0;
+      AD_HIP(hipMemcpyAsync(&first, bad.p, sizeof(first), hipMemcpyDeviceToHost, s));
+      AD_HIP(hipStreamSynchronize(s));
+      if (first != ~0ull)
+        AD_FAIL(AD_ERR_DIVISION_BY_ZERO,
+                "conv: division by zero in deconvolution: at frequency bin " + std::to_string(first));
+    }
+    run.inverse(s);
+    AD_HIP(hipMemcpyAsync(out, run.res.p, (size_t)olen * sizeof(double), hipMemcpyDeviceToHost, s));
+    AD_HIP(hipStreamSynchronize(s));
+  });
+}
+
+int ad_inverse_filter(const double* kernel, int64_t m, int64_t length, double epsilon, double* out, int device) {
+  return guard([&] {
+    // deconvolve.go:354-394
+    if (m <= 0 || !kernel) AD_FAIL(AD_ERR_EMPTY_KERNEL, "conv: empty kernel");
+    if (length < 0) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "negative inverse-filter length");
+    if (epsilon <= 0) epsilon = 1e-6;
+    if (length == 0) return;
+    if (!out) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "null output");
+    const int64_t N = next_pow2(length);
+    DeviceScope ds(pick_device(device));
+    hipStream_t s = nullptr;
+    SpectralRun run(N);
+    DevBuf<double> xr;
+    const double* src[1] = {kernel};
+    const int64_t len[1] = {m < N ? m : N};  // kernel truncated to the transform (:367)
+    stage_real(xr, N, src, len, 1, s);
+    run.forward(xr.p, 1, s);
+    launch_spec_op(kSpecInvFilt, run.spec.p, nullptr, N, epsilon, nullptr, s);
+    run.inverse(s);
+    AD_HIP(hipMemcpyAsync(out, run.res.p, (size_t)length * sizeof(double), hipMemcpyDeviceToHost, s));
+    AD_HIP(hipStreamSynchronize(s));
+  });
+}
+
+}  // extern "C"

@@ -249,10 +249,18 @@ template <int PC, int NH, bool FIRST, int DQ>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MacOcc<PC, NH>::W))) void k_fdl_mac(MacArgs a) {
   constexpr int BW = 32 / NH;  // bin pairs per wave
   const int lg = xcd_remap(blockIdx.x, gridDim.x);
-  const int ry = lg % a.ny;
-  const int t = lg / a.ny;
-  const int bx = t % a.nx;
-  const int c = t / a.nx;
+  int ry, bx, c;
+  if (a.bx_fast) {  // neighbouring waves: neighbouring bin groups of the same rows
+    bx = lg % a.nx;
+    const int t = lg / a.nx;
+    ry = t % a.ny;
+    c = t / a.ny;
+  } else {  // neighbouring waves: consecutive runs of one bin group
+    ry = lg % a.ny;
+    const int t = lg / a.ny;
+    bx = t % a.nx;
+    c = t / a.nx;
+  }
   const int lane = threadIdx.x;
   const bool ph = NH == 2 && lane >= 32;
   const bool mi = NH == 2 ? ((lane >> 4) & 1) : (lane >> 5);
@@ -275,10 +283,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MacOcc<PC, N
   ZEpilogue<NH> epi;
   epi.S = 0.125 / (double)a.M;
   epi.sS = sgn * epi.S;
-  // Z rows are stored even bins first, then odd bins (zpos), so K3's split
-  // inverse reads each half with fully contiguous wave loads; bin M (only
-  // a partner, never an output) writes into the padding column M.
-  const int zpos = k < a.M ? ((k & 1) ? (a.M >> 1) + (k >> 1) : (k >> 1)) : a.M;
+  // Z rows in wave-lane order (zrow_pos): one aligned 1-KiB run per wave row.
+  const int zpos = zrow_pos(k, a.M);
   epi.zc = a.Y + (int64_t)c * a.y_ch_stride + zpos;
   epi.jstride = a.MS;
   epi.tw = (k < a.M) ? c_scale(c_conj(a.twN[k]), epi.S) : make_double2(0.0, 0.0);
@@ -288,9 +294,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MacOcc<PC, N
     const int pb = a.p0 + (ph ? PC : 0);  // this lane's first partition
     double2 h[PC];
 #pragma unroll
+    for (int q = 0; q < PC; ++q) h[q] = Hc[(int64_t)min(pb + q, a.P - 1) * a.MS];
+#pragma unroll
     for (int q = 0; q < PC; ++q) {
-      const double2 hv = Hc[(int64_t)min(pb + q, a.P - 1) * a.MS];
-      h[q] = up(hv);
+      h[q] = up(h[q]);
       if (pb + q >= a.P) h[q] = make_double2(0.0, 0.0);
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -317,6 +324,196 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MacOcc<PC, N
       st.advance<PC>();
     }
   }
+}
+
+// ---------------------------------------------------------------------------
+// K2 with the X stream staged through LDS by LDS-DMA (global_load_lds_dwordx4):
+// the same bin-stationary MAC as k_fdl_mac, but the prefetched X rows sit in
+// a per-wave LDS ring of DL rows (1 KiB each) instead of VGPRs.  At PC = 16
+// the h and accumulator registers (128 VGPRs) leave room for only 4 rows in
+// registers at 2 waves/SIMD, i.e. 8 KiB in flight per SIMD, which at HBM
+// latency caps K2 near 4.5 TB/s; the LDS ring keeps DL rows in flight per
+// wave at no VGPR cost.
+//
+// The DMAs are inline asm (hipcc would drain every LDS-DMA with vmcnt(0)
+// before the first LDS read), so their completion is counted here.  The
+// vector-memory counter retires in issue order on gfx9; per row the issue
+// order is: [wait row U] [ds_read row U] [DMA row U + DL] [store output U]:
+//   warm-up group:        DL - 1 operations follow row U's DMA
+//   first output group:   DL - 1 + min(U, DL)
+//   steady state:         2 DL - 1
+// (more operations in flight than counted only makes a wait conservative).
+// Rows past the run (logical index > lend) read the ring's zero row, so the
+// tail prefetch is L2 hits instead of HBM rows.
+// ---------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+struct XRing {
+  const double2* Xc;
+  int Q, MS;
+  int64_t lx;    // logical index of row 0 of the current group (ph = 0)
+  int64_t lend;  // last logical row any output of the run needs (ph = 0)
+  int sl;        // ring slot of lx
+  int dph;       // row offset of the ph = 1 half (-PC)
+  bool ph;
+  __device__ __forceinline__ int slot(int off) const {  // wave-uniform
+    int s = sl + off;
+    if (s >= Q) s -= Q;
+    if (s < 0) s += Q;
+    const int64_t g = lx + off;
+    return (g >= 0 && g <= lend) ? s : Q;
+  }
+  // DMA row lx + off (+ dph for ph = 1) into LDS at byte address lds (+16 B per lane).
+  __device__ __forceinline__ void issue(int off, unsigned lds) const {
+    const int r0 = slot(off), r1 = slot(off + dph);
+    const int row = ph ? r1 : r0;
+    const double2* p = Xc + (int64_t)row * MS;
+    unsigned keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(p), "s"(lds)
+        : "memory");
+  }
+  template <int PC>
+  __device__ __forceinline__ void advance() {
+    lx += PC;
+    sl += PC;
+    if (sl >= Q) sl -= Q;
+  }
+};
+
+template <int DL>
+__device__ __forceinline__ unsigned ring_addr(const double2* ring, int slot) {
+  return (unsigned)(uintptr_t)(lds_void_t*)(ring + slot * 64);
+}
+
+// GRP: 0 warm-up group, 1 first output group, 2 steady state.
+template <int PC, int DL, int U, int GRP>
+struct RowL {
+  template <int Q>
+  __device__ static __forceinline__ void macs(double2 (&acc)[PC], const double2 (&h)[PC], const double2 x) {
+    if constexpr (Q < PC) {
+      cmac(acc[(U + Q) % PC], x, h[Q]);
+      macs<Q + 1>(acc, h, x);
+    }
+  }
+  static constexpr int wait_count() {
+    return GRP == 0 ? DL - 1 : (GRP == 1 ? DL - 1 + (U < DL ? U : DL) : 2 * DL - 1);
+  }
+  template <bool FIRST, class UP, class EPI>
+  __device__ static __forceinline__ void run(double2 (&acc)[PC], const double2 (&h)[PC], double2* ring,
+                                             const XRing& st, const UP& up, const EPI& epi, int i) {
+    if constexpr (U < PC) {
+      constexpr int S = U % DL;
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(wait_count()) : "memory");
+      const double2 xr = ring[S * 64 + threadIdx.x];
+      // the fake operand holds the DMA that refills slot S behind this read
+      asm volatile("" ::"v"(xr.x), "v"(xr.y));
+      st.issue(U + DL, ring_addr<DL>(ring, S));
+      const double2 x = up(xr);
+      if constexpr (GRP == 0) {
+        macs<PC - U>(acc, h, x);
+      } else {
+        macs<0>(acc, h, x);
+        epi.template store<FIRST>(acc[U], i + U);
+        acc[U] = make_double2(0.0, 0.0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      RowL<PC, DL, U + 1, GRP>::template run<FIRST>(acc, h, ring, st, up, epi, i);
+    }
+  }
+};
+
+// Occupancy target of the LDS-ring variant: no X registers, so PC = 16 fits 3 waves.
+template <int PC, int NH>
+struct MacOccL {
+  static constexpr int W = PC <= 8 ? 4 : 3;
+};
+template <int PC, int NH, bool FIRST, int DL>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MacOccL<PC, NH>::W))) void k_fdl_mac_lds(MacArgs a) {
+  static_assert(DL <= 16 && PC % DL == 0, "ring depth: slots must repeat every group");
+  __shared__ double2 ring[DL * 64];
+  constexpr int BW = 32 / NH;
+  const int lg = xcd_remap(blockIdx.x, gridDim.x);
+  int ry, bx, c;
+  if (a.bx_fast) {  // neighbouring waves: neighbouring bin groups of the same rows
+    bx = lg % a.nx;
+    const int t = lg / a.nx;
+    ry = t % a.ny;
+    c = t / a.ny;
+  } else {  // neighbouring waves: consecutive runs of one bin group
+    ry = lg % a.ny;
+    const int t = lg / a.ny;
+    bx = t % a.nx;
+    c = t / a.nx;
+  }
+  const int lane = threadIdx.x;
+  const bool ph = NH == 2 && lane >= 32;
+  const bool mi = NH == 2 ? ((lane >> 4) & 1) : (lane >> 5);
+  const int l = lane & (BW - 1);
+  const bool paired = bx < a.M / (2 * BW);
+  const int k = paired ? (mi ? a.M - (bx * BW + l) : bx * BW + l) : a.M / 2;
+  const int j0 = ry * a.R;
+  const int j1 = min(j0 + a.R, a.jc);
+  const int ir = a.ir_index ? a.ir_index[c] : (c % a.n_ir);
+  const int kz = k & (a.M - 1);
+  const double2* Hc = a.H + (int64_t)ir * a.h_ir_stride + kz;
+  const double2* Xc = a.X + (int64_t)c * a.x_ch_stride + kz;
+  const double sgn = mi ? -1.0 : 1.0;
+  Unpack<NH> up;
+  up.s = sgn;
+  up.tw = (k < a.M) ? a.twN[k] : make_double2(-1.0, 0.0);
+  up.stw = c_scale(up.tw, sgn);
+  ZEpilogue<NH> epi;
+  epi.S = 0.125 / (double)a.M;
+  epi.sS = sgn * epi.S;
+  const int zpos = zrow_pos(k, a.M);
+  epi.zc = a.Y + (int64_t)c * a.y_ch_stride + zpos;
+  epi.jstride = a.MS;
+  epi.tw = (k < a.M) ? c_scale(c_conj(a.twN[k]), epi.S) : make_double2(0.0, 0.0);
+  epi.stw = c_scale(epi.tw, sgn);
+
+  XRing st;
+  st.Xc = Xc;
+  st.Q = a.Q;
+  st.MS = a.MS;
+  st.lx = a.g0 + j0 - PC - a.p0;
+  st.lend = a.g0 + j1 - 1 - a.p0;
+  st.sl = (int)(((st.lx % a.Q) + a.Q) % a.Q);
+  st.dph = -PC;
+  st.ph = ph;
+  // ring prologue first: its DMAs overlap the H loads
+#pragma unroll
+  for (int d = 1; d <= DL; ++d) st.issue(d, ring_addr<DL>(ring, d % DL));
+
+  const int pb = a.p0 + (ph ? PC : 0);
+  double2 h[PC];
+  // all PC loads in flight at once, then separated one by one
+#pragma unroll
+  for (int q = 0; q < PC; ++q) h[q] = Hc[(int64_t)min(pb + q, a.P - 1) * a.MS];
+#pragma unroll
+  for (int q = 0; q < PC; ++q) {
+    h[q] = up(h[q]);
+    if (pb + q >= a.P) h[q] = make_double2(0.0, 0.0);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  double2 acc[PC];
+#pragma unroll
+  for (int q = 0; q < PC; ++q) acc[q] = make_double2(0.0, 0.0);
+
+  RowL<PC, DL, 1, 0>::template run<FIRST>(acc, h, ring, st, up, epi, j0);
+  st.advance<PC>();
+  if (j0 < j1) {
+    RowL<PC, DL, 0, 1>::template run<FIRST>(acc, h, ring, st, up, epi, j0);
+    st.advance<PC>();
+  }
+  for (int i = j0 + PC; i < j1; i += PC) {
+    RowL<PC, DL, 0, 2>::template run<FIRST>(acc, h, ring, st, up, epi, i);
+    st.advance<PC>();
+  }
+  // drain the tail DMAs before the wave (and its LDS) retires
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // ---------------------------------------------------------------------------
@@ -406,8 +603,43 @@ void mac_go_d(const MacArgs& a, dim3 grid, hipStream_t s) {
   }
 }
 
+int mac_bx_fast() {
+  static const int v = [] {
+    const char* e = std::getenv("AD_MAC_ORDER");
+    return (e && std::atoi(e) == 1) ? 1 : 0;
+  }();
+  return v;
+}
+
+// LDS-ring depth of k_fdl_mac_lds (0 = register prefetch k_fdl_mac).
+int mac_lds_depth() {
+  static const int d = [] {
+    const char* v = std::getenv("AD_MAC_LDS");
+    return v ? std::atoi(v) : 16;
+  }();
+  return d;
+}
+
+template <int PC, int NH, int DL>
+void mac_go_l(const MacArgs& a, dim3 grid, hipStream_t s) {
+  MacArgs c = a;
+  for (c.p0 = 0; c.p0 < a.P; c.p0 += NH * PC) {
+    if (c.p0 == 0)
+      hipLaunchKernelGGL((k_fdl_mac_lds<PC, NH, true, DL>), grid, dim3(64), 0, s, c);
+    else
+      hipLaunchKernelGGL((k_fdl_mac_lds<PC, NH, false, DL>), grid, dim3(64), 0, s, c);
+  }
+}
+
 template <int PC, int NH>
 void mac_go(const MacArgs& a, dim3 grid, hipStream_t s) {
+  if constexpr (PC >= 8) {
+    const int dl = mac_lds_depth();
+    if constexpr (PC >= 16) {
+      if (dl >= 16) return mac_go_l<PC, NH, 16>(a, grid, s);
+    }
+    if (dl >= 8) return mac_go_l<PC, NH, 8>(a, grid, s);
+  }
   if (PC >= 8 && mac_depth() == 8)
     mac_go_d<PC, NH, 8>(a, grid, s);
   else
@@ -424,6 +656,7 @@ bool launch_fdl_mac(int PC, int NH, const MacArgs& in, int channels, hipStream_t
   // runs must be whole groups of PC (<= 16) outputs so the overshoot of a run
   // never lands in the next run's rows
   if (a.jc > a.R) a.R = (a.R + 15) / 16 * 16;
+  a.bx_fast = mac_bx_fast();
   a.ny = (a.jc + a.R - 1) / a.R;
   const dim3 grid((unsigned)((int64_t)channels * a.nx * a.ny));
   if (NH == 1) {

@@ -7,6 +7,19 @@
 
 namespace adsp {
 
+// Position of bin q (0..M) in a Z row (k_fdl_mac output, K3 input), M >= 64.
+// Wave-lane order: the bins of K2's pair wave bx, 32bx + l and their mirrors
+// M - (32bx + l), sit at 64bx + l and 64bx + 32 + l, so every K2 row store is
+// one aligned 1-KiB line run per wave (a partial 128-B line shared by two
+// waves would reach HBM as a read-modify-write); bin M/2 sits at M, and bin M
+// (only a separation partner) at 32, which K3 never reads.
+__host__ __device__ inline int zrow_pos(int q, int M) {
+  if (q < M / 2) return ((q >> 5) << 6) + (q & 31);
+  if (q == M / 2) return M;
+  const int d = M - q;
+  return ((d >> 5) << 6) + 32 + (d & 31);
+}
+
 struct RfftArgs {
   const double* x;      // input samples, channel c at x + c*x_stride (call-relative index)
   int64_t x_stride;
@@ -35,6 +48,7 @@ struct MacArgs {
   int64_t g0;           // logical spectrum index of chunk block 0 (< 0: zeros)
   int nx, ny;           // bin-pair waves, output runs (set by the launcher)
   int p0;               // first partition of this launch's chunk (set by the launcher)
+  int bx_fast;          // grid order: bin groups fastest (1) or runs fastest (0) (set by the launcher)
   int MS;
   const double2* H;     // [n_ir][P][MS]
   int64_t h_ir_stride;  // P*MS

@@ -290,4 +290,16 @@ __device__ __forceinline__ int last_pass_index(int tid, int s) {
   return (jb / NS) * NS * R + (jb & (NS - 1)) + r * NS;
 }
 
+// Full FFT of the thread's V pass-0 values (forward or inverse); the result
+// sits in v at last_pass_index order.
+template <int M, int V, bool FWD, class TW>
+__device__ __forceinline__ void fft_run(double2* v, int tid, double2* lds, const TW& twM) {
+  using Plan = FftPlan<M, V>;
+  if constexpr (Plan::NPASS > 1) {
+    pass_compute_store<M, V, 0, FWD, TW>(v, tid, lds, twM);
+    run_middle_passes<M, V, FWD, 1, TW>(v, tid, lds, twM);
+  }
+  last_pass_compute<M, V, FWD, TW>(v, tid, twM);
+}
+
 }  // namespace adsp

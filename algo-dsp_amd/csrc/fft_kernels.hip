@@ -41,17 +41,6 @@ __device__ __forceinline__ double2 fetch_pair(const double* xc, const double* hc
   return make_double2(r0, r1);
 }
 
-// Full FFT of the thread's V pass-0 values (forward or inverse).
-template <int M, int V, bool FWD, class TW>
-__device__ __forceinline__ void fft_run(double2* v, int tid, double2* lds, const TW& twM) {
-  using Plan = FftPlan<M, V>;
-  if constexpr (Plan::NPASS > 1) {
-    pass_compute_store<M, V, 0, FWD, TW>(v, tid, lds, twM);
-    run_middle_passes<M, V, FWD, 1, TW>(v, tid, lds, twM);
-  }
-  last_pass_compute<M, V, FWD, TW>(v, tid, twM);
-}
-
 // Inverse store: the upper half of the time window (m >= M/2) to y.
 template <int M, int V>
 __device__ __forceinline__ void irfft_store_out(const double2* v, int tid, double* yc, int64_t ob, int64_t out_len,
@@ -131,7 +120,7 @@ __global__ __launch_bounds__((FftPlan<M, V>::BLOCK)) void k_irfft_store(IrfftArg
 #pragma unroll
   for (int s = 0; s < V; ++s) {
     const int k = pass0_index<M, V>(tid, s);
-    v[s] = active ? Zb[(k & 1) ? M / 2 + (k >> 1) : (k >> 1)] : make_double2(0.0, 0.0);  // even|odd row layout
+    v[s] = active ? Zb[zrow_pos(k, M)] : make_double2(0.0, 0.0);  // wave-lane row order
   }
   fft_run<M, V, false>(v, tid, lds, TwGlobal{a.twM});
   if (!active) return;
@@ -145,8 +134,8 @@ __global__ __launch_bounds__((FftPlan<M, V>::BLOCK)) void k_irfft_store(IrfftArg
 //   K1: Zr[k] = E[k] + W_M^k O[k], Zr[k+M/2] = E[k] - W_M^k O[k],
 //       E = FFT(z[2m]), O = FFT(z[2m+1]), z[m] = x[2m] + i x[2m+1];
 //   K3: z[M/2+m] = A[m] - W_M^-m B[m] (only the upper half is kept),
-//       A = IFFT(Z[2k]), B = IFFT(Z[2k+1]); k_fdl_mac stores Z rows as
-//       [even bins | odd bins], so A's and B's inputs are contiguous halves.
+//       A = IFFT(Z[2k]), B = IFFT(Z[2k+1]); k_fdl_mac stores Z rows in
+//       wave-lane order (zrow_pos), where bins 2k and 2k+1 are neighbours.
 // Each thread's E/O inputs are 32 contiguous bytes, and its outputs of
 // both halves are the same last-pass indices, so the radix-2 step needs no
 // exchange.  The LDS image is that of an M/2 transform (69.6 KiB at M = 8192),
@@ -239,9 +228,9 @@ __global__ __launch_bounds__((SplitPlan<M>::T)) __attribute__((amdgpu_waves_per_
   double2 av[V], bv[V];
 #pragma unroll
   for (int s = 0; s < V; ++s) {
-    const int k = pass0_index<M2, V>(tid, s);  // Z row = [even bins | odd bins] (k_fdl_mac)
-    av[s] = Zb[k];
-    bv[s] = Zb[M2 + k];
+    const int k = pass0_index<M2, V>(tid, s);  // bins 2k, 2k+1 in wave-lane row order (zrow_pos)
+    av[s] = Zb[zrow_pos(2 * k, M)];
+    bv[s] = Zb[zrow_pos(2 * k + 1, M)];
   }
   __syncthreads();  // twiddle tables
   fft_run<M2, V, false>(av, tid, lds, twS);

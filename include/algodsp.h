@@ -41,6 +41,7 @@ extern "C" {
 #define AD_ERR_STAGE_INDEX_OUT_OF_RANGE 7 /* conv.ErrStageIndexOutOfRange partitioned.go:14 */
 #define AD_ERR_INVALID_ARGUMENT 8         /* non-sentinel fmt.Errorf validation errors,
                                              e.g. streaming_overlap_save.go:50-52 */
+#define AD_ERR_DIVISION_BY_ZERO 9         /* conv.ErrDivisionByZero    deconvolve.go:14 */
 #define AD_ERR_DEVICE 100                 /* HIP runtime failure */
 #define AD_ERR_NO_DEVICE 101              /* no usable gfx950 device */
 #define AD_ERR_INTERNAL 102
@@ -228,6 +229,44 @@ int ad_fir_process_device(ad_fir* f, const double* d_src, int64_t src_stride, do
                           int64_t n, void* stream);
 int ad_fir_reset(ad_fir* f); /* :162-172 */
 void ad_fir_destroy(ad_fir* f);
+
+/* ---- spectral correlation / deconvolution (dsp/conv/correlate.go,
+ * dsp/conv/deconvolve.go) --------------------------------------
+ * One power-of-two FFT over the whole zero-padded signal, as the reference's
+ * algofft.NewPlan64(n) calls.  Inputs are host arrays copied in inside the
+ * call (the _device form takes device pointers on a caller stream).        */
+
+/* CorrelateFFT (correlate.go:111-172): out[n+m-1], index k = lag k-(m-1);
+ * FFT size nextPow2(n+m-1); empty a or b -> AD_ERR_EMPTY_INPUT.            */
+int ad_correlate_fft(const double* a, int64_t n, const double* b, int64_t m, double* out, int device);
+int ad_correlate_fft_device(const double* d_a, int64_t n, const double* d_b, int64_t m, double* d_out, int device,
+                            void* stream);
+
+/* DeconvMethod / DeconvOptions (deconvolve.go:20-63) */
+#define AD_DECONV_NAIVE 0
+#define AD_DECONV_REGULARIZED 1
+#define AD_DECONV_WIENER 2
+typedef struct {
+  int method;
+  double epsilon;         /* Regularized: <= 0 -> 1e-6 */
+  double noise_variance;  /* Wiener: <= 0 -> 1% of the signal variance */
+  double signal_variance; /* Wiener: <= 0 -> variance(signal) */
+} ad_deconv_options;
+ad_deconv_options ad_deconv_default_options(void); /* :57-63 {Regularized, 1e-6} */
+
+/* Deconvolve (deconvolve.go:72-101 and the three methods :104-323): circular
+ * spectral division at FFT size nextPow2(n) (the signal length);
+ * *out_len = n-m+1, or n when that is <= 0.  Empty signal ->
+ * AD_ERR_EMPTY_INPUT, empty kernel -> AD_ERR_EMPTY_KERNEL, naive method with
+ * |H[k]| < 1e-15 -> AD_ERR_DIVISION_BY_ZERO (first bin in ad_last_error);
+ * m > nextPow2(n) (the reference indexes out of range) -> AD_ERR_INVALID_ARGUMENT. */
+int ad_deconvolve(const double* signal, int64_t n, const double* kernel, int64_t m, const ad_deconv_options* opts,
+                  double* out, int64_t out_cap, int64_t* out_len, int device);
+
+/* InverseFilter (deconvolve.go:354-394): out[length] = real(IFFT(conj H /
+ * (|H|^2 + eps))), FFT size nextPow2(length), kernel truncated to it;
+ * eps <= 0 -> 1e-6; empty kernel -> AD_ERR_EMPTY_KERNEL.                   */
+int ad_inverse_filter(const double* kernel, int64_t m, int64_t length, double epsilon, double* out, int device);
 
 #ifdef __cplusplus
 }

@@ -44,7 +44,8 @@ enum {
   OR_ERR_INVALID_BLOCK_ORDER = 5,
   OR_ERR_EMPTY_IMPULSE_RESPONSE = 6,
   OR_ERR_STAGE_INDEX_OUT_OF_RANGE = 7,
-  OR_ERR_INVALID_ARGUMENT = 8
+  OR_ERR_INVALID_ARGUMENT = 8,
+  OR_ERR_DIVISION_BY_ZERO = 9
 };
 
 /* ---- FFT (algo-fft restatement) ---- */
@@ -55,6 +56,12 @@ int or_direct(const double* a, int64_t n, const double* b, int64_t m, double* ds
 int or_direct_circular(const double* a, int64_t n, const double* b, int64_t m, double* dst);
 int or_convolve(const double* a, int64_t n, const double* b, int64_t m, int mode, double* dst, int64_t dst_cap,
                 int64_t* dst_len);
+/* ---- dsp/conv/correlate.go, deconvolve.go (or_spectral.c) ---- */
+int or_correlate_fft(const double* a, int64_t n, const double* b, int64_t m, double* out);
+int or_deconvolve(const double* signal, int64_t n, const double* kernel, int64_t m, int method, double epsilon,
+                  double noise_var, double signal_var, double* out, int64_t out_cap, int64_t* out_len,
+                  int64_t* bad_bin);
+int or_inverse_filter(const double* kernel, int64_t m, int64_t length, double epsilon, double* out);
 /* high-precision (long double, compensated) full linear convolution: golden reference */
 void or_direct_ld(const double* a, int64_t n, const double* b, int64_t m, double* dst);
 
