@@ -26,6 +26,7 @@ AD_ERR_INVALID_BLOCK_ORDER = 5
 AD_ERR_EMPTY_IMPULSE_RESPONSE = 6
 AD_ERR_STAGE_INDEX_OUT_OF_RANGE = 7
 AD_ERR_INVALID_ARGUMENT = 8
+AD_ERR_DIVISION_BY_ZERO = 9
 AD_ERR_DEVICE = 100
 AD_ERR_NO_DEVICE = 101
 AD_ERR_INTERNAL = 102
@@ -73,6 +74,10 @@ class ErrInvalidArgument(ADError):
     pass
 
 
+class ErrDivisionByZero(ADError):
+    pass
+
+
 class ErrDevice(ADError):
     pass
 
@@ -86,6 +91,7 @@ _BY_CODE = {
     AD_ERR_EMPTY_IMPULSE_RESPONSE: ErrEmptyImpulseResponse,
     AD_ERR_STAGE_INDEX_OUT_OF_RANGE: ErrStageIndexOutOfRange,
     AD_ERR_INVALID_ARGUMENT: ErrInvalidArgument,
+    AD_ERR_DIVISION_BY_ZERO: ErrDivisionByZero,
 }
 
 class CompressorConfig(C.Structure):
@@ -95,6 +101,13 @@ class CompressorConfig(C.Structure):
                                           "release_ms", "rms_window_ms", "makeup_db", "sidechain_low_cut_hz",
                                           "sidechain_high_cut_hz")] + \
                [(n, C.c_int) for n in ("topology", "detector_mode", "feedback_ratio_scale", "auto_makeup")]
+
+
+class DeconvOptionsC(C.Structure):
+    """ad_deconv_options (include/algodsp.h)."""
+
+    _fields_ = [("method", C.c_int), ("epsilon", C.c_double), ("noise_variance", C.c_double),
+                ("signal_variance", C.c_double)]
 
 
 _lib = None
@@ -184,6 +197,12 @@ def _declare(L: C.CDLL) -> None:
         "ad_fir_process_device": (C.c_int, [vp, vp, i64, vp, i64, i64, vp]),
         "ad_fir_reset": (C.c_int, [vp]),
         "ad_fir_destroy": (None, [vp]),
+        "ad_correlate_fft": (C.c_int, [c_double_p, i64, c_double_p, i64, c_double_p, C.c_int]),
+        "ad_correlate_fft_device": (C.c_int, [vp, i64, vp, i64, vp, C.c_int, vp]),
+        "ad_deconv_default_options": (DeconvOptionsC, []),
+        "ad_deconvolve": (C.c_int, [c_double_p, i64, c_double_p, i64, C.POINTER(DeconvOptionsC), c_double_p, i64,
+                                    c_int64_p, C.c_int]),
+        "ad_inverse_filter": (C.c_int, [c_double_p, i64, i64, C.c_double, c_double_p, C.c_int]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

@@ -11,9 +11,12 @@ import ctypes as C
 
 import numpy as np
 
-from ._lib import (ADError, ErrEmptyImpulseResponse, ErrEmptyInput, ErrEmptyKernel, ErrInvalidArgument,
-                   ErrInvalidBlockOrder, ErrInvalidBlockSize, ErrLengthMismatch, ErrStageIndexOutOfRange, check,
-                   f64, lib, ptr)
+import dataclasses
+import math
+
+from ._lib import (ADError, DeconvOptionsC, ErrDivisionByZero, ErrEmptyImpulseResponse, ErrEmptyInput,
+                   ErrEmptyKernel, ErrInvalidArgument, ErrInvalidBlockOrder, ErrInvalidBlockSize, ErrLengthMismatch,
+                   ErrStageIndexOutOfRange, check, f64, lib, ptr)
 
 __all__ = [
     "ADError", "ErrEmptyInput", "ErrEmptyKernel", "ErrLengthMismatch", "ErrInvalidBlockSize",
@@ -22,6 +25,10 @@ __all__ = [
     "Direct", "DirectCircular", "Convolve", "ConvolveMode",
     "NewStreamingOverlapSave", "NewStreamingOverlapAdd", "NewOverlapSave", "NewOverlapAdd",
     "NewPartitionedConvolution", "OverlapAddConvolve", "OverlapSaveConvolve", "MultiChannelConvolver",
+    "ErrDivisionByZero", "Correlate", "CorrelateDirect", "CorrelateMode", "AutoCorrelate", "AutoCorrelateNormalized",
+    "CorrelateNormalized", "CorrelateFFT", "FindPeak", "LagFromIndex", "IndexFromLag",
+    "DeconvNaive", "DeconvRegularized", "DeconvWiener", "DeconvOptions", "DefaultDeconvOptions", "Deconvolve",
+    "InverseFilter", "SNR",
 ]
 
 ModeFull, ModeSame, ModeValid = 0, 1, 2  # conv.go:57-69
@@ -253,3 +260,160 @@ class MultiChannelConvolver(_Handle):
 def mixdown_device(d_chan: int, channels: int, stride: int, length: int, d_mix: int, stream: int = 0) -> None:
     check(lib().ad_conv_mixdown_device(C.c_void_p(d_chan), channels, stride, length, C.c_void_p(d_mix),
                                        C.c_void_p(stream)))
+
+
+# ---------------------------------------------------------------------------
+# dsp/conv/correlate.go
+# ---------------------------------------------------------------------------
+def _trim_to_mode(full: np.ndarray, lenA: int, lenB: int, mode: int) -> np.ndarray:
+    """conv.go:229-247 trimToMode (slicing only)."""
+    if mode == ModeSame:
+        start = (lenB - 1) // 2
+        return full[start:start + lenA].copy()
+    if mode == ModeValid:
+        return (full[lenB - 1:lenA] if lenA >= lenB else full[lenA - 1:lenB]).copy()
+    return full
+
+
+def Correlate(a, b) -> np.ndarray:
+    """correlate.go:16-29: Convolve(a, reverse(b)) on the GPU."""
+    x, y = f64(a), f64(b)
+    if x.size == 0 or y.size == 0:
+        raise ErrEmptyInput(1, "conv: empty input")
+    return Convolve(x, y[::-1].copy())
+
+
+def CorrelateDirect(a, b) -> np.ndarray:
+    """correlate.go:32-43: Direct(a, reverse(b)) (bit-exact GPU direct form)."""
+    x, y = f64(a), f64(b)
+    if x.size == 0 or y.size == 0:
+        raise ErrEmptyInput(1, "conv: empty input")
+    return Direct(x, y[::-1].copy())
+
+
+def CorrelateMode(a, b, mode: int) -> np.ndarray:
+    """correlate.go:46-53"""
+    x, y = f64(a), f64(b)
+    return _trim_to_mode(Correlate(x, y), x.size, y.size, mode)
+
+
+def AutoCorrelate(a) -> np.ndarray:
+    """correlate.go:58-60"""
+    return Correlate(a, a)
+
+
+def AutoCorrelateNormalized(a) -> np.ndarray:
+    """correlate.go:64-82: zero-lag value scaled to 1 (host rescale of the GPU result)."""
+    x = f64(a)
+    r = AutoCorrelate(x)
+    z = r[x.size - 1]
+    return r if z == 0 else r / z
+
+
+def _l2_norm(x: np.ndarray) -> float:
+    """correlate.go:175-183 (sequential sum of squares)."""
+    s = 0.0
+    for v in x.tolist():
+        s += v * v
+    return math.sqrt(s)
+
+
+def CorrelateNormalized(a, b) -> np.ndarray:
+    """correlate.go:87-108: divided by |a|*|b|."""
+    x, y = f64(a), f64(b)
+    r = Correlate(x, y)
+    p = _l2_norm(x) * _l2_norm(y)
+    return r if p == 0 else r / p
+
+
+def CorrelateFFT(a, b) -> np.ndarray:
+    """correlate.go:111-172: one nextPow2(n+m-1) FFT correlation on the GPU."""
+    x, y = f64(a), f64(b)
+    out = np.empty(max(x.size + y.size - 1, 0), dtype=np.float64)
+    check(lib().ad_correlate_fft(ptr(x), x.size, ptr(y), y.size, ptr(out), DEVICE))
+    return out
+
+
+def _fft_pass_count(N: int) -> int:
+    """Passes of the device FFT plan for size N (bigfft.hip BigFft::BigFft)."""
+    k = max(0, N.bit_length() - 1)
+    if k <= 3:
+        return 1
+    if k <= 12:
+        return 1
+    return (k + 8) // 9
+
+
+def FindPeak(corr):
+    """correlate.go:187-205: (index, value) of the first maximum; (-1, 0) when empty."""
+    c = f64(corr)
+    if c.size == 0:
+        return -1, 0.0
+    i = int(np.argmax(c))
+    return i, float(c[i])
+
+
+def LagFromIndex(index: int, lenB: int) -> int:
+    """correlate.go:210-212"""
+    return index - (lenB - 1)
+
+
+def IndexFromLag(lag: int, lenB: int) -> int:
+    """correlate.go:216-218"""
+    return lag + (lenB - 1)
+
+
+# ---------------------------------------------------------------------------
+# dsp/conv/deconvolve.go
+# ---------------------------------------------------------------------------
+DeconvNaive, DeconvRegularized, DeconvWiener = 0, 1, 2  # deconvolve.go:20-35
+
+
+@dataclasses.dataclass
+class DeconvOptions:
+    """deconvolve.go:37-54"""
+
+    Method: int = DeconvNaive
+    Epsilon: float = 0.0
+    NoiseVariance: float = 0.0
+    SignalVariance: float = 0.0
+
+
+def DefaultDeconvOptions() -> DeconvOptions:
+    """deconvolve.go:57-63"""
+    d = lib().ad_deconv_default_options()
+    return DeconvOptions(d.method, d.epsilon, d.noise_variance, d.signal_variance)
+
+
+def Deconvolve(signal, kernel, opts: DeconvOptions) -> np.ndarray:
+    """deconvolve.go:72-101 (naive / regularized / Wiener spectral division on the GPU)."""
+    x, h = f64(signal), f64(kernel)
+    o = DeconvOptionsC(int(opts.Method), float(opts.Epsilon), float(opts.NoiseVariance), float(opts.SignalVariance))
+    cap = max(x.size, 1)
+    out = np.empty(cap, dtype=np.float64)
+    n = C.c_int64()
+    check(lib().ad_deconvolve(ptr(x), x.size, ptr(h), h.size, C.byref(o), ptr(out), cap, C.byref(n), DEVICE))
+    return out[: n.value].copy()
+
+
+def InverseFilter(kernel, length: int, epsilon: float) -> np.ndarray:
+    """deconvolve.go:354-394"""
+    h = f64(kernel)
+    out = np.empty(max(int(length), 0), dtype=np.float64)
+    check(lib().ad_inverse_filter(ptr(h), h.size, int(length), float(epsilon), ptr(out), DEVICE))
+    return out
+
+
+def SNR(original, recovered) -> float:
+    """deconvolve.go:399-421 (host metric)."""
+    a, b = f64(original), f64(recovered)
+    if a.size != b.size or a.size == 0:
+        return -math.inf
+    sp = npow = 0.0
+    for x, y in zip(a.tolist(), b.tolist()):
+        sp += x * x
+        d = x - y
+        npow += d * d
+    if npow == 0:
+        return math.inf
+    return 10 * math.log10(sp / npow)

@@ -3,6 +3,7 @@
 #include "bigfft.hpp"
 
 #include <cmath>
+#include <cstdlib>
 #include <string>
 
 #include "ad_common.hpp"
@@ -14,10 +15,17 @@ namespace adsp {
 // One global Stockham pass of radix R (16 <= R <= 4096): F = BLOCK*16/R
 // butterflies per workgroup.
 // ---------------------------------------------------------------------------
-template <int R, bool FWD, bool REALIN, bool REALOUT>
-__global__ __launch_bounds__((FftPlan<R, 16>::BLOCK)) void k_fft_pass(FftPassArgs a) {
+// FW = butterflies per workgroup (Plan::F: 2 workgroups per CU; 8192/R: one
+// workgroup per CU with twice-longer contiguous runs per access).
+template <int R, int FW>
+struct PassShape {
+  static constexpr int T = FftPlan<R, 16>::T;
+  static constexpr int BLOCK = FW * T;
+};
+template <int R, int FW, bool FWD, bool REALIN, bool REALOUT>
+__global__ __launch_bounds__((PassShape<R, FW>::BLOCK)) void k_fft_pass(FftPassArgs a) {
   using Plan = FftPlan<R, 16>;
-  constexpr int V = 16, T = Plan::T, F = Plan::F, BLOCK = Plan::BLOCK, MP = Plan::MP;
+  constexpr int V = 16, T = Plan::T, F = FW, BLOCK = PassShape<R, FW>::BLOCK, MP = Plan::MP;
   __shared__ __attribute__((aligned(16))) double2 lds_all[F * MP];
   const int bt = blockIdx.y;
   const int64_t nb = a.N / R;  // butterflies
@@ -139,15 +147,34 @@ double2* upload(const std::vector<double2>& v) {
   return p;
 }
 
+int fft_wide() {
+  static const int v = [] {
+    const char* e = std::getenv("AD_FFT_WIDE");
+    return e ? std::atoi(e) : 0;
+  }();
+  return v;
+}
+
+template <int R, bool FWD, bool RI, bool RO>
+void go_pass(const FftPassArgs& a, int batch, hipStream_t s) {
+  const int64_t nb = a.N / R;
+  constexpr int F1 = FftPlan<R, 16>::F;
+  constexpr int F2 = (8192 / R) > F1 ? (8192 / R) : F1;
+  if (fft_wide() && F2 != F1 && nb >= F2) {
+    const dim3 grid((unsigned)((nb + F2 - 1) / F2), (unsigned)batch);
+    hipLaunchKernelGGL((k_fft_pass<R, F2, FWD, RI, RO>), grid, dim3(PassShape<R, F2>::BLOCK), 0, s, a);
+  } else {
+    const dim3 grid((unsigned)((nb + F1 - 1) / F1), (unsigned)batch);
+    hipLaunchKernelGGL((k_fft_pass<R, F1, FWD, RI, RO>), grid, dim3(PassShape<R, F1>::BLOCK), 0, s, a);
+  }
+}
+
 template <bool FWD, bool RI, bool RO>
 void launch_pass_r(int R, const FftPassArgs& a, int batch, hipStream_t s) {
-  const int64_t nb = a.N / R;
-#define AD_PASS(RR)                                                                                 \
-  case RR: {                                                                                        \
-    using Plan = FftPlan<RR, 16>;                                                                   \
-    const dim3 grid((unsigned)((nb + Plan::F - 1) / Plan::F), (unsigned)batch);                     \
-    hipLaunchKernelGGL((k_fft_pass<RR, FWD, RI, RO>), grid, dim3(Plan::BLOCK), 0, s, a);            \
-    break;                                                                                          \
+#define AD_PASS(RR)                          \
+  case RR: {                                 \
+    go_pass<RR, FWD, RI, RO>(a, batch, s);   \
+    break;                                   \
   }
   switch (R) {
     AD_PASS(16)

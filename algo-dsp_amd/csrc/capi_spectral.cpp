@@ -11,6 +11,9 @@
 
 #include <cmath>
 #include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
 #include <string>
 
 #include "ad_common.hpp"
@@ -34,29 +37,53 @@ double go_variance(const double* x, int64_t n) {
   return sum / (double)n;
 }
 
-// Forward FFTs of `batch` zero-padded real arrays already in xr ([batch][N]).
+// Per-device cache of FFT plans (twiddle tables) and grow-only work buffers,
+// so repeated calls of one size allocate nothing.  One lock per call: the
+// reference's functions are stateless, the cache is an implementation detail.
+struct DeviceCache {
+  std::mutex mu;
+  std::map<int64_t, std::unique_ptr<BigFft>> plans;
+  DevBuf<double2> spec, scratch;
+  DevBuf<double> xr, res;
+  DevBuf<unsigned long long> bad;
+};
+DeviceCache& cache(int dev) {
+  static std::mutex m;
+  static std::map<int, std::unique_ptr<DeviceCache>> all;
+  std::lock_guard<std::mutex> g(m);
+  auto& c = all[dev];
+  if (!c) c.reset(new DeviceCache);
+  return *c;
+}
+
+// Forward FFTs of `batch` zero-padded real arrays in xr ([batch][N]); inverse
+// of spec[0..N) into res (real part, 1/N as algo-fft's Inverse).
 struct SpectralRun {
   int64_t N;
-  BigFft fft;
-  DevBuf<double2> spec, scratch;
-  DevBuf<double> res;
-  explicit SpectralRun(int64_t n) : N(n), fft(n) {}
+  DeviceCache& dc;
+  BigFft* fft;
+  SpectralRun(DeviceCache& c, int64_t n) : N(n), dc(c) {
+    auto& p = dc.plans[n];
+    if (!p) p.reset(new BigFft(n));
+    fft = p.get();
+  }
   void forward(const double* xr_dev, int batch, hipStream_t s) {
-    spec.alloc((size_t)(N * batch));
-    scratch.alloc((size_t)(2 * N * batch));
-    fft.run(true, nullptr, xr_dev, N, N, spec.p, nullptr, N, 1.0, batch, scratch.p, s);
+    dc.spec.reserve((size_t)(N * batch));
+    dc.scratch.reserve((size_t)(2 * N * batch));
+    fft->run(true, nullptr, xr_dev, N, N, dc.spec.p, nullptr, N, 1.0, batch, dc.scratch.p, s);
   }
-  // inverse of spec[0..N) -> res (real part, 1/N as algo-fft's Inverse)
   void inverse(hipStream_t s) {
-    res.alloc((size_t)N);
-    fft.run(false, spec.p, nullptr, 0, N, nullptr, res.p, N, 1.0 / (double)N, 1, scratch.p, s);
+    dc.res.reserve((size_t)N);
+    fft->run(false, dc.spec.p, nullptr, 0, N, nullptr, dc.res.p, N, 1.0 / (double)N, 1, dc.scratch.p, s);
   }
+  double2* spec() const { return dc.spec.p; }
+  double* res() const { return dc.res.p; }
 };
 
 // Stages host arrays into one zero-padded [count][N] device buffer.
 void stage_real(DevBuf<double>& buf, int64_t N, const double* const* src, const int64_t* len, int count,
                 hipStream_t s) {
-  buf.alloc((size_t)(N * count));
+  buf.reserve((size_t)(N * count));
   AD_HIP(hipMemsetAsync(buf.p, 0, (size_t)(N * count) * sizeof(double), s));
   for (int i = 0; i < count; ++i)
     if (len[i] > 0)
@@ -82,21 +109,23 @@ int ad_correlate_fft(const double* a, int64_t n, const double* b, int64_t m, dou
   return guard([&] {
     if (n <= 0 || m <= 0 || !a || !b) AD_FAIL(AD_ERR_EMPTY_INPUT, "conv: empty input");
     if (!out) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "null output");
-    DeviceScope ds(pick_device(device));
+    const int dev = pick_device(device);
+    DeviceScope ds(dev);
+    DeviceCache& dc = cache(dev);
+    std::lock_guard<std::mutex> g(dc.mu);
     hipStream_t s = nullptr;
     const int64_t N = next_pow2(n + m - 1);  // correlate.go:119
-    SpectralRun run(N);
-    DevBuf<double> xr;
+    SpectralRun run(dc, N);
     const double* src[2] = {a, b};
     const int64_t len[2] = {n, m};
-    stage_real(xr, N, src, len, 2, s);
-    run.forward(xr.p, 2, s);
-    launch_spec_op(kSpecCorr, run.spec.p, run.spec.p + N, N, 0.0, nullptr, s);
+    stage_real(dc.xr, N, src, len, 2, s);
+    run.forward(dc.xr.p, 2, s);
+    launch_spec_op(kSpecCorr, run.spec(), run.spec() + N, N, 0.0, nullptr, s);
     run.inverse(s);
     // correlate.go:165-171: lags 0..n-1 from the front, -(m-1)..-1 from the back
-    AD_HIP(hipMemcpyAsync(out + (m - 1), run.res.p, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, s));
+    AD_HIP(hipMemcpyAsync(out + (m - 1), run.res(), (size_t)n * sizeof(double), hipMemcpyDeviceToHost, s));
     if (m > 1)
-      AD_HIP(hipMemcpyAsync(out, run.res.p + (N - m + 1), (size_t)(m - 1) * sizeof(double), hipMemcpyDeviceToHost,
+      AD_HIP(hipMemcpyAsync(out, run.res() + (N - m + 1), (size_t)(m - 1) * sizeof(double), hipMemcpyDeviceToHost,
                             s));
     AD_HIP(hipStreamSynchronize(s));
   });
@@ -107,24 +136,26 @@ int ad_correlate_fft_device(const double* a, int64_t n, const double* b, int64_t
   return guard([&] {
     if (n <= 0 || m <= 0 || !a || !b) AD_FAIL(AD_ERR_EMPTY_INPUT, "conv: empty input");
     if (!out) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "null output");
-    DeviceScope ds(pick_device(device));
+    const int dev = pick_device(device);
+    DeviceScope ds(dev);
+    DeviceCache& dc = cache(dev);
+    std::lock_guard<std::mutex> g(dc.mu);
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const int64_t N = next_pow2(n + m - 1);
-    SpectralRun run(N);
-    DevBuf<double> xr;
-    xr.alloc((size_t)(2 * N));
-    AD_HIP(hipMemsetAsync(xr.p, 0, (size_t)(2 * N) * sizeof(double), s));
-    AD_HIP(hipMemcpyAsync(xr.p, a, (size_t)n * sizeof(double), hipMemcpyDeviceToDevice, s));
-    AD_HIP(hipMemcpyAsync(xr.p + N, b, (size_t)m * sizeof(double), hipMemcpyDeviceToDevice, s));
-    run.forward(xr.p, 2, s);
-    launch_spec_op(kSpecCorr, run.spec.p, run.spec.p + N, N, 0.0, nullptr, s);
+    SpectralRun run(dc, N);
+    dc.xr.reserve((size_t)(2 * N));
+    AD_HIP(hipMemsetAsync(dc.xr.p, 0, (size_t)(2 * N) * sizeof(double), s));
+    AD_HIP(hipMemcpyAsync(dc.xr.p, a, (size_t)n * sizeof(double), hipMemcpyDeviceToDevice, s));
+    AD_HIP(hipMemcpyAsync(dc.xr.p + N, b, (size_t)m * sizeof(double), hipMemcpyDeviceToDevice, s));
+    run.forward(dc.xr.p, 2, s);
+    launch_spec_op(kSpecCorr, run.spec(), run.spec() + N, N, 0.0, nullptr, s);
     run.inverse(s);
-    AD_HIP(hipMemcpyAsync(out + (m - 1), run.res.p, (size_t)n * sizeof(double), hipMemcpyDeviceToDevice, s));
+    AD_HIP(hipMemcpyAsync(out + (m - 1), run.res(), (size_t)n * sizeof(double), hipMemcpyDeviceToDevice, s));
     if (m > 1)
-      AD_HIP(hipMemcpyAsync(out, run.res.p + (N - m + 1), (size_t)(m - 1) * sizeof(double), hipMemcpyDeviceToDevice,
+      AD_HIP(hipMemcpyAsync(out, run.res() + (N - m + 1), (size_t)(m - 1) * sizeof(double), hipMemcpyDeviceToDevice,
                             s));
-    // the temporaries are freed on return: finish the stream's work first
-    AD_HIP(hipStreamSynchronize(s));
+    // asynchronous on the caller's stream: the cached work buffers are reused
+    // only by later calls, which the lock and stream order serialise
   });
 }
 
@@ -163,30 +194,31 @@ int ad_deconvolve(const double* signal, int64_t n, const double* kernel, int64_t
     if (olen <= 0) olen = n;
     if (out_len) *out_len = olen;
     if (!out || out_cap < olen) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "output capacity too small");
-    DeviceScope ds(pick_device(device));
+    const int dev = pick_device(device);
+    DeviceScope ds(dev);
+    DeviceCache& dc = cache(dev);
+    std::lock_guard<std::mutex> g(dc.mu);
     hipStream_t s = nullptr;
-    SpectralRun run(N);
-    DevBuf<double> xr;
+    SpectralRun run(dc, N);
     const double* src[2] = {signal, kernel};
     const int64_t len[2] = {n, m};
-    stage_real(xr, N, src, len, 2, s);
-    run.forward(xr.p, 2, s);
-    DevBuf<unsigned long long> bad;
+    stage_real(dc.xr, N, src, len, 2, s);
+    run.forward(dc.xr.p, 2, s);
     if (op == kSpecNaive) {
-      bad.alloc(1);
-      AD_HIP(hipMemsetAsync(bad.p, 0xff, sizeof(unsigned long long), s));
+      dc.bad.reserve(1);
+      AD_HIP(hipMemsetAsync(dc.bad.p, 0xff, sizeof(unsigned long long), s));
     }
-    launch_spec_op(op, run.spec.p, run.spec.p + N, N, eps, bad.p, s);
+    launch_spec_op(op, run.spec(), run.spec() + N, N, eps, op == kSpecNaive ? dc.bad.p : nullptr, s);
     if (op == kSpecNaive) {
       unsigned long long first = 0;
-      AD_HIP(hipMemcpyAsync(&first, bad.p, sizeof(first), hipMemcpyDeviceToHost, s));
+      AD_HIP(hipMemcpyAsync(&first, dc.bad.p, sizeof(first), hipMemcpyDeviceToHost, s));
       AD_HIP(hipStreamSynchronize(s));
       if (first != ~0ull)
         AD_FAIL(AD_ERR_DIVISION_BY_ZERO,
                 "conv: division by zero in deconvolution: at frequency bin " + std::to_string(first));
     }
     run.inverse(s);
-    AD_HIP(hipMemcpyAsync(out, run.res.p, (size_t)olen * sizeof(double), hipMemcpyDeviceToHost, s));
+    AD_HIP(hipMemcpyAsync(out, run.res(), (size_t)olen * sizeof(double), hipMemcpyDeviceToHost, s));
     AD_HIP(hipStreamSynchronize(s));
   });
 }
@@ -200,17 +232,19 @@ int ad_inverse_filter(const double* kernel, int64_t m, int64_t length, double ep
     if (length == 0) return;
     if (!out) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "null output");
     const int64_t N = next_pow2(length);
-    DeviceScope ds(pick_device(device));
+    const int dev = pick_device(device);
+    DeviceScope ds(dev);
+    DeviceCache& dc = cache(dev);
+    std::lock_guard<std::mutex> g(dc.mu);
     hipStream_t s = nullptr;
-    SpectralRun run(N);
-    DevBuf<double> xr;
+    SpectralRun run(dc, N);
     const double* src[1] = {kernel};
     const int64_t len[1] = {m < N ? m : N};  // kernel truncated to the transform (:367)
-    stage_real(xr, N, src, len, 1, s);
-    run.forward(xr.p, 1, s);
-    launch_spec_op(kSpecInvFilt, run.spec.p, nullptr, N, epsilon, nullptr, s);
+    stage_real(dc.xr, N, src, len, 1, s);
+    run.forward(dc.xr.p, 1, s);
+    launch_spec_op(kSpecInvFilt, run.spec(), nullptr, N, epsilon, nullptr, s);
     run.inverse(s);
-    AD_HIP(hipMemcpyAsync(out, run.res.p, (size_t)length * sizeof(double), hipMemcpyDeviceToHost, s));
+    AD_HIP(hipMemcpyAsync(out, run.res(), (size_t)length * sizeof(double), hipMemcpyDeviceToHost, s));
     AD_HIP(hipStreamSynchronize(s));
   });
 }

@@ -41,9 +41,10 @@ def parse():
                    help="HIP events around every engine kernel launch inside the timed region")
     p.add_argument("--channels", type=int, default=2,
                    help="conv: channels per GPU (IR[c %% 2]); 2 = the stereo config, 8 = config 4's shard")
-    p.add_argument("--workload", choices=["conv", "fx", "stream"], default="conv",
+    p.add_argument("--workload", choices=["conv", "fx", "stream", "corr"], default="conv",
                    help="conv: BASELINE metric (overlap-save conv); fx: config 5 effect chain (256 ch); "
-                        "stream: config 2 streaming OLS (mono, 16384 taps, 4096-sample host blocks)")
+                        "stream: config 2 streaming OLS (mono, 16384 taps, 4096-sample host blocks); "
+                        "corr: CorrelateFFT of two 2^23-sample signals (SURVEY 8(f)3, device buffers)")
     return p.parse_args()
 
 
@@ -77,6 +78,8 @@ def main():
     args = parse()
     if args.workload == "fx":
         return main_fx(args)
+    if args.workload == "corr":
+        return main_corr(args)
     if args.workload == "stream":
         return main_stream(args)
     import numpy as np
@@ -270,6 +273,79 @@ def main_stream(args):
                    "block": B, "kernel_taps": 16384},
         "note": "latency-bound: each block = H2D copy + 3 kernels + D2H copy + sync",
         "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), flush=True)
+
+
+def main_corr(args):
+    """conv.CorrelateFFT (correlate.go:111-172) of two n-sample
+    signals, one nextPow2(2n-1) = 2^24-point transform pair on the device
+    (device-resident inputs/outputs; plans and work buffers cached).  Replicas only."""
+    import ctypes as C
+
+    import numpy as np
+    import torch
+
+    from algodsp import _lib, signals
+
+    dev = torch.device("cuda", 0)
+    n = args.samples if args.samples != (1 << 24) else (1 << 23)
+    a = torch.from_numpy(signals.white_noise(n, 0x5EED)).to(dev)
+    b = torch.from_numpy(signals.white_noise(n, 0x5EEE)).to(dev)
+    out = torch.empty(2 * n - 1, dtype=torch.float64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    L = _lib.lib()
+
+    def step():
+        _lib.check(L.ad_correlate_fft_device(C.c_void_p(a.data_ptr()), n, C.c_void_p(b.data_ptr()), n,
+                                             C.c_void_p(out.data_ptr()), 0, C.c_void_p(stream.cuda_stream)))
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(args.steps):
+        step()
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    ms = e0.elapsed_time(e1) / args.steps
+    N = 1 << (2 * n - 2).bit_length()
+    # algorithmic bytes per call: staging (memset + 2 copies), forward passes
+    # (batch 2: real in 8 B, complex 16 B), A*conj(B), inverse passes (real out),
+    # output copies -- see DESIGN.md "spectral row"
+    from algodsp.conv import _fft_pass_count
+    P = _fft_pass_count(N)
+    fwd = 2 * N * (8 + 16) + 2 * N * 32 * (P - 1)
+    inv = N * 32 * (P - 1) + N * (16 + 8)
+    alg = 2 * N * 8 + 2 * n * 16 + fwd + N * 48 + inv + (2 * n - 1) * 16
+    gbs = alg / (ms * 1e-3) / 1e9
+    cpu = None
+    if not args.no_cpu_baseline:
+        sys.path.insert(0, str(ROOT / "tests"))
+        import oracle_lib as O
+
+        m = 1 << 20
+        xa, xb = signals.white_noise(m, 1), signals.white_noise(m, 2)
+        tc = time.perf_counter()
+        O.correlate_fft(xa, xb)
+        dtc = time.perf_counter() - tc
+        cpu = {"value": 2 * m / dtc / 1e6, "unit": "Msamples/s", "cores": 1, "kind": "port",
+               "sample": f"oracle CorrelateFFT of two 2^20-sample signals (N = 2^21 radix-2); {dtc:.2f} s"}
+    line = {
+        "metric": "Msamples/sec, CorrelateFFT of two 2^23-sample signals (input samples per second)",
+        "value": round(2 * n / (ms * 1e-3) / 1e6, 3), "unit": "Msamples/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f64", "data": "synthetic: SplitMix64 white noise",
+        "config": {"workload": f"conv.CorrelateFFT n = m = {n}, FFT size {N} ({P} device passes), device buffers",
+                   "fft_size": N},
+        "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                     "note": "whole call: algorithmic bytes of all passes, pointwise op and copies / event time"},
+        "cpu_baseline": cpu,
+        "wall_ms_per_step": round(dt / args.steps * 1e3, 4),
     }
     print(json.dumps(line), flush=True)
 

@@ -58,6 +58,10 @@ def lib() -> C.CDLL:
             "or_pc_new": (C.c_int, [dp, i64, C.c_int, C.c_int, C.POINTER(vp)]),
             "or_pc_process_block": (C.c_int, [vp, dp, dp, i64]),
             "or_pc_reset": (None, [vp]),
+            "or_correlate_fft": (C.c_int, [dp, i64, dp, i64, dp]),
+            "or_deconvolve": (C.c_int, [dp, i64, dp, i64, C.c_int, C.c_double, C.c_double, C.c_double, dp, i64,
+                                        C.POINTER(i64), C.POINTER(i64)]),
+            "or_inverse_filter": (C.c_int, [dp, i64, i64, C.c_double, dp]),
             "or_pc_latency": (i64, [vp]),
             "or_pc_stage_count": (C.c_int, [vp]),
             "or_pc_stage_info": (C.c_int, [vp, C.c_int, C.POINTER(i64), C.POINTER(i64)]),
@@ -149,6 +153,36 @@ def convolve_mode(a, b, mode=0):
     n = i64()
     _ck(lib().or_convolve(P(a), a.size, P(b), b.size, mode, P(out), cap, C.byref(n)))
     return out[: n.value].copy()
+
+
+# ---- correlate.go / deconvolve.go ----
+def correlate_fft(a, b):
+    a, b = f64(a), f64(b)
+    out = np.empty(max(a.size + b.size - 1, 1))
+    _ck(lib().or_correlate_fft(P(a), a.size, P(b), b.size, P(out)))
+    return out[: a.size + b.size - 1]
+
+
+def deconvolve(signal, kernel, method=1, epsilon=0.0, noise_var=0.0, signal_var=0.0):
+    """Returns (output, bad_bin); raises OracleError on a non-zero status (bad_bin in .bad_bin)."""
+    x, h = f64(signal), f64(kernel)
+    cap = max(x.size, 1)
+    out = np.empty(cap)
+    n, bad = i64(), i64(-1)
+    rc = lib().or_deconvolve(P(x), x.size, P(h), h.size, method, epsilon, noise_var, signal_var, P(out), cap,
+                             C.byref(n), C.byref(bad))
+    if rc != 0:
+        e = OracleError(rc)
+        e.bad_bin = bad.value
+        raise e
+    return out[: n.value].copy()
+
+
+def inverse_filter(kernel, length, epsilon):
+    h = f64(kernel)
+    out = np.empty(max(length, 1))
+    _ck(lib().or_inverse_filter(P(h), h.size, length, epsilon, P(out)))
+    return out[:length]
 
 
 def fft(x, inverse=False):

@@ -333,3 +333,101 @@ def test_decode_f16_subnormal_quirk():
     assert O.decode_f16(0x3C00) == 1.0
     assert O.decode_f16(0xC000) == -2.0
     assert O.decode_f16(0x03FF) == 2.0 * (1023 / 1024) * 2.0 ** -14
+
+
+# ------------------------------------------------ correlate.go / deconvolve.go
+def _np_correlate_fft(a, b):
+    n, m = len(a), len(b)
+    N = 1 << max(0, (n + m - 2).bit_length())
+    r = np.fft.ifft(np.fft.fft(a, N) * np.conj(np.fft.fft(b, N))).real
+    return np.concatenate([r[N - m + 1:], r[:n]])
+
+
+def test_correlate_fft_kat():
+    # conv_test.go:463-485: CorrelateFFT([1..5], [1,2,3]) == Correlate within 1e-8
+    a, b = [1, 2, 3, 4, 5], [1, 2, 3]
+    r = O.correlate_fft(a, b)
+    ref = O.direct(a, b[::-1])  # Correlate = Convolve(a, reverse b); m <= 64 -> Direct
+    assert r.size == 7
+    assert np.max(np.abs(r - ref)) < 1e-8
+    assert np.allclose(ref, [3, 8, 14, 20, 26, 14, 5])
+
+
+@pytest.mark.parametrize("n,m", [(1, 1), (7, 3), (1000, 37), (4096, 4097), (30000, 2500)])
+def test_correlate_fft_matches_numpy(n, m):
+    a, b = signals.white_noise(n, 11), signals.white_noise(m, 12)
+    r = O.correlate_fft(a, b)
+    assert np.max(np.abs(r - _np_correlate_fft(a, b))) < 1e-10 * max(1.0, np.max(np.abs(r)))
+
+
+def test_correlate_autocorr_peak_kat():
+    # conv_test.go:244-265: cos(2 pi i / 32) auto-correlation peaks at zero lag (index n-1)
+    x = np.cos(2 * np.pi * np.arange(256) / 32)
+    r = O.correlate_fft(x, x)
+    assert int(np.argmax(r)) == 255
+
+
+def test_correlate_fft_empty():
+    with pytest.raises(O.OracleError) as e:
+        O.correlate_fft([], [1, 2])
+    assert e.value.code == 1
+
+
+def _np_deconv(s, h, eps=None):
+    n, m = len(s), len(h)
+    N = 1 << max(0, (n - 1).bit_length())
+    S, H = np.fft.fft(s, N), np.fft.fft(h, N)
+    R = S / H if eps is None else S * np.conj(H) / (np.abs(H) ** 2 + eps)
+    olen = n - m + 1 if n - m + 1 > 0 else n
+    return np.fft.ifft(R).real[:olen]
+
+
+@pytest.mark.parametrize("method,eps", [(0, None), (1, 1e-3), (1, 1e-6), (2, None)])
+def test_deconvolve_matches_numpy(method, eps):
+    orig = np.sin(2 * np.pi * np.arange(100) / 20)
+    h = np.array([0.25, 0.5, 0.25])
+    y = O.direct(orig, h)
+    if method == 0:
+        h = np.array([1.0, 0.3])  # no spectral zero (|H| >= 0.7)
+        y = O.direct(orig, h)
+    if method == 2:  # Wiener, auto variances: nsr = 0.01
+        got = O.deconvolve(y, h, 2)
+        ref = _np_deconv(y, h, 0.01)
+    else:
+        got = O.deconvolve(y, h, method, eps or 0.0)
+        ref = _np_deconv(y, h, eps)
+    assert got.size == y.size - h.size + 1
+    assert np.max(np.abs(got - ref)) < 1e-9 * max(1.0, np.max(np.abs(ref)))
+
+
+def test_deconvolve_reference_kats():
+    # conv_test.go:282-310 (regularized eps 1e-3: SNR logged only) and :563-583 (naive, identity kernel)
+    orig = np.sin(2 * np.pi * np.arange(100) / 20)
+    rec = O.deconvolve(O.direct(orig, [0.25, 0.5, 0.25]), [0.25, 0.5, 0.25], 1, 1e-3)
+    assert rec.size == 100 and np.all(np.isfinite(rec))
+    o2 = np.sin(2 * np.pi * np.arange(50) / 10)
+    rec2 = O.deconvolve(o2, [1.0], 0)
+    assert np.max(np.abs(rec2 - o2)) < 1e-12
+
+
+def test_deconvolve_errors_and_zero_bin():
+    # conv_test.go:619-631; deconvolve.go:146-154 (first bin with |H| < 1e-15)
+    with pytest.raises(O.OracleError) as e:
+        O.deconvolve([], [1, 2])
+    assert e.value.code == 1
+    with pytest.raises(O.OracleError) as e:
+        O.deconvolve([1, 2], [])
+    assert e.value.code == 2
+    with pytest.raises(O.OracleError) as e:
+        O.deconvolve([1.0, 2.0, 3.0, 4.0], [1.0, 1.0], 0)  # H = 1 + W^k: zero at k = N/2 = 2
+    assert e.value.code == 9 and e.value.bad_bin == 2
+
+
+def test_inverse_filter_kat():
+    # conv_test.go:312-340: InverseFilter([.5, 1, .5], 64, 1e-3) -> conv with kernel has a dominant peak
+    inv = O.inverse_filter([0.5, 1.0, 0.5], 64, 1e-3)
+    r = O.direct([0.5, 1.0, 0.5], inv)
+    assert np.max(r) > 0.1
+    H = np.fft.fft([0.5, 1.0, 0.5], 64)
+    ref = np.fft.ifft(np.conj(H) / (np.abs(H) ** 2 + 1e-3)).real
+    assert np.max(np.abs(inv - ref)) < 1e-9 * np.max(np.abs(ref))
