@@ -25,7 +25,9 @@ struct PassShape {
 template <int R, int FW, bool FWD, bool REALIN, bool REALOUT>
 __global__ __launch_bounds__((PassShape<R, FW>::BLOCK)) void k_fft_pass(FftPassArgs a) {
   using Plan = FftPlan<R, 16>;
-  constexpr int V = 16, T = Plan::T, F = FW, BLOCK = PassShape<R, FW>::BLOCK, MP = Plan::MP;
+  // per-butterfly LDS stride: odd when a 16-lane group stays inside one
+  // transform (T >= 16), so the jj-fastest staging accesses spread over the banks
+  constexpr int V = 16, T = Plan::T, F = FW, BLOCK = PassShape<R, FW>::BLOCK, MP = Plan::MP + (T >= 16 ? 1 : 0);
   __shared__ __attribute__((aligned(16))) double2 lds_all[F * MP];
   const int bt = blockIdx.y;
   const int64_t nb = a.N / R;  // butterflies
@@ -47,7 +49,7 @@ __global__ __launch_bounds__((PassShape<R, FW>::BLOCK)) void k_fft_pass(FftPassA
         v = a.in[bt * a.in_batch + g];
       }
     }
-    lds_all[jj * MP + lds_pad(r)] = v;
+    lds_all[jj * MP + lds_slot(r)] = v;
   }
   __syncthreads();
 
@@ -56,7 +58,7 @@ __global__ __launch_bounds__((PassShape<R, FW>::BLOCK)) void k_fft_pass(FftPassA
   const int64_t j = j0 + f;
   double2 v[V];
 #pragma unroll
-  for (int s = 0; s < V; ++s) v[s] = lds[lds_pad(pass0_index<R, V>(tid, s))];
+  for (int s = 0; s < V; ++s) v[s] = lds[lds_slot(pass0_index<R, V>(tid, s))];
   if (a.Ns > 1) {  // pre-twiddle W_{Ns R}^{(j mod Ns) r} = W_N^{(j mod Ns) r N/(Ns R)}
     const int64_t jm = j & (a.Ns - 1);
     const int64_t step = a.N / (a.Ns * R);
@@ -73,7 +75,7 @@ __global__ __launch_bounds__((PassShape<R, FW>::BLOCK)) void k_fft_pass(FftPassA
   fft_run<R, V, FWD>(v, tid, lds, TwGlobal{a.twR});
   __syncthreads();
 #pragma unroll
-  for (int s = 0; s < V; ++s) lds[lds_pad(last_pass_index<R, V>(tid, s))] = v[s];
+  for (int s = 0; s < V; ++s) lds[lds_slot(last_pass_index<R, V>(tid, s))] = v[s];
   __syncthreads();
 
   // stage out: output rr of butterfly j goes to (j/Ns) Ns R + (j mod Ns) + rr Ns
@@ -91,7 +93,7 @@ __global__ __launch_bounds__((PassShape<R, FW>::BLOCK)) void k_fft_pass(FftPassA
     }
     const int64_t jo = j0 + jj;
     if (jo >= nb) continue;
-    const double2 val = lds_all[jj * MP + lds_pad(rr)];
+    const double2 val = lds_all[jj * MP + lds_slot(rr)];
     const int64_t o = (jo & ~(Ns - 1)) * R + (jo & (Ns - 1)) + (int64_t)rr * Ns;
     if constexpr (REALOUT)
       a.out_real[bt * a.out_batch + o] = val.x * a.scale;

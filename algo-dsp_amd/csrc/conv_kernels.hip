@@ -183,6 +183,7 @@ struct ZEpilogue {
   // address in the same instruction; bin M stores into padding column M.
   template <bool FIRST>
   __device__ __forceinline__ void store(double2 y, int64_t j) const {
+
     if constexpr (NH == 2) {
       double2 a, b;
       xpair<true>(y, a, b);
@@ -615,7 +616,7 @@ int mac_bx_fast() {
 int mac_lds_depth() {
   static const int d = [] {
     const char* v = std::getenv("AD_MAC_LDS");
-    return v ? std::atoi(v) : 16;
+    return v ? std::atoi(v) : 8;
   }();
   return d;
 }
@@ -647,12 +648,42 @@ void mac_go(const MacArgs& a, dim3 grid, hipStream_t s) {
 }
 }  // namespace
 
+// Resident waves per SIMD of the K2 variant that launch_fdl_mac will pick.
+int mac_waves_per_simd(int PC, int NH) {
+  const bool lds = PC >= 8 && mac_lds_depth() >= 8;
+  if (lds) return PC <= 8 ? 4 : 3;  // MacOccL (VGPR-bound; the 8-row ring is 8 KiB per wave)
+  return PC <= 4 ? 4 : (PC == 8 ? 3 : 2);  // MacOcc
+}
+
+int device_cus() {
+  static const int n = [] {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+    return cus;
+  }();
+  return n;
+}
+
 bool launch_fdl_mac(int PC, int NH, const MacArgs& in, int channels, hipStream_t s) {
   if (channels <= 0 || in.jc <= 0) return true;
   MacArgs a = in;
   const int BW = 32 / NH;
   if (a.M < 2 * BW) return false;  // a pair wave needs M/2 >= BW bins
   a.nx = a.M / (2 * BW) + 1;        // pair waves + the middle-bin wave
+  if (a.R <= 0) {
+    // Auto run length: the fewest runs that still fill every SIMD to its
+    // resident-wave limit in ONE round.  A second, partial round leaves a
+    // tail of idle SIMDs, and longer runs re-read fewer warm-up rows and H
+    // spectra (stereo 2 x 2064 blocks at M = 8192: R = 192, 2838 waves,
+    // K2 237 us vs 285 us at R = 64).
+    const int64_t slots = (int64_t)mac_waves_per_simd(PC, NH) * 4 * device_cus();
+    const int64_t per_run = (int64_t)channels * a.nx;
+    int64_t ny = std::max<int64_t>(1, slots / per_run);
+    ny = std::min<int64_t>(ny, (a.jc + 31) / 32);  // runs of at least 32 blocks
+    ny = std::max<int64_t>(ny, 1);
+    a.R = (int)((a.jc + ny - 1) / ny);
+  }
   // runs must be whole groups of PC (<= 16) outputs so the overshoot of a run
   // never lands in the next run's rows
   if (a.jc > a.R) a.R = (a.R + 15) / 16 * 16;

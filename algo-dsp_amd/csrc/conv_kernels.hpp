@@ -59,7 +59,7 @@ struct MacArgs {
   int64_t y_ch_stride;
   const double2* twN;   // W_{2M}^k, k < M
   int jc;
-  int R;                // output blocks per wave run
+  int R;                // output blocks per wave run (0: auto, one resident round of waves)
   int P;                // partitions
   int M;                // bins 0..M
 };

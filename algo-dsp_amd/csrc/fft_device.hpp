@@ -10,9 +10,12 @@
 //   * one M-point complex FFT is done by M/V threads, each holding V = 8 or
 //     16 complex128 values in VGPRs; passes are radix-V (the first pass may
 //     be radix 2/4/8), so M = 4096 at V = 16 takes three passes;
-//   * the LDS image is interleaved double2 padded by one element per 16
-//     (pad(i) = i + i/16) so the stride-R butterfly writes of a Stockham
-//     pass hit distinct 16-B slots of the 256-B bank row (ds_write_b128);
+//   * the LDS image is interleaved double2 with an XOR swizzle inside each
+//     aligned 16-element block (lds_slot) so every 16-lane group of a
+//     ds_read/ds_write_b128 -- the consecutive reads and the stride-NS
+//     Stockham writes of every pass, NS = 1, 8, 64, 512 at M = 4096 -- hits
+//     16 distinct 16-B slots of the 256-B bank row (no padding; the earlier
+//     i + i/16 padding left a 2-way conflict on the NS = 8 writes);
 //   * a workgroup of max(M/V, 256) threads carries max(1, 256V/M) FFTs
 //     (fft_kernels.hip splits M >= 2048 into two M/2 transforms so that two
 //     workgroups share a CU);
@@ -135,12 +138,22 @@ struct FftPlan {
   static constexpr int T = M / V;                  // threads per FFT
   static constexpr int BLOCK = T > 256 ? T : 256;  // workgroup size
   static constexpr int F = BLOCK / T;              // FFTs per workgroup
-  static constexpr int MP = M + M / 16;            // padded LDS elements per FFT
+  // LDS elements per FFT: several FFTs share a 16-lane group when T < 16; the
+  // stride T (mod 16) puts each one on its own part of the bank row
+  static constexpr int MP = M + (T < 16 ? T : 0);
   static constexpr int radix(int p) { return p == 0 ? R0 : V; }
   static constexpr int ns(int p) { return p == 0 ? 1 : R0 * (1 << (LOGV * (p - 1))); }
 };
 
-__device__ __forceinline__ int lds_pad(int i) { return i + (i >> 4); }
+// Swizzled LDS index: the low 4 bits XOR g(i >> 4), g(q) = (q ^ ((q & 4) << 1)) & 15,
+// a bijection on each aligned 16-block (tools/lds_conflicts.py checks the plans).
+__device__ __forceinline__ int lds_slot(int i) {
+  const int q = i >> 4;
+  return i ^ ((q ^ ((q & 4) << 1)) & 15);
+}
+// Twiddle-table slot: stride-8 reads (the NS = 64 pass at M = 4096) and
+// consecutive reads both spread over 16 slots.
+__device__ __forceinline__ int tw_slot(int i) { return i ^ ((i >> 3) & 7); }
 
 // Twiddle sources.  TwGlobal reads W_M^e from the HBM table.  TwLds reads it
 // from two small LDS tables, W^e = lo[e mod 2^S] * hi[e >> S] (S = ceil(log2 M / 2),
@@ -165,8 +178,8 @@ struct TwLds {
   const double2* hi;  // LDS: W^(i 2^S), i < M / 2^S
   __device__ __forceinline__ double2 operator()(int e) const {
     using Sp = TwSplit<M>;
-    if constexpr (Sp::NHI == 1) return lo[e];
-    const double2 a = lo[e & (Sp::NLO - 1)];
+    if constexpr (Sp::NHI == 1) return lo[tw_slot(e)];
+    const double2 a = lo[tw_slot(e & (Sp::NLO - 1))];
     const double2 b = hi[e >> Sp::S];
     return c_mul(a, b);
   }
@@ -177,8 +190,12 @@ struct TwLds {
 template <int M, int STRIDE = 1>
 __device__ __forceinline__ TwLds<M> tw_lds_fill(double2* ltab, const double2* __restrict__ g, int tid, int nthreads) {
   using Sp = TwSplit<M>;
-  for (int i = tid; i < Sp::N; i += nthreads)
-    ltab[i] = (i < Sp::NLO) ? g[i * STRIDE] : g[((i - Sp::NLO) << Sp::S) * STRIDE];
+  for (int i = tid; i < Sp::N; i += nthreads) {
+    if (i < Sp::NLO)
+      ltab[tw_slot(i)] = g[i * STRIDE];
+    else
+      ltab[i] = g[((i - Sp::NLO) << Sp::S) * STRIDE];
+  }
   return TwLds<M>{ltab, ltab + Sp::NLO};
 }
 
@@ -218,7 +235,7 @@ __device__ __forceinline__ void pass_compute_store(double2* v, int tid, double2*
     const int jb = tid + b * Plan::T;
     const int base = (jb / NS) * NS * R + (jb & (NS - 1));
 #pragma unroll
-    for (int r = 0; r < R; ++r) lds[lds_pad(base + r * NS)] = v[b * R + r];
+    for (int r = 0; r < R; ++r) lds[lds_slot(base + r * NS)] = v[b * R + r];
   }
 }
 
@@ -232,7 +249,7 @@ __device__ __forceinline__ void pass_load(double2* v, int tid, const double2* ld
   for (int b = 0; b < NB; ++b) {
     const int jb = tid + b * Plan::T;
 #pragma unroll
-    for (int r = 0; r < R; ++r) v[b * R + r] = lds[lds_pad(jb + r * (M / R))];
+    for (int r = 0; r < R; ++r) v[b * R + r] = lds[lds_slot(jb + r * (M / R))];
   }
 }
 

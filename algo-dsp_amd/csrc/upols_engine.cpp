@@ -47,7 +47,7 @@ Upols::Upols(int device, const double* kernels, int n_ir, int64_t K, int L, int 
   NH_ = pick_nh(P_);
   PC_ = pick_pc(P_, NH_);
   Q_ = jc_max_ + P_ + 2 * PC_ + 1;
-  R_ = std::max(1, env_int("AD_MAC_R", 64));
+  R_ = env_int("AD_MAC_R", 0);  // 0: the launcher sizes runs to one resident round of waves
 
   // Twiddle tables, computed in long double on the host.
   std::vector<double2> tw(2 * (size_t)M_);
@@ -244,7 +244,7 @@ void Upols::run(const double* d_in, int64_t in_stride, int64_t n, double* d_out,
     m.Y = Y_.p;
     m.y_ch_stride = (int64_t)(jc_max_ + 16) * MS_;
     m.jc = jc;
-    m.R = std::min(R_, jc);
+    m.R = R_ > 0 ? std::min(R_, jc) : 0;
     m.P = P_;
     m.M = M_;
     m.twN = tw_.p + M_;
