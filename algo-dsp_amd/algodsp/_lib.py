@@ -169,6 +169,7 @@ def _declare(L: C.CDLL) -> None:
         "ad_conv_multi_create": (C.c_int, [c_double_p, C.c_int, i64, i64, C.c_int, C.POINTER(C.c_int32), i64,
                                            C.c_int, C.POINTER(vp)]),
         "ad_conv_multi_process_device": (C.c_int, [vp, vp, i64, i64, vp, i64, i64, vp]),
+        "ad_conv_multi_process_device_segment": (C.c_int, [vp, vp, i64, i64, vp, i64, i64, i64, i64, vp]),
         "ad_conv_mixdown_device": (C.c_int, [vp, C.c_int, i64, i64, vp, vp]),
         "ad_conv_profile_enable": (C.c_int, [vp, C.c_int]),
         "ad_conv_profile_read": (C.c_int, [vp, c_double_p, c_int64_p, c_double_p]),

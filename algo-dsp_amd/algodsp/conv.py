@@ -256,6 +256,14 @@ class MultiChannelConvolver(_Handle):
         check(lib().ad_conv_multi_process_device(self._h, C.c_void_p(d_in), in_stride, in_len, C.c_void_p(d_out),
                                                  out_stride, out_len, C.c_void_p(stream)))
 
+    def process_device_segment(self, d_in: int, in_stride: int, in_len: int, d_out: int, out_stride: int,
+                               out_len: int, out_begin: int, out_end: int, stream: int = 0) -> None:
+        """process_device restricted to outputs [out_begin, out_end): segments of one
+        signal run in order and together equal one process_device call."""
+        check(lib().ad_conv_multi_process_device_segment(self._h, C.c_void_p(d_in), in_stride, in_len,
+                                                         C.c_void_p(d_out), out_stride, out_len, out_begin,
+                                                         out_end, C.c_void_p(stream)))
+
 
 def mixdown_device(d_chan: int, channels: int, stride: int, length: int, d_mix: int, stream: int = 0) -> None:
     check(lib().ad_conv_mixdown_device(C.c_void_p(d_chan), channels, stride, length, C.c_void_p(d_mix),

@@ -34,7 +34,9 @@ def stereo_partial_mix(y: np.ndarray, channel_ids) -> np.ndarray:
     return mix
 
 
-def reduce_mix(mix_tensor, dist) -> None:
+def reduce_mix(mix_tensor, dist, async_op: bool = False):
     """Sum the per-rank partial mixes into rank 0's tensor (RCCL over xGMI on
-    the GPU path, gloo in the CPU tests)."""
-    dist.reduce(mix_tensor, dst=0, op=dist.ReduceOp.SUM)
+    the GPU path, gloo in the CPU tests).  async_op: returns the work handle;
+    on RCCL the reduce runs on the process group's stream after the work
+    already queued on the current stream, overlapping what is queued next."""
+    return dist.reduce(mix_tensor, dst=0, op=dist.ReduceOp.SUM, async_op=async_op)

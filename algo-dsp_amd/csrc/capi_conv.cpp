@@ -85,6 +85,7 @@ struct ad_conv {
 
   std::unique_ptr<Upols> eng;  // FFT path
   int64_t hop = 0;
+  int64_t seg_next = -1;  // next out_begin of a segmented offline call (-1: none open)
 
   // time-domain streaming path (hop too small for the FFT engine)
   bool direct_stream = false;
@@ -649,6 +650,30 @@ int ad_conv_multi_process_device(ad_conv* h, const double* d_in, int64_t in_stri
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);  // NULL = the default (null) stream
     h->eng->begin_offline(s);
     h->eng->run(d_in, in_stride, in_len, d_out, out_stride, out_len, /*use_hist=*/false, s);
+    h->seg_next = -1;
+  });
+}
+
+int ad_conv_multi_process_device_segment(ad_conv* h, const double* d_in, int64_t in_stride, int64_t in_len,
+                                         double* d_out, int64_t out_stride, int64_t out_len, int64_t out_begin,
+                                         int64_t out_end, void* stream) {
+  return guard([&] {
+    if (!h || h->kind != Kind::Multi) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "not a multi-channel convolver");
+    if (in_len <= 0) AD_FAIL(AD_ERR_EMPTY_INPUT, "conv: empty input");
+    if (out_len > in_len + h->K - 1 || out_len <= 0)
+      AD_FAIL(AD_ERR_LENGTH_MISMATCH, "conv: buffer length mismatch");
+    const int64_t L = h->eng->hop();
+    out_end = std::min(out_end, out_len);
+    if (out_begin < 0 || out_begin >= out_end || out_begin % L != 0 || (out_end % L != 0 && out_end != out_len))
+      AD_FAIL(AD_ERR_INVALID_ARGUMENT, "conv segment: bounds must be hop multiples within the output");
+    if (out_begin != 0 && out_begin != h->seg_next)
+      AD_FAIL(AD_ERR_INVALID_ARGUMENT, "conv segment: segments must follow each other in order");
+    DeviceScope ds(h->device);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (out_begin == 0) h->eng->begin_offline(s);
+    h->eng->run(d_in, in_stride, in_len, d_out, out_stride, out_len, /*use_hist=*/false, s, out_begin / L,
+                (out_end + L - 1) / L);
+    h->seg_next = out_end < out_len ? out_end : -1;
   });
 }
 

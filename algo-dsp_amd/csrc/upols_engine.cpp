@@ -192,16 +192,19 @@ void Upols::begin_offline(hipStream_t) {
 }
 
 void Upols::run(const double* d_in, int64_t in_stride, int64_t n, double* d_out, int64_t out_stride, int64_t out_len,
-                bool use_hist, hipStream_t s) {
+                bool use_hist, hipStream_t s, int64_t jb, int64_t je) {
   if (out_len <= 0) return;
-  const int64_t J = (out_len + L_ - 1) / L_;
+  if (je < 0) je = (out_len + L_ - 1) / L_;
+  const int64_t J = je - jb;
+  if (J <= 0) return;
   const int in_aligned = ((reinterpret_cast<uintptr_t>(d_in) & 15) == 0) && (in_stride % 2 == 0);
   const int out_aligned = ((reinterpret_cast<uintptr_t>(d_out) & 15) == 0) && (out_stride % 2 == 0);
   // balanced chunks of at most jc_max blocks (no tiny tail launch)
   const int64_t nchunks = (J + jc_max_ - 1) / jc_max_;
   const int64_t jc_even = (J + nchunks - 1) / nchunks;
-  for (int64_t cs = 0; cs < J; cs += jc_even) {
-    const int jc = (int)std::min<int64_t>(jc_even, J - cs);
+  for (int64_t cr = 0; cr < J; cr += jc_even) {
+    const int jc = (int)std::min<int64_t>(jc_even, J - cr);
+    const int64_t cs = jb + cr;  // first output block of this chunk
     const int slot0 = (int)(g_next_ % Q_);
 
     RfftArgs a{};
@@ -210,7 +213,7 @@ void Upols::run(const double* d_in, int64_t in_stride, int64_t n, double* d_out,
     a.n = n;
     a.xhist = use_hist ? hist_[hcur_].p : nullptr;
     // the last chunk's last window leaves the next call's history in the other buffer
-    a.hist_out = (use_hist && cs + jc >= J) ? hist_[hcur_ ^ 1].p : nullptr;
+    a.hist_out = (use_hist && cr + jc >= J) ? hist_[hcur_ ^ 1].p : nullptr;
     a.hist_stride = L_;
     a.s0 = cs * L_;
     a.jc = jc;

@@ -36,8 +36,11 @@ class Upols {
   // Runs ceil(out_len/L) blocks for all channels.  d_in: [C][in_stride],
   // n valid samples.  d_out: [C][out_stride], out_len samples written.
   // use_hist: the L samples before the call come from the streaming history.
+  // [jb, je): the output blocks to run (je < 0: through the end of out_len).
+  // Offline segments of one signal run in increasing order (the delay line
+  // carries from one segment to the next).
   void run(const double* d_in, int64_t in_stride, int64_t n, double* d_out, int64_t out_stride, int64_t out_len,
-           bool use_hist, hipStream_t s);
+           bool use_hist, hipStream_t s, int64_t jb = 0, int64_t je = -1);
   // Saves the last L input samples of the call into the streaming history.
   // Streaming calls (use_hist) refresh the history inside K1; kept for API
   // symmetry, a no-op.

@@ -37,6 +37,11 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-sample", type=int, default=1 << 25, help="samples of one channel for the CPU leg")
     p.add_argument("--mixdown", choices=["auto", "on", "off"], default="auto")
+    p.add_argument("--pipeline", choices=["on", "off"], default="on",
+                   help="N > 1: overlap step i's mixdown reduce with step i+1's convolution (two output buffers)")
+    p.add_argument("--segments", type=int, default=1,
+                   help="output segments per step (ad_conv_multi_process_device_segment); each segment's "
+                        "mixdown reduce starts as soon as it is computed")
     p.add_argument("--kernel-timing", choices=["on", "off"], default="on",
                    help="HIP events around every engine kernel launch inside the timed region")
     p.add_argument("--channels", type=int, default=2,
@@ -93,9 +98,9 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
     mixdown = world > 1 if args.mixdown == "auto" else args.mixdown == "on"
+    if world > 1 or mixdown:  # --mixdown on at N = 1 (under torchrun) exercises the RCCL path
+        dist.init_process_group("nccl", device_id=dev)
 
     ir = irlib.large_church()                       # [2][131072], Large Church zero padded
     K = ir.shape[1]
@@ -109,24 +114,56 @@ def main():
     ids = list(shard.channel_group(rank, world, C * world))  # this rank's global channel ids
     x_host = np.stack([signals.white_noise(n, 0x5EED + c) for c in ids])
     x = torch.from_numpy(x_host).to(dev)
-    y = torch.empty((C, out_len), dtype=torch.float64, device=dev)
-    mix = y if C == 2 else torch.empty((2, out_len), dtype=torch.float64, device=dev)
+    # Two output buffers when the mixdown runs: step i's RCCL reduce (on the
+    # process group's own stream) overlaps step i+1's convolution into the
+    # other buffer; a buffer is rewritten only after its reduce has finished.
+    # The last step's reduce completes inside the timed region.
+    nbuf = 2 if (mixdown and args.pipeline == "on") else 1
+    ys = [torch.empty((C, out_len), dtype=torch.float64, device=dev) for _ in range(nbuf)]
+    mixes = [y if C == 2 else torch.empty((2, out_len), dtype=torch.float64, device=dev) for y in ys]
+    y = ys[0]
     del x_host
 
     eng = conv.MultiChannelConvolver(ir, hop=args.hop, channels=C, ir_index=shard.ir_index(ids),
                                      chunk_blocks=args.chunk, device=local)
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
+    blocks = -(-out_len // args.hop)
+    cuts = [min(out_len, args.hop * (blocks * i // args.segments)) for i in range(args.segments + 1)]
+    segs = [(b, e) for b, e in zip(cuts[:-1], cuts[1:]) if e > b]
+    pending = [[] for _ in range(nbuf)]
+    it = [0]
 
     def step():
-        eng.process_device(x.data_ptr(), n, n, y.data_ptr(), out_len, out_len, sptr)
-        if mixdown:
-            if C != 2:  # stereo partial mix of this rank's channel group (even -> L, odd -> R)
-                conv.mixdown_device(y.data_ptr(), C, out_len, out_len, mix.data_ptr(), sptr)
-            shard.reduce_mix(mix, dist)
+        i = it[0] % nbuf
+        it[0] += 1
+        for w in pending[i]:  # the reduce that last read this buffer
+            w.wait()
+        pending[i] = []
+        yb, mb = ys[i], mixes[i]
+        for b, e in segs:
+            if len(segs) == 1:
+                eng.process_device(x.data_ptr(), n, n, yb.data_ptr(), out_len, out_len, sptr)
+            else:
+                eng.process_device_segment(x.data_ptr(), n, n, yb.data_ptr(), out_len, out_len, b, e, sptr)
+            if mixdown:
+                if C != 2:  # stereo partial mix of this rank's channel group (even -> L, odd -> R)
+                    conv.mixdown_device(yb.data_ptr() + 8 * b, C, out_len, e - b, mb.data_ptr() + 16 * b, sptr)
+                    parts = [mb.view(-1)[2 * b:2 * e]]
+                else:
+                    parts = [mb[0, b:e], mb[1, b:e]]
+                for t in parts:
+                    pending[i].append(shard.reduce_mix(t, dist, async_op=True))
+
+    def drain():
+        for i in range(nbuf):
+            for w in pending[i]:
+                w.wait()
+            pending[i] = []
 
     for _ in range(args.warmup):
         step()
+    drain()
     torch.cuda.synchronize(dev)
     eng.profile_read()  # clear
 
@@ -138,6 +175,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    drain()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -146,6 +184,7 @@ def main():
         eng.profile_enable(True)
         for _ in range(max(2, args.steps // 2)):
             step()
+        drain()
         torch.cuda.synchronize(dev)
     eng.profile_enable(False)
     prof = eng.profile_read()
@@ -224,7 +263,7 @@ def main():
         if cpu:
             line["speedup_vs_cpu"] = round(value / cpu["value"], 1)
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
 

@@ -140,6 +140,19 @@ int ad_conv_multi_create(const double* kernels, int n_ir, int64_t kernel_len, in
  * Device pointers; asynchronous on `stream` (NULL = default stream).      */
 int ad_conv_multi_process_device(ad_conv* h, const double* d_in, int64_t in_stride, int64_t in_len, double* d_out,
                                  int64_t out_stride, int64_t out_len, void* stream);
+/* The same full linear convolution computed one output segment at a time:
+ * this call writes d_out[c][out_begin .. min(out_end, out_len)) only.
+ * out_begin == 0 starts a new signal; a later segment must start where the
+ * previous one ended (the frequency-domain delay line carries over), and
+ * out_begin / out_end are multiples of the hop (out_end may also be out_len).
+ * Segments let a caller overlap per-segment work, such as the multi-GPU
+ * mixdown reduce, with the next segment's convolution.  Results are identical
+ * to one ad_conv_multi_process_device call.  No reference counterpart: it is
+ * the batch OverlapSave.Process (overlap_save.go:126-254) split by output
+ * range.  Out-of-order segments return AD_ERR_INVALID_ARGUMENT.            */
+int ad_conv_multi_process_device_segment(ad_conv* h, const double* d_in, int64_t in_stride, int64_t in_len,
+                                         double* d_out, int64_t out_stride, int64_t out_len, int64_t out_begin,
+                                         int64_t out_end, void* stream);
 /* Live kernel timing (HIP events recorded around every launch on the launch
  * stream) for the FFT engine of a handle.  Kernel index: 0 window rFFT,
  * 1 frequency-domain delay-line MAC, 2 inverse rFFT + overlap-save store.

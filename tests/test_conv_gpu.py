@@ -269,3 +269,32 @@ def test_mixdown(gpu):
     xn = x.cpu().numpy()
     np.testing.assert_allclose(mix.cpu().numpy()[0], xn[0] + xn[2] + xn[4], atol=1e-15)
     np.testing.assert_allclose(mix.cpu().numpy()[1], xn[1] + xn[3] + xn[5], atol=1e-15)
+
+
+@pytest.mark.parametrize("hop,nseg", [(1024, 3), (8192, 4)])
+def test_multi_segments_equal_one_call(gpu, hop, nseg):
+    """ad_conv_multi_process_device_segment: consecutive output segments of one
+    signal reproduce the single-call result bit for bit (the delay line carries
+    over), and out-of-order segments are rejected."""
+    import torch
+
+    ir = irlib.large_church()[:, :40000]
+    n = 100_000
+    x = np.stack([signals.white_noise(n, 0x5EED + c) for c in range(2)])
+    want, _ = _multi_run(ir, x, hop=hop, chunk=5)
+    out_len = n + ir.shape[1] - 1
+    eng = conv.MultiChannelConvolver(ir, hop=hop, channels=2, chunk_blocks=5)
+    dx = torch.from_numpy(x).cuda()
+    dy = torch.zeros((2, out_len), dtype=torch.float64, device="cuda")
+    blocks = -(-out_len // hop)
+    cuts = [min(out_len, hop * (blocks * i // nseg)) for i in range(nseg + 1)]
+    for _ in range(2):  # a second pass restarts at out_begin = 0
+        for b, e in zip(cuts[:-1], cuts[1:]):
+            eng.process_device_segment(dx.data_ptr(), n, n, dy.data_ptr(), out_len, out_len, b, e)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(dy.cpu().numpy(), want)
+    eng.process_device_segment(dx.data_ptr(), n, n, dy.data_ptr(), out_len, out_len, 0, cuts[1])
+    with pytest.raises(Exception):
+        eng.process_device_segment(dx.data_ptr(), n, n, dy.data_ptr(), out_len, out_len, cuts[2], cuts[3])
+    with pytest.raises(Exception):
+        eng.process_device_segment(dx.data_ptr(), n, n, dy.data_ptr(), out_len, out_len, 1, cuts[1])
