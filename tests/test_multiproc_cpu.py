@@ -37,9 +37,20 @@ def _worker(rank, world, port, q):
         ids = list(shard.channel_group(rank, world, TOTAL_CH))
         y = np.stack([_channel_output(c) for c in ids])
         mix = torch.from_numpy(shard.stereo_partial_mix(y, ids))
+        base = mix.clone()
         shard.reduce_mix(mix, dist)
         if rank == 0:
             q.put(mix.numpy())
+        # bench.py's pipelined form: two steps in flight on two buffers, each
+        # reduced asynchronously per (row, output segment), waited on later
+        bufs = [base * (s + 1) for s in range(2)]
+        cuts = [0, 1024, 2048, base.shape[1]]
+        works = [shard.reduce_mix(b[r, lo:hi], dist, async_op=True)
+                 for b in bufs for lo, hi in zip(cuts[:-1], cuts[1:]) for r in range(2)]
+        for w in works:
+            w.wait()
+        if rank == 0:
+            q.put([b.numpy() for b in bufs])
         dist.barrier()
     finally:
         dist.destroy_process_group()
@@ -55,11 +66,14 @@ def test_channel_shard_reduce_world2():
     for p in procs:
         p.start()
     got = q.get(timeout=240)
+    piped = q.get(timeout=240)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     full = shard.stereo_partial_mix(np.stack([_channel_output(c) for c in range(TOTAL_CH)]), range(TOTAL_CH))
     np.testing.assert_allclose(got, full, rtol=0, atol=1e-12 * np.max(np.abs(full)))
+    for s, b in enumerate(piped):
+        np.testing.assert_allclose(b, full * (s + 1), rtol=0, atol=1e-12 * np.max(np.abs(full)) * (s + 1))
 
 
 def test_channel_groups_partition():
