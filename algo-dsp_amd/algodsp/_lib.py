@@ -185,6 +185,12 @@ def _declare(L: C.CDLL) -> None:
         "ad_fx_chain_compressor_metrics": (C.c_int, [vp, C.c_int, c_double_p, c_double_p, c_double_p]),
         "ad_fx_chain_eq_state": (C.c_int, [vp, c_double_p, i64]),
         "ad_fx_chain_destroy": (None, [vp]),
+        "ad_fx_graph_create": (C.c_int, [vp, C.c_int, C.c_int, C.c_int, C.POINTER(vp)]),
+        "ad_fx_graph_process": (C.c_int, [vp, c_double_p, i64]),
+        "ad_fx_graph_process_device": (C.c_int, [vp, vp, i64, i64, vp]),
+        "ad_fx_graph_reset": (C.c_int, [vp]),
+        "ad_fx_graph_op_count": (C.c_int, [vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+        "ad_fx_graph_destroy": (None, [vp]),
         "ad_biquad_chain_process": (C.c_int, [c_double_p, c_double_p, C.c_double, c_double_p, C.c_int, C.c_int, i64,
                                               C.c_int]),
         "ad_conv_reverb_create": (C.c_int, [c_double_p, i64, C.c_int, C.c_int, C.POINTER(vp)]),

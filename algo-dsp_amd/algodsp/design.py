@@ -105,3 +105,112 @@ def config5_eq(fs: float = 48000.0):
         ([high_shelf(8000.0, 2.0, 0.707, fs)], 1.0),
         ([lowpass(18000.0, 0.707, fs)], 1.0),
     ]
+
+
+# ---- Butterworth / Linkwitz-Riley cascades (crossover nodes) --------------
+def butterworth_q(order, index):  # butterworthQ pass/common.go:20-30
+    theta = math.pi * float(2 * index + 1) / (2 * float(order))
+    s = math.sin(theta)
+    if s == 0:
+        return 1 / math.sqrt(2)
+    return 1 / (2 * s)
+
+
+def _bw_first_order(freq, fs, high):  # butterworthFirstOrderLP/HP pass/common.go:34-70
+    if fs <= 0 or freq <= 0 or freq >= fs / 2:
+        return _ZERO
+    k = math.tan(math.pi * freq / fs)
+    norm = 1 / (1 + k)
+    return (norm, -norm, 0.0, (k - 1) * norm, 0.0) if high else (k * norm, k * norm, 0.0, (k - 1) * norm, 0.0)
+
+
+def butterworth_lp(freq, order, fs):  # ButterworthLP pass/butterworth.go:12-30
+    if order <= 0:
+        return None
+    secs = [lowpass(freq, butterworth_q(order, i), fs) for i in range(order // 2 - 1, -1, -1)]
+    if order % 2:
+        secs.append(_bw_first_order(freq, fs, False))
+    return secs
+
+
+def butterworth_hp(freq, order, fs):  # ButterworthHP pass/butterworth.go:35-53
+    if order <= 0:
+        return None
+    secs = [highpass(freq, butterworth_q(order, i), fs) for i in range(order // 2 - 1, -1, -1)]
+    if order % 2:
+        secs.append(_bw_first_order(freq, fs, True))
+    return secs
+
+
+def _lr_orders(order):  # linkwitzRileyPrototypeOrders pass/linkwitz_riley.go:116-122
+    return (order // 2, (order + 1) // 2) if order >= 2 else None
+
+
+def linkwitz_riley_lp(freq, order, fs):  # LinkwitzRileyLP pass/linkwitz_riley.go:23-45
+    o = _lr_orders(order)
+    if o is None or fs <= 0 or freq <= 0 or freq >= fs / 2:
+        return None
+    return butterworth_lp(freq, o[0], fs) + butterworth_lp(freq, o[1], fs)
+
+
+def linkwitz_riley_hp(freq, order, fs, inverted=False):  # pass/linkwitz_riley.go:61-105
+    o = _lr_orders(order)
+    if o is None or fs <= 0 or freq <= 0 or freq >= fs / 2:
+        return None
+    secs = butterworth_hp(freq, o[0], fs) + butterworth_hp(freq, o[1], fs)
+    if inverted:  # negate the first section's B coefficients
+        b0, b1, b2, a1, a2 = secs[0]
+        secs[0] = (-b0, -b1, -b2, a1, a2)
+    return secs
+
+
+def crossover(freq, order, fs):
+    """crossover.New (filter/crossover/crossover.go:31-65): (LP sections, HP
+    sections) of a two-way Linkwitz-Riley network, HP polarity-inverted for
+    orders = 2 mod 4; None where New returns an error."""
+    if order <= 0 or order % 2 or fs <= 0 or freq <= 0 or freq >= fs / 2:
+        return None
+    lp = linkwitz_riley_lp(freq, order, fs)
+    hp = linkwitz_riley_hp(freq, order, fs, inverted=(order % 4 == 2))
+    if lp is None or hp is None:
+        return None
+    return lp, hp
+
+
+class RBJDesigner:
+    """A FilterDesigner (effectchain/runtime_filter_pitch_reverb.go:18-24) for
+    the batched graph runtime: family "rbj" (one cookbook section) and
+    "butterworth" (lowpass/highpass cascades of the given order).  The
+    reference injects the webdemo's designer here; any designer works, since
+    the coefficients it returns are inputs to both the GPU and the oracle."""
+
+    KINDS = ("lowpass", "highpass", "peak", "lowshelf", "highshelf")
+
+    def NormalizeFamily(self, family):
+        return family if family in ("rbj", "butterworth") else "rbj"
+
+    def NormalizeFamilyForType(self, kind, family):
+        return family if kind in ("lowpass", "highpass") else "rbj"
+
+    def NormalizeOrder(self, kind, family, order):
+        return max(1, min(int(order), 8)) if family == "butterworth" else 2
+
+    def ClampShape(self, kind, family, freq, fs, q):
+        return q
+
+    def BuildChain(self, family, kind, order, freq, gain_db, q, fs):
+        """-> (sections [(b0, b1, b2, a1, a2)], chain gain)"""
+        if family == "butterworth":
+            secs = butterworth_lp(freq, order, fs) if kind == "lowpass" else butterworth_hp(freq, order, fs)
+            return secs, 1.0
+        if kind == "lowpass":
+            return [lowpass(freq, q, fs)], 1.0
+        if kind == "highpass":
+            return [highpass(freq, q, fs)], 1.0
+        if kind == "peak":
+            return [peak(freq, gain_db, q, fs)], 1.0
+        if kind == "lowshelf":
+            return [low_shelf(freq, gain_db, q, fs)], 1.0
+        if kind == "highshelf":
+            return [high_shelf(freq, gain_db, q, fs)], 1.0
+        raise NotImplementedError(f"RBJDesigner: filter kind {kind!r}")

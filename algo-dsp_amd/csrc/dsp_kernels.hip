@@ -642,6 +642,24 @@ __global__ __launch_bounds__(256) void k_decode_f16(const uint16_t* __restrict__
 
 }  // namespace
 
+// Fan-in average (mixParentEdgesInto, chain_process.go:295-318): the Go code
+// zeroes mixBuf, adds each parent's block in edge order, then scales by
+// 1/len(parents); the same rounded adds and one rounded multiply here.
+__global__ __launch_bounds__(256) void k_fx_mix(FxMixArgs a) {
+#pragma clang fp contract(off)
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int c = blockIdx.y;
+  if (t >= a.n) return;
+  double acc = 0.0;
+  for (int k = 0; k < a.nsrc; ++k) acc += a.src[k][(int64_t)c * a.src_stride[k] + t];
+  a.dst[(int64_t)c * a.dst_stride + t] = acc * (1.0 / (double)a.nsrc);
+}
+
+void launch_fx_mix(const FxMixArgs& a, hipStream_t s) {
+  if (a.n <= 0 || a.channels <= 0) return;
+  hipLaunchKernelGGL(k_fx_mix, dim3((unsigned)((a.n + 255) / 256), (unsigned)a.channels), dim3(256), 0, s, a);
+}
+
 void launch_decode_f16(const uint16_t* in, int64_t frames, int channels, double* out, hipStream_t s) {
   const int64_t n = frames * channels;
   if (n <= 0) return;

@@ -68,6 +68,18 @@ struct ChainArgs {
 // stages: bit 0 EQ, bit 1 compressor, bit 2 Freeverb
 void launch_chain(int stages, const ChainArgs& a, hipStream_t s);
 
+// Fan-in average of an effect-chain graph node (mixParentEdgesInto,
+// chain_process.go:295-318): dst = (0 + src0 + src1 + ...) * (1/nsrc).
+struct FxMixArgs {
+  const double* src[8];
+  int64_t src_stride[8];
+  int nsrc;
+  double* dst;
+  int64_t dst_stride, n;
+  int channels;
+};
+void launch_fx_mix(const FxMixArgs& a, hipStream_t s);
+
 // FIR block filter over [hist (N-1) | block (n)] per channel.
 struct FirArgs {
   const double* h;  // [N]

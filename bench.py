@@ -46,6 +46,8 @@ def parse():
                    help="HIP events around every engine kernel launch inside the timed region")
     p.add_argument("--channels", type=int, default=2,
                    help="conv: channels per GPU (IR[c %% 2]); 2 = the stereo config, 8 = config 4's shard")
+    p.add_argument("--graph", choices=["config5", "branched"], default=None,
+                   help="fx workload: run an effectchain graph through the batched graph runtime")
     p.add_argument("--workload", choices=["conv", "fx", "stream", "corr"], default="conv",
                    help="conv: BASELINE metric (overlap-save conv); fx: config 5 effect chain (256 ch); "
                         "stream: config 2 streaming OLS (mono, 16384 taps, 4096-sample host blocks); "
@@ -412,9 +414,15 @@ def main_fx(args):
     eq = design.config5_eq(fs)
     comp_cfg = {"auto_makeup": 0, "makeup_db": 0.0}  # runtime_dynamics.go:46-54
     verb = (0.22, 1.0, 0.72, 0.45, 0.015)
-    fx = processors.EffectChain(C, eq, comp_cfg, verb, fs, device=local)
     x = torch.from_numpy(np.stack([0.5 * signals.white_noise(n, 0x5EED + c) for c in range(C)])).to(dev)
     sptr = torch.cuda.current_stream(dev).cuda_stream
+    if args.graph:  # the batched effectchain graph runtime
+        from algodsp import effectchain
+
+        fx = effectchain.Chain(fs, C, designer=design.RBJDesigner(), device=local)
+        fx.LoadGraph(effectchain.EXAMPLE_GRAPHS[args.graph])
+    else:
+        fx = processors.EffectChain(C, eq, comp_cfg, verb, fs, device=local)
 
     def step():
         fx.process_device(x.data_ptr(), n, n, sptr)
@@ -461,8 +469,11 @@ def main_fx(args):
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic: 0.5 x SplitMix64 white noise, 48 kHz",
-            "config": {"workload": f"effectchain filter x5 (RBJ) -> dyn-compressor -> reverb-freeverb, {C} ch x "
-                                   f"{n} samples per GPU per step, fused per sample",
+            "config": {"workload": (f"effectchain graph '{args.graph}' through the batched graph runtime "
+                                    f"({fx.op_count()[0]} device ops per call), {C} ch x {n} samples per GPU per step"
+                                    if args.graph else
+                                    f"effectchain filter x5 (RBJ) -> dyn-compressor -> reverb-freeverb, {C} ch x "
+                                    f"{n} samples per GPU per step, fused per sample"),
                        "channels_per_gpu": C, "samples_per_channel": n,
                        "parallelism": "replicas" if world > 1 else "single GPU"},
             "roofline": {"bound": "hbm", "achieved": round(value * 16e6 / 1e9, 3), "peak": HBM_PEAK_GBS,

@@ -42,6 +42,8 @@ extern "C" {
 #define AD_ERR_INVALID_ARGUMENT 8         /* non-sentinel fmt.Errorf validation errors,
                                              e.g. streaming_overlap_save.go:50-52 */
 #define AD_ERR_DIVISION_BY_ZERO 9         /* conv.ErrDivisionByZero    deconvolve.go:14 */
+#define AD_ERR_UNKNOWN_EFFECT 10          /* effectchain.ErrUnknownEffect chain.go:11 (here: a node
+                                             type the GPU graph runtime does not run) */
 #define AD_ERR_DEVICE 100                 /* HIP runtime failure */
 #define AD_ERR_NO_DEVICE 101              /* no usable gfx950 device */
 #define AD_ERR_INTERNAL 102
@@ -215,6 +217,62 @@ int ad_fx_chain_compressor_metrics(ad_fx_chain* h, int channel, double* input_pe
 /* EQ section state [channels][nsec][2] {d0, d1} (Chain.State, chain.go:122-130). */
 int ad_fx_chain_eq_state(ad_fx_chain* h, double* state, int64_t cap);
 void ad_fx_chain_destroy(ad_fx_chain* h);
+
+/* ---- batched effectchain graph (dsp/effectchain, 8(f)4) -------------------
+ * `channels` copies of one effect-chain graph, each with its own state, run
+ * together (one lane per channel).  Replaces effectchain.Chain.Process
+ * (chain_process.go:11-33) for graphs made of the node types below; the
+ * host-side graph compiler (JSON parse + Kahn order, graph.go:57-165, node
+ * Configure param clamps, runtime_*.go) lives in the caller and passes the
+ * nodes in topological order, node 0 being `_input`.
+ * Per node (processNode, chain_process.go:136-175): the input is the
+ * average of the parents' outputs (mixParentEdgesInto :295-318: zeros with
+ * no parent, a copy for one, sum in edge order * 1/k for k), then
+ *   AD_FXN_SPLIT_FREQ  LR crossover: low = LP chain, high = HP chain, read by
+ *                      consumers through parent port 0 / 1 (crossover.go:80-94,
+ *                      chain_process.go:177-227; not affected by `bypassed`);
+ *   AD_FXN_OUTPUT / AD_FXN_PASS ("split", "sum") / bypassed: mix only;
+ *   AD_FXN_BIQUAD      biquad.Chain.ProcessBlock, sections [nsec][6] as in
+ *                      ad_fx_chain_set_eq (filter* nodes, runtime_filter_pitch_reverb.go:186-195);
+ *   AD_FXN_COMPRESSOR  Compressor.ProcessInPlace with *comp (dyn-compressor,
+ *                      and dyn-limiter = NewLimiter's ratio 100 / attack 0.1 ms /
+ *                      hard knee / no makeup config, limiter.go:11-44);
+ *   AD_FXN_FREEVERB    reverb.Reverb.ProcessInPlace, verb = {wet, dry,
+ *                      room_size, damp, gain} (runtime_filter_pitch_reverb.go:330-345).
+ * The result is the output node's buffer.  Linear runs of in-place nodes fuse
+ * into one launch (bit-identical, see capi_fxgraph.cpp).  Other node types
+ * return AD_ERR_UNKNOWN_EFFECT; the configs are copied at create.          */
+#define AD_FXN_INPUT 0
+#define AD_FXN_OUTPUT 1
+#define AD_FXN_PASS 2
+#define AD_FXN_SPLIT_FREQ 3
+#define AD_FXN_BIQUAD 4
+#define AD_FXN_COMPRESSOR 5
+#define AD_FXN_FREEVERB 6
+#define AD_FX_MAX_PARENTS 8
+typedef struct ad_fx_node {
+  int type;
+  int bypassed;
+  int n_parents;
+  const int32_t* parents;      /* indices of earlier nodes, in the graph's edge order */
+  const int32_t* parent_ports; /* NULL: all 0; 1 = a split-freq node's high band */
+  const double* sections;      /* BIQUAD: [nsec][6]; SPLIT_FREQ: low-band (LP) chain */
+  int nsec;
+  const double* sections2;     /* SPLIT_FREQ: high-band (HP) chain [nsec2][6] */
+  int nsec2;
+  const ad_compressor_config* comp; /* COMPRESSOR */
+  double verb[5];                   /* FREEVERB: wet, dry, room_size, damp, gain */
+} ad_fx_node;
+typedef struct ad_fx_graph ad_fx_graph;
+int ad_fx_graph_create(const ad_fx_node* nodes, int n_nodes, int channels, int device, ad_fx_graph** out);
+/* buf [channels][n] (host) / [channels][stride] (device), processed in place. */
+int ad_fx_graph_process(ad_fx_graph* g, double* buf, int64_t n);
+int ad_fx_graph_process_device(ad_fx_graph* g, double* d_buf, int64_t stride, int64_t n, void* stream);
+int ad_fx_graph_reset(ad_fx_graph* g); /* every node runtime's Reset() */
+/* Compiled size: device ops per call, buffers (including the caller's) and
+ * streams the independent branches are spread over (the caller's included). */
+int ad_fx_graph_op_count(const ad_fx_graph* g, int* launches, int* buffers, int* lanes);
+void ad_fx_graph_destroy(ad_fx_graph* g);
 
 /* One-shot biquad.Chain.ProcessBlock over `channels` chains sharing one
  * coefficient set coeffs [sections][5] {b0,b1,b2,a1,a2} and gain (chain.go:59-70);

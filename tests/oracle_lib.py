@@ -425,3 +425,76 @@ def irlib_read(data: bytes):
         _ck(lib().or_irlib_get(data, len(data), i, name, 256, C.byref(fs), C.byref(ch), C.byref(ln), P(buf)))
         res.append((name.value.decode(), fs.value, buf.reshape(ch.value, ln.value)))
     return res
+
+
+# ---- effectchain graph (chain_process.go:11-319), one channel -------------
+class FxGraph:
+    """Restatement of effectchain.Chain.Process over the oracle's node
+    runtimes for ONE channel: nodes in topological order, input of a node =
+    mixParentEdgesInto (zeros / copy / sum in edge order * 1/k), split-freq ->
+    crossover LP/HP chains read by port, _output/bypassed mix only, others in
+    place; the result is the _output buffer.  `nodes` is the compiled list of
+    algodsp.effectchain: dicts {type, bypassed, parents [(idx, port)],
+    sections, sections2 ([n][5] + gain), comp (field dict), verb}."""
+
+    def __init__(self, nodes, fs):
+        self.nodes = nodes
+        self.rt = []
+        for d in nodes:
+            t = d["type"]
+            if t == "biquad":
+                secs, gain = d["sections"]
+                self.rt.append(["biquad", np.asarray(secs, dtype=np.float64).ravel(), np.zeros(2 * len(secs)), gain])
+            elif t == "split":
+                lp, hp = d["sections"], d["sections2"]
+                self.rt.append(["split", np.asarray(lp, dtype=np.float64).ravel(), np.zeros(2 * len(lp)),
+                                np.asarray(hp, dtype=np.float64).ravel(), np.zeros(2 * len(hp))])
+            elif t == "comp":
+                cfg = {k: v for k, v in d["comp"].items() if k != "sample_rate"}
+                self.rt.append(["comp", Compressor(d["comp"]["sample_rate"], **cfg)])
+            elif t == "verb":
+                v = Freeverb()
+                v.set(*d["verb"])
+                self.rt.append(["verb", v])
+            else:
+                self.rt.append([t])
+
+    def process(self, block):
+        n = len(block)
+        buf, low, high = {}, {}, {}
+        for i, d in enumerate(self.nodes):
+            if i == 0:
+                buf[0] = np.array(block, dtype=np.float64)
+                continue
+            par = d["parents"]
+
+            def src(e):
+                j, port = e
+                if self.nodes[j]["type"] == "split":
+                    return high[j] if port == 1 else low[j]
+                return buf[j]
+
+            if not par:
+                dst = np.zeros(n)
+            elif len(par) == 1:
+                dst = src(par[0]).copy()
+            else:
+                mix = np.zeros(n)
+                for e in par:
+                    mix = mix + src(e)
+                dst = mix * (1.0 / len(par))
+            buf[i] = dst
+            r = self.rt[i]
+            if r[0] == "split":
+                low[i], r[2] = biquad_chain_block(r[1], r[2], 1.0, dst)
+                high[i], r[4] = biquad_chain_block(r[3], r[4], 1.0, dst)
+                continue
+            if d["type"] in ("output", "pass") or d["bypassed"]:
+                continue
+            if r[0] == "biquad":
+                buf[i], r[2] = biquad_chain_block(r[1], r[2], r[3], dst)
+            elif r[0] == "comp":
+                buf[i] = r[1].process_in_place(dst)
+            elif r[0] == "verb":
+                buf[i] = r[1].process_in_place(dst)
+        return buf[[i for i, d in enumerate(self.nodes) if d["type"] == "output"][0]]

@@ -1,0 +1,195 @@
+"""Batched effectchain graph runtime: `channels` copies of one
+dsp/effectchain graph on the GPU vs the oracle's restatement of
+Chain.Process (chain_process.go:11-319) channel by channel.
+
+Tolerance: <= 1e-12 RMS (the compressor's log2/exp2 come from the GPU math
+library vs the host libm, see test_dsp_gpu.py); the biquad, Freeverb, mix
+and crossover paths are bit-exact.  The CPU tests cover the host-side graph
+compiler (graph.go parse/order rules) and the crossover designer against the
+reference's own crossover test properties (crossover_test.go:73-161).
+"""
+import json
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+from algodsp import design, effectchain as E, signals
+
+RMS_TOL = 1e-12
+FS = 48000.0
+
+
+def rms(a, b):
+    return float(np.sqrt(np.mean((np.asarray(a) - np.asarray(b)) ** 2)))
+
+
+def graph(nodes, edges):
+    return json.dumps({
+        "nodes": [{"id": "_input", "type": "_input"}, {"id": "_output", "type": "_output"}] + nodes,
+        "connections": [dict(zip(("from", "to", "fromPortIndex"), e)) for e in edges],
+    })
+
+
+CONFIG5 = graph(
+    [{"id": "hp", "type": "filter-highpass", "params": {"freq": 40, "q": 0.707}},
+     {"id": "ls", "type": "filter-lowshelf", "params": {"freq": 100, "gain": 3, "q": 0.707}},
+     {"id": "pk", "type": "filter-peak", "params": {"freq": 1000, "gain": -2, "q": 1}},
+     {"id": "hs", "type": "filter-highshelf", "params": {"freq": 8000, "gain": 2, "q": 0.707}},
+     {"id": "lp", "type": "filter-lowpass", "params": {"freq": 18000, "q": 0.707}},
+     {"id": "comp", "type": "dyn-compressor", "params": {"thresholdDB": -20, "ratio": 4}},
+     {"id": "verb", "type": "reverb-freeverb", "params": {}}],
+    [("_input", "hp"), ("hp", "ls"), ("ls", "pk"), ("pk", "hs"), ("hs", "lp"), ("lp", "comp"),
+     ("comp", "verb"), ("verb", "_output")])
+
+# split-freq crossover, a limiter on the low band, Freeverb on the high band,
+# a dry path straight from the input, a bypassed node and a fan-in of three
+BRANCHED = graph(
+    [{"id": "xo", "type": "split-freq", "params": {"freqHz": 800}},
+     {"id": "lim", "type": "dyn-limiter", "params": {"thresholdDB": -6, "releaseMs": 50}},
+     {"id": "eq", "type": "filter-peak", "params": {"freq": 3000, "gain": 4, "q": 2}},
+     {"id": "verb", "type": "reverb-freeverb", "params": {"wet": 0.5, "roomSize": 0.9}},
+     {"id": "byp", "type": "dyn-compressor", "bypassed": True, "params": {"ratio": 10}},
+     {"id": "comp", "type": "dyn-compressor", "params": {"thresholdDB": -30, "ratio": 3, "kneeDB": 0}}],
+    [("_input", "xo"), ("xo", "lim", 0), ("xo", "eq", 1), ("eq", "verb"), ("_input", "byp"),
+     ("lim", "comp"), ("comp", "_output"), ("verb", "_output"), ("byp", "_output")])
+
+
+# ------------------------------------------------------------------ CPU tests
+def test_parse_graph_rules():
+    g = E.parse_graph(graph([{"id": "a", "type": "split"}, {"id": "", "type": "x"}, {"id": "b", "type": "sum"}],
+                            [("_input", "a"), ("a", "b"), ("b", "_output"), ("a", "a"), ("a", "ghost")]))
+    assert set(g.Order) == {"_input", "_output", "a", "b"}
+    assert g.Order.index("_input") < g.Order.index("a") < g.Order.index("b") < g.Order.index("_output")
+    assert len(g.Incoming["a"]) == 1  # self-loop and unknown target dropped
+    with pytest.raises(E.GraphError):
+        E.parse_graph(graph([{"id": "a", "type": "split"}, {"id": "b", "type": "split"}],
+                            [("a", "b"), ("b", "a")]))
+    assert E.parse_graph(json.dumps({"nodes": [{"id": "_input", "type": "_input"}]})).Order == []
+    assert E.parse_graph("").Order == []
+    with pytest.raises(E.GraphError):
+        E.parse_graph("{not json")
+
+
+def test_param_clamps():
+    p = E.Params("c", "dyn-compressor", num={"thresholdDB": -90, "ratio": 500, "attackMs": 0.0})
+    c = E.compressor_config(p, FS)
+    assert (c.threshold_db, c.ratio, c.attack_ms, c.auto_makeup) == (-60, 100, 0.1, 0)
+    lim = E.limiter_config(E.Params("l", "dyn-limiter", num={"thresholdDB": float("nan")}), FS)
+    assert (lim.threshold_db, lim.ratio, lim.attack_ms, lim.knee_db) == (-0.1, 100.0, 0.1, 0.0)
+    assert E.freeverb_params(E.Params("v", "reverb-freeverb", num={"roomSize": 2})) == (0.22, 1, 0.98, 0.45, 0.015)
+    lp, hp = E.split_freq_sections(E.Params("x", "split-freq", num={"freqHz": 1e6}), FS)
+    assert lp == design.crossover(FS * 0.5 * 0.95, 4, FS)[0]
+
+
+def _chain_response(secs, f, fs):
+    z = np.exp(-2j * np.pi * f / fs)
+    h = 1.0
+    for b0, b1, b2, a1, a2 in secs:
+        h *= (b0 + b1 * z + b2 * z * z) / (1 + a1 * z + a2 * z * z)
+    return h
+
+
+@pytest.mark.parametrize("order", [2, 4, 8, 12])
+def test_crossover_allpass_sum(order):
+    """crossover_test.go:73-103: |LP + HP| = 0 dB within 0.1 dB at 20 Hz .. 20 kHz."""
+    lp, hp = design.crossover(1000, order, FS)
+    for f in (20, 50, 100, 200, 500, 1000, 2000, 5000, 10000, 20000):
+        mag = 20 * np.log10(abs(_chain_response(lp, f, FS) + _chain_response(hp, f, FS)))
+        assert abs(mag) < 0.1
+    assert design.crossover(1000, 3, FS) is None and design.crossover(30000, 4, FS) is None
+
+
+def test_unknown_effects_rejected():
+    for t in ("chorus", "filter-moog", "dyn-lookahead", "vocoder", "reverb-conv"):
+        ch = E.Chain(FS, 2, designer=design.RBJDesigner())
+        with pytest.raises(E.UnknownEffect):
+            ch.LoadGraph(graph([{"id": "n", "type": t}], [("_input", "n"), ("n", "_output")]))
+
+
+# ------------------------------------------------------------------ GPU tests
+def _run_both(g, C, n, calls=1, designer=None, scale=0.5):
+    ch = E.Chain(FS, C, designer=designer or design.RBJDesigner())
+    ch.LoadGraph(g)
+    oracles = [O.FxGraph(ch.spec, FS) for _ in range(C)]
+    worst = 0.0
+    for k in range(calls):
+        x = np.stack([scale * signals.white_noise(n, 1000 * k + c) for c in range(C)])
+        y = x.copy()
+        assert ch.Process(y)
+        for c in range(C):
+            want = oracles[c].process(x[c])
+            worst = max(worst, rms(y[c], want))
+            assert np.max(np.abs(y[c] - want)) < 1e-10
+    return ch, worst
+
+
+@pytest.mark.gpu
+def test_config5_graph_fuses_and_matches(gpu):
+    ch, err = _run_both(CONFIG5, 5, 3000, calls=2)
+    assert err < RMS_TOL
+    launches, buffers, lanes = ch.op_count()
+    assert (launches, buffers, lanes) == (1, 1, 1)  # filter x5 -> compressor -> Freeverb in one in-place launch
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 777, 4096])
+def test_branched_graph(gpu, n):
+    ch, err = _run_both(BRANCHED, 3, n, calls=3)
+    assert err < RMS_TOL
+    assert ch.op_count()[2] >= 2  # the crossover's two bands run on their own streams
+
+
+@pytest.mark.gpu
+def test_crossover_impulse_energy(gpu):
+    """crossover_test.go:138-161: LP + HP of an impulse is allpass (energy 1 +- 0.001);
+    the output node averages the two bands, so the sum is 2 * out."""
+    g = graph([{"id": "xo", "type": "split-freq", "params": {"freqHz": 1000}}],
+              [("_input", "xo"), ("xo", "_output", 0), ("xo", "_output", 1)])
+    ch = E.Chain(FS, 2)
+    ch.LoadGraph(g)
+    x = np.zeros((2, 4096))
+    x[:, 0] = 1.0
+    ch.Process(x)
+    e = np.sum((2 * x) ** 2, axis=1)
+    assert np.all(np.abs(e - 1.0) < 0.001)
+
+
+@pytest.mark.gpu
+def test_unconnected_and_passthrough_nodes(gpu):
+    """A node without parents processes zeros; without a designer, filter nodes
+    keep the passthrough chain {B0: 1} (registry_defaults.go:152-158)."""
+    g = graph([{"id": "v", "type": "reverb-freeverb"}, {"id": "f", "type": "filter-lowpass"},
+               {"id": "s", "type": "sum"}],
+              [("_input", "f"), ("f", "s"), ("s", "_output"), ("v", "_output")])
+    ch = E.Chain(FS, 2, designer=None)
+    ch.LoadGraph(g)
+    x = np.stack([signals.white_noise(500, c) for c in range(2)])
+    y = x.copy()
+    ch.Process(y)
+    oracle = O.FxGraph(ch.spec, FS)
+    np.testing.assert_array_equal(y[1], oracle.process(x[1]))
+    np.testing.assert_array_equal(y, x * 0.5)
+
+
+@pytest.mark.gpu
+def test_reset_and_device_path(gpu):
+    import torch
+
+    ch = E.Chain(FS, 4, designer=design.RBJDesigner())
+    ch.LoadGraph(BRANCHED)
+    x = np.stack([0.5 * signals.white_noise(2048, c) for c in range(4)])
+    first = x.copy()
+    ch.Process(first)
+    ch.Process(x.copy())
+    ch.Reset()
+    again = x.copy()
+    ch.Process(again)
+    np.testing.assert_array_equal(again, first)
+    ch.Reset()
+    d = torch.zeros((4, 3000), dtype=torch.float64, device="cuda")
+    d[:, :2048] = torch.from_numpy(x).cuda()
+    ch.process_device(d.data_ptr(), 3000, 2048)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(d[:, :2048].cpu().numpy(), first)
+    assert not d[:, 2048:].any()
