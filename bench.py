@@ -5,10 +5,12 @@
 
   python bench.py --gpus N --steps K --warmup W
 
-N > 1 (torchrun, one rank per GPU): every rank convolves its own stereo
-channel pair (weak scaling; channel group per GPU) and the
-per-rank stereo outputs are summed to rank 0 with one RCCL reduce over xGMI
-(the north star's stereo mixdown), inside the timed step.
+N > 1 (torchrun, one rank per GPU): config 4's shard (BASELINE.json
+configs[3]): every rank convolves its own group of 8 channels x 2^22 samples
+(ch c with IR[c mod 2]) -- the same 2^25 samples per GPU per step as the N = 1
+stereo config, so per-GPU work is fixed (weak scaling) -- and the per-rank
+stereo partial mixes are summed to rank 0 with one RCCL reduce over xGMI (the
+north star's stereo mixdown), inside the timed step.
 Rank 0 prints one JSON line.
 """
 from __future__ import annotations
@@ -31,7 +33,8 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--samples", type=int, default=1 << 24, help="samples per channel per step")
+    p.add_argument("--samples", type=int, default=None,
+                   help="samples per channel per step (default 2^24 at N = 1, 2^22 at N > 1)")
     p.add_argument("--hop", type=int, default=8192)
     p.add_argument("--chunk", type=int, default=0, help="blocks per channel per engine chunk (0 = auto)")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -44,8 +47,9 @@ def parse():
                         "mixdown reduce starts as soon as it is computed")
     p.add_argument("--kernel-timing", choices=["on", "off"], default="on",
                    help="HIP events around every engine kernel launch inside the timed region")
-    p.add_argument("--channels", type=int, default=2,
-                   help="conv: channels per GPU (IR[c %% 2]); 2 = the stereo config, 8 = config 4's shard")
+    p.add_argument("--channels", type=int, default=None,
+                   help="conv: channels per GPU (IR[c %% 2]); default 2 (the stereo config) at N = 1, "
+                        "8 (config 4's shard) at N > 1")
     p.add_argument("--graph", choices=["config5", "branched"], default=None,
                    help="fx workload: run an effectchain graph through the batched graph runtime")
     p.add_argument("--workload", choices=["conv", "fx", "stream", "corr"], default="conv",
@@ -104,6 +108,12 @@ def main():
     if world > 1 or mixdown:  # --mixdown on at N = 1 (under torchrun) exercises the RCCL path
         dist.init_process_group("nccl", device_id=dev)
 
+    # N = 1: config 3 (stereo x 2^24). N > 1: config 4's shard (8 ch x 2^22 per
+    # GPU): same samples per GPU, a 4x smaller stereo mixdown per step to reduce.
+    if args.channels is None:
+        args.channels = 8 if world > 1 else 2
+    if args.samples is None:
+        args.samples = (1 << 22) if world > 1 else (1 << 24)
     ir = irlib.large_church()                       # [2][131072], Large Church zero padded
     K = ir.shape[1]
     n = args.samples
@@ -237,7 +247,10 @@ def main():
                     "(f16, reference decodeF16), zero padded 95432->131072 taps",
             "config": {
                 "workload": ("OverlapSave partitioned conv, stereo, 131072-tap IR, full linear convolution "
-                             if C == 2 else f"{C}-channel x 131072-tap IR convolution (IR[c mod 2]) ") +
+                             if C == 2 and world == 1 else
+                             f"{C * world}-channel x 131072-tap IR convolution reverb (IR[c mod 2]), channels "
+                             f"sharded {C}-per-GPU, RCCL stereo mixdown " if mixdown else
+                             f"{C}-channel x 131072-tap IR convolution (IR[c mod 2]) ") +
                             f"({C} ch x {n} samples per GPU per step)",
                 "channels_per_gpu": C,
                 "samples_per_channel": n,
@@ -280,7 +293,7 @@ def main_stream(args):
 
     ir = irlib.large_church()[0, :16384]
     B = 4096
-    nblk = max(1, args.samples // B) if args.samples != (1 << 24) else 2048
+    nblk = max(1, args.samples // B) if args.samples else 2048
     x = signals.white_noise(nblk * B, 0x5EED)
     y = np.empty_like(x)
     s = conv.NewStreamingOverlapSave(ir, B)
@@ -330,7 +343,7 @@ def main_corr(args):
     from algodsp import _lib, signals
 
     dev = torch.device("cuda", 0)
-    n = args.samples if args.samples != (1 << 24) else (1 << 23)
+    n = args.samples or (1 << 23)
     a = torch.from_numpy(signals.white_noise(n, 0x5EED)).to(dev)
     b = torch.from_numpy(signals.white_noise(n, 0x5EEE)).to(dev)
     out = torch.empty(2 * n - 1, dtype=torch.float64, device=dev)
@@ -410,7 +423,7 @@ def main_fx(args):
         dist.init_process_group("nccl", device_id=dev)
     fs = 48000.0
     C = 256
-    n = args.samples if args.samples != (1 << 24) else (1 << 20)
+    n = args.samples or (1 << 20)
     eq = design.config5_eq(fs)
     comp_cfg = {"auto_makeup": 0, "makeup_db": 0.0}  # runtime_dynamics.go:46-54
     verb = (0.22, 1.0, 0.72, 0.45, 0.015)

@@ -1,7 +1,9 @@
 set -u
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_fxgraph.py -p no:cacheprovider > gpurun_out/t_fx.log 2>&1; rc=$?; tail -5 gpurun_out/t_fx.log; [ $rc -eq 0 ] || exit $rc
-for g in "--graph config5" "--graph branched"; do
-timeout -k 10 200 python bench.py --workload fx --steps 3 --warmup 1 --no-cpu-baseline $g > gpurun_out/bfx.log 2>&1 || { cat gpurun_out/bfx.log; exit 1; }
-grep -o '"value": [0-9.]*' gpurun_out/bfx.log; grep -o '"workload": "[^"]*' gpurun_out/bfx.log
-done
+B="--steps 5 --warmup 2 --no-cpu-baseline"
+timeout -k 10 200 python bench.py $B > gpurun_out/b1.log 2>&1 || { tail gpurun_out/b1.log; exit 1; }
+grep -o '"value": [0-9.]*\|"ms_per_step": [0-9.]*' gpurun_out/b1.log | tr '\n' ' '; echo
+timeout -k 10 200 python bench.py $B --channels 8 --samples 4194304 > gpurun_out/b2.log 2>&1 || { tail gpurun_out/b2.log; exit 1; }
+grep -o '"value": [0-9.]*\|"ms_per_step": [0-9.]*' gpurun_out/b2.log | tr '\n' ' '; echo
+timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29511 bench.py $B --channels 8 --samples 4194304 --mixdown on > gpurun_out/b3.log 2>&1 || { tail gpurun_out/b3.log; exit 1; }
+grep -o '"value": [0-9.]*\|"ms_per_step": [0-9.]*\|"workload": "[^"]*' gpurun_out/b3.log | tr '\n' ' '; echo
