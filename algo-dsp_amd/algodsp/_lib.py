@@ -164,6 +164,7 @@ def _declare(L: C.CDLL) -> None:
         "ad_conv_destroy": (None, [vp]),
         "ad_conv_direct": (C.c_int, [c_double_p, i64, c_double_p, i64, c_double_p, C.c_int]),
         "ad_conv_direct_circular": (C.c_int, [c_double_p, i64, c_double_p, i64, c_double_p, C.c_int]),
+        "ad_conv_direct_device": (C.c_int, [C.c_void_p, i64, C.c_void_p, i64, C.c_void_p, C.c_void_p]),
         "ad_conv_convolve": (C.c_int, [c_double_p, i64, c_double_p, i64, C.c_int, c_double_p, i64, c_int64_p,
                                        C.c_int]),
         "ad_conv_multi_create": (C.c_int, [c_double_p, C.c_int, i64, i64, C.c_int, C.POINTER(C.c_int32), i64,

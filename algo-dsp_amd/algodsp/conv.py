@@ -195,6 +195,13 @@ def Direct(a, b) -> np.ndarray:
     return out
 
 
+def direct_device(d_a: int, n: int, d_b: int, m: int, d_dst: int, stream: int = 0) -> None:
+    """conv.DirectTo (conv.go:97-154) on device buffers (d_dst: n+m-1 f64),
+    enqueued on `stream`."""
+    check(lib().ad_conv_direct_device(C.c_void_p(d_a), int(n), C.c_void_p(d_b), int(m), C.c_void_p(d_dst),
+                                      C.c_void_p(stream or 0)))
+
+
 def DirectCircular(a, b) -> np.ndarray:
     """conv.go:158-173"""
     x, y = f64(a), f64(b)

@@ -547,6 +547,17 @@ int ad_conv_direct(const double* a, int64_t n, const double* b, int64_t m, doubl
   });
 }
 
+int ad_conv_direct_device(const double* d_a, int64_t n, const double* d_b, int64_t m, double* d_dst, void* stream) {
+  // conv.DirectTo conv.go:97-154 on device-resident buffers (dst: n+m-1)
+  return guard([&] {
+    if (n <= 0) AD_FAIL(AD_ERR_EMPTY_INPUT, "conv: empty input");
+    if (m <= 0) AD_FAIL(AD_ERR_EMPTY_KERNEL, "conv: empty kernel");
+    if (!d_a || !d_b || !d_dst) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "conv: null device buffer");
+    launch_direct(d_a, n, d_b, m, d_dst, (hipStream_t)stream);
+    AD_HIP(hipGetLastError());
+  });
+}
+
 int ad_conv_direct_circular(const double* a, int64_t n, const double* b, int64_t m, double* dst, int device) {
   // conv.DirectCircular conv.go:158-173
   return guard([&] {

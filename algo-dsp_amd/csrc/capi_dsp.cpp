@@ -395,12 +395,14 @@ int ad_biquad_chain_process(const double* coeffs, double* state, double gain, do
 // ---------------------------------------------------------------------------
 struct ad_fir {
   int device = 0, channels = 0;
-  int64_t N = 0, cap = 0;
-  hipStream_t stream = nullptr;
-  DevBuf<double> h;     // [N]
-  DevBuf<double> xbuf;  // [C][N-1 + cap]
-  DevBuf<double> ybuf;  // [C][cap]
-  DevBuf<double> hbuf;  // [C][N-1] history staging (the shift may overlap)
+  int64_t N = 0;
+  hipStream_t stream = nullptr;       // host-buffer calls
+  hipStream_t last = nullptr;         // stream of the last call (Reset orders after it)
+  DevBuf<double> h;                   // [N]
+  DevBuf<double> hist[2];             // [C][N-1] delay line, ping-pong (cur = hist[cur])
+  int cur = 0;
+  DevBuf<double> stage;               // [C][n]: in-place calls read a copy of the input
+  DevBuf<double> io_in, io_out;       // host-buffer calls
   ~ad_fir() {
     if (stream) {
       (void)hipStreamSynchronize(stream);
@@ -411,54 +413,54 @@ struct ad_fir {
 
 namespace {
 
-void fir_reserve(ad_fir* f, int64_t n) {
-  if (n <= f->cap) return;
-  const int64_t hist = f->N - 1;
-  DevBuf<double> nx;
-  nx.alloc((size_t)f->channels * (hist + n));
-  if (hist > 0) {
-    if (f->cap > 0) {
-      AD_HIP(hipMemcpy2DAsync(nx.p, (hist + n) * sizeof(double), f->xbuf.p, (hist + f->cap) * sizeof(double),
-                              hist * sizeof(double), f->channels, hipMemcpyDeviceToDevice, f->stream));
-    } else {
-      AD_HIP(hipMemsetAsync(nx.p, 0, nx.n * sizeof(double), f->stream));
-    }
-  }
-  AD_HIP(hipStreamSynchronize(f->stream));
-  std::swap(f->xbuf.p, nx.p);
-  std::swap(f->xbuf.n, nx.n);
-  f->ybuf.alloc((size_t)f->channels * n);
-  f->cap = n;
-}
-
 // y = FIR(x) for n new samples per channel, device in/out; updates history.
+// The kernel reads the old delay line and the input directly; the next
+// delay line (last N-1 samples of [hist | src]) is built in the other
+// history buffer first, so nothing the kernel reads is written meanwhile.
+// An in-place call (dst overlaps src) reads a staged copy of src.
 void fir_run(ad_fir* f, const double* d_src, int64_t src_stride, double* d_dst, int64_t dst_stride, int64_t n,
              hipStream_t s) {
-  fir_reserve(f, n);
-  const int64_t hist = f->N - 1, xs = hist + f->cap;
-  AD_HIP(hipMemcpy2DAsync(f->xbuf.p + hist, xs * sizeof(double), d_src, src_stride * sizeof(double),
-                          n * sizeof(double), f->channels, hipMemcpyDeviceToDevice, s));
+  const int64_t hn = f->N - 1;
+  const size_t C = (size_t)f->channels;
+  const char* s0 = reinterpret_cast<const char*>(d_src);
+  const char* s1 = reinterpret_cast<const char*>(d_src + (C - 1) * src_stride + n);
+  const char* d0 = reinterpret_cast<const char*>(d_dst);
+  const char* d1 = reinterpret_cast<const char*>(d_dst + (C - 1) * dst_stride + n);
+  if (s0 < d1 && d0 < s1) {
+    f->stage.reserve(C * n);
+    AD_HIP(hipMemcpy2DAsync(f->stage.p, n * sizeof(double), d_src, src_stride * sizeof(double), n * sizeof(double),
+                            C, hipMemcpyDeviceToDevice, s));
+    d_src = f->stage.p;
+    src_stride = n;
+  }
+  const double* hold = f->hist[f->cur].p;
+  if (hn > 0) {
+    double* hnew = f->hist[f->cur ^ 1].p;
+    if (n >= hn) {
+      AD_HIP(hipMemcpy2DAsync(hnew, hn * sizeof(double), d_src + (n - hn), src_stride * sizeof(double),
+                              hn * sizeof(double), C, hipMemcpyDeviceToDevice, s));
+    } else {
+      AD_HIP(hipMemcpy2DAsync(hnew, hn * sizeof(double), hold + n, hn * sizeof(double), (hn - n) * sizeof(double),
+                              C, hipMemcpyDeviceToDevice, s));
+      AD_HIP(hipMemcpy2DAsync(hnew + (hn - n), hn * sizeof(double), d_src, src_stride * sizeof(double),
+                              n * sizeof(double), C, hipMemcpyDeviceToDevice, s));
+    }
+  }
   FirArgs a{};
   a.h = f->h.p;
   a.N = f->N;
-  a.x = f->xbuf.p;
-  a.xstride = xs;
-  a.y = f->ybuf.p;
-  a.ystride = f->cap;
+  a.hist = hold;
+  a.src = d_src;
+  a.sstride = src_stride;
+  a.y = d_dst;
+  a.ystride = dst_stride;
   a.n = n;
   a.channels = f->channels;
   a.reversed = f->N >= 32;
   launch_fir(a, s);
   AD_HIP(hipGetLastError());
-  AD_HIP(hipMemcpy2DAsync(d_dst, dst_stride * sizeof(double), f->ybuf.p, f->cap * sizeof(double),
-                          n * sizeof(double), f->channels, hipMemcpyDeviceToDevice, s));
-  if (hist > 0) {  // new history = last N-1 samples of [hist | block]
-    f->hbuf.reserve((size_t)f->channels * hist);
-    AD_HIP(hipMemcpy2DAsync(f->hbuf.p, hist * sizeof(double), f->xbuf.p + n, xs * sizeof(double),
-                            hist * sizeof(double), f->channels, hipMemcpyDeviceToDevice, s));
-    AD_HIP(hipMemcpy2DAsync(f->xbuf.p, xs * sizeof(double), f->hbuf.p, hist * sizeof(double),
-                            hist * sizeof(double), f->channels, hipMemcpyDeviceToDevice, s));
-  }
+  if (hn > 0) f->cur ^= 1;
+  f->last = s;
 }
 
 }  // namespace
@@ -482,6 +484,12 @@ int ad_fir_create(const double* coeffs, int64_t n_taps, int channels, int device
       f->h.alloc((size_t)n_taps);
       AD_HIP(hipMemcpy(f->h.p, coeffs, n_taps * sizeof(double), hipMemcpyHostToDevice));
     }
+    if (n_taps > 1) {
+      for (auto& hb : f->hist) {
+        hb.alloc((size_t)channels * (n_taps - 1));
+        AD_HIP(hipMemset(hb.p, 0, hb.n * sizeof(double)));
+      }
+    }
     raw = f.release();
   });
   if (rc == AD_OK && out) *out = raw;
@@ -496,11 +504,12 @@ int ad_fir_process_block_to(ad_fir* f, double* dst, const double* src, int64_t n
       return;
     }
     DeviceScope ds(f->device);
-    DevBuf<double> io;
-    io.alloc((size_t)f->channels * n);
-    AD_HIP(hipMemcpyAsync(io.p, src, io.n * sizeof(double), hipMemcpyHostToDevice, f->stream));
-    fir_run(f, io.p, n, io.p, n, n, f->stream);
-    AD_HIP(hipMemcpyAsync(dst, io.p, io.n * sizeof(double), hipMemcpyDeviceToHost, f->stream));
+    const size_t cnt = (size_t)f->channels * n;
+    f->io_in.reserve(cnt);
+    f->io_out.reserve(cnt);
+    AD_HIP(hipMemcpyAsync(f->io_in.p, src, cnt * sizeof(double), hipMemcpyHostToDevice, f->stream));
+    fir_run(f, f->io_in.p, n, f->io_out.p, n, n, f->stream);
+    AD_HIP(hipMemcpyAsync(dst, f->io_out.p, cnt * sizeof(double), hipMemcpyDeviceToHost, f->stream));
     AD_HIP(hipStreamSynchronize(f->stream));
   });
 }
@@ -519,11 +528,14 @@ int ad_fir_process_device(ad_fir* f, const double* d_src, int64_t src_stride, do
 }
 
 int ad_fir_reset(ad_fir* f) {
+  // filter.go:162-172; ordered after the last call, on the stream it used
   return guard([&] {
     if (!f) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "null FIR handle");
     DeviceScope ds(f->device);
-    if (f->xbuf.p) AD_HIP(hipMemsetAsync(f->xbuf.p, 0, f->xbuf.n * sizeof(double), f->stream));
-    AD_HIP(hipStreamSynchronize(f->stream));
+    hipStream_t s = f->last ? f->last : f->stream;
+    for (auto& hb : f->hist)
+      if (hb.p) AD_HIP(hipMemsetAsync(hb.p, 0, hb.n * sizeof(double), s));
+    AD_HIP(hipStreamSynchronize(s));
   });
 }
 

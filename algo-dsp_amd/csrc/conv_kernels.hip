@@ -524,19 +524,79 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MacOccL<PC, 
 // Output-stationary: one lane per output sample, so no atomics are needed and
 // the accumulation order is exactly the reference's.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_direct(const double* __restrict__ a, int64_t n, const double* __restrict__ b,
-                                                int64_t m, double* __restrict__ dst) {
+// LDS-tiled form: a workgroup owns 256 consecutive outputs (wave w: k0 +
+// 64 w + lane) and walks the input index i upward in chunks of DC.  The taps
+// b[k - i] a chunk meets sit in LDS (taps outside [0, m) stored as zeros);
+// a[i] is wave-uniform and comes through scalar loads straight into the
+// v_mul's SGPR operand.  Each wave loops only over its own i range
+// [kw - m + 1, kw + 63] (80 % useful at m = 256); a lane whose output does
+// not take term i multiplies a zero tap, and acc + (+-0) == acc exactly (acc
+// starts at +0 and an IEEE sum is never -0 unless both addends are), so the
+// per-output value is still the reference's increasing-i sum of rounded
+// products with rounded adds.  The identity fails only for a non-finite a[i]
+// (inf * 0 = NaN): a chunk holding one takes the per-lane bounds-checked loop.
+constexpr int DC = 1024;
+__global__ __launch_bounds__(256) void k_direct_lds(const double* __restrict__ a, int64_t n,
+                                                    const double* __restrict__ b, int64_t m,
+                                                    double* __restrict__ dst) {
 #pragma clang fp contract(off)
-  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (k >= n + m - 1) return;
-  const int64_t lo = k - m + 1 > 0 ? k - m + 1 : 0;
-  const int64_t hi = k < n - 1 ? k : n - 1;
+  constexpr int DT = 256;
+  __shared__ double sb[DT + DC];
+  const int t = threadIdx.x;
+  const int64_t k0 = (int64_t)blockIdx.x * DT;
+  const int64_t kw = k0 + __builtin_amdgcn_readfirstlane(t & ~63);  // first output of this wave
+  const int64_t k = k0 + t;
+  const int64_t out = n + m - 1;
+  // inputs reaching this tile: i in [k0 - m + 1, k0 + DT - 1] and [0, n)
+  const int64_t ilo = k0 - m + 1 > 0 ? k0 - m + 1 : 0;
+  const int64_t ihi = (k0 + DT - 1 < n - 1) ? k0 + DT - 1 : n - 1;
+  const int64_t wlo = kw - m + 1, whi = kw + 63;  // this wave's i range
+  const int64_t lo = k - m + 1, hi = k;           // this lane's
   double acc = 0.0;
-  for (int64_t i = lo; i <= hi; ++i) {
-    const double t = b[k - i] * a[i];
-    acc = acc + t;
+  for (int64_t i0 = ilo; i0 <= ihi; i0 += DC) {
+    const int cn = (int)(ihi - i0 + 1 < DC ? ihi - i0 + 1 : DC);
+    const int64_t bb = k0 - i0 - (DC - 1);  // sb[u] = b[bb + u]
+    __syncthreads();
+    int bad = 0;
+    for (int u = t; u < cn; u += 256) bad |= !__builtin_isfinite(a[i0 + u]);
+    for (int u = t; u < DT + DC; u += 256) {
+      const int64_t j = bb + u;
+      sb[u] = (j >= 0 && j < m) ? b[j] : 0.0;
+    }
+    bad = __syncthreads_or(bad);
+    const int s0 = __builtin_amdgcn_readfirstlane((int)(wlo > i0 ? wlo - i0 : 0));
+    const int s1 = __builtin_amdgcn_readfirstlane((int)(whi < i0 + cn - 1 ? whi - i0 : cn - 1));
+    const double* sbt = sb + t + (DC - 1);  // sbt[-ii] = b[k - (i0 + ii)]
+    const double* ai = a + i0;
+    if (!bad) {
+      int ii = s0;
+      for (; ii + 7 <= s1; ii += 8) {
+        double av[8], bv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) av[u] = ai[ii + u];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) bv[u] = sbt[-(ii + u)];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const double p = bv[u] * av[u];
+          acc = acc + p;
+        }
+      }
+      for (; ii <= s1; ++ii) {
+        const double p = sbt[-ii] * ai[ii];
+        acc = acc + p;
+      }
+    } else {
+      for (int ii = s0; ii <= s1; ++ii) {
+        const int64_t i = i0 + ii;
+        if (i >= lo && i <= hi) {
+          const double p = sbt[-ii] * ai[ii];
+          acc = acc + p;
+        }
+      }
+    }
   }
-  dst[k] = acc;
+  if (k < out) dst[k] = acc;
 }
 
 // conv.DirectCircularTo (conv.go:176-189): dst[(i+j)%n] += a[i]*b[j], i outer.
@@ -714,7 +774,7 @@ bool launch_fdl_mac(int PC, int NH, const MacArgs& in, int channels, hipStream_t
 
 void launch_direct(const double* a, int64_t n, const double* b, int64_t m, double* dst, hipStream_t s) {
   const int64_t out = n + m - 1;
-  hipLaunchKernelGGL(k_direct, dim3((unsigned)((out + 255) / 256)), dim3(256), 0, s, a, n, b, m, dst);
+  hipLaunchKernelGGL(k_direct_lds, dim3((unsigned)((out + 255) / 256)), dim3(256), 0, s, a, n, b, m, dst);
 }
 
 void launch_direct_circular(const double* a, const double* b, int64_t n, double* dst, hipStream_t s) {

@@ -587,24 +587,65 @@ __global__ __launch_bounds__(320) void k_chain_pipe(ChainArgs a) {
   }
 #undef PIPE_SYNC
 }
-// fir.Filter block paths (filter.go:64-104 / 109-149).  Output-parallel: one
-// lane per output sample, summing in the reference's term order.
+// fir.Filter block paths (filter.go:64-104 / 109-149).  Output-parallel: a
+// workgroup owns 256 consecutive outputs of one channel, one lane per output
+// sample, summing in the reference's term order q = 0, 1, ... with a rounded
+// product and a rounded add:
+//   reversed (taps >= 32, the block path's dot): term q = h[q] * x[i-(N-1)+q]
+//   ring     (taps <  32, ProcessSample's loop): term q = h[q] * x[i-q]
+// where x[< 0] is the delay line.  Taps are walked in chunks of FQ; the input
+// window a chunk meets (256 + FQ - 1 samples, from the delay line and the new
+// block) is staged in LDS, and h[q] is wave-uniform (scalar loads).
+constexpr int FQ = 1024;
 __global__ __launch_bounds__(256) void k_fir(FirArgs a) {
 #pragma clang fp contract(off)
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  __shared__ double w[256 + FQ];
+  const int t = threadIdx.x;
   const int c = blockIdx.y;
-  if (i >= a.n) return;
-  const double* xc = a.x + (int64_t)c * a.xstride + (a.N - 1) + i;  // xc[0] = x[i], xc[-k] = x[i-k]
+  const int64_t i0 = (int64_t)blockIdx.x * 256;
+  const int64_t hn = a.N - 1;
+  const double* hc = a.hist + (int64_t)c * hn;
+  const double* xc = a.src + (int64_t)c * a.sstride;
   double acc = 0.0;
-  if (a.reversed) {
-    // dot(coeffs, linear[pos+1 .. pos+N]): h[j] pairs with x[i - (N-1) + j]
-    const double* xs = xc - (a.N - 1);
-    for (int64_t j = 0; j < a.N; ++j) acc += a.h[j] * xs[j];
-  } else {
-    // ProcessSample: y += coeffs[k] * delay[pos - k] (filter.go:46-69)
-    for (int64_t k = 0; k < a.N; ++k) acc += a.h[k] * xc[-k];
+  for (int64_t q0 = 0; q0 < a.N; q0 += FQ) {
+    const int cq = (int)(a.N - q0 < FQ ? a.N - q0 : FQ);
+    // window start: reversed w[v] = x[i0 - hn + q0 + v]; ring w[v] = x[i0 - q0 - cq + 1 + v]
+    const int64_t g0 = a.reversed ? i0 - hn + q0 : i0 - q0 - cq + 1;
+    __syncthreads();
+    for (int v = t; v < 256 + cq - 1; v += 256) {
+      const int64_t g = g0 + v;
+      w[v] = g < 0 ? hc[hn + g] : (g < a.n ? xc[g] : 0.0);
+    }
+    __syncthreads();
+    const double* hq = a.h + q0;
+    if (a.reversed) {
+      const double* wt = w + t;  // term q0 + u: wt[u]
+      int u = 0;
+      for (; u + 7 < cq; u += 8) {
+        double hv[8], xv[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) hv[e] = hq[u + e];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) xv[e] = wt[u + e];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const double p = hv[e] * xv[e];
+          acc = acc + p;
+        }
+      }
+      for (; u < cq; ++u) {
+        const double p = hq[u] * wt[u];
+        acc = acc + p;
+      }
+    } else {
+      const double* wt = w + t + cq - 1;  // term q0 + u: wt[-u]
+      for (int u = 0; u < cq; ++u) {
+        const double p = hq[u] * wt[-u];
+        acc = acc + p;
+      }
+    }
   }
-  a.y[(int64_t)c * a.ystride + i] = acc;
+  if (i0 + t < a.n) a.y[(int64_t)c * a.ystride + i0 + t] = acc;
 }
 
 // decodeF16 (internal/webdemo/irlib.go:68-97), reference quirk kept: a
@@ -640,6 +681,45 @@ __global__ __launch_bounds__(256) void k_decode_f16(const uint16_t* __restrict__
   out[(int64_t)c * frames + f] = (double)decode_f16(in[i]);
 }
 
+// Mono / stereo form: a lane decodes 4 whole frames (one 8- or 16-byte load
+// of the interleaved codes) and stores 4 consecutive doubles per channel.
+template <int CH>
+__global__ __launch_bounds__(256) void k_decode_f16_v(const uint16_t* __restrict__ in, int64_t frames,
+                                                      double* __restrict__ out) {
+  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;  // frames 4g .. 4g+3
+  const int64_t f0 = 4 * g;
+  if (f0 >= frames) return;
+  if (f0 + 4 <= frames) {
+    uint32_t w[2 * CH];
+    if constexpr (CH == 1) {
+      const uint2 v = *reinterpret_cast<const uint2*>(in + f0);
+      w[0] = v.x;
+      w[1] = v.y;
+    } else {
+      const uint4 v = *reinterpret_cast<const uint4*>(in + 2 * f0);
+      w[0] = v.x;
+      w[1] = v.y;
+      w[2] = v.z;
+      w[3] = v.w;
+    }
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      double d[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int e = j * CH + c;  // code index within the 4 frames
+        d[j] = (double)decode_f16((w[e >> 1] >> (16 * (e & 1))) & 0xFFFFu);
+      }
+      double2* o = reinterpret_cast<double2*>(out + (int64_t)c * frames + f0);
+      o[0] = make_double2(d[0], d[1]);
+      o[1] = make_double2(d[2], d[3]);
+    }
+  } else {
+    for (int64_t f = f0; f < frames; ++f)
+      for (int c = 0; c < CH; ++c) out[(int64_t)c * frames + f] = (double)decode_f16(in[f * CH + c]);
+  }
+}
+
 }  // namespace
 
 // Fan-in average (mixParentEdgesInto, chain_process.go:295-318): the Go code
@@ -663,7 +743,16 @@ void launch_fx_mix(const FxMixArgs& a, hipStream_t s) {
 void launch_decode_f16(const uint16_t* in, int64_t frames, int channels, double* out, hipStream_t s) {
   const int64_t n = frames * channels;
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_decode_f16, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, in, frames, channels, out);
+  // vector form when every row and the input are 16-byte aligned
+  const bool al = ((uintptr_t)in % 16 == 0) && ((uintptr_t)out % 16 == 0) && frames % 2 == 0;
+  const unsigned g4 = (unsigned)((frames + 1023) / 1024);
+  if (al && channels == 1) {
+    hipLaunchKernelGGL(k_decode_f16_v<1>, dim3(g4), dim3(256), 0, s, in, frames, out);
+  } else if (al && channels == 2) {
+    hipLaunchKernelGGL(k_decode_f16_v<2>, dim3(g4), dim3(256), 0, s, in, frames, out);
+  } else {
+    hipLaunchKernelGGL(k_decode_f16, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, in, frames, channels, out);
+  }
 }
 
 template <bool EQ, bool COMP, bool VERB>

@@ -82,11 +82,12 @@ void launch_fx_mix(const FxMixArgs& a, hipStream_t s);
 
 // FIR block filter over [hist (N-1) | block (n)] per channel.
 struct FirArgs {
-  const double* h;  // [N]
+  const double* h;     // [N]
   int64_t N;
-  const double* x;  // [channels][xstride]: N-1 history samples then n new ones
-  int64_t xstride;
-  double* y;  // [channels][ystride]
+  const double* hist;  // [channels][N-1]: the delay line before this block
+  const double* src;   // [channels][sstride]: n new samples
+  int64_t sstride;
+  double* y;           // [channels][ystride]
   int64_t ystride, n;
   int channels;
   int reversed;  // taps >= 32: y[i] = sum_j h[j] x[i-N+1+j]; else sum_k h[k] x[i-k]

@@ -120,6 +120,9 @@ void ad_conv_destroy(ad_conv* h);
 /* conv.Direct / DirectTo (conv.go:76-154): bit-exact input-stationary
  * scatter-add order.  dst has n+m-1 elements.                             */
 int ad_conv_direct(const double* a, int64_t n, const double* b, int64_t m, double* dst, int device);
+/* conv.DirectTo (conv.go:97-154) on device buffers: d_dst has n+m-1
+ * elements; enqueued on `stream` (NULL: the default stream), not synced.  */
+int ad_conv_direct_device(const double* d_a, int64_t n, const double* d_b, int64_t m, double* d_dst, void* stream);
 /* conv.DirectCircular (conv.go:158-189): n == m, dst has n elements.      */
 int ad_conv_direct_circular(const double* a, int64_t n, const double* b, int64_t m, double* dst, int device);
 /* conv.Convolve / ConvolveMode (conv.go:194-247).  dst_cap is the capacity

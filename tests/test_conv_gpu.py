@@ -32,13 +32,40 @@ def test_direct_kat(gpu, case):
     np.testing.assert_allclose(conv.Direct(case["a"], case["b"]), case["expected"], atol=case["tol"], rtol=0)
 
 
-@pytest.mark.parametrize("n,m", [(1, 1), (7, 3), (100, 15), (100, 16), (48000, 256), (300, 1000), (5, 64)])
+@pytest.mark.parametrize("n,m", [(1, 1), (7, 3), (100, 15), (100, 16), (48000, 256), (300, 1000), (5, 64),
+                                 (3000, 2500), (5000, 1025), (1025, 4097), (70000, 3)])
 def test_direct_bit_exact(gpu, n, m):
     a = signals.white_noise(n, 100 + n)
     b = signals.white_noise(m, 200 + m)
     got = conv.Direct(a, b)
     want = O.direct(a, b)
     assert np.array_equal(got, want), float(np.max(np.abs(got - want)))
+
+
+def test_direct_non_finite(gpu):
+    """inf / NaN inputs: the LDS kernel's zero-tap shortcut must not turn an
+    untaken inf * 0 into NaN (chunks holding one take the bounds-checked loop)."""
+    a = signals.white_noise(3000, 7)
+    b = signals.white_noise(300, 8)
+    a[5], a[1500], a[2999] = np.inf, -np.inf, np.nan
+    b[17] = np.inf
+    got, want = conv.Direct(a, b), O.direct(a, b)
+    assert np.array_equal(got, want, equal_nan=True)
+
+
+def test_direct_device(gpu):
+    import torch
+
+    n, m = 1 << 16, 256
+    a, b = signals.white_noise(n, 3), signals.make_test_kernel(m)
+    da, db = torch.from_numpy(a).cuda(), torch.from_numpy(b).cuda()
+    dd = torch.empty(n + m - 1, dtype=torch.float64, device="cuda")
+    s = torch.cuda.current_stream()
+    conv.direct_device(da.data_ptr(), n, db.data_ptr(), m, dd.data_ptr(), s.cuda_stream)
+    s.synchronize()
+    assert np.array_equal(dd.cpu().numpy(), O.direct(a, b))
+    with pytest.raises(conv.ErrEmptyKernel):
+        conv.direct_device(da.data_ptr(), n, db.data_ptr(), 0, dd.data_ptr())
 
 
 def test_direct_circular(gpu):

@@ -228,6 +228,44 @@ def test_fir_vs_oracle(gpu, taps):
             assert rms(got[c], want) <= RMS_TOL
 
 
+@pytest.mark.parametrize("taps", [7, 300, 1500])
+def test_fir_device_paths(gpu, taps):
+    """ad_fir_process_device: out-of-place and in-place calls on device
+    buffers, blocks shorter and longer than the taps (delay-line ping-pong),
+    more taps than one LDS chunk (1024), and Reset ordered after the last
+    call's stream."""
+    import torch
+
+    h = signals.make_test_kernel(taps)
+    C, n = 4, 5000
+    x = np.stack([signals.white_noise(n, 60 + c) for c in range(C)])
+    cuts = [(0, 3), (3, 1700), (1700, 1710), (1710, 5000)]
+    f = P.Filter(h, channels=C)
+    s = torch.cuda.current_stream()
+    dx = torch.from_numpy(x).cuda()
+    dy = torch.zeros_like(dx)
+    for k, (lo, hi) in enumerate(cuts):
+        if k % 2:  # in place: dst is the source itself
+            tmp = dx.clone()
+            f.process_device(tmp.data_ptr() + 8 * lo, n, tmp.data_ptr() + 8 * lo, n, hi - lo, s.cuda_stream)
+            dy[:, lo:hi] = tmp[:, lo:hi]
+        else:
+            f.process_device(dx.data_ptr() + 8 * lo, n, dy.data_ptr() + 8 * lo, n, hi - lo, s.cuda_stream)
+    s.synchronize()
+    got = dy.cpu().numpy()
+    for c in range(C):
+        of = O.Fir(h)
+        want = np.concatenate([of.process_block(x[c, lo:hi]) for lo, hi in cuts])
+        if taps < 32:
+            assert np.array_equal(got[c], want)
+        else:
+            assert rms(got[c], want) <= RMS_TOL
+    f.Reset()
+    f.process_device(dx.data_ptr(), n, dy.data_ptr(), n, n, s.cuda_stream)
+    s.synchronize()
+    assert rms(dy.cpu().numpy()[1], O.Fir(h).process_block(x[1])) <= RMS_TOL
+
+
 def test_fir_block_to_and_reset(gpu):
     h = signals.make_test_kernel(40)
     x = signals.white_noise(500, 3)
@@ -260,6 +298,18 @@ def test_decode_f16_all_codes(gpu):
     assert same.all(), np.flatnonzero(~same)[:10]
     # subnormal quirk (irlib.go:87): 0x0001 decodes to 2^-23, twice IEEE's 2^-24
     assert got[1] == 2.0 ** -23
+
+
+@pytest.mark.parametrize("channels,frames", [(1, 65536), (2, 32768), (2, 1030), (2, 1031), (1, 7), (3, 5000)])
+def test_decode_f16_layouts(gpu, channels, frames):
+    """Interleaved AUDI codes -> channel-major f64: the mono/stereo vector
+    kernel (4 frames per lane, scalar tail) and the generic one."""
+    from algodsp import irlib
+
+    codes = (np.arange(frames * channels, dtype=np.int64) * 7919 % 65536).astype(np.uint16)
+    got = irlib.decode_f16_gpu(codes, channels)
+    want = np.array([O.decode_f16(int(h)) for h in codes], dtype=np.float64).reshape(frames, channels).T
+    assert np.array_equal(got, want, equal_nan=True)
 
 
 def test_irlib_gpu_decode_matches_oracle(gpu):

@@ -1,9 +1,4 @@
 set -u
 mkdir -p gpurun_out
-B="--steps 5 --warmup 2 --no-cpu-baseline"
-timeout -k 10 200 python bench.py $B > gpurun_out/b1.log 2>&1 || { tail gpurun_out/b1.log; exit 1; }
-grep -o '"value": [0-9.]*\|"ms_per_step": [0-9.]*' gpurun_out/b1.log | tr '\n' ' '; echo
-timeout -k 10 200 python bench.py $B --channels 8 --samples 4194304 > gpurun_out/b2.log 2>&1 || { tail gpurun_out/b2.log; exit 1; }
-grep -o '"value": [0-9.]*\|"ms_per_step": [0-9.]*' gpurun_out/b2.log | tr '\n' ' '; echo
-timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29511 bench.py $B --channels 8 --samples 4194304 --mixdown on > gpurun_out/b3.log 2>&1 || { tail gpurun_out/b3.log; exit 1; }
-grep -o '"value": [0-9.]*\|"ms_per_step": [0-9.]*\|"workload": "[^"]*' gpurun_out/b3.log | tr '\n' ' '; echo
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_dsp_gpu.py -k "decode or irlib" -p no:cacheprovider > gpurun_out/t_dec.log 2>&1; rc=$?; tail -5 gpurun_out/t_dec.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 400 python -u tools/rows_bench.py > gpurun_out/rows.log 2>&1; rc=$?; grep -o '"row": "[^"]*\|"value": [0-9.]*\|"frac": [0-9.]*' gpurun_out/rows.log | paste -sd' ' | sed 's/"row"/\n"row"/g'; exit $rc

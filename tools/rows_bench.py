@@ -1,0 +1,293 @@
+#!/usr/bin/env python3
+"""Per-row measurement of SURVEY 8(a)'s hot-path functions on one MI355X.
+
+For every row: the device entry point on HBM-resident buffers, timed with HIP
+events on the stream the work is enqueued on (torch's current stream, passed
+through the C ABI), its algorithmic bytes or flops -> roofline fraction, and
+the oracle (CPU restatement of the reference, 1 core) timed on a bounded
+sample of the same workload beside it.  Host-buffer rows (streaming and
+partitioned convolution, batch OverlapSave / OverlapAdd) are wall-clock per
+call through the same ABI a Go caller would use (PCIe included).
+
+  python tools/rows_bench.py [--out gpurun_out/rows.json] [--quick]
+
+Peaks: HBM 8.0 TB/s (MI355X_MICROARCH.md); FP64 vector 78.6 TFLOP/s (MI355X
+spec sheet, FMA counted as 2 flops).  Rows bound by serial per-channel
+recurrences (biquad, compressor, Freeverb) are reported against HBM with
+their 16 B/sample, and the note says they are latency-bound, not HBM-bound.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import pathlib
+import sys
+import time
+
+ROOT = pathlib.Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT / "algo-dsp_amd"))
+sys.path.insert(0, str(ROOT / "tests"))
+
+HBM = 8000.0     # GB/s
+FP64 = 78.6      # TFLOP/s, FMA = 2 flops
+
+
+def dev_time(fn, reps: int, warm: int = 2):
+    """Mean ms per call of fn(stream_ptr) between HIP events on torch's current stream."""
+    import torch
+
+    s = torch.cuda.current_stream()
+    for _ in range(warm):
+        fn(s.cuda_stream)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(reps):
+        fn(s.cuda_stream)
+    e1.record(s)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def cpu_time(fn, budget_s: float = 1.5, max_reps: int = 1000):
+    t0 = time.perf_counter()
+    fn()
+    reps, dt = 1, time.perf_counter() - t0
+    while dt < budget_s and reps < max_reps:
+        fn()
+        reps += 1
+        dt = time.perf_counter() - t0
+    return dt / reps
+
+
+def row(name, ref, workload, units, unit_name, ms, cpu_s, cpu_units, cpu_sample, bound, alg, note=""):
+    """alg: algorithmic bytes (bound 'hbm') or flops (bound 'fp64') of one call."""
+    r = {"row": name, "reference": ref, "workload": workload,
+         "value": round(units / (ms * 1e-3) / 1e6, 3), "unit": f"M{unit_name}/s", "ms_per_call": round(ms, 5)}
+    if bound == "hbm":
+        ach = alg / (ms * 1e-3) / 1e9
+        r["roofline"] = {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM, "unit": "GB/s",
+                         "frac": round(ach / HBM, 5), "alg_bytes": alg}
+    elif bound == "fp64":
+        ach = alg / (ms * 1e-3) / 1e12
+        r["roofline"] = {"bound": "fp64-valu", "achieved": round(ach, 3), "peak": FP64, "unit": "TFLOP/s",
+                         "frac": round(ach / FP64, 5), "alg_flops": alg}
+    else:
+        r["roofline"] = None
+    if cpu_s is not None:
+        cv = cpu_units / cpu_s / 1e6
+        r["cpu_baseline"] = {"value": round(cv, 4), "unit": f"M{unit_name}/s", "cores": 1, "kind": "port",
+                             "sample": cpu_sample}
+        r["speedup_vs_cpu"] = round(r["value"] / cv, 1)
+    if note:
+        r["note"] = note
+    print(json.dumps(r), flush=True)
+    return r
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=str(ROOT / "gpurun_out" / "rows.json"))
+    ap.add_argument("--quick", action="store_true", help="smaller sizes (CPU-side smoke of the script)")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+
+    import oracle_lib as O
+    from algodsp import conv, design, irlib, processors, signals
+    from algodsp._lib import lib
+
+    import ctypes as C
+
+    torch.cuda.set_device(0)
+    cuda = torch.device("cuda", 0)
+    rows = []
+    q = args.quick
+
+    # ---- a1 conv.Direct: config 1 (48000 x 256) and a chip-filling size --------
+    m = 256
+    b = signals.make_test_kernel(m)
+    for n, tag in ((48000, "config 1: 1 s mono 48 kHz"), (1 << (18 if q else 22), "2^22 samples")):
+        a = signals.white_noise(n, 0x5EED)
+        da, db = torch.from_numpy(a).to(cuda), torch.from_numpy(b).to(cuda)
+        dd = torch.empty(n + m - 1, dtype=torch.float64, device=cuda)
+        ms = dev_time(lambda s: conv.direct_device(da.data_ptr(), n, db.data_ptr(), m, dd.data_ptr(), s),
+                      reps=50 if n < 100000 else 10)
+        assert np.array_equal(dd.cpu().numpy(), O.direct(a, b)), "Direct parity"
+        nc = 48000
+        ac = signals.white_noise(nc, 0x5EED)
+        cs = cpu_time(lambda: O.direct(ac, b))
+        rows.append(row("a1", "conv.Direct / DirectTo conv.go:76-154", f"{tag} x {m}-tap makeTestKernel",
+                        n, "samples", ms, cs, nc, f"oracle Direct, 1 x {nc} samples x {m} taps",
+                        "fp64", 2.0 * n * m,
+                        "no FMA (reference order: rounded product, rounded add), so the VALU ceiling of "
+                        "this form is half the FMA peak"))
+
+    # ---- a11 fir.Filter: 256 taps, 64 channels ---------------------------------
+    taps = 256
+    ch, n = 64, 1 << (16 if q else 20)
+    h = signals.make_test_kernel(taps)
+    f = processors.Filter(h, channels=ch)
+    x = torch.from_numpy(np.stack([signals.white_noise(n, 0x5EED + c) for c in range(ch)])).to(cuda)
+    y = torch.empty_like(x)
+
+    def fir(s):
+        f.process_device(x.data_ptr(), n, y.data_ptr(), n, n, s)
+    ms = dev_time(fir, reps=5)
+    f.Reset()
+    fir(torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    nc = 1 << 18
+    xc = signals.white_noise(nc, 0x5EED)
+    fo = O.Fir(h)
+    want = fo.process_block(x[0, :4096].cpu().numpy())
+    assert np.sqrt(np.mean((y[0, :4096].cpu().numpy() - want) ** 2)) <= 1e-12, "FIR parity"
+    cs = cpu_time(lambda: O.Fir(h).process_block(xc), budget_s=1.0)
+    rows.append(row("a11", "fir.Filter.ProcessBlockTo filter.go:119-159", f"{taps} taps, {ch} ch x {n} samples",
+                    ch * n, "samples", ms, cs, nc, f"oracle Fir.ProcessBlock, 1 x {nc} samples",
+                    "fp64", 2.0 * ch * n * taps))
+
+    # ---- a12-a17 per-sample processors (config 5 shapes: 256 ch x 2^20) --------
+    fs = 48000.0
+    eq = design.config5_eq(fs)
+    comp_cfg = {"auto_makeup": 0, "makeup_db": 0.0}
+    verb = (0.22, 1.0, 0.72, 0.45, 0.015)
+    nc = 1 << 21
+    vc = 0.5 * signals.white_noise(nc, 0x5EED)
+
+    def cpu_eq():
+        v = vc
+        for co, g in eq:
+            v, _ = O.biquad_chain_block(np.ravel(co), np.zeros(2 * len(co)), g, v)
+
+    def cpu_comp():
+        O.Compressor(fs, **comp_cfg).process_in_place(vc)
+
+    def cpu_verb():
+        o = O.Freeverb()
+        o.set(*verb)
+        o.process_in_place(vc)
+
+    procs = [
+        ("a12-a14", "biquad.Chain.ProcessBlock chain.go:59-70 (section.go:56-138), config-5 EQ: 5 RBJ sections",
+         dict(eq=eq), cpu_eq, "oracle biquad chains (avx2-registered 4x unroll)"),
+        ("a15-a16", "dynamics.Compressor.ProcessInPlace compressor.go:362-366 (core.go:274-540)",
+         dict(compressor=comp_cfg), cpu_comp, "oracle Compressor (libm log2/pow)"),
+        ("a17", "reverb.Reverb.ProcessInPlace reverb.go:185-189 (Freeverb)",
+         dict(freeverb=verb), cpu_verb, "oracle Freeverb"),
+    ]
+    for chn, n in ((256, 1 << (16 if q else 20)), (16384, 1 << (12 if q else 15))):
+        xb = torch.from_numpy(np.stack([0.5 * signals.white_noise(n, 0x5EED + c) for c in range(min(chn, 256))]))
+        xb = xb.repeat(chn // xb.shape[0], 1).contiguous().to(cuda)
+        for name, ref, kw, cfn, cdesc in procs:
+            fx = processors.EffectChain(chn, sample_rate=fs, **kw)
+            ms = dev_time(lambda s: fx.process_device(xb.data_ptr(), n, n, s), reps=3, warm=1)
+            cs = cpu_time(cfn, budget_s=1.0) if chn == 256 else None
+            rows.append(row(name, ref, f"{chn} ch x {n} samples (fused per-sample kernel)", chn * n, "samples",
+                            ms, cs, nc, f"{cdesc}, 1 x {nc} samples", "hbm", 16.0 * chn * n,
+                            "serial per-channel recurrence: bound by dependent-op latency x channels in flight, "
+                            "not by HBM; 16 B/sample is the in+out stream"))
+            fx.close()
+        del xb
+
+    # ---- config 5: the fused effect chain ------------------------------------
+    chn, n = 256, 1 << (16 if q else 20)
+    xb = torch.from_numpy(np.stack([0.5 * signals.white_noise(n, 0x5EED + c) for c in range(chn)])).to(cuda)
+    fx = processors.EffectChain(chn, eq, comp_cfg, verb, fs)
+    ms = dev_time(lambda s: fx.process_device(xb.data_ptr(), n, n, s), reps=3, warm=1)
+    cs = cpu_time(lambda: (cpu_eq(), cpu_comp(), cpu_verb()), budget_s=1.0)
+    rows.append(row("a18 (config 5)", "effectchain.Chain.Process chain_process.go:11-319",
+                    f"filter x5 -> dyn-compressor -> reverb-freeverb, {chn} ch x {n} samples", chn * n, "samples",
+                    ms, cs, nc, f"oracle EQ + Compressor + Freeverb, 1 x {nc} samples", "hbm", 16.0 * chn * n,
+                    "latency-bound serial recurrences (see a12-a17)"))
+    fx.close()
+    del xb
+
+    # ---- 8(f)2 IRLB decodeF16 --------------------------------------------------
+    frames, chn = 1 << (20 if q else 24), 2
+    raw = torch.randint(0, 65536, (frames * chn,), dtype=torch.int32).to(torch.int16).to(cuda)
+    out = torch.empty((chn, frames), dtype=torch.float64, device=cuda)
+    ms = dev_time(lambda s: lib().ad_decode_f16_device(C.c_void_p(raw.data_ptr()), frames, chn,
+                                                       C.c_void_p(out.data_ptr()), C.c_void_p(s)), reps=10)
+    rr = raw[:8192].cpu().numpy().view(np.uint16)
+    assert np.array_equal(out[:, :4096].cpu().numpy().T.ravel(), np.array([O.decode_f16(int(v)) for v in rr]), equal_nan=True), \
+        "decodeF16 parity"
+    img = (ROOT / "data" / "irs.irlib").read_bytes()
+    nc = sum(v[2].size for v in O.irlib_read(img))
+    cs = cpu_time(lambda: O.irlib_read(img), budget_s=1.0)
+    rows.append(row("8(f)2", "webdemo decodeF16 irlib.go:136-170", f"{chn} ch x {frames} frames interleaved f16",
+                    chn * frames, "samples", ms, cs, nc, f"oracle IRLB read of data/irs.irlib ({nc} samples)",
+                    "hbm", 10.0 * chn * frames))
+
+    # ---- host-buffer rows: streaming, partitioned, batch ----------------------
+    ir = irlib.large_church()
+    k16 = ir[0, :16384]
+    B = 4096
+    nblk = 128 if q else 1024
+    xs = signals.white_noise(nblk * B, 0x5EED)
+    ys = np.empty_like(xs)
+    for ctor, name, ref in ((conv.NewStreamingOverlapSave, "a5", "StreamingOverlapSaveT.ProcessBlockTo "
+                             "streaming_overlap_save.go:152-164"),
+                            (conv.NewStreamingOverlapAdd, "a6", "StreamingOverlapAddT.ProcessBlockTo "
+                             "streaming_overlap_add.go")):
+        s = ctor(k16, B)
+        for i in range(16):
+            s.ProcessBlockTo(ys[i * B:(i + 1) * B], xs[i * B:(i + 1) * B])
+        s.Reset()
+        t0 = time.perf_counter()
+        for i in range(nblk):
+            s.ProcessBlockTo(ys[i * B:(i + 1) * B], xs[i * B:(i + 1) * B])
+        ms = (time.perf_counter() - t0) / nblk * 1e3
+        o = O.Streaming(k16, B, ola=(name == "a6"))
+        cs = cpu_time(lambda: o.process_block(xs[:B]), budget_s=1.0)
+        rows.append(row(name, ref, f"config 2: mono, K=16384, B={B}, host buffers, one block per call", B,
+                        "samples", ms, cs, B, "oracle streaming block (N=32768 complex FFT)", None, 0,
+                        "latency-bound: per-block wall time incl. PCIe in/out and 3 kernel launches"))
+
+    lam = 128
+    kpc = ir[0, :95432]
+    pc = conv.NewPartitionedConvolution(kpc, 7, 13)
+    nb = 256 if q else 2048
+    xp = signals.white_noise(nb * lam, 1)
+    yp = np.empty(lam)
+    for i in range(64):
+        pc.ProcessBlock(xp[i * lam:(i + 1) * lam], yp)
+    t0 = time.perf_counter()
+    for i in range(nb):
+        pc.ProcessBlock(xp[i * lam:(i + 1) * lam], yp)
+    ms = (time.perf_counter() - t0) / nb * 1e3
+    op = O.Partitioned(kpc, 7, 13)
+    ncb = 512
+    cs = cpu_time(lambda: [op.process_block(xp[i * lam:(i + 1) * lam]) for i in range(ncb)], budget_s=1.0,
+                  max_reps=4)
+    rows.append(row("a9/a10", "PartitionedConvolution.ProcessBlock partitioned.go:348-396",
+                    f"Large Church L (95432 taps), minOrder 7 / maxOrder 13 (latency {lam}), host buffers", lam,
+                    "samples", ms, cs, ncb * lam, f"oracle PartitionedConvolution, {ncb} blocks", None, 0,
+                    "latency-bound: mean per-block wall time incl. PCIe"))
+
+    nbt = 1 << (18 if q else 22)
+    xbt = signals.white_noise(nbt, 3)
+    for ctor, name, ref, ocls in ((conv.NewOverlapSave, "a4", "OverlapSave.Process overlap_save.go:126-254",
+                                   O.OverlapSave),
+                                  (conv.NewOverlapAdd, "a3", "OverlapAdd.Process overlap_add.go:108-164",
+                                   O.OverlapAdd)):
+        e = ctor(k16)
+        e.Process(xbt[:1 << 16])
+        t0 = time.perf_counter()
+        for _ in range(3):
+            e.Process(xbt)
+        ms = (time.perf_counter() - t0) / 3 * 1e3
+        oc = ocls(k16)
+        ncs = 1 << 18
+        cs = cpu_time(lambda: oc.process(xbt[:ncs]), budget_s=1.0, max_reps=3)
+        rows.append(row(name, ref, f"mono {nbt} samples x 16384 taps, host buffers (PCIe in + out)", nbt,
+                        "samples", ms, cs, ncs, f"oracle {ocls.__name__}.Process, {ncs} samples", None, 0,
+                        "host-buffer call: PCIe-bound (16 B/sample over ~50 GB/s)"))
+
+    pathlib.Path(args.out).parent.mkdir(parents=True, exist_ok=True)
+    pathlib.Path(args.out).write_text(json.dumps(rows, indent=1))
+
+
+if __name__ == "__main__":
+    main()
