@@ -71,6 +71,7 @@ void check_comp_config(const ad_compressor_config& g) {
 // ---------------------------------------------------------------------------
 // effect chain handle
 // ---------------------------------------------------------------------------
+constexpr int kFxSlots = 3;  // chunk buffers in flight (staged engine)
 struct ad_fx_chain {
   int device = 0, channels = 0, cpad = 0;
   hipStream_t stream = nullptr;
@@ -91,8 +92,27 @@ struct ad_fx_chain {
   DevBuf<double> vbuf;
   // host-call staging
   DevBuf<double> work;
+  // staged engine (fx_staged.hip): stage streams eq / gain / comb / allpass,
+  // per-slot events, double-buffered time-major chunk buffers
+  bool staged_ok = true;  // the graph runtime turns the staged engine off when it runs branches concurrently
+  hipStream_t st[2] = {};
+  hipEvent_t ev_last = nullptr;  // end of the last call on its caller stream (quiesce waits for it)
+  hipEvent_t ev_in = nullptr;
+  hipEvent_t ev[3][kFxSlots] = {};
+  DevBuf<double> xT[kFxSlots], vT[kFxSlots], envT[kFxSlots], inT[kFxSlots], coT[kFxSlots];
+  int64_t tmax = 0;
 
   ~ad_fx_chain() {
+    for (hipStream_t x : st)
+      if (x) {
+        (void)hipStreamSynchronize(x);
+        (void)hipStreamDestroy(x);
+      }
+    for (auto& e2 : ev)
+      for (hipEvent_t e : e2)
+        if (e) (void)hipEventDestroy(e);
+    if (ev_in) (void)hipEventDestroy(ev_in);
+    if (ev_last) (void)hipEventDestroy(ev_last);
     if (stream) {
       (void)hipStreamSynchronize(stream);
       (void)hipStreamDestroy(stream);
@@ -101,6 +121,14 @@ struct ad_fx_chain {
 };
 
 namespace {
+
+// wait for everything enqueued on the handle's own and stage streams
+void fx_quiesce(ad_fx_chain* h) {
+  for (hipStream_t x : h->st)
+    if (x) AD_HIP(hipStreamSynchronize(x));
+  if (h->ev_last) AD_HIP(hipEventSynchronize(h->ev_last));
+  AD_HIP(hipStreamSynchronize(h->stream));
+}
 
 void fx_reset_comp(ad_fx_chain* h) {
   if (!h->comp_on) return;
@@ -120,7 +148,122 @@ void fx_reset_verb(ad_fx_chain* h) {
   AD_HIP(hipMemsetAsync(h->vbuf.p, 0, h->vbuf.n * sizeof(double), h->stream));
 }
 
+// The staged engine runs the chain as stage kernels over time chunks of T
+// samples on three streams: chunk i's EQ/detector + gain (the caller's
+// stream), combs and allpasses overlap chunk i-1's and i-2's later stages.
+// Three queues in all, so the stages keep their own hardware queues
+// (GPU_MAX_HW_QUEUES is 4, and streams sharing a queue serialise at every
+// cross-stream wait).  Chunk buffers come in kFxSlots slots; chunk i reuses
+// slot i % kFxSlots only after chunk i - kFxSlots's allpasses (the last
+// reader) are done: that slot's event, recorded for chunk i - kFxSlots, is
+// its latest record when chunk i is enqueued.  Feed-forward compressor only
+// (the feedback topology's gain feeds its own detector).
+bool fx_staged_ok(const ad_fx_chain* h) {
+  const char* v = std::getenv("AD_FX_STAGED");  // read per call: tests compare both engines
+  const bool on = !(v && v[0] == '0');
+  return on && h->staged_ok && (!h->comp_on || !h->cp.topology_fb) && h->nsec <= kMaxSecPerPass &&
+         (h->nsec > 0 || h->comp_on || h->verb_on);
+}
+
+int64_t fx_chunk() {
+  const char* v = std::getenv("AD_FX_CHUNK");
+  const int64_t t = v ? std::atoll(v) : 0;
+  return t >= 256 ? t : (int64_t)16384;
+}
+
+void fx_run_staged(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hipStream_t s) {
+  const bool eq = h->nsec > 0, comp = h->comp_on, verb = h->verb_on;
+  const int64_t T = std::min(fx_chunk(), n);
+  if (!h->st[0]) {
+    for (auto& x : h->st) AD_HIP(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
+    for (auto& e2 : h->ev)
+      for (auto& e : e2) AD_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    AD_HIP(hipEventCreateWithFlags(&h->ev_in, hipEventDisableTiming));
+  }
+  const bool need_x = eq || comp, need_v = comp || (eq && !verb);
+  if (T > h->tmax || (need_x && !h->xT[0].p) || (need_v && !h->vT[0].p) || (comp && !h->envT[0].p) ||
+      (verb && !h->inT[0].p)) {  // (re)size the chunk buffers once no stage is running
+    for (hipStream_t x : h->st) AD_HIP(hipStreamSynchronize(x));
+    AD_HIP(hipStreamSynchronize(s));
+    const size_t r = (size_t)h->cpad * std::max(T, h->tmax);
+    for (int k = 0; k < kFxSlots; ++k) {
+      if (need_x) h->xT[k].alloc(r);
+      if (need_v) h->vT[k].alloc(r);
+      if (comp) h->envT[k].alloc(r);
+      if (verb) {
+        h->inT[k].alloc(r);
+        h->coT[k].alloc(r * kVerbCombs);
+      }
+    }
+    h->tmax = std::max(T, h->tmax);
+  }
+  // stage streams: the caller's stream runs input transpose + EQ/detector +
+  // gain; st[0] the combs, st[1] the allpasses (three queues in all)
+  hipStream_t sc = h->st[0], sa = h->st[1];
+  enum { EE = 0, EC = 1, EA = 2 };
+  if (verb) {
+    AD_HIP(hipEventRecord(h->ev_in, s));
+    AD_HIP(hipStreamWaitEvent(sc, h->ev_in, 0));
+    AD_HIP(hipStreamWaitEvent(sa, h->ev_in, 0));
+  }
+  int64_t i = 0;
+  int k = 0;
+  for (int64_t t0 = 0; t0 < n; t0 += T, ++i) {
+    k = (int)(i % kFxSlots);
+    const bool reuse = i >= kFxSlots;  // slot k was used by chunk i - kFxSlots
+    FxStageArgs a{};
+    a.channels = h->channels;
+    a.cpad = h->cpad;
+    a.len = std::min(T, n - t0);
+    a.buf = d_buf + t0;
+    a.stride = stride;
+    a.xT = h->xT[k].p;
+    a.vT = h->vT[k].p;
+    a.envT = h->envT[k].p;
+    a.inT = h->inT[k].p;
+    a.coT = h->coT[k].p;
+    a.tmax = h->tmax;
+    a.eq.nsec = h->nsec;
+    a.eq.sec = h->sec_dev.p;
+    a.eq.sec_ch_stride = h->eq_uniform ? 0 : (int64_t)h->nsec * kSecStride;
+    a.eq.state = h->eq_state.p;
+    a.cp = h->cp;
+    a.cs = h->cs.p;
+    a.rms_ring = h->ring.p;
+    a.vp = h->vp;
+    a.vs = h->vs.p;
+    a.vbuf = h->vbuf.p;
+    if (verb && reuse) AD_HIP(hipStreamWaitEvent(s, h->ev[EA][k], 0));  // inT / coT of that chunk consumed
+    if (eq || comp) {
+      launch_fx_transpose_in(a, a.xT, s);
+      launch_fx_eq(a, comp, (verb && !comp) ? kFxOutInT : kFxOutVT, s);
+      if (comp) launch_fx_gain(a, !verb, s);
+      if (!comp && !verb) launch_fx_transpose_out(a, a.vT, s);
+    } else {
+      launch_fx_transpose_in(a, a.inT, s);
+    }
+    if (verb) {
+      AD_HIP(hipEventRecord(h->ev[EE][k], s));
+      AD_HIP(hipStreamWaitEvent(sc, h->ev[EE][k], 0));
+      launch_fx_comb(a, sc);
+      AD_HIP(hipEventRecord(h->ev[EC][k], sc));
+      AD_HIP(hipStreamWaitEvent(sa, h->ev[EC][k], 0));
+      launch_fx_allpass(a, sa);
+      AD_HIP(hipEventRecord(h->ev[EA][k], sa));
+    }
+  }
+  AD_HIP(hipGetLastError());
+  if (verb) AD_HIP(hipStreamWaitEvent(s, h->ev[EA][k], 0));  // the last chunk's allpasses follow all work
+}
+
 void fx_run(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hipStream_t s) {
+  if (n <= 0) return;
+  if (!h->ev_last) AD_HIP(hipEventCreateWithFlags(&h->ev_last, hipEventDisableTiming));
+  if (fx_staged_ok(h)) {
+    fx_run_staged(h, d_buf, stride, n, s);
+    AD_HIP(hipEventRecord(h->ev_last, s));
+    return;
+  }
   ChainArgs a{};
   a.buf = d_buf;
   a.stride = stride;
@@ -157,6 +300,7 @@ void fx_run(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hipStream_
     s0 += ns;
   } while (s0 < h->nsec);
   AD_HIP(hipGetLastError());
+  AD_HIP(hipEventRecord(h->ev_last, s));
   if (want_prof) {
     std::vector<unsigned long long> v(prof.n);
     AD_HIP(hipStreamSynchronize(s));
@@ -166,6 +310,19 @@ void fx_run(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hipStream_
                                 100.0 * v[w * 2] / v[w * 2 + 1]);
   }
 }
+
+}  // namespace
+
+namespace adsp {
+// Internal (not in the C ABI): an effect-chain graph whose branches run on
+// several streams keeps each chain on its caller's stream, since the staged
+// engine's two extra streams per chain would outnumber the hardware queues.
+void fx_chain_allow_staged(ad_fx_chain* h, bool on) {
+  if (h) h->staged_ok = on;
+}
+}  // namespace adsp
+
+namespace {
 
 template <class Fn>
 int fx_guard(ad_fx_chain* h, Fn&& fn) {
@@ -217,7 +374,7 @@ int ad_fx_chain_create(int channels, int device, ad_fx_chain** out) {
 int ad_fx_chain_set_eq(ad_fx_chain* h, const double* sections, int nsec, int per_channel) {
   return fx_guard(h, [&] {
     if (nsec < 0 || (nsec > 0 && !sections)) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "bad EQ section table");
-    AD_HIP(hipStreamSynchronize(h->stream));
+    fx_quiesce(h);
     const bool keep_state = nsec == h->nsec;
     h->nsec = nsec;
     h->eq_uniform = !per_channel;
@@ -234,7 +391,7 @@ int ad_fx_chain_set_eq(ad_fx_chain* h, const double* sections, int nsec, int per
 
 int ad_fx_chain_set_compressor(ad_fx_chain* h, const ad_compressor_config* cfg) {
   return fx_guard(h, [&] {
-    AD_HIP(hipStreamSynchronize(h->stream));
+    fx_quiesce(h);
     if (!cfg) {
       h->comp_on = false;
       return;
@@ -248,14 +405,14 @@ int ad_fx_chain_set_compressor(ad_fx_chain* h, const ad_compressor_config* cfg) 
       h->cs.alloc((size_t)h->channels);
       h->ring.alloc((size_t)h->channels * p.rms_n);
       fx_reset_comp(h);
-      AD_HIP(hipStreamSynchronize(h->stream));
+      fx_quiesce(h);
     }
   });
 }
 
 int ad_fx_chain_set_freeverb(ad_fx_chain* h, double wet, double dry, double room_size, double damp, double gain) {
   return fx_guard(h, [&] {
-    AD_HIP(hipStreamSynchronize(h->stream));
+    fx_quiesce(h);
     // SetWet/SetDry/SetRoomSize/SetDamp/SetGain (reverb.go:192-220)
     h->vp.wet = wet;
     h->vp.dry = dry;
@@ -269,7 +426,7 @@ int ad_fx_chain_set_freeverb(ad_fx_chain* h, double wet, double dry, double room
       h->vs.alloc((size_t)h->channels);
       h->vbuf.alloc((size_t)kVerbLen * h->cpad);
       fx_reset_verb(h);
-      AD_HIP(hipStreamSynchronize(h->stream));
+      fx_quiesce(h);
     }
   });
 }
@@ -283,7 +440,7 @@ int ad_fx_chain_reset(ad_fx_chain* h) {
     if (h->eq_state.p) AD_HIP(hipMemsetAsync(h->eq_state.p, 0, h->eq_state.n * sizeof(double), h->stream));
     fx_reset_comp(h);
     fx_reset_verb(h);
-    AD_HIP(hipStreamSynchronize(h->stream));
+    fx_quiesce(h);
   });
 }
 
@@ -296,7 +453,7 @@ int ad_fx_chain_process(ad_fx_chain* h, double* buf, int64_t n) {
     AD_HIP(hipMemcpyAsync(h->work.p, buf, bytes, hipMemcpyHostToDevice, h->stream));
     fx_run(h, h->work.p, n, n, h->stream);
     AD_HIP(hipMemcpyAsync(buf, h->work.p, bytes, hipMemcpyDeviceToHost, h->stream));
-    AD_HIP(hipStreamSynchronize(h->stream));
+    fx_quiesce(h);
   });
 }
 
@@ -312,7 +469,7 @@ int ad_fx_chain_compressor_metrics(ad_fx_chain* h, int channel, double* input_pe
   return fx_guard(h, [&] {
     if (!h->comp_on) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "compressor stage not configured");
     if (channel < 0 || channel >= h->channels) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "channel out of range");
-    AD_HIP(hipStreamSynchronize(h->stream));
+    fx_quiesce(h);
     CompChState s{};
     AD_HIP(hipMemcpy(&s, h->cs.p + channel, sizeof(s), hipMemcpyDeviceToHost));
     if (input_peak) *input_peak = s.in_peak;
@@ -325,7 +482,7 @@ int ad_fx_chain_eq_state(ad_fx_chain* h, double* state, int64_t cap) {
   return fx_guard(h, [&] {
     const int64_t need = (int64_t)h->channels * h->nsec * 2;
     if (cap < need) AD_FAIL(AD_ERR_LENGTH_MISMATCH, "state buffer too small");
-    AD_HIP(hipStreamSynchronize(h->stream));
+    fx_quiesce(h);
     // device layout: per pass slab [C][ns][2]; return [C][nsec][2]
     std::vector<double> raw((size_t)need);
     if (need) AD_HIP(hipMemcpy(raw.data(), h->eq_state.p, need * sizeof(double), hipMemcpyDeviceToHost));

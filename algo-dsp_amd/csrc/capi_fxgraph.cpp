@@ -36,6 +36,10 @@
 
 using namespace adsp;
 
+namespace adsp {
+void fx_chain_allow_staged(ad_fx_chain* h, bool on);  // capi_dsp.cpp
+}
+
 namespace {
 
 void ck(int rc) {
@@ -275,6 +279,8 @@ void schedule(ad_fx_graph* g) {
   }
   // the caller's stream (lane 0) waits for every other lane's last op
   g->lanes_used = used;
+  for (FxOp& op : g->ops)
+    if (op.kind == FxOp::CHAIN) adsp::fx_chain_allow_staged(op.chain, used == 1);
   for (int l = 1; l < used; ++l)
     if (tail[l] >= 0) {
       g->ops[tail[l]].signal = true;

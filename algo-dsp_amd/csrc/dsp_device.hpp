@@ -1,0 +1,41 @@
+// Device helpers shared by the per-sample processor kernels
+// (dsp_kernels.hip, fx_staged.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "dsp_kernels.hpp"
+
+namespace adsp {
+
+// Go math.Log2 (frexp split + Log(frac)*(1/Ln2) + exp), core.go via compressor_math.go:8-20.
+__device__ __forceinline__ double go_log2(double x) {
+#pragma clang fp contract(off)
+  int e;
+  const double frac = frexp(x, &e);
+  if (frac == 0.5) return (double)(e - 1);
+  return log(frac) * 1.4426950408889634074 + (double)e;
+}
+
+// dynamicsCore.GainForLevel (core.go:288-329).  2^y via exp2 (Go:
+// math.Pow(2, y); both within an ulp).
+__device__ __forceinline__ double gain_for_level(const CompParams& p, double level) {
+#pragma clang fp contract(off)
+  if (level <= 0.0) return 1.0;
+  const double overshoot = go_log2(level) - p.threshold_log2;
+  if (!p.knee_on) {
+    if (overshoot <= 0.0) return 1.0;
+    return exp2(-overshoot * p.cf);
+  }
+  double eff;
+  if (overshoot < -p.half_knee) return 1.0;
+  if (overshoot > p.half_knee) {
+    eff = overshoot;
+  } else {
+    const double s = overshoot + p.half_knee;
+    eff = s * s * 0.5 * p.inv_knee_width_log2;
+  }
+  return exp2(-eff * p.cf);
+}
+
+}  // namespace adsp

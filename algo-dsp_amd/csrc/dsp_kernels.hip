@@ -26,51 +26,15 @@
 
 #include <cstdlib>
 
+#include "dsp_device.hpp"
 #include "dsp_kernels.hpp"
 
 namespace adsp {
 
 namespace {
 
-constexpr int kCombLen[kVerbCombs] = {1116, 1188, 1277, 1356, 1422, 1491, 1557, 1617};  // reverb.go:12-19
-constexpr int kApLen[kVerbAllpass] = {556, 441, 341, 225};                             // reverb.go:21-24
 constexpr int kVerbD = 2;                                                              // samples per chunk
 
-__host__ __device__ constexpr int comb_off(int i) { return i == 0 ? 0 : comb_off(i - 1) + kCombLen[i - 1]; }
-__host__ __device__ constexpr int ap_off(int i) {
-  return i == 0 ? comb_off(kVerbCombs) : ap_off(i - 1) + kApLen[i - 1];
-}
-static_assert(ap_off(kVerbAllpass) == kVerbLen, "Freeverb delay-line layout");
-
-// Go math.Log2 (frexp split + Log(frac)*(1/Ln2) + exp), core.go via compressor_math.go:8-20.
-__device__ __forceinline__ double go_log2(double x) {
-#pragma clang fp contract(off)
-  int e;
-  const double frac = frexp(x, &e);
-  if (frac == 0.5) return (double)(e - 1);
-  return log(frac) * 1.4426950408889634074 + (double)e;
-}
-
-// dynamicsCore.GainForLevel (core.go:288-329).  2^y via exp2 (Go:
-// math.Pow(2, y); both within an ulp).
-__device__ __forceinline__ double gain_for_level(const CompParams& p, double level) {
-#pragma clang fp contract(off)
-  if (level <= 0.0) return 1.0;
-  const double overshoot = go_log2(level) - p.threshold_log2;
-  if (!p.knee_on) {
-    if (overshoot <= 0.0) return 1.0;
-    return exp2(-overshoot * p.cf);
-  }
-  double eff;
-  if (overshoot < -p.half_knee) return 1.0;
-  if (overshoot > p.half_knee) {
-    eff = overshoot;
-  } else {
-    const double s = overshoot + p.half_knee;
-    eff = s * s * 0.5 * p.inv_knee_width_log2;
-  }
-  return exp2(-eff * p.cf);
-}
 
 template <bool EQ, bool COMP, bool VERB>
 __global__ __launch_bounds__(64) void k_chain(ChainArgs a) {

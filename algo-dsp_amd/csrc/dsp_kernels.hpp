@@ -42,6 +42,14 @@ struct CompChState {
 // reverb.Reverb (Freeverb) parameters and per-channel state.
 constexpr int kVerbCombs = 8, kVerbAllpass = 4;
 constexpr int kVerbLen = 1116 + 1188 + 1277 + 1356 + 1422 + 1491 + 1557 + 1617 + 556 + 441 + 341 + 225;  // 12587
+constexpr int kCombLen[kVerbCombs] = {1116, 1188, 1277, 1356, 1422, 1491, 1557, 1617};  // reverb.go:12-19
+constexpr int kApLen[kVerbAllpass] = {556, 441, 341, 225};                             // reverb.go:21-24
+// delay lines of one channel column in vbuf ([pos][cpad]): combs, then allpasses
+__host__ __device__ constexpr int comb_off(int i) { return i == 0 ? 0 : comb_off(i - 1) + kCombLen[i - 1]; }
+__host__ __device__ constexpr int ap_off(int i) {
+  return i == 0 ? comb_off(kVerbCombs) : ap_off(i - 1) + kApLen[i - 1];
+}
+static_assert(ap_off(kVerbAllpass) == kVerbLen, "Freeverb delay-line layout");
 struct VerbParams {
   double wet, dry, gain, feedback, damp_a, damp_b, ap_feedback;
 };
@@ -67,6 +75,37 @@ struct ChainArgs {
 
 // stages: bit 0 EQ, bit 1 compressor, bit 2 Freeverb
 void launch_chain(int stages, const ChainArgs& a, hipStream_t s);
+
+// Staged effect chain (fx_staged.hip): the chain split by recurrence into
+// kernels that run concurrently on their own streams over time chunks, each
+// stage on its own CUs.  Chunk-local buffers are time-major [t][cpad].
+struct FxStageArgs {
+  int channels, cpad;
+  int64_t len;           // samples in this chunk
+  double* buf;           // user buffer at the chunk start, [channels][stride]
+  int64_t stride;
+  double* xT;            // chunk input        [len][cpad] (transposed user buffer)
+  double* vT;            // EQ output          [len][cpad]
+  double* envT;          // envelope           [len][cpad]
+  double* inT;           // reverb input       [len][cpad] (compressor output / EQ output / input)
+  double* coT;           // comb outputs   [8][tmax][cpad]
+  int64_t tmax;
+  EqArgs eq;
+  CompParams cp;
+  CompChState* cs;
+  double* rms_ring;
+  VerbParams vp;
+  VerbChState* vs;
+  double* vbuf;
+};
+// stage kernels; `mode` selects where a stage writes (see fx_staged.hip)
+void launch_fx_eq(const FxStageArgs& a, bool comp, int out_mode, hipStream_t s);
+void launch_fx_gain(const FxStageArgs& a, bool to_user, hipStream_t s);
+void launch_fx_transpose_in(const FxStageArgs& a, double* dstT, hipStream_t s);   // user -> dstT
+void launch_fx_transpose_out(const FxStageArgs& a, const double* srcT, hipStream_t s);  // srcT -> user
+void launch_fx_comb(const FxStageArgs& a, hipStream_t s);
+void launch_fx_allpass(const FxStageArgs& a, hipStream_t s);
+constexpr int kFxOutVT = 1, kFxOutInT = 2;
 
 // Fan-in average of an effect-chain graph node (mixParentEdgesInto,
 // chain_process.go:295-318): dst = (0 + src0 + src1 + ...) * (1/nsrc).

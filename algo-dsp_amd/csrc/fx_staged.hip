@@ -1,0 +1,567 @@
+// Staged effect chain: biquad EQ -> feed-forward Compressor -> Freeverb,
+// split by recurrence into stage kernels that run concurrently on their own
+// streams over time chunks (host side: fx_run_staged in capi_dsp.cpp).
+//
+// Reference behaviour (all bit-for-bit the same operations as the fused
+// kernels in dsp_kernels.hip, which restate these files):
+//   biquad.Chain.ProcessBlock        dsp/filter/biquad/chain.go:59-70, section.go:47-53
+//   Compressor.ProcessSample         dsp/effects/dynamics/compressor.go:348-359, core.go:274-400
+//   updateMetrics                    compressor.go:411-423
+//   Reverb.ProcessSample (Freeverb)  dsp/effects/reverb/reverb.go:57-117, 169-182
+//
+// Why stages: at config 5 (256 channels) one lane per channel gives four
+// 64-channel waves, and the fused kernels keep one CU per 64 channels busy
+// issuing ~300 dependent FP64 instructions per sample.  Only some of that is
+// serial in time:
+//   K_eq    EQ sections (one wave per section, LDS ring between them) and
+//           the compressor detector / envelope            serial, 1 CU / 64 ch
+//   K_gain  gain(env) = 2^(-cf*knee(log2 env - T)), out = v*g*makeup,
+//           metrics                                       parallel over samples
+//   K_comb  one wave per comb filter (8 per 64 channels)  serial, 8 CUs / 64 ch
+//   K_ap    ordered comb sum, 4 allpasses, wet/dry mix    parallel within blocks
+//           of 128 samples (every allpass delay is >= 225)
+// so each stage gets its own CUs, and the transcendental-heavy gain stage
+// runs on the whole chip.  Chunk buffers between stages are time-major
+// [t][cpad] (one 512-byte row per sample per 64 channels); the user buffer
+// is channel-major [c][stride].
+#include <hip/hip_runtime.h>
+
+#include "dsp_device.hpp"
+#include "dsp_kernels.hpp"
+
+namespace adsp {
+
+namespace {
+
+constexpr int kEqP = 8;    // samples per pipeline step of K_eq
+constexpr int kEqPF = 4;   // K_eq input prefetch depth (steps)
+constexpr int kApB = 128;  // K_ap block (<= the shortest allpass delay, 225)
+constexpr int kApW = 8;    // waves of K_ap
+constexpr int kApG = 4;    // samples a K_ap wave loads together
+constexpr int kCombB = 16; // K_comb samples per load/store batch
+
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
+// Workgroup barrier for LDS hand-offs only.  __syncthreads() is a release /
+// acquire fence at workgroup scope: it waits for every outstanding global
+// load and store of the wave (vmcnt(0)), i.e. one HBM round trip per
+// barrier, and it drains the input prefetch.  Here only the LDS writes must
+// land before the other waves read them.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// ---------------------------------------------------------------------------
+// K_eq: waves 0 .. ns-1 run EQ section w on step k - w (a step is kEqP
+// samples); wave ns (COMP) runs the side-chain prefilter, detector and
+// envelope.  Consecutive waves hand over through a two-slot LDS ring: at
+// step k wave w writes slot (k - w) & 1 and wave w + 1 reads slot
+// (k - w - 1) & 1, one barrier per step.  Input xT, output (the last
+// section's, or the input when ns = 0) vT or inT, envelope envT: all
+// time-major rows, so every access is one coalesced 512-byte row.  Full
+// steps take a branch-free path; only a chunk's last step masks samples.
+// ---------------------------------------------------------------------------
+template <bool FULL>
+__device__ __forceinline__ void eq_section_step(const double (&q)[kSecStride], double& d0, double& d1,
+                                                const double (&x)[kEqP], double (&y)[kEqP], int nreal) {
+#pragma clang fp contract(off)
+#pragma unroll
+  for (int d = 0; d < kEqP; ++d) {
+    const double v = x[d] * q[0];
+    const double yy = q[1] * v + d0;
+    const double n0 = q[2] * v - q[4] * yy + d1;
+    const double n1 = q[3] * v - q[5] * yy;
+    if (FULL || d < nreal) {  // padding leaves the state untouched
+      d0 = n0;
+      d1 = n1;
+    }
+    y[d] = yy;
+  }
+}
+
+template <bool COMP>
+__global__ __launch_bounds__(64 * (kMaxSecPerPass + 1)) void k_fx_eq(FxStageArgs a, int out_mode) {
+#pragma clang fp contract(off)
+  __shared__ double ring[kMaxSecPerPass][2][kEqP][64];
+  const int w = wave_id();
+  const int l = threadIdx.x & 63;
+  const int c = blockIdx.x * 64 + l;
+  const bool active = c < a.channels;
+  const int cc = active ? c : a.channels - 1;
+  const int ns = a.eq.nsec;
+  const int W = ns + (COMP ? 1 : 0);
+  const int64_t len = a.len;
+  const int64_t nst = (len + kEqP - 1) / kEqP;
+  const int64_t steps = nst + W - 1;
+  const int cp = a.cpad;
+  const double* xin = a.xT + c;
+  double* tmo = (out_mode == kFxOutInT ? a.inT : a.vT) + c;
+
+  // wave 0's input rows, kEqPF steps ahead in rotating register blocks
+  // (a step of a section wave is ~0.3 us; HBM latency under load is a few)
+  double xq[kEqPF][kEqP];
+  if (w == 0) {
+#pragma unroll
+    for (int b = 0; b < kEqPF; ++b)
+#pragma unroll
+      for (int d = 0; d < kEqP; ++d) xq[b][d] = xin[min((int64_t)(b * kEqP + d), len - 1) * cp];
+  }
+  auto take_input = [&](int64_t my, double (&x)[kEqP]) {
+#pragma unroll
+    for (int d = 0; d < kEqP; ++d) x[d] = xq[0][d];
+#pragma unroll
+    for (int b = 0; b + 1 < kEqPF; ++b)
+#pragma unroll
+      for (int d = 0; d < kEqP; ++d) xq[b][d] = xq[b + 1][d];
+#pragma unroll
+    for (int d = 0; d < kEqP; ++d) xq[kEqPF - 1][d] = xin[min((my + kEqPF) * kEqP + d, len - 1) * cp];
+  };
+  auto emit = [&](int64_t my, const double (&y)[kEqP], int nreal) {
+    double* o = tmo + my * kEqP * cp;
+#pragma unroll
+    for (int d = 0; d < kEqP; ++d)
+      if (d < nreal) o[d * cp] = y[d];
+  };
+
+  if (w < ns) {
+    // ---- EQ section w (section.go:47-53 with the chain gain as pre-gain)
+    const double* sec = a.eq.sec + (int64_t)cc * a.eq.sec_ch_stride + w * kSecStride;
+    double q[kSecStride];
+#pragma unroll
+    for (int k = 0; k < kSecStride; ++k) q[k] = sec[k];
+    double* st = a.eq.state + ((int64_t)cc * ns + w) * 2;
+    double d0 = st[0], d1 = st[1];
+    const bool to_ring = w < ns - 1 || COMP;
+    const bool last = w == ns - 1;
+    for (int64_t k = 0; k < steps; ++k) {
+      const int64_t my = k - w;
+      if (my >= 0 && my < nst) {
+        double x[kEqP], y[kEqP];
+        if (w == 0) {
+          take_input(my, x);
+        } else {
+#pragma unroll
+          for (int d = 0; d < kEqP; ++d) x[d] = ring[w - 1][(my & 1)][d][l];
+        }
+        const int nreal = (int)min((int64_t)kEqP, len - my * kEqP);
+        if (nreal == kEqP)
+          eq_section_step<true>(q, d0, d1, x, y, nreal);
+        else
+          eq_section_step<false>(q, d0, d1, x, y, nreal);
+        if (to_ring) {
+#pragma unroll
+          for (int d = 0; d < kEqP; ++d) ring[w][(my & 1)][d][l] = y[d];
+        }
+        if (last) emit(my, y, nreal);
+      }
+      lds_barrier();
+    }
+    if (active) {
+      st[0] = d0;
+      st[1] = d1;
+    }
+  } else if constexpr (COMP) {
+    // ---- detector + envelope (core.go:274-286, 331-400)
+    const CompParams& p = a.cp;
+    CompChState cs = a.cs[cc];
+    double* rring = a.rms_ring + (int64_t)cc * p.rms_n;
+    double* eo = a.envT + c;
+    for (int64_t k = 0; k < steps; ++k) {
+      const int64_t my = k - w;
+      if (my >= 0 && my < nst) {
+        double x[kEqP], e[kEqP];
+        const int nreal = (int)min((int64_t)kEqP, len - my * kEqP);
+        if (ns == 0) {
+          take_input(my, x);
+          emit(my, x, nreal);  // v = the input
+        } else {
+#pragma unroll
+          for (int d = 0; d < kEqP; ++d) x[d] = ring[ns - 1][(my & 1)][d][l];
+        }
+#pragma unroll
+        for (int d = 0; d < kEqP; ++d) {
+          const bool real = d < nreal;
+          double sc = x[d];  // applyPrefilter core.go:390-400
+          if (p.lp_on) {
+            const double nl = cs.lp + p.lp_alpha * (sc - cs.lp);
+            sc = nl;
+            if (real) cs.lp = nl;
+          }
+          if (p.hp_on) {
+            const double nh = cs.hp + p.hp_alpha * (sc - cs.hp);
+            sc = sc - nh;
+            if (real) cs.hp = nh;
+          }
+          double src = fabs(sc);
+          if (p.detector_rms && real) {  // updateRMS core.go:361-388
+            const double sq = src * src;
+            if (cs.rms_filled == p.rms_n)
+              cs.rms_sum -= rring[cs.rms_index];
+            else
+              cs.rms_filled++;
+            if (active) rring[cs.rms_index] = sq;
+            cs.rms_sum += sq;
+            if (++cs.rms_index >= p.rms_n) cs.rms_index = 0;
+            const double mean = cs.rms_sum / (double)p.rms_n;
+            src = mean <= 0.0 ? 0.0 : sqrt(mean);
+          }
+          const double ne = src > cs.env ? cs.env + (src - cs.env) * p.attack : src + (cs.env - src) * p.release;
+          if (real) cs.env = ne;
+          e[d] = ne;
+        }
+        double* o = eo + my * kEqP * cp;
+#pragma unroll
+        for (int d = 0; d < kEqP; ++d)
+          if (d < nreal) o[d * cp] = e[d];
+      }
+      lds_barrier();
+    }
+    if (active) {  // only the fields this stage owns
+      CompChState* o = a.cs + c;
+      o->env = cs.env;
+      o->lp = cs.lp;
+      o->hp = cs.hp;
+      o->rms_sum = cs.rms_sum;
+      o->rms_index = cs.rms_index;
+      o->rms_filled = cs.rms_filled;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K_gain: out = v * g(env) * makeup per (channel, sample), parallel.  A
+// workgroup takes a 64-sample x 64-channel tile (lane = channel, wave w =
+// samples 16w .. 16w+15).  to_user: the tile is transposed through LDS and
+// stored channel-major into the user buffer; otherwise it goes to inT.
+// Metrics (updateMetrics): input/output peaks are maxima of non-negative
+// values and the gain reduction is the minimum gain (every g <= 1 since the
+// ratio >= 1, so `gr == 1 || g < gr` is a min from gr = 1); they combine with
+// integer atomics on the IEEE bit patterns, which order like the values.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void atomic_max_pos(double* p, double v) {
+  atomicMax(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v));
+}
+__device__ __forceinline__ void atomic_min_pos(double* p, double v) {
+  atomicMin(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v));
+}
+
+template <bool TO_USER>
+__global__ __launch_bounds__(256) void k_fx_gain(FxStageArgs a) {
+#pragma clang fp contract(off)
+  __shared__ double tile[64][65];
+  __shared__ double red[3][4][64];
+  const int w = wave_id();
+  const int l = threadIdx.x & 63;
+  const int c = blockIdx.y * 64 + l;
+  const int64_t t0 = (int64_t)blockIdx.x * 64;
+  const CompParams& p = a.cp;
+  double ip = 0.0, op = 0.0, gr = 1.0;
+#pragma unroll 4
+  for (int j = 0; j < 16; ++j) {
+    const int tl = w * 16 + j;
+    const int64_t t = t0 + tl;
+    double out = 0.0;
+    if (t < a.len) {
+      const double v = a.vT[t * a.cpad + c];
+      const double g = gain_for_level(p, a.envT[t * a.cpad + c]);
+      out = v * g * p.makeup_lin;
+      const double il = fabs(v), ol = fabs(out);
+      if (il > ip) ip = il;
+      if (ol > op) op = ol;
+      if (g < gr) gr = g;
+      if (!TO_USER) a.inT[t * a.cpad + c] = out;
+    }
+    if (TO_USER) tile[tl][l] = out;
+  }
+  red[0][w][l] = ip;
+  red[1][w][l] = op;
+  red[2][w][l] = gr;
+  __syncthreads();
+  if (w == 0 && c < a.channels) {
+#pragma unroll
+    for (int k = 1; k < 4; ++k) {
+      if (red[0][k][l] > ip) ip = red[0][k][l];
+      if (red[1][k][l] > op) op = red[1][k][l];
+      if (red[2][k][l] < gr) gr = red[2][k][l];
+    }
+    CompChState* cs = a.cs + c;
+    if (ip > 0.0) atomic_max_pos(&cs->in_peak, ip);
+    if (op > 0.0) atomic_max_pos(&cs->out_peak, op);
+    if (gr < 1.0) atomic_min_pos(&cs->gr, gr);
+  }
+  if (TO_USER) {
+    // lane = sample, wave w = channels 16w .. 16w+15 of the tile
+    const int64_t t = t0 + l;
+#pragma unroll 4
+    for (int j = 0; j < 16; ++j) {
+      const int cl = w * 16 + j;
+      const int ch = blockIdx.y * 64 + cl;
+      if (ch < a.channels && t < a.len) a.buf[(int64_t)ch * a.stride + t] = tile[l][cl];
+    }
+  }
+}
+
+// user buffer [c][t] <-> time-major [t][cpad], 64 x 64 tiles through LDS
+__global__ __launch_bounds__(256) void k_fx_transpose_in(FxStageArgs a, double* dstT) {
+  __shared__ double tile[64][65];
+  const int w = wave_id();
+  const int l = threadIdx.x & 63;
+  const int64_t t0 = (int64_t)blockIdx.x * 64;
+  const int cb = blockIdx.y * 64;
+#pragma unroll 4
+  for (int j = 0; j < 16; ++j) {  // lane = sample
+    const int cl = w * 16 + j;
+    const int ch = min(cb + cl, a.channels - 1);
+    const int64_t t = min(t0 + l, a.len - 1);
+    tile[cl][l] = a.buf[(int64_t)ch * a.stride + t];
+  }
+  __syncthreads();
+#pragma unroll 4
+  for (int j = 0; j < 16; ++j) {  // lane = channel
+    const int64_t t = t0 + w * 16 + j;
+    if (t < a.len) dstT[t * a.cpad + cb + l] = tile[l][w * 16 + j];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_fx_transpose_out(FxStageArgs a, const double* srcT) {
+  __shared__ double tile[64][65];
+  const int w = wave_id();
+  const int l = threadIdx.x & 63;
+  const int64_t t0 = (int64_t)blockIdx.x * 64;
+  const int cb = blockIdx.y * 64;
+#pragma unroll 4
+  for (int j = 0; j < 16; ++j) {  // lane = channel
+    const int64_t t = min(t0 + w * 16 + j, a.len - 1);
+    tile[w * 16 + j][l] = srcT[t * a.cpad + cb + l];
+  }
+  __syncthreads();
+#pragma unroll 4
+  for (int j = 0; j < 16; ++j) {  // lane = sample
+    const int cl = w * 16 + j;
+    const int64_t t = t0 + l;
+    if (cb + cl < a.channels && t < a.len) a.buf[(int64_t)(cb + cl) * a.stride + t] = tile[l][cl];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K_comb: comb filter i (blockIdx.y) of 64 channels, one wave, serial in
+// time (comb.process reverb.go:101-117):
+//   output = line[idx]; fs = output*damp_b + fs*damp_a (flushed below 1e-23);
+//   line[idx] = gain*in + fs*feedback; idx = (idx+1) mod len
+// The line is read kCombB samples at a time (the values were written >= 1116
+// samples earlier) two batches ahead, and written back after the batch.  Lanes
+// past the channel count work on their own padding column of vbuf and
+// never store state.  Output: coT[i][t][c].
+// ---------------------------------------------------------------------------
+template <bool FULL>
+__device__ __forceinline__ void comb_batch(const VerbParams& p, double& fs, const double (&dl)[kCombB],
+                                           const double (&xg)[kCombB], double (&nv)[kCombB], int nb) {
+#pragma clang fp contract(off)
+#pragma unroll
+  for (int j = 0; j < kCombB; ++j) {
+    const double output = dl[j];
+    double f = output * p.damp_b + fs * p.damp_a;
+    if (fabs(f) < 1e-23) f = 0.0;
+    if (FULL || j < nb) fs = f;
+    nv[j] = p.gain * xg[j] + fs * p.feedback;
+  }
+}
+
+__global__ __launch_bounds__(64) void k_fx_comb(FxStageArgs a) {
+#pragma clang fp contract(off)
+  const int i = blockIdx.y;
+  const int l = threadIdx.x;
+  const int c = blockIdx.x * 64 + l;
+  const bool active = c < a.channels;
+  const int cc = active ? c : a.channels - 1;
+  const int clen = kCombLen[i];
+  const int cp = a.cpad;
+  double* line = a.vbuf + (int64_t)comb_off(i) * cp + c;
+  double* co = a.coT + (int64_t)i * a.tmax * cp + c;
+  const double* in = a.inT + c;
+  const VerbParams& p = a.vp;
+  int idx = a.vs[cc].comb_idx[i];
+  double fs = a.vs[cc].filter_store[i];
+  const int64_t len = a.len;
+  // three batches in flight: batch m sits in buffer m % 3 and is loaded two
+  // batches before it runs (~100 samples of lead at ~80 cycles/sample)
+  double dl[3][kCombB], xg[3][kCombB];
+  int lpos = idx;     // line position of the next batch to load
+  int64_t lt = 0;     // its first sample
+  auto load = [&](int b) {
+    int pos = lpos;
+#pragma unroll
+    for (int j = 0; j < kCombB; ++j) {
+      dl[b][j] = line[(int64_t)pos * cp];
+      xg[b][j] = in[min(lt + j, len - 1) * cp];
+      if (++pos >= clen) pos = 0;
+    }
+    lpos = pos;
+    lt += kCombB;
+  };
+  auto run = [&](int b, int64_t t0) {
+    const int nb = (int)min((int64_t)kCombB, len - t0);
+    double nv[kCombB];
+    if (nb == kCombB)
+      comb_batch<true>(p, fs, dl[b], xg[b], nv, nb);
+    else
+      comb_batch<false>(p, fs, dl[b], xg[b], nv, nb);
+    int pos = idx;
+#pragma unroll
+    for (int j = 0; j < kCombB; ++j) {
+      if (j < nb) {
+        co[(t0 + j) * cp] = dl[b][j];
+        line[(int64_t)pos * cp] = nv[j];
+      }
+      if (++pos >= clen) pos = 0;
+    }
+    idx += nb;
+    if (idx >= clen) idx -= clen;
+  };
+  load(0);
+  load(1);
+  for (int64_t t0 = 0; t0 < len; t0 += 3 * kCombB) {
+    load(2);
+    run(0, t0);
+    if (t0 + kCombB >= len) break;
+    load(0);
+    run(1, t0 + kCombB);
+    if (t0 + 2 * kCombB >= len) break;
+    load(1);
+    run(2, t0 + 2 * kCombB);
+  }
+  if (active) {
+    a.vs[c].comb_idx[i] = idx;
+    a.vs[c].filter_store[i] = fs;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K_ap: acc = (((0 + c0) + c1) + ... + c7), the four allpasses in series
+// (allpass.process reverb.go:57-68: out = line[idx] - acc;
+// line[idx] = acc + line[idx]*0.5), y = acc*wet + in*dry.  Within a block of
+// kApB = 128 samples every (channel, sample) is independent: an allpass
+// reads its line 225..556 samples back, i.e. before the block, and no two
+// samples of a block touch the same line position.  A workgroup of kApW
+// waves serves 64 channels (lane = channel; wave w takes samples
+// 16w .. 16w+15 of a block, kApG at a time with every load issued before
+// the arithmetic); y is transposed through LDS and stored channel-major.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(64 * kApW) void k_fx_allpass(FxStageArgs a) {
+#pragma clang fp contract(off)
+  constexpr int SPW = kApB / kApW;  // samples per wave per block
+  __shared__ double tile[kApB][65];
+  const int w = wave_id();
+  const int l = threadIdx.x & 63;
+  const int c = blockIdx.x * 64 + l;
+  const bool active = c < a.channels;
+  const int cc = active ? c : a.channels - 1;
+  const int cp = a.cpad;
+  const VerbParams& p = a.vp;
+  int base[kVerbAllpass];  // line position of the block's first sample
+#pragma unroll
+  for (int i = 0; i < kVerbAllpass; ++i) base[i] = a.vs[cc].ap_idx[i];
+  const int64_t len = a.len;
+  const int64_t cstride = a.tmax * cp;
+  for (int64_t b0 = 0; b0 < len; b0 += kApB) {
+#pragma unroll
+    for (int g = 0; g < SPW; g += kApG) {
+      const int tl0 = w * SPW + g;
+      double cv[kApG][kVerbCombs], bo[kApG][kVerbAllpass], xin[kApG];
+      double* q[kApG][kVerbAllpass];
+#pragma unroll
+      for (int s = 0; s < kApG; ++s) {
+        const int64_t t = min(b0 + tl0 + s, len - 1);  // clamped rows are never stored
+        const double* cot = a.coT + t * cp + c;
+#pragma unroll
+        for (int i = 0; i < kVerbCombs; ++i) cv[s][i] = cot[i * cstride];
+#pragma unroll
+        for (int i = 0; i < kVerbAllpass; ++i) {
+          int pos = base[i] + tl0 + s;
+          if (pos >= kApLen[i]) pos -= kApLen[i];
+          q[s][i] = a.vbuf + (int64_t)(ap_off(i) + pos) * cp + c;
+          bo[s][i] = *q[s][i];
+        }
+        xin[s] = a.inT[t * cp + c];
+      }
+#pragma unroll
+      for (int s = 0; s < kApG; ++s) {
+        const bool real = b0 + tl0 + s < len;
+        double acc = 0.0;
+#pragma unroll
+        for (int i = 0; i < kVerbCombs; ++i) acc += cv[s][i];
+#pragma unroll
+        for (int i = 0; i < kVerbAllpass; ++i) {
+          const double output = bo[s][i] - acc;
+          if (real) *q[s][i] = acc + bo[s][i] * p.ap_feedback;
+          acc = output;
+        }
+        tile[tl0 + s][l] = acc * p.wet + xin[s] * p.dry;
+      }
+    }
+    lds_barrier();  // the tile (LDS only)
+    // lane = sample (two halves of the block), wave w = channels 8w .. 8w+7
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int ch = blockIdx.x * 64 + w * 8 + j;
+#pragma unroll
+      for (int h = 0; h < kApB / 64; ++h) {
+        const int tl = h * 64 + l;
+        if (ch < a.channels && b0 + tl < len) a.buf[(int64_t)ch * a.stride + b0 + tl] = tile[tl][w * 8 + j];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < kVerbAllpass; ++i) {
+      base[i] += kApB;
+      if (base[i] >= kApLen[i]) base[i] -= kApLen[i];
+    }
+    __syncthreads();  // line writes of this block are read by other waves 225+ samples on
+  }
+  if (active && w == 0) {
+#pragma unroll
+    for (int i = 0; i < kVerbAllpass; ++i) a.vs[c].ap_idx[i] = (int)((a.vs[c].ap_idx[i] + len % kApLen[i]) % kApLen[i]);
+  }
+}
+
+}  // namespace
+
+void launch_fx_eq(const FxStageArgs& a, bool comp, int out_mode, hipStream_t s) {
+  const int W = a.eq.nsec + (comp ? 1 : 0);
+  if (W == 0 || a.len <= 0) return;
+  const dim3 grid((unsigned)((a.channels + 63) / 64)), block((unsigned)(64 * W));
+  if (comp)
+    hipLaunchKernelGGL(k_fx_eq<true>, grid, block, 0, s, a, out_mode);
+  else
+    hipLaunchKernelGGL(k_fx_eq<false>, grid, block, 0, s, a, out_mode);
+}
+
+void launch_fx_gain(const FxStageArgs& a, bool to_user, hipStream_t s) {
+  if (a.len <= 0) return;
+  const dim3 grid((unsigned)((a.len + 63) / 64), (unsigned)((a.channels + 63) / 64));
+  if (to_user)
+    hipLaunchKernelGGL(k_fx_gain<true>, grid, dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL(k_fx_gain<false>, grid, dim3(256), 0, s, a);
+}
+
+void launch_fx_transpose_in(const FxStageArgs& a, double* dstT, hipStream_t s) {
+  if (a.len <= 0) return;
+  const dim3 grid((unsigned)((a.len + 63) / 64), (unsigned)((a.channels + 63) / 64));
+  hipLaunchKernelGGL(k_fx_transpose_in, grid, dim3(256), 0, s, a, dstT);
+}
+
+void launch_fx_transpose_out(const FxStageArgs& a, const double* srcT, hipStream_t s) {
+  if (a.len <= 0) return;
+  const dim3 grid((unsigned)((a.len + 63) / 64), (unsigned)((a.channels + 63) / 64));
+  hipLaunchKernelGGL(k_fx_transpose_out, grid, dim3(256), 0, s, a, srcT);
+}
+
+void launch_fx_comb(const FxStageArgs& a, hipStream_t s) {
+  if (a.len <= 0) return;
+  hipLaunchKernelGGL(k_fx_comb, dim3((unsigned)((a.channels + 63) / 64), kVerbCombs), dim3(64), 0, s, a);
+}
+
+void launch_fx_allpass(const FxStageArgs& a, hipStream_t s) {
+  if (a.len <= 0) return;
+  hipLaunchKernelGGL(k_fx_allpass, dim3((unsigned)((a.channels + 63) / 64)), dim3(64 * kApW), 0, s, a);
+}
+
+}  // namespace adsp

@@ -205,6 +205,59 @@ def test_effect_chain_config5(gpu):
         assert rms(y[c], v) <= RMS_TOL, rms(y[c], v)
 
 
+# ------------------------------------------------------------------ staged engine == fused kernels
+STAGED_CASES = {
+    "eq": dict(eq=True),
+    "comp": dict(comp={}),
+    "comp-rms-sidechain": dict(comp={"detector_mode": 1, "rms_window_ms": 3.0, "sidechain_low_cut_hz": 80.0,
+                                     "sidechain_high_cut_hz": 6000.0}),
+    "verb": dict(verb=True),
+    "eq-verb": dict(eq=True, verb=True),
+    "eq-comp": dict(eq=True, comp={"knee_db": 0.0, "auto_makeup": 1}),
+    "config5": dict(eq=True, comp={"auto_makeup": 0, "makeup_db": 0.0}, verb=True),
+}
+
+
+@pytest.mark.parametrize("case", list(STAGED_CASES), ids=list(STAGED_CASES))
+def test_staged_engine_matches_fused(gpu, case, monkeypatch):
+    """The staged engine (stage kernels over time chunks on four streams)
+    computes every value with the fused kernels' operations: outputs, EQ
+    state and compressor metrics are identical, over chunk boundaries
+    (AD_FX_CHUNK=256), calls that end mid-chunk, and a partial channel group."""
+    fs = 48000.0
+    cfg = STAGED_CASES[case]
+    eq = design.config5_eq(fs) if cfg.get("eq") else ()
+    comp = cfg.get("comp")
+    verb = (0.3, 0.8, 0.8, 0.3, 0.02) if cfg.get("verb") else None
+    C, n = 70, 3000
+    x = np.stack([0.5 * signals.white_noise(n, 900 + c) * (1 + 0.02 * c) for c in range(C)])
+    outs = {}
+    for staged in ("1", "0"):
+        monkeypatch.setenv("AD_FX_STAGED", staged)
+        monkeypatch.setenv("AD_FX_CHUNK", "256")
+        fx = P.EffectChain(C, eq, comp, verb, fs)
+        y = x.copy()
+        parts = []
+        for lo, hi in [(0, 700), (700, 701), (701, 3000)]:
+            b = y[:, lo:hi].copy()
+            fx.Process(b)
+            parts.append(b)
+        outs[staged] = (np.concatenate(parts, axis=1), fx)
+    a, b = outs["1"][0], outs["0"][0]
+    assert np.array_equal(a, b), float(np.max(np.abs(a - b)))
+    if comp is not None:
+        from algodsp._lib import lib
+        import ctypes as Cc
+
+        for c in (0, 33, 69):
+            m = []
+            for k in ("1", "0"):
+                v = [Cc.c_double() for _ in range(3)]
+                lib().ad_fx_chain_compressor_metrics(outs[k][1]._h, c, *[Cc.byref(t) for t in v])
+                m.append([t.value for t in v])
+            assert m[0] == m[1], (c, m)
+
+
 # ------------------------------------------------------------------ FIR
 @pytest.mark.parametrize("taps", [1, 5, 31, 32, 64, 257])
 def test_fir_vs_oracle(gpu, taps):
