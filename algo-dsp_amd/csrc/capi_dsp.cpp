@@ -233,6 +233,7 @@ void fx_run_staged(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hip
     a.vp = h->vp;
     a.vs = h->vs.p;
     a.vbuf = h->vbuf.p;
+    if (const char* dv = std::getenv("AD_FX_DBG")) a.dbg = std::atoi(dv);
     if (verb && reuse) AD_HIP(hipStreamWaitEvent(s, h->ev[EA][k], 0));  // inT / coT of that chunk consumed
     if (eq || comp) {
       launch_fx_transpose_in(a, a.xT, s);

@@ -37,7 +37,6 @@ constexpr int kEqP = 8;    // samples per pipeline step of K_eq
 constexpr int kEqPF = 4;   // K_eq input prefetch depth (steps)
 constexpr int kApB = 128;  // K_ap block (<= the shortest allpass delay, 225)
 constexpr int kApW = 8;    // waves of K_ap
-constexpr int kApG = 4;    // samples a K_ap wave loads together
 constexpr int kCombB = 16; // K_comb samples per load/store batch
 
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
@@ -374,11 +373,16 @@ __global__ __launch_bounds__(64) void k_fx_comb(FxStageArgs a) {
   const int cc = active ? c : a.channels - 1;
   const int clen = kCombLen[i];
   const int cp = a.cpad;
-  double* line = a.vbuf + (int64_t)comb_off(i) * cp + c;
-  double* co = a.coT + (int64_t)i * a.tmax * cp + c;
-  const double* in = a.inT + c;
+  // Row pointers are wave-uniform (scalar registers); a lane adds only its
+  // channel c, so every access is a saddr + lane-offset load or store.  All
+  // channels of a handle advance their delay lines together (every call
+  // processes every channel over the same samples, Reset clears all), so
+  // the ring index is uniform and lane 0's copy drives the addresses.
+  double* line = a.vbuf + (int64_t)comb_off(i) * cp;
+  double* co = a.coT + (int64_t)i * a.tmax * cp;
+  const double* in = a.inT;
   const VerbParams& p = a.vp;
-  int idx = a.vs[cc].comb_idx[i];
+  int idx = __builtin_amdgcn_readfirstlane(a.vs[cc].comb_idx[i]);
   double fs = a.vs[cc].filter_store[i];
   const int64_t len = a.len;
   // three batches in flight: batch m sits in buffer m % 3 and is loaded two
@@ -390,8 +394,8 @@ __global__ __launch_bounds__(64) void k_fx_comb(FxStageArgs a) {
     int pos = lpos;
 #pragma unroll
     for (int j = 0; j < kCombB; ++j) {
-      dl[b][j] = line[(int64_t)pos * cp];
-      xg[b][j] = in[min(lt + j, len - 1) * cp];
+      dl[b][j] = (line + (int64_t)pos * cp)[c];
+      xg[b][j] = (in + min(lt + j, len - 1) * cp)[c];
       if (++pos >= clen) pos = 0;
     }
     lpos = pos;
@@ -408,8 +412,8 @@ __global__ __launch_bounds__(64) void k_fx_comb(FxStageArgs a) {
 #pragma unroll
     for (int j = 0; j < kCombB; ++j) {
       if (j < nb) {
-        co[(t0 + j) * cp] = dl[b][j];
-        line[(int64_t)pos * cp] = nv[j];
+        (co + (t0 + j) * cp)[c] = dl[b][j];
+        (line + (int64_t)pos * cp)[c] = nv[j];
       }
       if (++pos >= clen) pos = 0;
     }
@@ -440,73 +444,74 @@ __global__ __launch_bounds__(64) void k_fx_comb(FxStageArgs a) {
 // line[idx] = acc + line[idx]*0.5), y = acc*wet + in*dry.  Within a block of
 // kApB = 128 samples every (channel, sample) is independent: an allpass
 // reads its line 225..556 samples back, i.e. before the block, and no two
-// samples of a block touch the same line position.  A workgroup of kApW
-// waves serves 64 channels (lane = channel; wave w takes samples
-// 16w .. 16w+15 of a block, kApG at a time with every load issued before
-// the arithmetic); y is transposed through LDS and stored channel-major.
+// samples of a block touch the same line position.  So a workgroup serves
+// only 16 channels (16 workgroups at 256 channels: the stage is bound by
+// memory round trips, and more CUs keep more of them in flight): lane =
+// channel (16) x sample phase (4); wave w, phase h takes samples
+// 4w + h + 32j, j = 0..3, of a block, with all 52 loads of its four samples
+// issued before the arithmetic.  y is transposed through LDS and stored
+// channel-major.
 // ---------------------------------------------------------------------------
+constexpr int kApCh = 16;
 __global__ __launch_bounds__(64 * kApW) void k_fx_allpass(FxStageArgs a) {
 #pragma clang fp contract(off)
-  constexpr int SPW = kApB / kApW;  // samples per wave per block
-  __shared__ double tile[kApB][65];
+  constexpr int J = kApB / (kApW * 4);  // samples per lane per block
+  __shared__ double tile[kApCh][kApB + 1];
   const int w = wave_id();
   const int l = threadIdx.x & 63;
-  const int c = blockIdx.x * 64 + l;
+  const int cl = l & (kApCh - 1), ph = l >> 4;
+  const int c = blockIdx.x * kApCh + cl;
   const bool active = c < a.channels;
   const int cc = active ? c : a.channels - 1;
   const int cp = a.cpad;
   const VerbParams& p = a.vp;
-  int base[kVerbAllpass];  // line position of the block's first sample
+  int base[kVerbAllpass];  // line position of the block's first sample (uniform, see K_comb)
 #pragma unroll
-  for (int i = 0; i < kVerbAllpass; ++i) base[i] = a.vs[cc].ap_idx[i];
+  for (int i = 0; i < kVerbAllpass; ++i) base[i] = __builtin_amdgcn_readfirstlane(a.vs[cc].ap_idx[i]);
   const int64_t len = a.len;
   const int64_t cstride = a.tmax * cp;
   for (int64_t b0 = 0; b0 < len; b0 += kApB) {
+    double cv[J][kVerbCombs], bo[J][kVerbAllpass], xin[J];
+    int pos[J][kVerbAllpass];
 #pragma unroll
-    for (int g = 0; g < SPW; g += kApG) {
-      const int tl0 = w * SPW + g;
-      double cv[kApG][kVerbCombs], bo[kApG][kVerbAllpass], xin[kApG];
-      double* q[kApG][kVerbAllpass];
+    for (int j = 0; j < J; ++j) {
+      const int tl = 4 * w + ph + 32 * j;
+      const int64_t t = min(b0 + tl, len - 1);  // clamped rows are never stored
+      const double* cot = a.coT + t * cp + c;
 #pragma unroll
-      for (int s = 0; s < kApG; ++s) {
-        const int64_t t = min(b0 + tl0 + s, len - 1);  // clamped rows are never stored
-        const double* cot = a.coT + t * cp + c;
+      for (int i = 0; i < kVerbCombs; ++i) cv[j][i] = cot[i * cstride];
 #pragma unroll
-        for (int i = 0; i < kVerbCombs; ++i) cv[s][i] = cot[i * cstride];
-#pragma unroll
-        for (int i = 0; i < kVerbAllpass; ++i) {
-          int pos = base[i] + tl0 + s;
-          if (pos >= kApLen[i]) pos -= kApLen[i];
-          q[s][i] = a.vbuf + (int64_t)(ap_off(i) + pos) * cp + c;
-          bo[s][i] = *q[s][i];
-        }
-        xin[s] = a.inT[t * cp + c];
+      for (int i = 0; i < kVerbAllpass; ++i) {
+        int q = base[i] + tl;
+        if (q >= kApLen[i]) q -= kApLen[i];
+        pos[j][i] = q;
+        bo[j][i] = a.vbuf[(int64_t)(ap_off(i) + q) * cp + c];
       }
+      xin[j] = a.inT[t * cp + c];
+    }
 #pragma unroll
-      for (int s = 0; s < kApG; ++s) {
-        const bool real = b0 + tl0 + s < len;
-        double acc = 0.0;
+    for (int j = 0; j < J; ++j) {
+      const int tl = 4 * w + ph + 32 * j;
+      const bool real = b0 + tl < len;
+      double acc = 0.0;
 #pragma unroll
-        for (int i = 0; i < kVerbCombs; ++i) acc += cv[s][i];
+      for (int i = 0; i < kVerbCombs; ++i) acc += cv[j][i];
 #pragma unroll
-        for (int i = 0; i < kVerbAllpass; ++i) {
-          const double output = bo[s][i] - acc;
-          if (real) *q[s][i] = acc + bo[s][i] * p.ap_feedback;
-          acc = output;
-        }
-        tile[tl0 + s][l] = acc * p.wet + xin[s] * p.dry;
+      for (int i = 0; i < kVerbAllpass; ++i) {
+        const double output = bo[j][i] - acc;
+        if (real) a.vbuf[(int64_t)(ap_off(i) + pos[j][i]) * cp + c] = acc + bo[j][i] * p.ap_feedback;
+        acc = output;
       }
+      tile[cl][tl] = acc * p.wet + xin[j] * p.dry;
     }
     lds_barrier();  // the tile (LDS only)
-    // lane = sample (two halves of the block), wave w = channels 8w .. 8w+7
+    // consecutive threads = consecutive samples of one channel
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int ch = blockIdx.x * 64 + w * 8 + j;
-#pragma unroll
-      for (int h = 0; h < kApB / 64; ++h) {
-        const int tl = h * 64 + l;
-        if (ch < a.channels && b0 + tl < len) a.buf[(int64_t)ch * a.stride + b0 + tl] = tile[tl][w * 8 + j];
-      }
+    for (int r = 0; r < kApCh * kApB / (64 * kApW); ++r) {
+      const int e = r * 64 * kApW + threadIdx.x;
+      const int ch = e / kApB, tl = e % kApB;
+      const int cg = blockIdx.x * kApCh + ch;
+      if (cg < a.channels && b0 + tl < len) a.buf[(int64_t)cg * a.stride + b0 + tl] = tile[ch][tl];
     }
 #pragma unroll
     for (int i = 0; i < kVerbAllpass; ++i) {
@@ -515,7 +520,7 @@ __global__ __launch_bounds__(64 * kApW) void k_fx_allpass(FxStageArgs a) {
     }
     __syncthreads();  // line writes of this block are read by other waves 225+ samples on
   }
-  if (active && w == 0) {
+  if (active && w == 0 && ph == 0) {
 #pragma unroll
     for (int i = 0; i < kVerbAllpass; ++i) a.vs[c].ap_idx[i] = (int)((a.vs[c].ap_idx[i] + len % kApLen[i]) % kApLen[i]);
   }
@@ -561,7 +566,7 @@ void launch_fx_comb(const FxStageArgs& a, hipStream_t s) {
 
 void launch_fx_allpass(const FxStageArgs& a, hipStream_t s) {
   if (a.len <= 0) return;
-  hipLaunchKernelGGL(k_fx_allpass, dim3((unsigned)((a.channels + 63) / 64)), dim3(64 * kApW), 0, s, a);
+  hipLaunchKernelGGL(k_fx_allpass, dim3((unsigned)((a.channels + kApCh - 1) / kApCh)), dim3(64 * kApW), 0, s, a);
 }
 
 }  // namespace adsp
