@@ -234,6 +234,13 @@ void fx_run_staged(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hip
     a.vs = h->vs.p;
     a.vbuf = h->vbuf.p;
     if (const char* dv = std::getenv("AD_FX_DBG")) a.dbg = std::atoi(dv);
+    static DevBuf<unsigned long long> eprof;
+    const bool want_prof = std::getenv("AD_FX_PROF") != nullptr && i == 0;
+    if (want_prof) {
+      eprof.reserve(32);
+      AD_HIP(hipMemsetAsync(eprof.p, 0, 32 * sizeof(unsigned long long), s));
+      a.prof = eprof.p;
+    }
     if (verb && reuse) AD_HIP(hipStreamWaitEvent(s, h->ev[EA][k], 0));  // inT / coT of that chunk consumed
     if (eq || comp) {
       launch_fx_transpose_in(a, a.xT, s);
@@ -242,6 +249,15 @@ void fx_run_staged(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hip
       if (!comp && !verb) launch_fx_transpose_out(a, a.vT, s);
     } else {
       launch_fx_transpose_in(a, a.inT, s);
+    }
+    if (want_prof) {
+      unsigned long long v[32];
+      AD_HIP(hipStreamSynchronize(s));
+      AD_HIP(hipMemcpy(v, eprof.p, sizeof(v), hipMemcpyDeviceToHost));
+      for (int w = 0; w < 9; ++w)
+        if (v[2 * w] || v[2 * w + 1])
+          fprintf(stderr, "fx K_eq wave %d: compute %llu, barrier wait %llu ticks (chunk of %lld)\n", w, v[2 * w],
+                  v[2 * w + 1], (long long)a.len);
     }
     if (verb) {
       AD_HIP(hipEventRecord(h->ev[EE][k], s));

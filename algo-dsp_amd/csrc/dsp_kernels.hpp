@@ -98,6 +98,7 @@ struct FxStageArgs {
   VerbChState* vs;
   double* vbuf;
   int dbg;  // diagnostics only (AD_FX_DBG): bit 0 skip K_eq global stores, bit 1 skip its barrier, bit 2 skip its input loads
+  unsigned long long* prof;  // diagnostics only (AD_FX_PROF): K_eq per wave {compute, barrier wait} clock ticks
 };
 // stage kernels; `mode` selects where a stage writes (see fx_staged.hip)
 void launch_fx_eq(const FxStageArgs& a, bool comp, int out_mode, hipStream_t s);

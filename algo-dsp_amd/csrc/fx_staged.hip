@@ -130,7 +130,9 @@ __global__ __launch_bounds__(64 * (kMaxSecPerPass + 1)) void k_fx_eq(FxStageArgs
     double d0 = st[0], d1 = st[1];
     const bool to_ring = w < ns - 1 || COMP;
     const bool last = w == ns - 1;
+    unsigned long long tc = 0, tb = 0;
     for (int64_t k = 0; k < steps; ++k) {
+      const unsigned long long t0c = a.prof ? clock64() : 0;
       const int64_t my = k - w;
       if (my >= 0 && my < nst) {
         double x[kEqP], y[kEqP];
@@ -151,7 +153,16 @@ __global__ __launch_bounds__(64 * (kMaxSecPerPass + 1)) void k_fx_eq(FxStageArgs
         }
         if (last) emit(my, y, nreal);
       }
+      const unsigned long long t1c = a.prof ? clock64() : 0;
       lds_barrier();
+      if (a.prof) {
+        tc += t1c - t0c;
+        tb += clock64() - t1c;
+      }
+    }
+    if (a.prof && l == 0 && blockIdx.x == 0) {
+      a.prof[2 * w] = tc;
+      a.prof[2 * w + 1] = tb;
     }
     if (active) {
       st[0] = d0;
