@@ -161,6 +161,10 @@ void fx_reset_verb(ad_fx_chain* h) {
 bool fx_staged_ok(const ad_fx_chain* h) {
   const char* v = std::getenv("AD_FX_STAGED");  // read per call: tests compare both engines
   const bool on = !(v && v[0] == '0');
+  // With Freeverb, beyond ~8k channels the fused kernels fill the chip on
+  // their own and win (tools/fx_crossover.py: 16384 ch config 5 fused 22.2
+  // vs staged 11.6 Gsamples/s; 4096 ch staged 9.7 vs fused 8.3).
+  if (h->verb_on && h->channels > 8192) return false;
   return on && h->staged_ok && (!h->comp_on || !h->cp.topology_fb) && h->nsec <= kMaxSecPerPass &&
          (h->nsec > 0 || h->comp_on || h->verb_on);
 }
