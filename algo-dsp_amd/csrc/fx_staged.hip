@@ -77,16 +77,17 @@ __device__ __forceinline__ void eq_section_step(const double (&q)[kSecStride], d
 }
 
 template <bool COMP>
-__global__ __launch_bounds__(64 * (kMaxSecPerPass + 1)) void k_fx_eq(FxStageArgs a, int out_mode) {
+__global__ __launch_bounds__(64 * (kMaxSecPerPass + 2)) void k_fx_eq(FxStageArgs a, int out_mode) {
 #pragma clang fp contract(off)
   __shared__ double ring[kMaxSecPerPass][2][kEqP][64];
+  __shared__ double xring[2][kEqP][64];  // input rows, written by the loader wave one step ahead
   const int w = wave_id();
   const int l = threadIdx.x & 63;
   const int c = blockIdx.x * 64 + l;
   const bool active = c < a.channels;
   const int cc = active ? c : a.channels - 1;
   const int ns = a.eq.nsec;
-  const int W = ns + (COMP ? 1 : 0);
+  const int W = ns + (COMP ? 1 : 0);  // compute waves; wave W is the loader
   const int64_t len = a.len;
   const int64_t nst = (len + kEqP - 1) / kEqP;
   const int64_t steps = nst + W - 1;
@@ -94,24 +95,14 @@ __global__ __launch_bounds__(64 * (kMaxSecPerPass + 1)) void k_fx_eq(FxStageArgs
   const double* xin = a.xT + c;
   double* tmo = (out_mode == kFxOutInT ? a.inT : a.vT) + c;
 
-  // wave 0's input rows, kEqPF steps ahead in rotating register blocks
-  // (a step of a section wave is ~0.3 us; HBM latency under load is a few)
-  double xq[kEqPF][kEqP];
-  if (w == 0) {
-#pragma unroll
-    for (int b = 0; b < kEqPF; ++b)
-#pragma unroll
-      for (int d = 0; d < kEqP; ++d) xq[b][d] = xin[min((int64_t)(b * kEqP + d), len - 1) * cp];
-  }
+  // Wave 0's input comes from xring, filled by the loader wave (wave W):
+  // it loads each step's rows kEqPF steps before it writes them to LDS, in
+  // register buffers named at compile time (its loop is unrolled by kEqPF),
+  // so its waits are on loads issued kEqPF steps earlier, and its own short
+  // body keeps it ahead of the barrier lockstep.
   auto take_input = [&](int64_t my, double (&x)[kEqP]) {
 #pragma unroll
-    for (int d = 0; d < kEqP; ++d) x[d] = xq[0][d];
-#pragma unroll
-    for (int b = 0; b + 1 < kEqPF; ++b)
-#pragma unroll
-      for (int d = 0; d < kEqP; ++d) xq[b][d] = xq[b + 1][d];
-#pragma unroll
-    for (int d = 0; d < kEqP; ++d) xq[kEqPF - 1][d] = xin[min((my + kEqPF) * kEqP + d, len - 1) * cp];
+    for (int d = 0; d < kEqP; ++d) x[d] = xring[(my & 1)][d][l];
   };
   auto emit = [&](int64_t my, const double (&y)[kEqP], int nreal) {
     double* o = tmo + my * kEqP * cp;
@@ -120,7 +111,39 @@ __global__ __launch_bounds__(64 * (kMaxSecPerPass + 1)) void k_fx_eq(FxStageArgs
       if (d < nreal) o[d * cp] = y[d];
   };
 
-  if (w < ns) {
+  if (w == W) {
+    // ---- loader
+    double buf[kEqPF][kEqP];
+    auto fetch = [&](double (&dst)[kEqP], int64_t step) {
+      if (step < nst) {
+#pragma unroll
+        for (int d = 0; d < kEqP; ++d) dst[d] = xin[min(step * kEqP + d, len - 1) * cp];
+      }
+    };
+    auto put = [&](const double (&src)[kEqP], int64_t step) {
+      if (step < nst) {
+#pragma unroll
+        for (int d = 0; d < kEqP; ++d) xring[(step & 1)][d][l] = src[d];
+      }
+    };
+#pragma unroll
+    for (int b = 0; b < kEqPF; ++b) fetch(buf[b], b);
+    put(buf[0], 0);
+    fetch(buf[0], kEqPF);
+    lds_barrier();
+    // at step k: write step k+1 (from buf[(k+1) % PF]), then load step k+1+PF into it
+    for (int64_t k = 0; k < steps; k += kEqPF) {
+#pragma unroll
+      for (int u = 0; u < kEqPF; ++u) {
+        if (k + u < steps) {
+          const int b = (u + 1) % kEqPF;
+          put(buf[b], k + u + 1);
+          fetch(buf[b], k + u + 1 + kEqPF);
+          lds_barrier();
+        }
+      }
+    }
+  } else if (w < ns) {
     // ---- EQ section w (section.go:47-53 with the chain gain as pre-gain)
     const double* sec = a.eq.sec + (int64_t)cc * a.eq.sec_ch_stride + w * kSecStride;
     double q[kSecStride];
@@ -131,6 +154,7 @@ __global__ __launch_bounds__(64 * (kMaxSecPerPass + 1)) void k_fx_eq(FxStageArgs
     const bool to_ring = w < ns - 1 || COMP;
     const bool last = w == ns - 1;
     unsigned long long tc = 0, tb = 0;
+    lds_barrier();  // the loader's prologue (step 0 in xring)
     for (int64_t k = 0; k < steps; ++k) {
       const unsigned long long t0c = a.prof ? clock64() : 0;
       const int64_t my = k - w;
@@ -174,7 +198,10 @@ __global__ __launch_bounds__(64 * (kMaxSecPerPass + 1)) void k_fx_eq(FxStageArgs
     CompChState cs = a.cs[cc];
     double* rring = a.rms_ring + (int64_t)cc * p.rms_n;
     double* eo = a.envT + c;
+    lds_barrier();  // the loader's prologue (step 0 in xring)
+    unsigned long long tc = 0, tb = 0;
     for (int64_t k = 0; k < steps; ++k) {
+      const unsigned long long t0c = a.prof ? clock64() : 0;
       const int64_t my = k - w;
       if (my >= 0 && my < nst) {
         double x[kEqP], e[kEqP];
@@ -222,7 +249,16 @@ __global__ __launch_bounds__(64 * (kMaxSecPerPass + 1)) void k_fx_eq(FxStageArgs
         for (int d = 0; d < kEqP; ++d)
           if (d < nreal) o[d * cp] = e[d];
       }
+      const unsigned long long t1c = a.prof ? clock64() : 0;
       lds_barrier();
+      if (a.prof) {
+        tc += t1c - t0c;
+        tb += clock64() - t1c;
+      }
+    }
+    if (a.prof && l == 0 && blockIdx.x == 0) {
+      a.prof[2 * w] = tc;
+      a.prof[2 * w + 1] = tb;
     }
     if (active) {  // only the fields this stage owns
       CompChState* o = a.cs + c;
@@ -542,7 +578,7 @@ __global__ __launch_bounds__(64 * kApW) void k_fx_allpass(FxStageArgs a) {
 void launch_fx_eq(const FxStageArgs& a, bool comp, int out_mode, hipStream_t s) {
   const int W = a.eq.nsec + (comp ? 1 : 0);
   if (W == 0 || a.len <= 0) return;
-  const dim3 grid((unsigned)((a.channels + 63) / 64)), block((unsigned)(64 * W));
+  const dim3 grid((unsigned)((a.channels + 63) / 64)), block((unsigned)(64 * (W + 1)));  // + the loader
   if (comp)
     hipLaunchKernelGGL(k_fx_eq<true>, grid, block, 0, s, a, out_mode);
   else
