@@ -213,7 +213,20 @@ void stream_convolve(ad_conv* h, const double* in, int64_t n, double* out) {
     h->pin_n = (size_t)n;
   }
   std::memcpy(h->pin_in, in, n * sizeof(double));
-  h->eng->run(h->pin_in_dev, n, n, h->pin_out_dev, n, n, /*use_hist=*/true, s);
+  static const bool staged = [] {  // A/B: AD_STREAM_STAGE=0 lets K1/K3 touch the mapped buffers directly
+    const char* v = std::getenv("AD_STREAM_STAGE");
+    return !(v && v[0] == '0');
+  }();
+  if (staged) {
+    // wide copy kernels move the block over PCIe; K1 and K3 then work on HBM
+    h->din.reserve((size_t)n);
+    h->dout.reserve((size_t)n);
+    launch_copy_f64(h->pin_in_dev, h->din.p, n, s);
+    h->eng->run(h->din.p, n, n, h->dout.p, n, n, /*use_hist=*/true, s);
+    launch_copy_f64(h->dout.p, h->pin_out_dev, n, s);
+  } else {
+    h->eng->run(h->pin_in_dev, n, n, h->pin_out_dev, n, n, /*use_hist=*/true, s);
+  }
   AD_HIP(hipStreamSynchronize(s));
   std::memcpy(out, h->pin_out, n * sizeof(double));
 }

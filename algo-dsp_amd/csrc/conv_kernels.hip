@@ -629,6 +629,16 @@ __global__ __launch_bounds__(256) void k_stream_direct(const double* __restrict_
   y[i] = acc;
 }
 
+// Streaming block staging: host-mapped (zero-copy) <-> device buffer.  One
+// workgroup reading 32 KiB over PCIe is bound by the few requests one CU
+// keeps in flight (K1 alone took 16.5 us per 4096-sample block); a grid of
+// one double per lane spreads the block over many CUs.
+__global__ __launch_bounds__(64) void k_copy_f64(const double* __restrict__ src, double* __restrict__ dst,
+                                                 int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (i < n) dst[i] = src[i];
+}
+
 // Stereo mixdown: mix[0][t] = sum over even channels, mix[1][t] = odd channels.
 __global__ __launch_bounds__(256) void k_mixdown(const double* __restrict__ ch, int channels, int64_t stride,
                                                  int64_t len, double* __restrict__ mix) {
@@ -783,6 +793,11 @@ void launch_direct_circular(const double* a, const double* b, int64_t n, double*
 
 void launch_stream_direct(const double* h, int64_t K, const double* buf, int64_t B, double* y, hipStream_t s) {
   hipLaunchKernelGGL(k_stream_direct, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s, h, K, buf, B, y);
+}
+
+void launch_copy_f64(const double* src, double* dst, int64_t n, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_copy_f64, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, src, dst, n);
 }
 
 void launch_mixdown(const double* ch, int channels, int64_t stride, int64_t len, double* mix, hipStream_t s) {

@@ -82,6 +82,7 @@ struct IrfftArgs {
 bool launch_window_rfft(int M, const RfftArgs& a, hipStream_t s);
 bool launch_irfft_store(int M, const IrfftArgs& a, hipStream_t s);
 bool launch_fdl_mac(int PC, int NH, const MacArgs& a, int channels, hipStream_t s);
+void launch_copy_f64(const double* src, double* dst, int64_t n, hipStream_t s);
 void launch_direct(const double* a, int64_t n, const double* b, int64_t m, double* dst, hipStream_t s);
 void launch_direct_circular(const double* a, const double* b, int64_t n, double* dst, hipStream_t s);
 void launch_stream_direct(const double* h, int64_t K, const double* buf, int64_t B, double* y, hipStream_t s);
