@@ -81,13 +81,17 @@ __global__ __launch_bounds__(64 * (kMaxSecPerPass + 2)) void k_fx_eq(FxStageArgs
 #pragma clang fp contract(off)
   __shared__ double ring[kMaxSecPerPass][2][kEqP][64];
   __shared__ double xring[2][kEqP][64];  // input rows, written by the loader wave one step ahead
-  const int w = wave_id();
+  const int wid = wave_id();
   const int l = threadIdx.x & 63;
   const int c = blockIdx.x * 64 + l;
   const bool active = c < a.channels;
   const int cc = active ? c : a.channels - 1;
   const int ns = a.eq.nsec;
   const int W = ns + (COMP ? 1 : 0);  // compute waves; wave W is the loader
+  // Pipeline role of this wave: sections 0 .. ns-1, detector ns, loader W.
+  // Waves land on SIMD wid % 4; with three or more sections the detector
+  // (the longest recurrence) takes wave 3 so that its SIMD is its own.
+  const int w = (wid == W || !COMP || ns < 3) ? wid : (wid == 3 ? ns : (wid < 3 ? wid : wid - 1));
   const int64_t len = a.len;
   const int64_t nst = (len + kEqP - 1) / kEqP;
   const int64_t steps = nst + W - 1;
@@ -213,6 +217,17 @@ __global__ __launch_bounds__(64 * (kMaxSecPerPass + 2)) void k_fx_eq(FxStageArgs
 #pragma unroll
           for (int d = 0; d < kEqP; ++d) x[d] = ring[ns - 1][(my & 1)][d][l];
         }
+        if (!p.lp_on && !p.hp_on && !p.detector_rms && nreal == kEqP) {
+          // peak detector, no side-chain filters, a full step: the bare recurrence
+#pragma unroll
+          for (int d = 0; d < kEqP; ++d) {
+            const double src = fabs(x[d]);
+            const double ne =
+                src > cs.env ? cs.env + (src - cs.env) * p.attack : src + (cs.env - src) * p.release;
+            cs.env = ne;
+            e[d] = ne;
+          }
+        } else {
 #pragma unroll
         for (int d = 0; d < kEqP; ++d) {
           const bool real = d < nreal;
@@ -244,10 +259,16 @@ __global__ __launch_bounds__(64 * (kMaxSecPerPass + 2)) void k_fx_eq(FxStageArgs
           if (real) cs.env = ne;
           e[d] = ne;
         }
+        }
         double* o = eo + my * kEqP * cp;
+        if (nreal == kEqP) {
 #pragma unroll
-        for (int d = 0; d < kEqP; ++d)
-          if (d < nreal) o[d * cp] = e[d];
+          for (int d = 0; d < kEqP; ++d) o[d * cp] = e[d];
+        } else {
+#pragma unroll
+          for (int d = 0; d < kEqP; ++d)
+            if (d < nreal) o[d * cp] = e[d];
+        }
       }
       const unsigned long long t1c = a.prof ? clock64() : 0;
       lds_barrier();
