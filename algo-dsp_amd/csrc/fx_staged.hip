@@ -41,6 +41,16 @@ constexpr int kCombB = 16; // K_comb samples per load/store batch
 
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 
+// A pointer the compiler can prove wave-uniform (SGPR pair), so that p[lane]
+// becomes a scalar-base + 32-bit VGPR-offset access with no 64-bit VALU add.
+template <class T>
+__device__ __forceinline__ T* uniform_ptr(T* p) {
+  const uint64_t v = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return reinterpret_cast<T*>(((uint64_t)hi << 32) | lo);
+}
+
 // Workgroup barrier for LDS hand-offs only.  __syncthreads() is a release /
 // acquire fence at workgroup scope: it waits for every outstanding global
 // load and store of the wave (vmcnt(0)), i.e. one HBM round trip per
@@ -440,6 +450,7 @@ __global__ __launch_bounds__(64) void k_fx_comb(FxStageArgs a) {
   const bool active = c < a.channels;
   const int cc = active ? c : a.channels - 1;
   const int clen = kCombLen[i];
+  const unsigned uc = (unsigned)c;  // zero-extended lane offset: lets loads use scalar base + 32-bit VGPR offset
   const int cp = a.cpad;
   // Row pointers are wave-uniform (scalar registers); a lane adds only its
   // channel c, so every access is a saddr + lane-offset load or store.  All
@@ -454,17 +465,34 @@ __global__ __launch_bounds__(64) void k_fx_comb(FxStageArgs a) {
   double fs = a.vs[cc].filter_store[i];
   const int64_t len = a.len;
   // three batches in flight: batch m sits in buffer m % 3 and is loaded two
-  // batches before it runs (~100 samples of lead at ~80 cycles/sample)
+  // batches before it runs (~100 samples of lead at ~80 cycles/sample).
+  // A batch whose line positions do not wrap and whose samples are all real
+  // (all but ~1.5 % at kCombB = 16, clen >= 1116) walks uniform row pointers
+  // by one row per sample: no per-sample wrap test, clamp or multiply.
   double dl[3][kCombB], xg[3][kCombB];
   int lpos = idx;     // line position of the next batch to load
   int64_t lt = 0;     // its first sample
   auto load = [&](int b) {
     int pos = lpos;
+    if (pos + kCombB <= clen && lt + kCombB <= len) {
+      const double* lr = uniform_ptr(line + (int64_t)pos * cp);
+      const double* ir = uniform_ptr(in + lt * cp);
 #pragma unroll
-    for (int j = 0; j < kCombB; ++j) {
-      dl[b][j] = (line + (int64_t)pos * cp)[c];
-      xg[b][j] = (in + min(lt + j, len - 1) * cp)[c];
-      if (++pos >= clen) pos = 0;
+      for (int j = 0; j < kCombB; ++j) {
+        dl[b][j] = lr[uc];
+        xg[b][j] = ir[uc];
+        lr += cp;
+        ir += cp;
+      }
+      pos += kCombB;
+      if (pos >= clen) pos -= clen;
+    } else {
+#pragma unroll
+      for (int j = 0; j < kCombB; ++j) {
+        dl[b][j] = (line + (int64_t)pos * cp)[uc];
+        xg[b][j] = (in + min(lt + j, len - 1) * cp)[uc];
+        if (++pos >= clen) pos = 0;
+      }
     }
     lpos = pos;
     lt += kCombB;
@@ -472,18 +500,31 @@ __global__ __launch_bounds__(64) void k_fx_comb(FxStageArgs a) {
   auto run = [&](int b, int64_t t0) {
     const int nb = (int)min((int64_t)kCombB, len - t0);
     double nv[kCombB];
-    if (nb == kCombB)
+    if (nb == kCombB && idx + kCombB <= clen) {
       comb_batch<true>(p, fs, dl[b], xg[b], nv, nb);
-    else
-      comb_batch<false>(p, fs, dl[b], xg[b], nv, nb);
-    int pos = idx;
+      double* cr = uniform_ptr(co + t0 * cp);
+      double* lr = uniform_ptr(line + (int64_t)idx * cp);
 #pragma unroll
-    for (int j = 0; j < kCombB; ++j) {
-      if (j < nb) {
-        (co + (t0 + j) * cp)[c] = dl[b][j];
-        (line + (int64_t)pos * cp)[c] = nv[j];
+      for (int j = 0; j < kCombB; ++j) {
+        cr[uc] = dl[b][j];
+        lr[uc] = nv[j];
+        cr += cp;
+        lr += cp;
       }
-      if (++pos >= clen) pos = 0;
+    } else {
+      if (nb == kCombB)
+        comb_batch<true>(p, fs, dl[b], xg[b], nv, nb);
+      else
+        comb_batch<false>(p, fs, dl[b], xg[b], nv, nb);
+      int pos = idx;
+#pragma unroll
+      for (int j = 0; j < kCombB; ++j) {
+        if (j < nb) {
+          (co + (t0 + j) * cp)[uc] = dl[b][j];
+          (line + (int64_t)pos * cp)[uc] = nv[j];
+        }
+        if (++pos >= clen) pos = 0;
+      }
     }
     idx += nb;
     if (idx >= clen) idx -= clen;
@@ -501,8 +542,8 @@ __global__ __launch_bounds__(64) void k_fx_comb(FxStageArgs a) {
     run(2, t0 + 2 * kCombB);
   }
   if (active) {
-    a.vs[c].comb_idx[i] = idx;
-    a.vs[c].filter_store[i] = fs;
+    a.vs[uc].comb_idx[i] = idx;
+    a.vs[uc].filter_store[i] = fs;
   }
 }
 
