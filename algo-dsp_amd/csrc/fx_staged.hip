@@ -106,8 +106,9 @@ __global__ __launch_bounds__(64 * (kMaxSecPerPass + 2)) void k_fx_eq(FxStageArgs
   const int64_t nst = (len + kEqP - 1) / kEqP;
   const int64_t steps = nst + W - 1;
   const int cp = a.cpad;
-  const double* xin = a.xT + c;
-  double* tmo = (out_mode == kFxOutInT ? a.inT : a.vT) + c;
+  const unsigned uc = (unsigned)c;
+  const double* xin = a.xT;  // uniform row pointers; a lane indexes [uc]
+  double* tmo = out_mode == kFxOutInT ? a.inT : a.vT;
 
   // Wave 0's input comes from xring, filled by the loader wave (wave W):
   // it loads each step's rows kEqPF steps before it writes them to LDS, in
@@ -118,20 +119,37 @@ __global__ __launch_bounds__(64 * (kMaxSecPerPass + 2)) void k_fx_eq(FxStageArgs
 #pragma unroll
     for (int d = 0; d < kEqP; ++d) x[d] = xring[(my & 1)][d][l];
   };
-  auto emit = [&](int64_t my, const double (&y)[kEqP], int nreal) {
-    double* o = tmo + my * kEqP * cp;
+  // time-major rows of step `my`: full steps walk a uniform row pointer
+  auto put_rows = [&](double* base, int64_t my, const double (&y)[kEqP], int nreal) {
+    double* o = uniform_ptr(base + my * kEqP * cp);
+    if (nreal == kEqP) {
 #pragma unroll
-    for (int d = 0; d < kEqP; ++d)
-      if (d < nreal) o[d * cp] = y[d];
+      for (int d = 0; d < kEqP; ++d) {
+        o[uc] = y[d];
+        o += cp;
+      }
+    } else {
+#pragma unroll
+      for (int d = 0; d < kEqP; ++d)
+        if (d < nreal) o[(int64_t)d * cp + uc] = y[d];
+    }
   };
+  auto emit = [&](int64_t my, const double (&y)[kEqP], int nreal) { put_rows(tmo, my, y, nreal); };
 
   if (w == W) {
     // ---- loader
     double buf[kEqPF][kEqP];
     auto fetch = [&](double (&dst)[kEqP], int64_t step) {
-      if (step < nst) {
+      if ((step + 1) * kEqP <= len) {
+        const double* r = uniform_ptr(xin + step * kEqP * cp);
 #pragma unroll
-        for (int d = 0; d < kEqP; ++d) dst[d] = xin[min(step * kEqP + d, len - 1) * cp];
+        for (int d = 0; d < kEqP; ++d) {
+          dst[d] = r[uc];
+          r += cp;
+        }
+      } else if (step < nst) {
+#pragma unroll
+        for (int d = 0; d < kEqP; ++d) dst[d] = xin[min(step * kEqP + d, len - 1) * cp + uc];
       }
     };
     auto put = [&](const double (&src)[kEqP], int64_t step) {
@@ -211,7 +229,7 @@ __global__ __launch_bounds__(64 * (kMaxSecPerPass + 2)) void k_fx_eq(FxStageArgs
     const CompParams& p = a.cp;
     CompChState cs = a.cs[cc];
     double* rring = a.rms_ring + (int64_t)cc * p.rms_n;
-    double* eo = a.envT + c;
+    double* eo = a.envT;
     lds_barrier();  // the loader's prologue (step 0 in xring)
     unsigned long long tc = 0, tb = 0;
     for (int64_t k = 0; k < steps; ++k) {
@@ -270,15 +288,7 @@ __global__ __launch_bounds__(64 * (kMaxSecPerPass + 2)) void k_fx_eq(FxStageArgs
           e[d] = ne;
         }
         }
-        double* o = eo + my * kEqP * cp;
-        if (nreal == kEqP) {
-#pragma unroll
-          for (int d = 0; d < kEqP; ++d) o[d * cp] = e[d];
-        } else {
-#pragma unroll
-          for (int d = 0; d < kEqP; ++d)
-            if (d < nreal) o[d * cp] = e[d];
-        }
+        put_rows(eo, my, e, nreal);
       }
       const unsigned long long t1c = a.prof ? clock64() : 0;
       lds_barrier();
