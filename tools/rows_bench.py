@@ -184,7 +184,7 @@ def main():
             fx = processors.EffectChain(chn, sample_rate=fs, **kw)
             ms = dev_time(lambda s: fx.process_device(xb.data_ptr(), n, n, s), reps=3, warm=1)
             cs = cpu_time(cfn, budget_s=1.0) if chn == 256 else None
-            rows.append(row(name, ref, f"{chn} ch x {n} samples (fused per-sample kernel)", chn * n, "samples",
+            rows.append(row(name, ref, f"{chn} ch x {n} samples (effect-chain engine)", chn * n, "samples",
                             ms, cs, nc, f"{cdesc}, 1 x {nc} samples", "hbm", 16.0 * chn * n,
                             "serial per-channel recurrence: bound by dependent-op latency x channels in flight, "
                             "not by HBM; 16 B/sample is the in+out stream"))
