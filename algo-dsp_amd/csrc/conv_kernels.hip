@@ -371,7 +371,9 @@ struct XRing {
     const double2* p = Xc + (int64_t)row * MS;
     unsigned keep;
     asm volatile(
-        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+        // nt: the X rows are streamed once per run (K2 250 -> 230 us at the
+        // bench config; K3 after it +12 us, the whole step unchanged to +2 %)
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
         : "=&s"(keep)
         : "v"(p), "s"(lds)
         : "memory");
