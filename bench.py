@@ -140,6 +140,7 @@ def main():
                                      chunk_blocks=args.chunk, device=local)
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
+    side = torch.cuda.Stream(dev)  # mixdown + reduce
     blocks = -(-out_len // args.hop)
     cuts = [min(out_len, args.hop * (blocks * i // args.segments)) for i in range(args.segments + 1)]
     segs = [(b, e) for b, e in zip(cuts[:-1], cuts[1:]) if e > b]
@@ -159,13 +160,21 @@ def main():
             else:
                 eng.process_device_segment(x.data_ptr(), n, n, yb.data_ptr(), out_len, out_len, b, e, sptr)
             if mixdown:
-                if C != 2:  # stereo partial mix of this rank's channel group (even -> L, odd -> R)
-                    conv.mixdown_device(yb.data_ptr() + 8 * b, C, out_len, e - b, mb.data_ptr() + 16 * b, sptr)
-                    parts = [mb.view(-1)[2 * b:2 * e]]
-                else:
-                    parts = [mb[0, b:e], mb[1, b:e]]
-                for t in parts:
-                    pending[i].append(shard.reduce_mix(t, dist, async_op=True))
+                # the mixdown kernel and the reduce run on a side stream, after
+                # this segment's convolution: the next step's convolution (into
+                # the other output buffer) overlaps them
+                done = torch.cuda.Event()
+                done.record(stream)
+                with torch.cuda.stream(side):
+                    side.wait_event(done)
+                    if C != 2:  # stereo partial mix of this rank's channel group (even -> L, odd -> R)
+                        conv.mixdown_device(yb.data_ptr() + 8 * b, C, out_len, e - b, mb.data_ptr() + 16 * b,
+                                            side.cuda_stream)
+                        parts = [mb.view(-1)[2 * b:2 * e]]
+                    else:
+                        parts = [mb[0, b:e], mb[1, b:e]]
+                    for t in parts:
+                        pending[i].append(shard.reduce_mix(t, dist, async_op=True))
 
     def drain():
         for i in range(nbuf):

@@ -1,7 +1,6 @@
 set -u
-cp algo-dsp_amd/libalgodsp_hip.so /tmp/base.so
-for v in base nt nt2 base nt nt2; do
-  case $v in nt) cp algo-dsp_amd/libalgodsp_hip_nt.so algo-dsp_amd/libalgodsp_hip.so;; nt2) cp algo-dsp_amd/libalgodsp_hip_nt2.so algo-dsp_amd/libalgodsp_hip.so;; *) cp /tmp/base.so algo-dsp_amd/libalgodsp_hip.so;; esac
-  echo "$v $(timeout -k 10 200 python bench.py --steps 8 --warmup 2 --no-cpu-baseline 2>/dev/null | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], {k:round(v["avg_us"],1) for k,v in d["kernels"].items()})')"
-done
-cp /tmp/base.so algo-dsp_amd/libalgodsp_hip.so
+B="--steps 8 --warmup 2 --no-cpu-baseline"
+timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29511 bench.py $B --channels 8 --samples 4194304 --mixdown on > gpurun_out/b3.log 2>&1 || { tail gpurun_out/b3.log; exit 1; }
+grep -o '"value": [0-9.]*\|"ms_per_step": [0-9.]*' gpurun_out/b3.log | tr '\n' ' '; echo
+timeout -k 10 300 python bench.py $B --channels 8 --samples 4194304 > gpurun_out/b2.log 2>&1 || { tail gpurun_out/b2.log; exit 1; }
+grep -o '"value": [0-9.]*\|"ms_per_step": [0-9.]*' gpurun_out/b2.log | tr '\n' ' '; echo
