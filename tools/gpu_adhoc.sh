@@ -1,6 +1,5 @@
 set -u
-B="--steps 8 --warmup 2 --no-cpu-baseline"
-timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29511 bench.py $B --channels 8 --samples 4194304 --mixdown on > gpurun_out/b3.log 2>&1 || { tail gpurun_out/b3.log; exit 1; }
-grep -o '"value": [0-9.]*\|"ms_per_step": [0-9.]*' gpurun_out/b3.log | tr '\n' ' '; echo
-timeout -k 10 300 python bench.py $B --channels 8 --samples 4194304 > gpurun_out/b2.log 2>&1 || { tail gpurun_out/b2.log; exit 1; }
-grep -o '"value": [0-9.]*\|"ms_per_step": [0-9.]*' gpurun_out/b2.log | tr '\n' ' '; echo
+AD_K3_PERSIST=1 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_conv_gpu.py -p no:cacheprovider 2>&1 | tail -2
+for v in 0 1 0 1; do
+  echo "persist=$v $(AD_K3_PERSIST=$v timeout -k 10 200 python bench.py --steps 8 --warmup 2 --no-cpu-baseline 2>/dev/null | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], {k:round(v["avg_us"],1) for k,v in d["kernels"].items()})')"
+done
