@@ -178,6 +178,7 @@ def _declare(L: C.CDLL) -> None:
         "ad_fx_chain_create": (C.c_int, [C.c_int, C.c_int, C.POINTER(vp)]),
         "ad_fx_chain_set_eq": (C.c_int, [vp, c_double_p, C.c_int, C.c_int]),
         "ad_fx_chain_set_compressor": (C.c_int, [vp, C.POINTER(CompressorConfig)]),
+        "ad_fx_chain_set_expander": (C.c_int, [vp, C.POINTER(CompressorConfig), C.c_int, C.c_double, C.c_double]),
         "ad_fx_chain_set_freeverb": (C.c_int, [vp, C.c_double, C.c_double, C.c_double, C.c_double, C.c_double]),
         "ad_fx_chain_disable_freeverb": (C.c_int, [vp]),
         "ad_fx_chain_reset": (C.c_int, [vp]),

@@ -13,7 +13,8 @@ its runtime's Configure does (runtime_dynamics.go, runtime_filter_pitch_reverb.g
 chain_process.go:177-227 for split-freq).  The compiled node list goes to
 ad_fx_graph_create (include/algodsp.h), which runs every node on the GPU;
 there is no CPU path.  Node types outside {filter*, dyn-compressor,
-dyn-limiter, reverb-freeverb, split-freq, split, sum, _input, _output} raise
+dyn-limiter, dyn-gate, dyn-expander, reverb-freeverb, split-freq, split, sum,
+_input, _output} raise
 UnknownEffect (the GPU runtime's ErrUnknownEffect).
 """
 from __future__ import annotations
@@ -52,7 +53,8 @@ class _Node(C.Structure):
                 ("parents", C.POINTER(C.c_int32)), ("parent_ports", C.POINTER(C.c_int32)),
                 ("sections", C.POINTER(C.c_double)), ("nsec", C.c_int),
                 ("sections2", C.POINTER(C.c_double)), ("nsec2", C.c_int),
-                ("comp", C.POINTER(CompressorConfig)), ("verb", C.c_double * 5)]
+                ("comp", C.POINTER(CompressorConfig)), ("verb", C.c_double * 5),
+                ("dyn_mode", C.c_int), ("dyn_range_db", C.c_double), ("dyn_hold_ms", C.c_double)]
 
 
 def clamp(v, lo, hi):  # core.Clamp
@@ -159,6 +161,38 @@ def limiter_config(p: Params, fs: float) -> CompressorConfig:
     c.threshold_db = clamp(p.GetNum("thresholdDB", -0.1), -24, 0)
     c.release_ms = clamp(p.GetNum("releaseMs", 100), 1, 5000)
     return c
+
+
+def gate_config(p: Params, fs: float):
+    """gateRuntime.Configure (runtime_dynamics.go:130-170) on NewGate defaults:
+    (config, range dB, hold ms).  Topology and detector stay NewGate's
+    (feed-forward, peak)."""
+    c = CompressorConfig()
+    lib().ad_compressor_default_config(C.byref(c), float(fs))
+    c.threshold_db = clamp(p.GetNum("thresholdDB", -40), -80, 0)
+    c.ratio = clamp(p.GetNum("ratio", 10), 1, 100)
+    c.knee_db = clamp(p.GetNum("kneeDB", 6), 0, 24)
+    c.attack_ms = clamp(p.GetNum("attackMs", 0.1), 0.1, 1000)
+    c.release_ms = clamp(p.GetNum("releaseMs", 100), 1, 5000)
+    c.auto_makeup, c.makeup_db, c.feedback_ratio_scale = 0, 0.0, 0
+    return c, clamp(p.GetNum("rangeDB", -80), -120, 0), clamp(p.GetNum("holdMs", 50), 0, 5000)
+
+
+def expander_config(p: Params, fs: float):
+    """expanderRuntime.Configure (runtime_dynamics.go:180-235) on NewExpander
+    defaults: (config, range dB, hold ms = 0)."""
+    c = CompressorConfig()
+    lib().ad_compressor_default_config(C.byref(c), float(fs))
+    c.threshold_db = clamp(p.GetNum("thresholdDB", -35), -80, 0)
+    c.ratio = clamp(p.GetNum("ratio", 2), 1, 100)
+    c.knee_db = clamp(p.GetNum("kneeDB", 6), 0, 24)
+    c.attack_ms = clamp(p.GetNum("attackMs", 1), 0.1, 1000)
+    c.release_ms = clamp(p.GetNum("releaseMs", 100), 1, 5000)
+    c.topology = 1 if p.Str.get("topology", "") == "feedback" else 0  # normalize.go:185-194
+    c.detector_mode = 1 if p.Str.get("detector", "") == "rms" else 0  # normalize.go:196-205
+    c.rms_window_ms = clamp(p.GetNum("rmsWindowMs", 30), 1, 1000)
+    c.auto_makeup, c.makeup_db, c.feedback_ratio_scale = 0, 0.0, 0
+    return c, clamp(p.GetNum("rangeDB", -60), -120, 0), 0.0
 
 
 def freeverb_params(p: Params):
@@ -303,6 +337,15 @@ class Chain:
                 keep.append(cfg)
                 d.comp = C.pointer(cfg)
                 sd.update(type="comp", comp={f: getattr(cfg, f) for f, _ in cfg._fields_})
+            elif t in ("dyn-gate", "dyn-expander"):
+                d.type = FXN_COMPRESSOR
+                gate = t == "dyn-gate"
+                cfg, rng, hold = gate_config(p, fs) if gate else expander_config(p, fs)
+                keep.append(cfg)
+                d.comp = C.pointer(cfg)
+                d.dyn_mode, d.dyn_range_db, d.dyn_hold_ms = (2 if gate else 1), rng, hold
+                sd.update(type="comp", comp={f: getattr(cfg, f) for f, _ in cfg._fields_},
+                          expander=dict(gate=gate, range_db=rng, hold_ms=hold))
             elif t == "reverb-freeverb":
                 d.type = FXN_FREEVERB
                 for j, v in enumerate(freeverb_params(p)):

@@ -168,6 +168,45 @@ class Compressor(_FxChain):
         return ip.value, op.value, gr.value
 
 
+class Expander(Compressor):
+    """dynamics.Expander (expander.go) on `channels` lanes: the compressor's
+    detector core with the downward-expansion gain and a range floor.
+    Defaults of NewExpander (expander.go:9-15)."""
+
+    GATE = False
+
+    def __init__(self, sample_rate: float = 48000.0, channels: int = 1, device: int = DEVICE, **cfg):
+        _FxChain.__init__(self, channels, device)
+        self.cfg = CompressorConfig()
+        lib().ad_compressor_default_config(C.byref(self.cfg), float(sample_rate))
+        defaults = dict(threshold_db=-40.0, ratio=10.0, knee_db=6.0, attack_ms=0.1, release_ms=100.0) \
+            if self.GATE else dict(threshold_db=-35.0, ratio=2.0, knee_db=6.0, attack_ms=1.0, release_ms=100.0)
+        self.range_db = cfg.pop("range_db", -80.0 if self.GATE else -60.0)
+        self.hold_ms = cfg.pop("hold_ms", 50.0 if self.GATE else 0.0)
+        for k, v in {**defaults, **cfg}.items():
+            setattr(self.cfg, k, v)
+        self._apply()
+
+    def _apply(self):
+        check(lib().ad_fx_chain_set_expander(self._h, C.byref(self.cfg), int(self.GATE), float(self.range_db),
+                                             float(self.hold_ms)))
+
+    def SetRange(self, db):  # expander.go / gate.go SetRange
+        self.range_db = db
+        self._apply()
+
+
+class Gate(Expander):
+    """dynamics.Gate (gate.go): Expander gain plus a hold counter; defaults of
+    NewGate (gate.go:9-17)."""
+
+    GATE = True
+
+    def SetHold(self, ms):  # gate.go:196-223
+        self.hold_ms = ms
+        self._apply()
+
+
 class Reverb(_FxChain):
     """reverb.Reverb (Freeverb, reverb.go:33-235) with NewReverb defaults."""
 

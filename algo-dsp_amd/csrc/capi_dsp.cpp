@@ -165,6 +165,7 @@ bool fx_staged_ok(const ad_fx_chain* h) {
   // their own and win (tools/fx_crossover.py: 16384 ch config 5 fused 22.2
   // vs staged 11.6 Gsamples/s; 4096 ch staged 9.7 vs fused 8.3).
   if (h->verb_on && h->channels > 8192) return false;
+  if (h->comp_on && h->cp.mode == 2) return false;  // the gate's hold counter is serial in its gain
   return on && h->staged_ok && (!h->comp_on || !h->cp.topology_fb) && h->nsec <= kMaxSecPerPass &&
          (h->nsec > 0 || h->comp_on || h->verb_on);
 }
@@ -419,6 +420,44 @@ int ad_fx_chain_set_compressor(ad_fx_chain* h, const ad_compressor_config* cfg) 
     }
     check_comp_config(*cfg);
     const CompParams p = comp_params(*cfg);
+    const bool fresh = !h->comp_on || p.rms_n != h->cp.rms_n;
+    h->cp = p;
+    h->comp_on = true;
+    if (fresh) {
+      h->cs.alloc((size_t)h->channels);
+      h->ring.alloc((size_t)h->channels * p.rms_n);
+      fx_reset_comp(h);
+      fx_quiesce(h);
+    }
+  });
+}
+
+int ad_fx_chain_set_expander(ad_fx_chain* h, const ad_compressor_config* cfg, int gate, double range_db,
+                             double hold_ms) {
+  // NewExpander / NewGate (expander.go:70-108, gate.go:82-126) and their setters' ranges
+  return fx_guard(h, [&] {
+    fx_quiesce(h);
+    if (!cfg) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "nil expander config");
+    ad_compressor_config g = *cfg;
+    check_comp_config(g);
+    if (!(g.ratio >= 1.0 && g.ratio <= 100.0)) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "dynamics: ratio must be in [1, 100]");
+    if (!(g.knee_db >= 0.0 && g.knee_db <= 24.0)) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "dynamics: knee must be in [0, 24] dB");
+    if (!(g.attack_ms >= 0.1 && g.attack_ms <= 1000.0))
+      AD_FAIL(AD_ERR_INVALID_ARGUMENT, "dynamics: attack must be in [0.1, 1000] ms");
+    if (!(g.release_ms >= 1.0 && g.release_ms <= 5000.0))
+      AD_FAIL(AD_ERR_INVALID_ARGUMENT, "dynamics: release must be in [1, 5000] ms");
+    if (!(range_db >= -120.0 && range_db <= 0.0)) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "dynamics: range must be in [-120, 0] dB");
+    if (gate && !(hold_ms >= 0.0 && hold_ms <= 5000.0))
+      AD_FAIL(AD_ERR_INVALID_ARGUMENT, "dynamics: hold must be in [0, 5000] ms");
+    // the expander/gate core: no makeup, feedback time constants not ratio-scaled
+    g.auto_makeup = 0;
+    g.makeup_db = 0.0;
+    g.feedback_ratio_scale = 0;
+    CompParams p = comp_params(g);
+    p.mode = gate ? 2 : 1;
+    p.ratio_m1 = g.ratio - 1.0;
+    p.range_lin = std::pow(10.0, range_db / 20.0);
+    p.hold_n = gate ? (int)(hold_ms * 0.001 * g.sample_rate) : 0;
     const bool fresh = !h->comp_on || p.rms_n != h->cp.rms_n;
     h->cp = p;
     h->comp_on = true;

@@ -65,11 +65,11 @@ struct FxOp {
 // Stage group under construction for the fusion pass.
 struct Group {
   std::vector<double> sections;  // [nsec][6]
-  const ad_compressor_config* comp = nullptr;
+  const ad_fx_node* dyn = nullptr;  // the dynamics node (compressor / limiter / expander / gate)
   const double* verb = nullptr;
   bool open = false;
   int buf = -1;
-  int level() const { return verb ? 3 : (comp ? 2 : (sections.empty() ? 0 : 1)); }
+  int level() const { return verb ? 3 : (dyn ? 2 : (sections.empty() ? 0 : 1)); }
 };
 
 }  // namespace
@@ -120,7 +120,13 @@ void flush(ad_fx_graph* g, Group& gr) {
   if (gr.level() > 0) {
     ad_fx_chain* c = new_chain(g);
     if (!gr.sections.empty()) ck(ad_fx_chain_set_eq(c, gr.sections.data(), (int)(gr.sections.size() / kSecStride), 0));
-    if (gr.comp) ck(ad_fx_chain_set_compressor(c, gr.comp));
+    if (gr.dyn) {
+      if (gr.dyn->dyn_mode == 0)
+        ck(ad_fx_chain_set_compressor(c, gr.dyn->comp));
+      else
+        ck(ad_fx_chain_set_expander(c, gr.dyn->comp, gr.dyn->dyn_mode == 2, gr.dyn->dyn_range_db,
+                                    gr.dyn->dyn_hold_ms));
+    }
     if (gr.verb) ck(ad_fx_chain_set_freeverb(c, gr.verb[0], gr.verb[1], gr.verb[2], gr.verb[3], gr.verb[4]));
     FxOp op{FxOp::CHAIN};
     op.dst = gr.buf;
@@ -159,6 +165,8 @@ void compile(ad_fx_graph* g, const ad_fx_node* nodes, int n) {
     if (d.type == AD_FXN_SPLIT_FREQ && (d.nsec <= 0 || !d.sections || d.nsec2 <= 0 || !d.sections2))
       AD_FAIL(AD_ERR_INVALID_ARGUMENT, "fx graph: split-freq node needs LP and HP sections");
     if (d.type == AD_FXN_COMPRESSOR && !d.comp) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "fx graph: compressor without config");
+    if (d.type == AD_FXN_COMPRESSOR && (d.dyn_mode < 0 || d.dyn_mode > 2))
+      AD_FAIL(AD_ERR_INVALID_ARGUMENT, "fx graph: bad dynamics mode");
   }
   if (out_node < 0) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "fx graph: no output node");
 
@@ -214,7 +222,7 @@ void compile(ad_fx_graph* g, const ad_fx_node* nodes, int n) {
     if (lvl == 1) {
       gr.sections.insert(gr.sections.end(), d.sections, d.sections + (size_t)d.nsec * kSecStride);
     } else if (lvl == 2) {
-      gr.comp = d.comp;
+      gr.dyn = &d;
     } else {
       gr.verb = d.verb;
     }

@@ -17,10 +17,34 @@ __device__ __forceinline__ double go_log2(double x) {
   return log(frac) * 1.4426950408889634074 + (double)e;
 }
 
+// calculateDownwardExpansionGain (expander.go:358-411), Expander and Gate.
+__device__ __forceinline__ double expansion_gain(const CompParams& p, double level) {
+#pragma clang fp contract(off)
+  if (level <= 0.0) return p.range_lin;
+  const double undershoot = p.threshold_log2 - go_log2(level);
+  double eff;
+  if (!p.knee_on) {
+    if (undershoot <= 0.0) return 1.0;
+    eff = undershoot;
+  } else {
+    if (undershoot < -p.half_knee) return 1.0;
+    if (undershoot > p.half_knee) {
+      eff = undershoot;
+    } else {
+      const double s = undershoot + p.half_knee;
+      eff = s * s * 0.5 * p.inv_knee_width_log2;
+    }
+  }
+  const double g = exp2(-eff * p.ratio_m1);
+  return g < p.range_lin ? p.range_lin : g;
+}
+
 // dynamicsCore.GainForLevel (core.go:288-329).  2^y via exp2 (Go:
-// math.Pow(2, y); both within an ulp).
+// math.Pow(2, y); both within an ulp).  Expander/Gate modes dispatch to
+// the downward-expansion gain.
 __device__ __forceinline__ double gain_for_level(const CompParams& p, double level) {
 #pragma clang fp contract(off)
+  if (p.mode) return expansion_gain(p, level);
   if (level <= 0.0) return 1.0;
   const double overshoot = go_log2(level) - p.threshold_log2;
   if (!p.knee_on) {

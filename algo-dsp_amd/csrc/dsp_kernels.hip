@@ -150,11 +150,19 @@ __global__ __launch_bounds__(64) void k_chain(ChainArgs a) {
           cs.env += (src - cs.env) * p.attack;
         else
           cs.env = src + (cs.env - src) * p.release;
-        const double g = gain_for_level(p, cs.env);
-        const double out = v * g * p.makeup_lin;
+        double g = gain_for_level(p, cs.env);
+        if (p.mode == 2) {  // gate hold (gate.go:361-366)
+          if (g >= 1.0) {
+            cs.hold = p.hold_n;
+          } else if (cs.hold > 0) {
+            cs.hold--;
+            g = 1.0;
+          }
+        }
+        const double out = v * g * p.makeup_lin;  // makeup_lin = 1 for the expander and gate
         if (p.topology_fb) {
           cs.prev_gain = g > 1e-9 ? g : 1e-9;
-          cs.prev_abs = fabs(out);
+          if (!p.mode) cs.prev_abs = fabs(out);  // the expander and gate keep only previousGain
         }
         const double il = fabs(v), ol = fabs(out);  // updateMetrics compressor.go:411-423
         if (il > cs.in_peak) cs.in_peak = il;
@@ -375,7 +383,15 @@ __global__ __launch_bounds__(320) void k_chain_pipe(ChainArgs a) {
 #pragma unroll 4
         for (int d = 0; d < kPipeD; ++d) {
           const double v = ring_v[r][d][l];
-          const double g = gain_for_level(p, ring_env[r][d][l]);
+          double g = gain_for_level(p, ring_env[r][d][l]);
+          if (p.mode == 2 && t0 + d < a.n) {  // gate hold (gate.go:361-366)
+            if (g >= 1.0) {
+              cs.hold = p.hold_n;
+            } else if (cs.hold > 0) {
+              cs.hold--;
+              g = 1.0;
+            }
+          }
           const double out = v * g * p.makeup_lin;
           if (t0 + d < a.n) {
             const double il = fabs(v), ol = fabs(out);
@@ -389,6 +405,7 @@ __global__ __launch_bounds__(320) void k_chain_pipe(ChainArgs a) {
       PIPE_SYNC();
     }
     if (active) {
+      a.cs[c].hold = cs.hold;
       a.cs[c].in_peak = cs.in_peak;
       a.cs[c].out_peak = cs.out_peak;
       a.cs[c].gr = cs.gr;

@@ -32,11 +32,19 @@ struct CompParams {
   double attack, release;  // already the feedback pair when that topology is scaled
   double lp_alpha, hp_alpha;
   int knee_on, topology_fb, detector_rms, lp_on, hp_on, rms_n;
+  // dynamics.Expander / dynamics.Gate (expander.go, gate.go): mode 1 / 2 use
+  // the downward-expansion gain (ratio_m1 = ratio - 1, floor range_lin), no
+  // makeup (makeup_lin = 1), and the gate holds the gain at 1 for hold_n
+  // samples after it was last >= 1.  mode 0 is the compressor.
+  int mode;
+  double ratio_m1, range_lin;
+  int hold_n;
 };
 
 struct CompChState {
   double env, lp, hp, rms_sum, prev_abs, prev_gain, in_peak, out_peak, gr;
   int rms_index, rms_filled;
+  int hold;  // gate hold counter
 };
 
 // reverb.Reverb (Freeverb) parameters and per-channel state.

@@ -208,6 +208,14 @@ void ad_compressor_default_config(ad_compressor_config* cfg, double sample_rate)
 int ad_fx_chain_create(int channels, int device, ad_fx_chain** out);
 int ad_fx_chain_set_eq(ad_fx_chain* h, const double* sections, int nsec, int per_channel);
 int ad_fx_chain_set_compressor(ad_fx_chain* h, const ad_compressor_config* cfg); /* NULL: stage off */
+/* dynamics.Expander / dynamics.Gate (expander.go, gate.go) as the chain's
+ * dynamics stage instead of the compressor: cfg gives threshold, ratio, knee,
+ * attack, release, detector, topology, RMS window and side-chain filters
+ * (makeup fields ignored: these have none); range_db is SetRange, hold_ms is
+ * the gate's SetHold (gate != 0).  Out-of-range values -> AD_ERR_INVALID_ARGUMENT
+ * (the setters' validation). */
+int ad_fx_chain_set_expander(ad_fx_chain* h, const ad_compressor_config* cfg, int gate, double range_db,
+                             double hold_ms);
 int ad_fx_chain_set_freeverb(ad_fx_chain* h, double wet, double dry, double room_size, double damp, double gain);
 int ad_fx_chain_disable_freeverb(ad_fx_chain* h);
 int ad_fx_chain_reset(ad_fx_chain* h); /* Chain/Compressor/Reverb Reset() */
@@ -265,6 +273,9 @@ typedef struct ad_fx_node {
   int nsec2;
   const ad_compressor_config* comp; /* COMPRESSOR */
   double verb[5];                   /* FREEVERB: wet, dry, room_size, damp, gain */
+  int dyn_mode;                     /* COMPRESSOR: 0 compressor / limiter, 1 expander (dyn-expander),
+                                       2 gate (dyn-gate); see ad_fx_chain_set_expander */
+  double dyn_range_db, dyn_hold_ms; /* expander / gate: SetRange, the gate's SetHold */
 } ad_fx_node;
 typedef struct ad_fx_graph ad_fx_graph;
 int ad_fx_graph_create(const ad_fx_node* nodes, int n_nodes, int channels, int device, ad_fx_graph** out);

@@ -56,6 +56,10 @@ struct or_comp {
   int hp_enabled;    /* sidechain low-cut = x - lp(x) */
   onepole hp_lp;
   double m_in_peak, m_out_peak, m_gr;
+  int mode;              /* 0 compressor, 1 expander, 2 gate */
+  double range_lin;      /* expander/gate floor (mathPower10(rangeDB/20)) */
+  int64_t hold_samples;  /* gate: int(holdMs * 0.001 * fs) */
+  int64_t hold_counter;
 };
 
 void or_comp_default_cfg(or_comp_cfg* c, double fs) { /* NewCompressor compressor.go:77-127 */
@@ -124,6 +128,7 @@ void or_comp_reset(or_comp* c) { /* core.go:572-586 + Compressor.Reset */
   c->m_in_peak = 0;
   c->m_out_peak = 0;
   c->m_gr = 1.0;
+  c->hold_counter = 0;
 }
 
 or_comp* or_comp_new(const or_comp_cfg* cfg) {
@@ -155,6 +160,49 @@ static double gain_for_level(const or_comp* c, double level) { /* core.go:288-32
   }
   return pow(2.0, -eff * cf);
 }
+
+/* calculateDownwardExpansionGain expander.go:358-411 */
+static double expansion_gain(const or_comp* c, double level) {
+  if (level <= 0) return c->range_lin;
+  const double undershoot = c->threshold_log2 - go_log2(level);
+  const double rf = c->cfg.ratio - 1.0;
+  if (c->cfg.knee_db <= 0) {
+    if (undershoot <= 0) return 1.0;
+    const double g = pow(2.0, -undershoot * rf);
+    return g < c->range_lin ? c->range_lin : g;
+  }
+  const double half = c->knee_width_log2 * 0.5;
+  double eff;
+  if (undershoot < -half) return 1.0;
+  if (undershoot > half) {
+    eff = undershoot;
+  } else {
+    const double s = undershoot + half;
+    eff = s * s * 0.5 * c->inv_knee_width_log2;
+  }
+  const double g = pow(2.0, -eff * rf);
+  return g < c->range_lin ? c->range_lin : g;
+}
+
+double or_comp_gain_for_level(const or_comp* c, double level) {
+  return c->mode ? expansion_gain(c, level) : gain_for_level(c, level);
+}
+
+void or_comp_set_expander(or_comp* c, int mode, double range_db, double hold_ms) {
+  /* NewExpander / NewGate: core with autoMakeup off, makeup 0 dB
+   * (expander.go:88-104, gate.go:106-122); the feedback-scaled time
+   * constants are not enabled by these constructors */
+  c->mode = mode;
+  c->cfg.auto_makeup = 0;
+  c->cfg.makeup_db = 0.0;
+  c->cfg.feedback_ratio_scale = 0;
+  comp_recalc(c);
+  c->range_lin = pow(10.0, range_db / 20.0);
+  c->hold_samples = mode == 2 ? (int64_t)(hold_ms * 0.001 * c->cfg.sample_rate) : 0;
+  c->hold_counter = 0;
+}
+
+int or_comp_hold_counter(const or_comp* c) { return (int)c->hold_counter; }
 
 static double update_rms(or_comp* c, double source) { /* core.go:361-388 */
   if (c->rms_n == 0) return source;
@@ -194,11 +242,28 @@ double or_comp_process_sample(or_comp* c, double x) {
     c->envelope += (src - c->envelope) * a;
   else
     c->envelope = src + (c->envelope - src) * r;
-  const double gain = gain_for_level(c, c->envelope);
-  const double out = x * gain * c->makeup_lin;
-  if (c->cfg.topology == 1) {
-    c->previous_gain = gain > MIN_FEEDBACK_GAIN_MEMORY ? gain : MIN_FEEDBACK_GAIN_MEMORY;
-    c->previous_abs = fabs(out);
+  double gain, out;
+  if (c->mode == 0) {
+    gain = gain_for_level(c, c->envelope);
+    out = x * gain * c->makeup_lin;
+    if (c->cfg.topology == 1) {
+      c->previous_gain = gain > MIN_FEEDBACK_GAIN_MEMORY ? gain : MIN_FEEDBACK_GAIN_MEMORY;
+      c->previous_abs = fabs(out);
+    }
+  } else {
+    /* Expander/Gate.ProcessSampleSidechain (expander.go, gate.go:354-375):
+     * only previousGain is kept for the feedback topology */
+    gain = expansion_gain(c, c->envelope);
+    if (c->mode == 2) {
+      if (gain >= 1.0) {
+        c->hold_counter = c->hold_samples;
+      } else if (c->hold_counter > 0) {
+        c->hold_counter--;
+        gain = 1.0;
+      }
+    }
+    if (c->cfg.topology == 1) c->previous_gain = gain > MIN_FEEDBACK_GAIN_MEMORY ? gain : MIN_FEEDBACK_GAIN_MEMORY;
+    out = x * gain;
   }
   /* updateMetrics compressor.go:411-423 */
   const double il = fabs(x), ol = fabs(out);

@@ -140,6 +140,13 @@ void or_comp_metrics(const or_comp* c, double* input_peak, double* output_peak, 
 void or_comp_params(const or_comp* c, double* threshold_log2, double* knee_width_log2, double* attack_coeff,
                     double* release_coeff, double* makeup_lin);
 void or_comp_free(or_comp* c);
+/* dynamics.Expander / dynamics.Gate (expander.go, gate.go): the same detector
+ * core with the downward-expansion gain (expander.go:358-411), no makeup,
+ * range floor; the gate adds a hold counter (gate.go:354-375).
+ * mode 1 = expander, 2 = gate.  Resets the hold counter. */
+void or_comp_set_expander(or_comp* c, int mode, double range_db, double hold_ms);
+int or_comp_hold_counter(const or_comp* c);
+double or_comp_gain_for_level(const or_comp* c, double level);
 
 /* ---- dsp/effects/reverb Freeverb ---- */
 typedef struct or_verb or_verb;

@@ -86,6 +86,9 @@ def lib() -> C.CDLL:
             "or_comp_metrics": (None, [vp, dp, dp, dp]),
             "or_comp_params": (None, [vp, dp, dp, dp, dp, dp]),
             "or_comp_free": (None, [vp]),
+            "or_comp_set_expander": (None, [vp, C.c_int, C.c_double, C.c_double]),
+            "or_comp_hold_counter": (C.c_int, [vp]),
+            "or_comp_gain_for_level": (C.c_double, [vp, C.c_double]),
             "or_verb_new": (vp, []),
             "or_verb_set": (None, [vp, C.c_double, C.c_double, C.c_double, C.c_double, C.c_double]),
             "or_verb_process_sample": (C.c_double, [vp, C.c_double]),
@@ -382,6 +385,26 @@ class Compressor:
             lib().or_comp_free(self.h)
 
 
+class Expander(Compressor):
+    """dynamics.Expander (mode 1) / dynamics.Gate (mode 2) over the oracle's
+    shared detector core; defaults of NewExpander / NewGate."""
+
+    def __init__(self, sample_rate=48000.0, gate=False, range_db=None, hold_ms=None, **kw):
+        base = dict(threshold_db=-40.0, ratio=10.0, knee_db=6.0, attack_ms=0.1, release_ms=100.0) if gate else \
+            dict(threshold_db=-35.0, ratio=2.0, knee_db=6.0, attack_ms=1.0, release_ms=100.0)
+        base.update(kw)
+        super().__init__(sample_rate, **base)
+        lib().or_comp_set_expander(self.h, 2 if gate else 1,
+                                   float((-80.0 if gate else -60.0) if range_db is None else range_db),
+                                   float((50.0 if gate else 0.0) if hold_ms is None else hold_ms))
+
+    def hold_counter(self):
+        return lib().or_comp_hold_counter(self.h)
+
+    def gain(self, level):
+        return lib().or_comp_gain_for_level(self.h, float(level))
+
+
 class Freeverb:
     def __init__(self):
         self.h = lib().or_verb_new()
@@ -451,7 +474,10 @@ class FxGraph:
                                 np.asarray(hp, dtype=np.float64).ravel(), np.zeros(2 * len(hp))])
             elif t == "comp":
                 cfg = {k: v for k, v in d["comp"].items() if k != "sample_rate"}
-                self.rt.append(["comp", Compressor(d["comp"]["sample_rate"], **cfg)])
+                if "expander" in d:
+                    self.rt.append(["comp", Expander(d["comp"]["sample_rate"], **d["expander"], **cfg)])
+                else:
+                    self.rt.append(["comp", Compressor(d["comp"]["sample_rate"], **cfg)])
             elif t == "verb":
                 v = Freeverb()
                 v.set(*d["verb"])

@@ -152,6 +152,56 @@ def test_compressor_vs_oracle(gpu, cfg):
         np.testing.assert_allclose(gm, om, rtol=1e-13, atol=0)
 
 
+# ------------------------------------------------------------------ Expander / Gate
+@pytest.mark.parametrize("kind,cfg", [
+    ("expander", {}),
+    ("expander", {"knee_db": 0.0, "ratio": 6.0, "threshold_db": -20.0, "range_db": -80.0}),
+    ("expander", {"topology": 1, "detector_mode": 1, "rms_window_ms": 20.0, "threshold_db": -25.0}),
+    ("expander", {"sidechain_low_cut_hz": 300.0, "sidechain_high_cut_hz": 5000.0}),
+    ("gate", {}),
+    ("gate", {"threshold_db": -20.0, "attack_ms": 0.1, "release_ms": 1.0, "hold_ms": 10.0, "knee_db": 0.0}),
+    ("gate", {"hold_ms": 0.0, "range_db": -120.0, "ratio": 100.0}),
+], ids=lambda v: v if isinstance(v, str) else (",".join(f"{k}={x}" for k, x in v.items()) or "defaults"))
+def test_expander_gate_vs_oracle(gpu, kind, cfg, monkeypatch):
+    """dynamics.Expander / dynamics.Gate (expander.go:358-440, gate.go:360-450)
+    on a bursty signal that opens and closes them, over a call boundary: the
+    output within 1e-12 RMS of the oracle and the metrics to 1e-13."""
+    C, n = 3, 6000
+    env = np.where((np.arange(n) // 900) % 2 == 0, 0.5, 0.003)
+    x = np.stack([env * signals.white_noise(n, 60 + c) for c in range(C)])
+    for staged in ("1", "0"):
+        monkeypatch.setenv("AD_FX_STAGED", staged)
+        ex = (P.Gate if kind == "gate" else P.Expander)(48000.0, channels=C, **cfg)
+        a, b = x[:, :2500].copy(), x[:, 2500:].copy()
+        ex.ProcessInPlace(a)
+        ex.ProcessInPlace(b)
+        got = np.concatenate([a, b], axis=1)
+        for c in range(C):
+            oc = O.Expander(48000.0, gate=kind == "gate", **cfg)
+            want = oc.process_in_place(x[c])
+            assert rms(got[c], want) <= RMS_TOL, rms(got[c], want)
+            assert float(np.max(np.abs(got[c] - want))) < 1e-12
+            np.testing.assert_allclose(np.array(ex.Metrics(c)), np.array(oc.metrics()), rtol=1e-13, atol=0)
+
+
+def test_gate_setters(gpu):
+    """SetRange / SetHold re-derive the parameters without touching the state."""
+    g = P.Gate(48000.0, channels=1, threshold_db=-20.0)
+    o = O.Expander(48000.0, gate=True, threshold_db=-20.0)
+    x = np.where(np.arange(4000) < 1500, 0.4, 0.001) * signals.white_noise(4000, 5)
+    a, b = x[None, :2000].copy(), x[None, 2000:].copy()
+    g.ProcessInPlace(a)
+    g.SetHold(0.0)
+    g.SetRange(-30.0)
+    g.ProcessInPlace(b)
+    want_a = o.process_in_place(x[:2000])
+    assert rms(a[0], want_a) <= RMS_TOL
+    assert np.all(np.abs(b[0]) <= np.abs(x[2000:]) + 1e-15)
+    assert np.min(np.abs(b[0][-500:]) / np.maximum(np.abs(x[2000:][-500:]), 1e-300)) >= 10 ** (-30 / 20) - 1e-12
+    with pytest.raises(Exception):
+        g.SetRange(10.0)
+
+
 # ------------------------------------------------------------------ Freeverb
 def test_freeverb_bit_exact(gpu):
     C, n = 65, 6000

@@ -100,6 +100,18 @@ def test_crossover_allpass_sum(order):
     assert design.crossover(1000, 3, FS) is None and design.crossover(30000, 4, FS) is None
 
 
+def test_dynamics_gate_expander_clamps():
+    """gateRuntime / expanderRuntime Configure (runtime_dynamics.go:130-235)."""
+    c, rng, hold = E.gate_config(E.Params("g", "dyn-gate", num={"thresholdDB": -99, "holdMs": 9000,
+                                                              "rangeDB": -200}), FS)
+    assert (c.threshold_db, c.ratio, c.attack_ms, rng, hold) == (-80, 10, 0.1, -120, 5000)
+    assert (c.auto_makeup, c.makeup_db, c.topology, c.detector_mode) == (0, 0.0, 0, 0)
+    c, rng, hold = E.expander_config(E.Params("e", "dyn-expander", num={"ratio": 0.5, "rmsWindowMs": 5000},
+                                              str_={"topology": "feedback", "detector": "rms"}), FS)
+    assert (c.threshold_db, c.ratio, c.attack_ms, c.rms_window_ms, rng, hold) == (-35, 1, 1, 1000, -60, 0.0)
+    assert (c.topology, c.detector_mode, c.feedback_ratio_scale) == (1, 1, 0)
+
+
 def test_unknown_effects_rejected():
     for t in ("chorus", "filter-moog", "dyn-lookahead", "vocoder", "reverb-conv"):
         ch = E.Chain(FS, 2, designer=design.RBJDesigner())
@@ -138,6 +150,37 @@ def test_branched_graph(gpu, n):
     ch, err = _run_both(BRANCHED, 3, n, calls=3)
     assert err < RMS_TOL
     assert ch.op_count()[2] >= 2  # the crossover's two bands run on their own streams
+
+
+# a gate on the low band and an RMS feedback expander on the high band of a
+# crossover, on a bursty signal so both open and close
+DYNAMICS = graph(
+    [{"id": "xo", "type": "split-freq", "params": {"freqHz": 1200}},
+     {"id": "gate", "type": "dyn-gate", "params": {"thresholdDB": -30, "holdMs": 5, "releaseMs": 20}},
+     {"id": "exp", "type": "dyn-expander", "params": {"thresholdDB": -28, "ratio": 4, "rangeDB": -40,
+                                                      "topology": "feedback", "detector": "rms"}},
+     {"id": "comp", "type": "dyn-compressor", "params": {"thresholdDB": -12}}],
+    [("_input", "xo"), ("xo", "gate", 0), ("xo", "exp", 1), ("gate", "comp"), ("comp", "_output"),
+     ("exp", "_output")])
+
+
+@pytest.mark.gpu
+def test_dynamics_gate_expander_graph(gpu):
+    C, n = 4, 6000
+    ch = E.Chain(FS, C, designer=design.RBJDesigner())
+    ch.LoadGraph(DYNAMICS)
+    oracles = [O.FxGraph(ch.spec, FS) for _ in range(C)]
+    env = np.where((np.arange(n) // 700) % 2 == 0, 0.6, 0.004)
+    x = np.stack([env * signals.white_noise(n, 50 + c) for c in range(C)])
+    y = x.copy()
+    for lo, hi in [(0, 1000), (1000, 1001), (1001, n)]:
+        b = y[:, lo:hi].copy()
+        assert ch.Process(b)
+        y[:, lo:hi] = b
+    for c in range(C):
+        want = oracles[c].process(x[c])
+        assert rms(y[c], want) < RMS_TOL
+        assert np.max(np.abs(y[c] - want)) < 1e-10
 
 
 @pytest.mark.gpu

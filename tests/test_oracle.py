@@ -431,3 +431,59 @@ def test_inverse_filter_kat():
     H = np.fft.fft([0.5, 1.0, 0.5], 64)
     ref = np.fft.ifft(np.conj(H) / (np.abs(H) ** 2 + 1e-3)).real
     assert np.max(np.abs(inv - ref)) < 1e-9 * np.max(np.abs(ref))
+
+
+# ------------------------------------------------------------------ Gate / Expander (dynamics/gate.go, expander.go)
+def test_gate_gain_kats():
+    """gate_test.go:352-458: unity above threshold, attenuation below it,
+    more attenuation for larger ratios (ratio 1 is unity), rangeLin at silence."""
+    g = O.Expander(48000.0, gate=True, threshold_db=-40.0)
+    assert all(g.gain(l) == 1.0 for l in (0.1, 0.5, 1.0))
+    assert g.gain(0.0) == 10 ** (-80 / 20)
+    g = O.Expander(48000.0, gate=True, threshold_db=-20.0, ratio=10.0, knee_db=0.0)
+    assert 0.0 < g.gain(0.05) < 1.0
+    prev = None
+    for ratio in (1.0, 2.0, 4.0, 10.0):
+        gr = O.Expander(48000.0, gate=True, threshold_db=-20.0, ratio=ratio, knee_db=0.0, range_db=-120.0).gain(0.01)
+        if ratio == 1.0:
+            assert gr == 1.0
+        else:
+            assert gr < prev
+        prev = gr
+    # the floor: gain never drops below rangeLin (gate_test.go:460-491)
+    g = O.Expander(48000.0, gate=True, threshold_db=-20.0, ratio=100.0, knee_db=0.0, range_db=-20.0)
+    assert g.gain(1e-6) == 10 ** (-20 / 20)
+
+
+def test_gate_hold_behaviour():
+    """gate_test.go:657-712 and 714-759: the hold counter is full after a loud
+    passage, reaches 0 after decay + hold, and refills on a loud return."""
+    g = O.Expander(48000.0, gate=True, threshold_db=-20.0, attack_ms=0.1, release_ms=1.0, hold_ms=10.0, knee_db=0.0)
+    for _ in range(2000):
+        g.process_sample(0.5)
+    assert g.hold_counter() == 480
+    for _ in range(1000 + 480):
+        g.process_sample(0.0)
+    assert g.hold_counter() == 0
+    g = O.Expander(48000.0, gate=True, threshold_db=-20.0, hold_ms=100.0, attack_ms=0.1)
+    for _ in range(2000):
+        g.process_sample(0.5)
+    full = g.hold_counter()
+    for _ in range(10):
+        g.process_sample(0.0)
+    for _ in range(2000):
+        g.process_sample(0.5)
+    assert g.hold_counter() == full == 4800
+
+
+def test_expander_gain_behaviour():
+    """expander_test.go:94-158: above-threshold pass-through, attenuation below,
+    and feedback vs feed-forward topologies differ."""
+    e = O.Expander(48000.0, threshold_db=-20.0, ratio=6.0, knee_db=0.0, range_db=-80.0)
+    assert e.process_in_place(np.full(1024, 0.5))[-1] >= 0.49
+    e = O.Expander(48000.0, threshold_db=-20.0, ratio=6.0, knee_db=0.0, range_db=-80.0)
+    assert e.process_in_place(np.full(1024, 0.02))[-1] < 0.02
+    kw = dict(threshold_db=-25.0, ratio=4.0, detector_mode=1, rms_window_ms=20.0)
+    fb = O.Expander(48000.0, topology=1, **kw).process_in_place(np.full(512, 0.05))[-1]
+    ff = O.Expander(48000.0, topology=0, **kw).process_in_place(np.full(512, 0.05))[-1]
+    assert fb != ff
