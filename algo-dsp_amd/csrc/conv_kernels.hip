@@ -27,6 +27,7 @@
 #include <algorithm>
 #include <cstdlib>
 
+#include "blocked_dot.hpp"
 #include "conv_kernels.hpp"
 #include "fft_device.hpp"
 
@@ -601,6 +602,67 @@ __global__ __launch_bounds__(256) void k_direct_lds(const double* __restrict__ a
   if (k < out) dst[k] = acc;
 }
 
+// Tap-stationary register-blocked form (the default).  The sum for output k
+// is read the other way round: y[k] = sum over j = m-1 down to 0 of
+// b[j] * a[k-j], which is the same increasing-i order.  b[j] is wave-uniform
+// (scalar loads) and a lane owns R consecutive outputs, so its inputs
+// a[k-j .. k-j+R-1] slide by one per term (blocked_dot.hpp: one R-wide LDS
+// read per R*R products).  Unlike the input-stationary form every lane of a
+// wave takes every term, except at the two ends of the signal where a lane
+// meets a[i] outside [0, n) stored as zero: b[j] * 0 = +-0 leaves the sum
+// unchanged unless b[j] is not finite, so a tap chunk holding a non-finite
+// tap takes the per-lane bounds-checked loop.  Taps are walked in chunks of
+// DC; the input window one chunk meets is 256 R + DC - 1 samples in LDS.
+template <int R>
+__global__ __launch_bounds__(256) void k_direct_reg(const double* __restrict__ a, int64_t n,
+                                                    const double* __restrict__ b, int64_t m,
+                                                    double* __restrict__ dst) {
+#pragma clang fp contract(off)
+  constexpr int DT = 256 * R;
+  __shared__ __attribute__((aligned(32))) double win[DT + DC + 8];
+  const int t = threadIdx.x;
+  const int64_t k0 = (int64_t)blockIdx.x * DT;
+  const int64_t out = n + m - 1;
+  // taps reaching this tile: k - j in [0, n) for some k in [k0, k0 + DT)
+  const int64_t jtop = m - 1 < k0 + DT - 1 ? m - 1 : k0 + DT - 1;
+  const int64_t jbot = k0 - n + 1 > 0 ? k0 - n + 1 : 0;
+  double acc[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) acc[r] = 0.0;
+  for (int64_t jhi = jtop; jhi >= jbot; jhi -= DC) {
+    const int cj = (int)(jhi - jbot + 1 < DC ? jhi - jbot + 1 : DC);
+    const int64_t g0 = k0 - jhi;  // win[1 + v] = a[g0 + v]
+    __syncthreads();
+    int bad = 0;
+    for (int u = t; u < cj; u += 256) bad |= !__builtin_isfinite(b[jhi - u]);
+    for (int v = t; v < DT + cj - 1; v += 256) {
+      const int64_t g = g0 + v;
+      win[1 + v] = (g >= 0 && g < n) ? a[g] : 0.0;
+    }
+    bad = __syncthreads_or(bad);
+    const double* wt = win + 1 + t * R;  // term u (j = jhi - u) of output r: wt[u + r]
+    if (!bad) {
+      blocked_dot<R, -1>(b + jhi, wt, cj, acc);
+    } else {
+      for (int u = 0; u < cj; ++u) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int64_t i = g0 + t * R + r + u;
+          if (i >= 0 && i < n) {
+            const double p = b[jhi - u] * wt[u + r];
+            acc[r] = acc[r] + p;
+          }
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int64_t k = k0 + t * R + r;
+    if (k < out) dst[k] = acc[r];
+  }
+}
+
 // conv.DirectCircularTo (conv.go:176-189): dst[(i+j)%n] += a[i]*b[j], i outer.
 // For output k the terms arrive in increasing i with j = (k - i) mod n.
 __global__ __launch_bounds__(256) void k_direct_circular(const double* __restrict__ a, const double* __restrict__ b,
@@ -786,7 +848,27 @@ bool launch_fdl_mac(int PC, int NH, const MacArgs& in, int channels, hipStream_t
 
 void launch_direct(const double* a, int64_t n, const double* b, int64_t m, double* dst, hipStream_t s) {
   const int64_t out = n + m - 1;
-  hipLaunchKernelGGL(k_direct_lds, dim3((unsigned)((out + 255) / 256)), dim3(256), 0, s, a, n, b, m, dst);
+  // R = 4 outputs per lane once that still gives >= 2 workgroups per CU;
+  // AD_DIRECT_R=0 selects the input-stationary k_direct_lds (A/B only).
+  static const int forced = [] {
+    const char* e = std::getenv("AD_DIRECT_R");
+    return e ? std::atoi(e) : -1;
+  }();
+  int R = forced >= 0 ? forced : (out >= 512 * 1024 ? 4 : out >= 512 * 512 ? 2 : 1);
+  switch (R) {
+    case 0:
+      hipLaunchKernelGGL(k_direct_lds, dim3((unsigned)((out + 255) / 256)), dim3(256), 0, s, a, n, b, m, dst);
+      break;
+    case 4:
+      hipLaunchKernelGGL(k_direct_reg<4>, dim3((unsigned)((out + 1023) / 1024)), dim3(256), 0, s, a, n, b, m, dst);
+      break;
+    case 2:
+      hipLaunchKernelGGL(k_direct_reg<2>, dim3((unsigned)((out + 511) / 512)), dim3(256), 0, s, a, n, b, m, dst);
+      break;
+    default:
+      hipLaunchKernelGGL(k_direct_reg<1>, dim3((unsigned)((out + 255) / 256)), dim3(256), 0, s, a, n, b, m, dst);
+      break;
+  }
 }
 
 void launch_direct_circular(const double* a, const double* b, int64_t n, double* dst, hipStream_t s) {

@@ -26,6 +26,7 @@
 
 #include <cstdlib>
 
+#include "blocked_dot.hpp"
 #include "dsp_device.hpp"
 #include "dsp_kernels.hpp"
 
@@ -577,56 +578,54 @@ __global__ __launch_bounds__(320) void k_chain_pipe(ChainArgs a) {
 // where x[< 0] is the delay line.  Taps are walked in chunks of FQ; the input
 // window a chunk meets (256 + FQ - 1 samples, from the delay line and the new
 // block) is staged in LDS, and h[q] is wave-uniform (scalar loads).
+//
+// A lane owns R consecutive outputs (blocked_dot.hpp): the window slides by
+// one sample per term, so one R-wide LDS read feeds R*R products and the
+// reversed path is bound by the FP64 VALU rather than LDS bandwidth.
 constexpr int FQ = 1024;
+template <int R>
 __global__ __launch_bounds__(256) void k_fir(FirArgs a) {
 #pragma clang fp contract(off)
-  __shared__ double w[256 + FQ];
+  constexpr int DT = 256 * R;
+  __shared__ __attribute__((aligned(32))) double w[DT + FQ + 8];
   const int t = threadIdx.x;
   const int c = blockIdx.y;
-  const int64_t i0 = (int64_t)blockIdx.x * 256;
+  const int64_t i0 = (int64_t)blockIdx.x * DT;
   const int64_t hn = a.N - 1;
   const double* hc = a.hist + (int64_t)c * hn;
   const double* xc = a.src + (int64_t)c * a.sstride;
-  double acc = 0.0;
+  double acc[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) acc[r] = 0.0;
   for (int64_t q0 = 0; q0 < a.N; q0 += FQ) {
     const int cq = (int)(a.N - q0 < FQ ? a.N - q0 : FQ);
-    // window start: reversed w[v] = x[i0 - hn + q0 + v]; ring w[v] = x[i0 - q0 - cq + 1 + v]
+    // window start: reversed w[1 + v] = x[i0 - hn + q0 + v]; ring w[1 + v] = x[i0 - q0 - cq + 1 + v]
     const int64_t g0 = a.reversed ? i0 - hn + q0 : i0 - q0 - cq + 1;
     __syncthreads();
-    for (int v = t; v < 256 + cq - 1; v += 256) {
+    for (int v = t; v < DT + cq - 1; v += 256) {
       const int64_t g = g0 + v;
-      w[v] = g < 0 ? hc[hn + g] : (g < a.n ? xc[g] : 0.0);
+      w[1 + v] = g < 0 ? hc[hn + g] : (g < a.n ? xc[g] : 0.0);
     }
     __syncthreads();
     const double* hq = a.h + q0;
+    const double* wt = w + 1 + t * R;
     if (a.reversed) {
-      const double* wt = w + t;  // term q0 + u: wt[u]
-      int u = 0;
-      for (; u + 7 < cq; u += 8) {
-        double hv[8], xv[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) hv[e] = hq[u + e];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) xv[e] = wt[u + e];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const double p = hv[e] * xv[e];
-          acc = acc + p;
-        }
-      }
-      for (; u < cq; ++u) {
-        const double p = hq[u] * wt[u];
-        acc = acc + p;
-      }
+      blocked_dot<R, 1>(hq, wt, cq, acc);  // term q0 + u of output r: wt[u + r]
     } else {
-      const double* wt = w + t + cq - 1;  // term q0 + u: wt[-u]
-      for (int u = 0; u < cq; ++u) {
-        const double p = hq[u] * wt[-u];
-        acc = acc + p;
+      for (int u = 0; u < cq; ++u) {  // term q0 + u of output r: wt[r + cq - 1 - u]
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const double p = hq[u] * wt[r + cq - 1 - u];
+          acc[r] = acc[r] + p;
+        }
       }
     }
   }
-  if (i0 + t < a.n) a.y[(int64_t)c * a.ystride + i0 + t] = acc;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int64_t i = i0 + t * R + r;
+    if (i < a.n) a.y[(int64_t)c * a.ystride + i] = acc[r];
+  }
 }
 
 // decodeF16 (internal/webdemo/irlib.go:68-97), reference quirk kept: a
@@ -769,7 +768,14 @@ void launch_chain(int stages, const ChainArgs& a, hipStream_t s) {
 
 void launch_fir(const FirArgs& a, hipStream_t s) {
   if (a.channels <= 0 || a.n <= 0) return;
-  hipLaunchKernelGGL(k_fir, dim3((unsigned)((a.n + 255) / 256), (unsigned)a.channels), dim3(256), 0, s, a);
+  // R = 4 outputs per lane once that still gives >= 2 workgroups per CU
+  const int64_t work = a.n * a.channels;
+  if (work >= 512 * 1024)
+    hipLaunchKernelGGL(k_fir<4>, dim3((unsigned)((a.n + 1023) / 1024), (unsigned)a.channels), dim3(256), 0, s, a);
+  else if (work >= 512 * 512)
+    hipLaunchKernelGGL(k_fir<2>, dim3((unsigned)((a.n + 511) / 512), (unsigned)a.channels), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL(k_fir<1>, dim3((unsigned)((a.n + 255) / 256), (unsigned)a.channels), dim3(256), 0, s, a);
 }
 
 }  // namespace adsp
