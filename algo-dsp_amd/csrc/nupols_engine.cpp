@@ -26,9 +26,11 @@ Nupols::Nupols(int device, const double* h, int64_t K, int64_t lambda, int64_t p
   }
   for (auto& s : st_) {
     AD_HIP(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
-    s.eng.reset(new Upols(device, h + s.T, 1, s.taps, (int)s.p, 1, nullptr, 1, s.stream));
-    AD_HIP(hipHostMalloc(reinterpret_cast<void**>(&s.in_h), s.p * sizeof(double), hipHostMallocMapped));
-    AD_HIP(hipHostMalloc(reinterpret_cast<void**>(&s.out_h), s.p * sizeof(double), hipHostMallocMapped));
+    s.cap = std::max<int64_t>(1, kBatchSamples / s.p);
+    s.eng.reset(new Upols(device, h + s.T, 1, s.taps, (int)s.p, 1, nullptr, (int)s.cap, s.stream));
+    const size_t bytes = (size_t)(s.cap * s.p) * sizeof(double);
+    AD_HIP(hipHostMalloc(reinterpret_cast<void**>(&s.in_h), bytes, hipHostMallocMapped));
+    AD_HIP(hipHostMalloc(reinterpret_cast<void**>(&s.out_h), bytes, hipHostMallocMapped));
     AD_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&s.in_d), s.in_h, 0));
     AD_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&s.out_d), s.out_h, 0));
   }
@@ -49,6 +51,7 @@ void Nupols::reset() {
   for (auto& s : st_) {
     s.eng->reset_stream(s.stream);
     s.done = 0;
+    s.pending = false;
   }
   for (auto& s : st_) AD_HIP(hipStreamSynchronize(s.stream));
   xin_.clear();
@@ -62,31 +65,42 @@ void Nupols::reset() {
 void Nupols::process(const double* in, int64_t n, double* out) {
   xin_.insert(xin_.end(), in, in + n);
   received_ += n;
-  // Rounds: every stage with a complete input block launches one run on its
-  // own stream; one synchronisation per round, then the block outputs are
-  // added into the accumulator at time offset T_s.
-  std::vector<int> due;
-  for (;;) {
-    due.clear();
-    for (int i = 0; i < (int)st_.size(); ++i) {
-      Stage& s = st_[i];
-      if (received_ - s.done < s.p) continue;
-      const int64_t off = s.done - xin_base_;
-      std::copy(xin_.begin() + off, xin_.begin() + off + s.p, s.in_h);
-      s.eng->run(s.in_d, s.p, s.p, s.out_d, s.p, s.p, /*use_hist=*/true, s.stream);
-      due.push_back(i);
-    }
-    if (due.empty()) break;
-    for (int i : due) AD_HIP(hipStreamSynchronize(st_[i].stream));
-    for (int i : due) {
-      Stage& s = st_[i];
-      const int64_t t0 = s.done + s.T;  // absolute output time of the block's first sample
-      const int64_t need = t0 + s.p - acc_base_;
-      if ((int64_t)acc_.size() < need) acc_.resize((size_t)need, 0.0);
-      for (int64_t k = 0; k < s.p; ++k) acc_[(size_t)(t0 - acc_base_ + k)] += s.out_h[k];
-      s.done += s.p;
+  // A stage run's block [d, d + p) first contributes to output time d + T_s,
+  // and T_s + lambda >= p_s, so a run launched for a block that completes in
+  // this call is never needed before the next call (the call emits up to
+  // time received - 1 - lambda).  Runs are therefore left in flight across
+  // calls: the device works while the caller produces the next block, and a
+  // run is synchronised only when its buffers are reused, or when a call
+  // emits an output it contributes to (calls longer than a stage's block).
+  auto finish = [&](Stage& s) {
+    AD_HIP(hipStreamSynchronize(s.stream));
+    const int64_t t0 = s.pend_d + s.T;  // absolute output time of the block's first sample
+    const int64_t need = t0 + s.pend_n - acc_base_;
+    if ((int64_t)acc_.size() < need) acc_.resize((size_t)need, 0.0);
+    auto it = acc_.begin() + (t0 - acc_base_);
+    for (int64_t k = 0; k < s.pend_n; ++k, ++it) *it += s.out_h[k];
+    s.pending = false;
+  };
+  for (bool launched = true; launched;) {
+    launched = false;
+    for (auto& s : st_) {
+      // every complete block of this stage (up to cap) in one launch
+      const int64_t nb = std::min((received_ - s.done) / s.p, s.cap);
+      if (nb == 0) continue;
+      if (s.pending) finish(s);  // in_h / out_h are reused
+      const int64_t len = nb * s.p, off = s.done - xin_base_;
+      std::copy(xin_.begin() + off, xin_.begin() + off + len, s.in_h);
+      s.eng->run(s.in_d, len, len, s.out_d, len, len, /*use_hist=*/true, s.stream);
+      s.pending = true;
+      s.pend_d = s.done;
+      s.pend_n = len;
+      s.done += len;
+      launched = true;
     }
   }
+  const int64_t last_u = emitted_ + n - 1 - lambda_;  // latest output time this call emits
+  for (auto& s : st_)
+    if (s.pending && s.pend_d + s.T <= last_u) finish(s);
   // Emit: y[o] = linear conv at o - lambda (complete by the T_s + lambda >= p_s rule).
   for (int64_t i = 0; i < n; ++i) {
     const int64_t u = emitted_ + i - lambda_;

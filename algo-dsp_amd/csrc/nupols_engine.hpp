@@ -11,8 +11,9 @@
 // every contribution arrive before it is emitted.  Stages run on their own
 // HIP streams (the small kernels of the short stages overlap the long ones),
 // read their input block straight from mapped pinned host memory and write
-// their output there too, so a call costs only the kernels of the stages due
-// plus one synchronisation.
+// their output there too.  All complete blocks of a stage in one call run as
+// one multi-block launch (up to kBatchSamples), so a call costs about one
+// launch per stage and one synchronisation, whatever its length.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -29,6 +30,7 @@ namespace adsp {
 
 class Nupols {
  public:
+  static constexpr int64_t kBatchSamples = 8192;  // input samples per stage launch (at most)
   // h: host [K] taps (K = the taps the reference convolves), lambda >= 64,
   // p_max <= 8192 (powers of two).
   Nupols(int device, const double* h, int64_t K, int64_t lambda, int64_t p_max);
@@ -43,9 +45,13 @@ class Nupols {
     int64_t p = 0, T = 0, taps = 0;
     std::unique_ptr<Upols> eng;
     hipStream_t stream = nullptr;
-    double *in_h = nullptr, *in_d = nullptr;    // mapped pinned [p]
-    double *out_h = nullptr, *out_d = nullptr;  // mapped pinned [p]
+    int64_t cap = 1;                            // blocks per launch (at most)
+    double *in_h = nullptr, *in_d = nullptr;    // mapped pinned [cap p]
+    double *out_h = nullptr, *out_d = nullptr;  // mapped pinned [cap p]
     int64_t done = 0;                           // input samples consumed
+    bool pending = false;                       // a launched run not yet added into acc_
+    int64_t pend_d = 0;                         // its first input sample
+    int64_t pend_n = 0;                         // its length (whole blocks)
   };
   int device_;
   int64_t lambda_;

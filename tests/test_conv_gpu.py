@@ -190,7 +190,8 @@ def test_partitioned_matches_oracle(gpu, K, lo, hi):
     assert g.Latency() == o.latency() == lat
     assert g.StageCount() == o.stage_count()
     assert [g.StageInfo(i) for i in range(g.StageCount())] == [o.stage_info(i) for i in range(o.stage_count())]
-    sizes = [lat + 3, 1, 2 * lat, lat - 1 if lat > 1 else 1, 5 * lat + 7]
+    # the last size exceeds a stage launch's batch (Nupols::kBatchSamples = 8192)
+    sizes = [lat + 3, 1, 2 * lat, lat - 1 if lat > 1 else 1, 5 * lat + 7, 20011]
     pos, step, got, want = 0, 0, [], []
     while pos < n:
         m = min(sizes[step % len(sizes)], n - pos)
