@@ -77,8 +77,8 @@ void Nupols::process(const double* in, int64_t n, double* out) {
     const int64_t t0 = s.pend_d + s.T;  // absolute output time of the block's first sample
     const int64_t need = t0 + s.pend_n - acc_base_;
     if ((int64_t)acc_.size() < need) acc_.resize((size_t)need, 0.0);
-    auto it = acc_.begin() + (t0 - acc_base_);
-    for (int64_t k = 0; k < s.pend_n; ++k, ++it) *it += s.out_h[k];
+    double* a = acc_.data() + (t0 - acc_base_);
+    for (int64_t k = 0; k < s.pend_n; ++k) a[k] += s.out_h[k];
     s.pending = false;
   };
   for (bool launched = true; launched;) {
@@ -89,7 +89,7 @@ void Nupols::process(const double* in, int64_t n, double* out) {
       if (nb == 0) continue;
       if (s.pending) finish(s);  // in_h / out_h are reused
       const int64_t len = nb * s.p, off = s.done - xin_base_;
-      std::copy(xin_.begin() + off, xin_.begin() + off + len, s.in_h);
+      std::memcpy(s.in_h, xin_.data() + off, (size_t)len * sizeof(double));
       s.eng->run(s.in_d, len, len, s.out_d, len, len, /*use_hist=*/true, s.stream);
       s.pending = true;
       s.pend_d = s.done;
@@ -114,16 +114,14 @@ void Nupols::process(const double* in, int64_t n, double* out) {
   emitted_ += n;
   // Drop what no later output or stage needs.
   const int64_t keep_out = emitted_ - lambda_;
-  while (acc_base_ < keep_out && !acc_.empty()) {
-    acc_.pop_front();
-    ++acc_base_;
-  }
+  const int64_t drop_acc = std::min<int64_t>(std::max<int64_t>(keep_out - acc_base_, 0), (int64_t)acc_.size());
+  acc_.erase(acc_.begin(), acc_.begin() + drop_acc);
+  acc_base_ += drop_acc;
   int64_t min_done = received_;
   for (auto& s : st_) min_done = std::min(min_done, s.done);
-  while (xin_base_ < min_done && !xin_.empty()) {
-    xin_.pop_front();
-    ++xin_base_;
-  }
+  const int64_t drop_in = std::min<int64_t>(std::max<int64_t>(min_done - xin_base_, 0), (int64_t)xin_.size());
+  xin_.erase(xin_.begin(), xin_.begin() + drop_in);
+  xin_base_ += drop_in;
 }
 
 }  // namespace adsp

@@ -248,23 +248,26 @@ def main():
     lam = 128
     kpc = ir[0, :95432]
     pc = conv.NewPartitionedConvolution(kpc, 7, 13)
-    nb = 256 if q else 2048
-    xp = signals.white_noise(nb * lam, 1)
-    yp = np.empty(lam)
-    for i in range(64):
-        pc.ProcessBlock(xp[i * lam:(i + 1) * lam], yp)
-    t0 = time.perf_counter()
-    for i in range(nb):
-        pc.ProcessBlock(xp[i * lam:(i + 1) * lam], yp)
-    ms = (time.perf_counter() - t0) / nb * 1e3
     op = O.Partitioned(kpc, 7, 13)
     ncb = 512
+    xp = signals.white_noise(96 * 4096, 1)
     cs = cpu_time(lambda: [op.process_block(xp[i * lam:(i + 1) * lam]) for i in range(ncb)], budget_s=1.0,
                   max_reps=4)
-    rows.append(row("a9/a10", "PartitionedConvolution.ProcessBlock partitioned.go:348-396",
-                    f"Large Church L (95432 taps), minOrder 7 / maxOrder 13 (latency {lam}), host buffers", lam,
-                    "samples", ms, cs, ncb * lam, f"oracle PartitionedConvolution, {ncb} blocks", None, 0,
-                    "latency-bound: mean per-block wall time incl. PCIe"))
+    # one latency-sized block per call, then 4096-sample calls (a stage's whole blocks in one launch)
+    for cb, nb in ((lam, 256 if q else 2048), (4096, 16 if q else 64)):
+        yp = np.empty(cb)
+        pc.Reset()
+        for i in range(16):
+            pc.ProcessBlock(xp[i * cb:(i + 1) * cb], yp)
+        t0 = time.perf_counter()
+        for i in range(nb):
+            pc.ProcessBlock(xp[i * cb:(i + 1) * cb], yp)
+        ms = (time.perf_counter() - t0) / nb * 1e3
+        rows.append(row("a9/a10", "PartitionedConvolution.ProcessBlock partitioned.go:348-396",
+                        f"Large Church L (95432 taps), minOrder 7 / maxOrder 13 (latency {lam}), "
+                        f"{cb}-sample calls, host buffers", cb,
+                        "samples", ms, cs, ncb * lam, f"oracle PartitionedConvolution, {ncb} blocks", None, 0,
+                        "latency-bound: mean per-call wall time incl. PCIe"))
 
     nbt = 1 << (18 if q else 22)
     xbt = signals.white_noise(nbt, 3)
