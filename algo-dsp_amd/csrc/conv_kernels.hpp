@@ -39,6 +39,7 @@ struct RfftArgs {
   int MS;
   const double2* twM;   // W_M^e, e < M
   const double2* twN;   // W_{2M}^k, k < M
+  int per_wg;           // windows per workgroup (set by the launcher, <= the plan's F)
 };
 
 struct MacArgs {

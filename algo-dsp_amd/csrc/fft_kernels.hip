@@ -71,8 +71,8 @@ __global__ __launch_bounds__((FftPlan<M, V>::BLOCK)) void k_window_rfft(RfftArgs
   __shared__ __attribute__((aligned(16))) double2 lds_all[Plan::F * Plan::MP];
   const int f = threadIdx.x / T;
   const int tid = threadIdx.x % T;
-  const int64_t e = (int64_t)xcd_remap_fft(blockIdx.x, gridDim.x) * Plan::F + f;
-  const bool active = e < (int64_t)a.channels * a.jc;
+  const int64_t e = (int64_t)xcd_remap_fft(blockIdx.x, gridDim.x) * a.per_wg + f;
+  const bool active = f < a.per_wg && e < (int64_t)a.channels * a.jc;
   const int c = active ? (int)(e / a.jc) : 0;
   const int j = active ? (int)(e % a.jc) : 0;
   double2* lds = lds_all + f * Plan::MP;
@@ -262,8 +262,13 @@ template <int M, int V>
 void rfft_go(const RfftArgs& a, hipStream_t s) {
   using Plan = FftPlan<M, V>;
   const int64_t items = (int64_t)a.channels * a.jc;
-  hipLaunchKernelGGL((k_window_rfft<M, V>), dim3((unsigned)((items + Plan::F - 1) / Plan::F)), dim3(Plan::BLOCK), 0,
-                     s, a);
+  // Full F windows per workgroup once the launch fills the chip; a small
+  // launch (a low-latency stage's few blocks, often read from mapped host
+  // memory) spreads its windows over up to 256 workgroups instead.
+  RfftArgs b = a;
+  b.per_wg = (int)std::min<int64_t>(Plan::F, std::max<int64_t>(1, (items + 255) / 256));
+  hipLaunchKernelGGL((k_window_rfft<M, V>), dim3((unsigned)((items + b.per_wg - 1) / b.per_wg)), dim3(Plan::BLOCK), 0,
+                     s, b);
 }
 template <int M>
 void rfft_split_go(const RfftArgs& a, hipStream_t s) {
