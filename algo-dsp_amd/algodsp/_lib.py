@@ -171,7 +171,13 @@ def _declare(L: C.CDLL) -> None:
                                            C.c_int, C.POINTER(vp)]),
         "ad_conv_multi_process_device": (C.c_int, [vp, vp, i64, i64, vp, i64, i64, vp]),
         "ad_conv_multi_process_device_segment": (C.c_int, [vp, vp, i64, i64, vp, i64, i64, i64, i64, vp]),
-        "ad_conv_mixdown_device": (C.c_int, [vp, C.c_int, i64, i64, vp, vp]),
+        "ad_conv_mixdown_device": (C.c_int, [vp, C.c_int, i64, i64, vp, i64, C.c_int, vp]),
+        "ad_comm_get_unique_id": (C.c_int, [C.POINTER(C.c_uint8)]),
+        "ad_comm_create": (C.c_int, [C.POINTER(C.c_uint8), C.c_int, C.c_int, C.c_int, C.POINTER(vp)]),
+        "ad_comm_destroy": (None, [vp]),
+        "ad_comm_rank": (C.c_int, [vp]),
+        "ad_comm_size": (C.c_int, [vp]),
+        "ad_mixdown_reduce": (C.c_int, [vp, vp, C.c_int, i64, i64, C.c_int, vp, i64, C.c_int, vp]),
         "ad_conv_profile_enable": (C.c_int, [vp, C.c_int]),
         "ad_conv_profile_read": (C.c_int, [vp, c_double_p, c_int64_p, c_double_p]),
         "ad_compressor_default_config": (None, [C.POINTER(CompressorConfig), C.c_double]),

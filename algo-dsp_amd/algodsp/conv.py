@@ -272,8 +272,12 @@ class MultiChannelConvolver(_Handle):
                                                          out_end, C.c_void_p(stream)))
 
 
-def mixdown_device(d_chan: int, channels: int, stride: int, length: int, d_mix: int, stream: int = 0) -> None:
+def mixdown_device(d_chan: int, channels: int, stride: int, length: int, d_mix: int, stream: int = 0,
+                   mix_stride: int | None = None, first_parity: int = 0) -> None:
+    """Stereo partial mix of a channel group (k_mixdown): L row at d_mix, R row
+    at d_mix + mix_stride (default: length) doubles."""
     check(lib().ad_conv_mixdown_device(C.c_void_p(d_chan), channels, stride, length, C.c_void_p(d_mix),
+                                       int(length if mix_stride is None else mix_stride), int(first_parity),
                                        C.c_void_p(stream)))
 
 

@@ -40,3 +40,52 @@ def reduce_mix(mix_tensor, dist, async_op: bool = False):
     on RCCL the reduce runs on the process group's stream after the work
     already queued on the current stream, overlapping what is queued next."""
     return dist.reduce(mix_tensor, dst=0, op=dist.ReduceOp.SUM, async_op=async_op)
+
+
+class Comm:
+    """The library's own RCCL communicator (include/algodsp.h ad_comm_*): the
+    path a cgo caller takes to shard without torch.distributed.  `bootstrap`
+    moves rank 0's 128-byte unique id to every rank (here: a torch.distributed
+    broadcast of the bytes; any transport works)."""
+
+    def __init__(self, rank: int, world: int, device: int, bootstrap=None):
+        import ctypes as C
+
+        from ._lib import check, lib
+
+        L = lib()
+        uid = (C.c_uint8 * 128)()
+        if rank == 0:
+            check(L.ad_comm_get_unique_id(uid))
+        if bootstrap is not None:
+            data = bootstrap(bytes(uid))
+            C.memmove(uid, data, 128)
+        h = C.c_void_p()
+        check(L.ad_comm_create(uid, int(world), int(rank), int(device), C.byref(h)))
+        self._h = h
+        self.rank, self.world = rank, world
+
+    def mixdown_reduce(self, d_chan: int, channels: int, stride: int, length: int, d_mix: int, mix_stride: int,
+                       first_parity: int = 0, root: int = 0, stream: int = 0) -> None:
+        """k_mixdown of this rank's channel group, then one in-place RCCL
+        sum-reduce of the [2][mix_stride] mix to `root`, both on `stream`."""
+        import ctypes as C
+
+        from ._lib import check, lib
+
+        check(lib().ad_mixdown_reduce(self._h, C.c_void_p(d_chan), int(channels), int(stride), int(length),
+                                      int(first_parity), C.c_void_p(d_mix), int(mix_stride), int(root),
+                                      C.c_void_p(stream)))
+
+    def close(self) -> None:
+        from ._lib import lib
+
+        if getattr(self, "_h", None):
+            lib().ad_comm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -16,10 +16,11 @@ _M1 = np.uint64(0xBF58476D1CE4E5B9)
 _M2 = np.uint64(0x94D049BB133111EB)
 
 
-def splitmix64(seed: int, n: int) -> np.ndarray:
-    """n outputs of SplitMix64 started at `seed` (vectorised)."""
+def splitmix64(seed: int, n: int, start: int = 0) -> np.ndarray:
+    """Outputs start .. start+n-1 of SplitMix64 started at `seed` (vectorised;
+    the generator is counter-based, so any slice is computed directly)."""
     with np.errstate(over="ignore"):
-        idx = np.arange(1, n + 1, dtype=np.uint64)
+        idx = np.arange(start + 1, start + n + 1, dtype=np.uint64)
         z = np.uint64(seed & 0xFFFFFFFFFFFFFFFF) + idx * _GOLDEN
         z = (z ^ (z >> np.uint64(30))) * _M1
         z = (z ^ (z >> np.uint64(27))) * _M2
@@ -27,9 +28,10 @@ def splitmix64(seed: int, n: int) -> np.ndarray:
     return z
 
 
-def white_noise(n: int, seed: int = 0x5EED) -> np.ndarray:
-    """Uniform [-1, 1) float64 white noise (seed 0x5EED + channel)."""
-    z = splitmix64(seed, n)
+def white_noise(n: int, seed: int = 0x5EED, start: int = 0) -> np.ndarray:
+    """Uniform [-1, 1) float64 white noise (SURVEY 8(d): seed 0x5EED + channel);
+    `start` returns samples start .. start+n-1 of the same sequence."""
+    z = splitmix64(seed, n, start)
     u = (z >> np.uint64(11)).astype(np.float64) * (1.0 / 9007199254740992.0)
     return u * 2.0 - 1.0
 

@@ -103,6 +103,13 @@ struct ad_conv {
   double* pin_out_dev = nullptr;
   size_t pin_n = 0;
 
+  // multi-channel device calls: the engine's delay line and scratch are
+  // shared by every caller stream, so a call on a new stream waits for the
+  // previous call's last launch (has_last: last may be the NULL stream)
+  hipStream_t last = nullptr;
+  bool has_last = false;
+  hipEvent_t done = nullptr;
+
   // partitioned: non-uniform multi-stage engine (latency >= 64)
   std::unique_ptr<Nupols> nup;
 
@@ -113,6 +120,10 @@ struct ad_conv {
   int64_t ylin_base = 0;         // linear-conv index of ylin.front()
 
   ~ad_conv() {
+    if (done) {
+      (void)hipEventSynchronize(done);
+      (void)hipEventDestroy(done);
+    }
     nup.reset();
     eng.reset();
     if (stream) (void)hipStreamSynchronize(stream);
@@ -134,6 +145,17 @@ ad_conv* new_handle(Kind k, int device) {
     AD_FAIL(AD_ERR_DEVICE, "hipStreamCreate failed");
   }
   return h;
+}
+
+// Orders a device call on stream s after the handle's previous one.
+void order_after_last(ad_conv* h, hipStream_t s) {
+  if (!h->done) AD_HIP(hipEventCreateWithFlags(&h->done, hipEventDisableTiming));
+  if (h->has_last && h->last != s) AD_HIP(hipStreamWaitEvent(s, h->done, 0));
+}
+void mark_last(ad_conv* h, hipStream_t s) {
+  AD_HIP(hipEventRecord(h->done, s));
+  h->last = s;
+  h->has_last = true;
 }
 
 // zero-latency streaming convolution state for `hop` sized chunks
@@ -515,8 +537,10 @@ int ad_conv_reset(ad_conv* h) {
   return guard([&] {
     if (!h) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "nil handle");
     DeviceScope ds(h->device);
+    if (h->has_last) AD_HIP(hipStreamWaitEvent(h->stream, h->done, 0));  // after the last device call
     if (h->nup) h->nup->reset();
     stream_reset(h);
+    h->has_last = false;
   });
 }
 
@@ -672,8 +696,10 @@ int ad_conv_multi_process_device(ad_conv* h, const double* d_in, int64_t in_stri
       AD_FAIL(AD_ERR_LENGTH_MISMATCH, "conv: buffer length mismatch");
     DeviceScope ds(h->device);
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);  // NULL = the default (null) stream
+    order_after_last(h, s);
     h->eng->begin_offline(s);
     h->eng->run(d_in, in_stride, in_len, d_out, out_stride, out_len, /*use_hist=*/false, s);
+    mark_last(h, s);
     h->seg_next = -1;
   });
 }
@@ -694,9 +720,11 @@ int ad_conv_multi_process_device_segment(ad_conv* h, const double* d_in, int64_t
       AD_FAIL(AD_ERR_INVALID_ARGUMENT, "conv segment: segments must follow each other in order");
     DeviceScope ds(h->device);
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    order_after_last(h, s);
     if (out_begin == 0) h->eng->begin_offline(s);
     h->eng->run(d_in, in_stride, in_len, d_out, out_stride, out_len, /*use_hist=*/false, s, out_begin / L,
                 (out_end + L - 1) / L);
+    mark_last(h, s);
     h->seg_next = out_end < out_len ? out_end : -1;
   });
 }
@@ -717,10 +745,13 @@ int ad_conv_profile_read(ad_conv* h, double* total_ms, int64_t* launches, double
 }
 
 int ad_conv_mixdown_device(const double* d_chan, int channels, int64_t stride, int64_t len, double* d_mix,
-                           void* stream) {
+                           int64_t mix_stride, int first_parity, void* stream) {
   return guard([&] {
     if (channels <= 0 || len <= 0) AD_FAIL(AD_ERR_EMPTY_INPUT, "empty mixdown");
-    launch_mixdown(d_chan, channels, stride, len, d_mix, reinterpret_cast<hipStream_t>(stream));
+    if (!d_chan || !d_mix) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "mixdown: null device buffer");
+    if (mix_stride < len || (channels > 1 && stride < len))
+      AD_FAIL(AD_ERR_LENGTH_MISMATCH, "mixdown: strides shorter than the mixed length");
+    launch_mixdown(d_chan, channels, stride, len, d_mix, mix_stride, first_parity, reinterpret_cast<hipStream_t>(stream));
     AD_HIP(hipGetLastError());
   });
 }

@@ -614,13 +614,19 @@ struct ad_fir {
   int device = 0, channels = 0;
   int64_t N = 0;
   hipStream_t stream = nullptr;       // host-buffer calls
-  hipStream_t last = nullptr;         // stream of the last call (Reset orders after it)
+  hipStream_t last = nullptr;         // stream of the last call (valid when has_last)
+  bool has_last = false;              // a call has been enqueued (last may be the NULL stream)
+  hipEvent_t done = nullptr;          // recorded on `last` after each call's last operation
   DevBuf<double> h;                   // [N]
   DevBuf<double> hist[2];             // [C][N-1] delay line, ping-pong (cur = hist[cur])
   int cur = 0;
   DevBuf<double> stage;               // [C][n]: in-place calls read a copy of the input
   DevBuf<double> io_in, io_out;       // host-buffer calls
   ~ad_fir() {
+    if (done) {
+      (void)hipEventSynchronize(done);
+      (void)hipEventDestroy(done);
+    }
     if (stream) {
       (void)hipStreamSynchronize(stream);
       (void)hipStreamDestroy(stream);
@@ -637,6 +643,10 @@ namespace {
 // An in-place call (dst overlaps src) reads a staged copy of src.
 void fir_run(ad_fir* f, const double* d_src, int64_t src_stride, double* d_dst, int64_t dst_stride, int64_t n,
              hipStream_t s) {
+  // The delay line, the staging copy and the ping-pong index are shared by
+  // every stream a caller uses: a call on a new stream first waits for the
+  // previous call's last operation.
+  if (f->has_last && f->last != s) AD_HIP(hipStreamWaitEvent(s, f->done, 0));
   const int64_t hn = f->N - 1;
   const size_t C = (size_t)f->channels;
   const char* s0 = reinterpret_cast<const char*>(d_src);
@@ -677,7 +687,9 @@ void fir_run(ad_fir* f, const double* d_src, int64_t src_stride, double* d_dst, 
   launch_fir(a, s);
   AD_HIP(hipGetLastError());
   if (hn > 0) f->cur ^= 1;
+  AD_HIP(hipEventRecord(f->done, s));
   f->last = s;
+  f->has_last = true;
 }
 
 }  // namespace
@@ -697,6 +709,7 @@ int ad_fir_create(const double* coeffs, int64_t n_taps, int channels, int device
     f->channels = channels;
     f->N = n_taps;
     AD_HIP(hipStreamCreateWithFlags(&f->stream, hipStreamNonBlocking));
+    AD_HIP(hipEventCreateWithFlags(&f->done, hipEventDisableTiming));
     if (n_taps > 0) {
       f->h.alloc((size_t)n_taps);
       AD_HIP(hipMemcpy(f->h.p, coeffs, n_taps * sizeof(double), hipMemcpyHostToDevice));
@@ -749,10 +762,14 @@ int ad_fir_reset(ad_fir* f) {
   return guard([&] {
     if (!f) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "null FIR handle");
     DeviceScope ds(f->device);
-    hipStream_t s = f->last ? f->last : f->stream;
+    // after the last call, whatever stream (NULL included) it was enqueued on
+    if (f->has_last) AD_HIP(hipStreamWaitEvent(f->stream, f->done, 0));
     for (auto& hb : f->hist)
-      if (hb.p) AD_HIP(hipMemsetAsync(hb.p, 0, hb.n * sizeof(double), s));
-    AD_HIP(hipStreamSynchronize(s));
+      if (hb.p) AD_HIP(hipMemsetAsync(hb.p, 0, hb.n * sizeof(double), f->stream));
+    AD_HIP(hipEventRecord(f->done, f->stream));
+    f->last = f->stream;
+    f->has_last = true;
+    AD_HIP(hipStreamSynchronize(f->stream));
   });
 }
 

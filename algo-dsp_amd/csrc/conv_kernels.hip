@@ -703,16 +703,19 @@ __global__ __launch_bounds__(64) void k_copy_f64(const double* __restrict__ src,
   if (i < n) dst[i] = src[i];
 }
 
-// Stereo mixdown: mix[0][t] = sum over even channels, mix[1][t] = odd channels.
+// Stereo mixdown of a channel group: mix[0][t] (L) sums the channels of even
+// global index, mix[mix_stride + t] (R) the odd ones; channel c of the group
+// has global index first + c, so only first's parity matters.
 __global__ __launch_bounds__(256) void k_mixdown(const double* __restrict__ ch, int channels, int64_t stride,
-                                                 int64_t len, double* __restrict__ mix) {
+                                                 int64_t len, double* __restrict__ mix, int64_t mix_stride,
+                                                 int first_parity) {
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (t >= len) return;
-  double l = 0.0, r = 0.0;
-  for (int c = 0; c < channels; c += 2) l += ch[(int64_t)c * stride + t];
-  for (int c = 1; c < channels; c += 2) r += ch[(int64_t)c * stride + t];
-  mix[t] = l;
-  mix[len + t] = r;
+  double e = 0.0, o = 0.0;  // group-local even / odd channels
+  for (int c = 0; c < channels; c += 2) e += ch[(int64_t)c * stride + t];
+  for (int c = 1; c < channels; c += 2) o += ch[(int64_t)c * stride + t];
+  mix[t] = first_parity ? o : e;
+  mix[mix_stride + t] = first_parity ? e : o;
 }
 
 // ---------------------------------------------------------------------------
@@ -884,8 +887,10 @@ void launch_copy_f64(const double* src, double* dst, int64_t n, hipStream_t s) {
   hipLaunchKernelGGL(k_copy_f64, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, src, dst, n);
 }
 
-void launch_mixdown(const double* ch, int channels, int64_t stride, int64_t len, double* mix, hipStream_t s) {
-  hipLaunchKernelGGL(k_mixdown, dim3((unsigned)((len + 255) / 256)), dim3(256), 0, s, ch, channels, stride, len, mix);
+void launch_mixdown(const double* ch, int channels, int64_t stride, int64_t len, double* mix, int64_t mix_stride,
+                    int first_parity, hipStream_t s) {
+  hipLaunchKernelGGL(k_mixdown, dim3((unsigned)((len + 255) / 256)), dim3(256), 0, s, ch, channels, stride, len, mix,
+                     mix_stride, first_parity & 1);
 }
 
 }  // namespace adsp

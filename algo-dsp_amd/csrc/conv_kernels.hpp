@@ -87,6 +87,7 @@ void launch_copy_f64(const double* src, double* dst, int64_t n, hipStream_t s);
 void launch_direct(const double* a, int64_t n, const double* b, int64_t m, double* dst, hipStream_t s);
 void launch_direct_circular(const double* a, const double* b, int64_t n, double* dst, hipStream_t s);
 void launch_stream_direct(const double* h, int64_t K, const double* buf, int64_t B, double* y, hipStream_t s);
-void launch_mixdown(const double* ch, int channels, int64_t stride, int64_t len, double* mix, hipStream_t s);
+void launch_mixdown(const double* ch, int channels, int64_t stride, int64_t len, double* mix, int64_t mix_stride,
+                    int first_parity, hipStream_t s);
 
 }  // namespace adsp

@@ -38,7 +38,7 @@ def parse():
     p.add_argument("--hop", type=int, default=8192)
     p.add_argument("--chunk", type=int, default=0, help="blocks per channel per engine chunk (0 = auto)")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-sample", type=int, default=1 << 25, help="samples of one channel for the CPU leg")
+    p.add_argument("--cpu-sample", type=int, default=1 << 24, help="samples per channel (per host thread) for the CPU leg")
     p.add_argument("--mixdown", choices=["auto", "on", "off"], default="auto")
     p.add_argument("--pipeline", choices=["on", "off"], default="on",
                    help="N > 1: overlap step i's mixdown reduce with step i+1's convolution (two output buffers)")
@@ -52,41 +52,106 @@ def parse():
                         "8 (config 4's shard) at N > 1")
     p.add_argument("--graph", choices=["config5", "branched"], default=None,
                    help="fx workload: run an effectchain graph through the batched graph runtime")
-    p.add_argument("--workload", choices=["conv", "fx", "stream", "corr"], default="conv",
-                   help="conv: BASELINE metric (overlap-save conv); fx: config 5 effect chain (256 ch); "
+    p.add_argument("--workload", choices=["conv", "shard", "fx", "stream", "corr"], default="conv",
+                   help="conv: BASELINE metric (overlap-save conv; config 3 at N = 1, config 4's shard at N > 1); "
+                        "shard: config 4's shard (8 ch x 2^22 per GPU + RCCL stereo mixdown) at any N; "
+                        "fx: config 5 effect chain (256 ch); "
                         "stream: config 2 streaming OLS (mono, 16384 taps, 4096-sample host blocks); "
                         "corr: CorrelateFFT of two 2^23-sample signals (SURVEY 8(f)3, device buffers)")
     return p.parse_args()
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(n: int) -> int:
+    """`--gpus N` outside a launcher: start N ranks (one process per GPU) with
+    torch.distributed.run and return its exit status.  Runs before anything
+    touches the GPU; the children see WORLD_SIZE = N."""
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(ROOT / "bench.py")] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def host_cores() -> int:
+    """Host cores this process may use, capped at the GPU box's per-GPU CPU
+    share (16): os.cpu_count() there reports the whole machine."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
 def cpu_baseline(ir, sample_len):
     """Times the oracle (C restatement of the reference's batch OverlapSave.Process,
-    dsp/conv/overlap_save.go:126-254, N = 262144, step 131073) on one host core
-    over a bounded sample of the same workload (one channel, `sample_len` samples)."""
+    dsp/conv/overlap_save.go:126-254, N = 262144, step 131073) over a bounded
+    sample of the same workload: one channel on one core, then one channel per
+    host core (ctypes releases the GIL, so T threads run T oracle instances in
+    parallel).  `value` is the all-cores rate."""
     sys.path.insert(0, str(ROOT / "tests"))
-    import numpy as np
+    from concurrent.futures import ThreadPoolExecutor
 
     import oracle_lib as O
     from algodsp import signals
 
-    x = signals.white_noise(sample_len, 0x5EED)
+    T = host_cores()
+    xs = [signals.white_noise(sample_len, 0x5EED + c) for c in range(T)]
     ols = O.OverlapSave(ir[0], 0)
     t0 = time.perf_counter()
-    ols.process(x)
-    dt = time.perf_counter() - t0
-    del np
+    ols.process(xs[0])
+    dt1 = time.perf_counter() - t0
+    del ols
+
+    def one(c):
+        return O.OverlapSave(ir[c % 2], 0).process(xs[c]).size
+
+    with ThreadPoolExecutor(T) as ex:
+        t0 = time.perf_counter()
+        list(ex.map(one, range(T)))
+        dtT = time.perf_counter() - t0
     return {
-        "value": sample_len / dt / 1e6,
+        "value": T * sample_len / dtT / 1e6,
         "unit": "Msamples/s",
-        "cores": 1,
+        "cores": T,
         "kind": "port",
-        "sample": f"1 channel x {sample_len} samples (2^{sample_len.bit_length() - 1}) white noise, "
-                  f"Large Church L (131072 taps), oracle OverlapSave.Process N=262144; {dt:.1f} s",
+        "single_core": sample_len / dt1 / 1e6,
+        "sample": f"oracle OverlapSave.Process (N=262144, Large Church 131072 taps) on {T} host threads, one "
+                  f"channel of {sample_len} white-noise samples each ({dtT:.1f} s; host cpu_count "
+                  f"{os.cpu_count()}, affinity share capped at 16); single_core: 1 channel on 1 thread ({dt1:.1f} s)",
     }
+
+
+def exact_window(x, h, t0, w):
+    """y[t0 .. t0+w) of the full linear convolution x * h by direct float64
+    dot products (numpy; independent of the engine and of the oracle)."""
+    import numpy as np
+
+    K = h.size
+    lo = t0 - K + 1
+    seg = x[max(lo, 0):t0 + w]
+    if lo < 0:
+        seg = np.concatenate([np.zeros(-lo), seg])
+    if seg.size < w + K - 1:
+        seg = np.concatenate([seg, np.zeros(w + K - 1 - seg.size)])
+    return np.convolve(seg, h, mode="valid")
 
 
 def main():
     args = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        return launch_ranks(args.gpus)
+    if env_world is not None and int(env_world) != args.gpus:
+        print(f"bench.py: WORLD_SIZE={env_world} but --gpus {args.gpus}", file=sys.stderr)
+        return 2
     if args.workload == "fx":
         return main_fx(args)
     if args.workload == "corr":
@@ -104,16 +169,17 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    mixdown = world > 1 if args.mixdown == "auto" else args.mixdown == "on"
-    if world > 1 or mixdown:  # --mixdown on at N = 1 (under torchrun) exercises the RCCL path
+    # config 4's shard (8 ch x 2^22 per GPU + the stereo mixdown) at N > 1, or
+    # at any N with --workload shard; config 3 (stereo x 2^24) at N = 1
+    shard_cfg = world > 1 or args.workload == "shard"
+    mixdown = shard_cfg if args.mixdown == "auto" else args.mixdown == "on"
+    if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    # N = 1: config 3 (stereo x 2^24). N > 1: config 4's shard (8 ch x 2^22 per
-    # GPU): same samples per GPU, a 4x smaller stereo mixdown per step to reduce.
     if args.channels is None:
-        args.channels = 8 if world > 1 else 2
+        args.channels = 8 if shard_cfg else 2
     if args.samples is None:
-        args.samples = (1 << 22) if world > 1 else (1 << 24)
+        args.samples = (1 << 22) if shard_cfg else (1 << 24)
     ir = irlib.large_church()                       # [2][131072], Large Church zero padded
     K = ir.shape[1]
     n = args.samples
@@ -121,20 +187,31 @@ def main():
     from algodsp import shard
 
     C = args.channels
-    if world > 1 and C % 2:
+    if mixdown and C % 2 and world > 1:
         raise SystemExit("--channels must be even for the multi-GPU stereo mixdown")
     ids = list(shard.channel_group(rank, world, C * world))  # this rank's global channel ids
     x_host = np.stack([signals.white_noise(n, 0x5EED + c) for c in ids])
     x = torch.from_numpy(x_host).to(dev)
-    # Two output buffers when the mixdown runs: step i's RCCL reduce (on the
-    # process group's own stream) overlaps step i+1's convolution into the
-    # other buffer; a buffer is rewritten only after its reduce has finished.
-    # The last step's reduce completes inside the timed region.
+    # Mixdown through the library's own RCCL communicator (ad_mixdown_reduce),
+    # the path a cgo caller takes: k_mixdown of this rank's group + one
+    # in-place sum-reduce to rank 0, on a side stream.  Two output buffers:
+    # step i's mixdown/reduce overlaps step i+1's convolution into the other
+    # buffer; a buffer is rewritten only after its reduce (event wait on the
+    # device, no host block).  The last step's reduce completes inside the
+    # timed region.
+    comm = None
+    if mixdown:
+        def bootstrap(uid: bytes) -> bytes:
+            if world == 1:
+                return uid
+            obj = [uid]
+            dist.broadcast_object_list(obj, src=0)
+            return obj[0]
+
+        comm = shard.Comm(rank, world, local, bootstrap)
     nbuf = 2 if (mixdown and args.pipeline == "on") else 1
     ys = [torch.empty((C, out_len), dtype=torch.float64, device=dev) for _ in range(nbuf)]
     mixes = [y if C == 2 else torch.empty((2, out_len), dtype=torch.float64, device=dev) for y in ys]
-    y = ys[0]
-    del x_host
 
     eng = conv.MultiChannelConvolver(ir, hop=args.hop, channels=C, ir_index=shard.ir_index(ids),
                                      chunk_blocks=args.chunk, device=local)
@@ -144,15 +221,14 @@ def main():
     blocks = -(-out_len // args.hop)
     cuts = [min(out_len, args.hop * (blocks * i // args.segments)) for i in range(args.segments + 1)]
     segs = [(b, e) for b, e in zip(cuts[:-1], cuts[1:]) if e > b]
-    pending = [[] for _ in range(nbuf)]
+    red_done = [None] * nbuf
     it = [0]
 
     def step():
         i = it[0] % nbuf
         it[0] += 1
-        for w in pending[i]:  # the reduce that last read this buffer
-            w.wait()
-        pending[i] = []
+        if red_done[i] is not None:  # the reduce that last read this buffer
+            stream.wait_event(red_done[i])
         yb, mb = ys[i], mixes[i]
         for b, e in segs:
             if len(segs) == 1:
@@ -160,27 +236,20 @@ def main():
             else:
                 eng.process_device_segment(x.data_ptr(), n, n, yb.data_ptr(), out_len, out_len, b, e, sptr)
             if mixdown:
-                # the mixdown kernel and the reduce run on a side stream, after
-                # this segment's convolution: the next step's convolution (into
-                # the other output buffer) overlaps them
                 done = torch.cuda.Event()
                 done.record(stream)
-                with torch.cuda.stream(side):
-                    side.wait_event(done)
-                    if C != 2:  # stereo partial mix of this rank's channel group (even -> L, odd -> R)
-                        conv.mixdown_device(yb.data_ptr() + 8 * b, C, out_len, e - b, mb.data_ptr() + 16 * b,
-                                            side.cuda_stream)
-                        parts = [mb.view(-1)[2 * b:2 * e]]
-                    else:
-                        parts = [mb[0, b:e], mb[1, b:e]]
-                    for t in parts:
-                        pending[i].append(shard.reduce_mix(t, dist, async_op=True))
+                side.wait_event(done)
+                # stereo group: the two output rows are the partial mix (no k_mixdown)
+                comm.mixdown_reduce(yb.data_ptr() + 8 * b, 0 if C == 2 else C, out_len, e - b,
+                                    mb.data_ptr() + 8 * b, out_len, ids[0] % 2, 0, side.cuda_stream)
+        if mixdown:
+            ev = torch.cuda.Event()
+            ev.record(side)
+            red_done[i] = ev
 
     def drain():
-        for i in range(nbuf):
-            for w in pending[i]:
-                w.wait()
-            pending[i] = []
+        if mixdown:
+            side.synchronize()
 
     for _ in range(args.warmup):
         step()
@@ -201,12 +270,14 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    last = (it[0] - 1) % nbuf
     if not live:  # kernel durations from a separate event-timed pass
         eng.profile_enable(True)
         for _ in range(max(2, args.steps // 2)):
             step()
         drain()
         torch.cuda.synchronize(dev)
+        last = (it[0] - 1) % nbuf
     eng.profile_enable(False)
     prof = eng.profile_read()
 
@@ -228,6 +299,42 @@ def main():
                    "share": v[0] / max(sum(p[0] for p in prof.values()), 1e-12)} for k, v in prof.items()}
 
     if rank == 0:
+        # Parity of the measured output itself: windows of the last step's
+        # result (the whole-job stereo mix on rank 0 when the mixdown runs)
+        # against exact float64 dot products -- the signal start, a K2 run
+        # boundary (auto run length: multiples of 16 blocks), the middle and
+        # the tail of the output.
+        L = args.hop
+        wins = sorted({t for t in (K - 32, 192 * L - 32, 16 * L - 7, out_len // 2, out_len - 64)
+                       if 0 <= t <= out_len - 64})
+        errs = []
+        if mixdown:
+            got = mixes[last].cpu().numpy()
+            for s_ in range(2):
+                for t0w in wins:
+                    ref = np.zeros(64)
+                    a0 = t0w - K + 1
+                    lo, hi = max(0, a0), min(n, t0w + 64)
+                    for c in range(C * world):
+                        if c % 2 == s_ and hi > lo:
+                            # the input span this window reads, regenerated (counter-based noise)
+                            seg = np.zeros(64 + K - 1)
+                            seg[lo - a0:hi - a0] = signals.white_noise(hi - lo, 0x5EED + c, start=lo)
+                            ref += np.convolve(seg, ir[c % 2], mode="valid")
+                    errs.append(got[s_, t0w:t0w + 64] - ref)
+        else:
+            got = ys[last].cpu().numpy()
+            for ci, c in enumerate(ids):
+                for t0w in wins:
+                    errs.append(got[ci, t0w:t0w + 64] - exact_window(x_host[ci], ir[c % 2], t0w, 64))
+        err = np.concatenate(errs)
+        parity = {"rms": float(np.sqrt(np.mean(err ** 2))), "max_abs": float(np.max(np.abs(err))),
+                  "outputs_checked": int(err.size),
+                  "against": "exact float64 dot products (numpy) over windows at " + ", ".join(map(str, wins)) +
+                             (" of the whole-job stereo mix" if mixdown else " of every channel"),
+                  "tolerance_rms": 1e-7}
+        if parity["rms"] > 1e-7:
+            print(f"bench.py: PARITY FAILURE {parity}", file=sys.stderr)
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(ir, args.cpu_sample)
@@ -240,6 +347,10 @@ def main():
                 traffic = tab[key]["hbm_bytes_per_launch"] if key else None
             except Exception:
                 traffic = None
+        workload = ("OverlapSave partitioned conv, stereo, 131072-tap IR, full linear convolution "
+                    if not shard_cfg else
+                    f"{C * world}-channel x 131072-tap IR convolution reverb (IR[c mod 2]), channels "
+                    f"sharded {C}-per-GPU" + (", RCCL stereo mixdown (ad_mixdown_reduce) " if mixdown else " "))
         line = {
             "metric": "Msamples/sec, overlap-save conv 131072-tap IR @48kHz; achieved HBM GB/s",
             "value": round(value, 3),
@@ -255,12 +366,8 @@ def main():
             "data": "synthetic: SplitMix64 white noise (seed 0x5EED+channel) x Large Church IR from web/irs.irlib "
                     "(f16, reference decodeF16), zero padded 95432->131072 taps",
             "config": {
-                "workload": ("OverlapSave partitioned conv, stereo, 131072-tap IR, full linear convolution "
-                             if C == 2 and world == 1 else
-                             f"{C * world}-channel x 131072-tap IR convolution reverb (IR[c mod 2]), channels "
-                             f"sharded {C}-per-GPU, RCCL stereo mixdown " if mixdown else
-                             f"{C}-channel x 131072-tap IR convolution (IR[c mod 2]) ") +
-                            f"({C} ch x {n} samples per GPU per step)",
+                "workload": workload + f"({C} ch x {n} samples per GPU per step)",
+                "baseline_config": "configs[3] shard" if shard_cfg else "configs[2]",
                 "channels_per_gpu": C,
                 "samples_per_channel": n,
                 "kernel_taps": K,
@@ -282,14 +389,18 @@ def main():
             },
             "kernels": {k: {kk: (round(vv, 3) if isinstance(vv, float) else vv) for kk, vv in v.items()}
                         for k, v in kernels.items()},
+            "parity": parity,
             "cpu_baseline": cpu,
         }
         if cpu:
             line["speedup_vs_cpu"] = round(value / cpu["value"], 1)
         print(json.dumps(line), flush=True)
+    if comm is not None:
+        comm.close()
     if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
+    return 0
 
 
 def main_stream(args):
@@ -510,4 +621,4 @@ def main_fx(args):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

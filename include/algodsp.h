@@ -166,10 +166,41 @@ int ad_conv_multi_process_device_segment(ad_conv* h, const double* d_in, int64_t
  * (DESIGN.md), then clears the counters.  Arrays have 3 entries.          */
 int ad_conv_profile_enable(ad_conv* h, int enable);
 int ad_conv_profile_read(ad_conv* h, double* total_ms, int64_t* launches, double* alg_bytes);
-/* Stereo mixdown of a channel group (build-defined):
- * d_mix[0][t] = sum of even channels, d_mix[1][t] = sum of odd channels. */
+/* Stereo mixdown of a channel group (build-defined; the
+ * reference defines no mixdown):
+ *   d_mix[t]              (L) = sum of the group's channels with an even global index,
+ *   d_mix[mix_stride + t] (R) = sum of those with an odd global index,
+ * t < len; channel c of the group has global index first + c and
+ * first_parity = first & 1.  d_chan [channels][stride].  Asynchronous on
+ * `stream`.  mix_stride >= len (L and R rows of one [2][mix_stride] buffer,
+ * so an output segment can be mixed into its place: pass d_chan + b and
+ * d_mix + b).                                                              */
 int ad_conv_mixdown_device(const double* d_chan, int channels, int64_t stride, int64_t len, double* d_mix,
-                           void* stream);
+                           int64_t mix_stride, int first_parity, void* stream);
+
+/* ---- multi-GPU mixdown over RCCL (SURVEY 8(b) ad_mixdown_reduce, 8(e)) ----
+ * One process per GPU; every rank convolves its own channel group and the
+ * stereo partial mixes are summed on `root` with ONE RCCL reduce over xGMI.
+ * The communicator is created from a unique id that rank 0 makes and the
+ * caller distributes (cgo side: any transport -- the reference has no
+ * multi-process layer).  librccl.so.1 is loaded on first use (no link-time
+ * dependency for single-GPU callers).                                      */
+#define AD_COMM_ID_BYTES 128
+typedef struct ad_comm ad_comm;
+int ad_comm_get_unique_id(uint8_t id[AD_COMM_ID_BYTES]);
+/* ncclCommInitRank over `nranks` ranks; `device` is this rank's GPU. */
+int ad_comm_create(const uint8_t id[AD_COMM_ID_BYTES], int nranks, int rank, int device, ad_comm** out);
+void ad_comm_destroy(ad_comm* comm);
+int ad_comm_rank(const ad_comm* comm);
+int ad_comm_size(const ad_comm* comm);
+/* k_mixdown of this rank's group into d_mix ([2][mix_stride], as
+ * ad_conv_mixdown_device), then an in-place sum-reduce of d_mix's 2 x len
+ * values to `root` (d_mix on root holds the whole job's stereo mix; on the
+ * other ranks it holds the rank's partial mix).  Both are enqueued on
+ * `stream` and the call returns without waiting.  channels == 0 skips the
+ * mixdown (d_mix already holds the partial mix, e.g. a stereo group).      */
+int ad_mixdown_reduce(ad_comm* comm, const double* d_chan, int channels, int64_t stride, int64_t len,
+                      int first_parity, double* d_mix, int64_t mix_stride, int root, void* stream);
 
 /* ======================================================================== */
 /* dsp/filter, dsp/effects: per-sample processors                           */

@@ -2,6 +2,7 @@
 symbol include/algodsp.h declares, and fails loudly (no CPU fallback) when
 no device is present."""
 import ctypes as C
+import pathlib
 import subprocess
 
 import numpy as np
@@ -67,3 +68,30 @@ def test_validation_errors_precede_device_use():
         conv.Direct([], [1.0])
     with pytest.raises(conv.ErrEmptyKernel):
         conv.Direct([1.0], [])
+
+
+def test_bench_world_size_mismatch_exits_before_gpu():
+    """bench.py --gpus N refuses a launcher world size that disagrees with N
+    (before anything touches the GPU) instead of silently running fewer ranks."""
+    import os
+    import subprocess
+    import sys
+
+    root = pathlib.Path(__file__).resolve().parent.parent
+    env = dict(os.environ, WORLD_SIZE="3", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, str(root / "bench.py"), "--gpus", "2"], env=env, capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 2
+    assert "WORLD_SIZE=3" in r.stderr
+
+
+def test_comm_rejects_bad_arguments_without_gpu():
+    """ad_comm_create / ad_mixdown_reduce validate before touching RCCL."""
+    import ctypes as C
+
+    L = _lib.lib()
+    h = C.c_void_p()
+    uid = (C.c_uint8 * 128)()
+    assert L.ad_comm_create(uid, 2, 5, 0, C.byref(h)) == _lib.AD_ERR_INVALID_ARGUMENT
+    assert not h.value
+    assert L.ad_mixdown_reduce(None, None, 2, 10, 10, 0, None, 10, 0, None) == _lib.AD_ERR_INVALID_ARGUMENT

@@ -297,6 +297,88 @@ def test_mixdown(gpu):
     xn = x.cpu().numpy()
     np.testing.assert_allclose(mix.cpu().numpy()[0], xn[0] + xn[2] + xn[4], atol=1e-15)
     np.testing.assert_allclose(mix.cpu().numpy()[1], xn[1] + xn[3] + xn[5], atol=1e-15)
+    # explicit mix stride + segment offset + odd first global channel
+    mix2 = torch.zeros((2, 1500), dtype=torch.float64, device="cuda")
+    conv.mixdown_device(x.data_ptr() + 8 * 300, 5, 1000, 600, mix2.data_ptr() + 8 * 300, mix_stride=1500,
+                        first_parity=1)
+    torch.cuda.synchronize()
+    m2 = mix2.cpu().numpy()
+    np.testing.assert_allclose(m2[1, 300:900], (xn[0] + xn[2] + xn[4])[300:900], atol=1e-15)
+    np.testing.assert_allclose(m2[0, 300:900], (xn[1] + xn[3])[300:900], atol=1e-15)
+    assert not m2[:, :300].any() and not m2[:, 900:].any()
+
+
+# ------------------------------------------- the exact instance bench.py times
+def _exact_window(x, h, t0, w):
+    """y[t0 .. t0+w) of the full linear convolution by direct float64 dot
+    products (np.convolve 'valid' over the window's input span)."""
+    K = h.size
+    lo = t0 - K + 1
+    seg = x[max(lo, 0):t0 + w]
+    if lo < 0:
+        seg = np.concatenate([np.zeros(-lo), seg])
+    if seg.size < w + K - 1:
+        seg = np.concatenate([seg, np.zeros(w + K - 1 - seg.size)])
+    return np.convolve(seg, h, mode="valid")
+
+
+def test_bench_instance_vs_oracle(gpu):
+    """BASELINE config 3 exactly as bench.py runs it (bench.py: hop 8192, auto
+    chunk, auto run length -> P = 16, one k_fdl_mac_lds<16,1,true,8> launch,
+    R = 192 on 256 CUs, stereo x 2^24 samples, one chunk): the whole output of
+    both channels against the oracle's batch OverlapSave.Process
+    (overlap_save.go:126-254), plus exact dot products on windows across the
+    K2 run boundaries and the signal ends."""
+    ir = irlib.large_church()
+    K = ir.shape[1]
+    n = 1 << 24
+    x = np.stack([signals.white_noise(n, 0x5EED + c) for c in range(2)])
+    y, eng = _multi_run(ir, x, hop=8192)
+    assert eng.FFTSize() == 16384
+    out_len = n + K - 1
+    for c in range(2):
+        want = O.OverlapSave(ir[c], 0).process(x[c])
+        assert want.size == out_len
+        assert rms(y[c], want) < FFT_RMS_TOL
+        assert np.max(np.abs(y[c] - want)) < 1e-9
+        del want
+    # run boundaries of the auto run length (multiples of 16 blocks around
+    # 192 blocks) and the chunk's first/last blocks
+    L = 8192
+    for c in range(2):
+        for t0 in [0, K - 64, 16 * L - 32, 192 * L - 32, 384 * L - 32, 193 * L - 7, n - 40, out_len - 64]:
+            got = y[c][t0:t0 + 64]
+            ref = _exact_window(x[c], ir[c], t0, got.size)
+            assert np.max(np.abs(got - ref)) < 1e-9, (c, t0)
+
+
+def test_config4_shard_mixdown_vs_oracle(gpu):
+    """BASELINE config 4's per-GPU shard exactly as bench.py --workload shard runs
+    it: 8 channels x 2^22 samples, channel c with IR[c mod 2] (131072 taps),
+    hop 8192, auto chunk / run length, then k_mixdown (L = even channels,
+    R = odd).  The mix is compared with the oracle's per-channel OverlapSave
+    outputs summed by parity."""
+    import torch
+
+    ir = irlib.large_church()
+    K = ir.shape[1]
+    C_, n = 8, 1 << 22
+    out_len = n + K - 1
+    x = np.stack([signals.white_noise(n, 0x5EED + c) for c in range(C_)])
+    eng = conv.MultiChannelConvolver(ir, hop=8192, channels=C_, ir_index=[c % 2 for c in range(C_)])
+    dx = torch.from_numpy(x).cuda()
+    dy = torch.empty((C_, out_len), dtype=torch.float64, device="cuda")
+    mix = torch.empty((2, out_len), dtype=torch.float64, device="cuda")
+    eng.process_device(dx.data_ptr(), n, n, dy.data_ptr(), out_len, out_len)
+    conv.mixdown_device(dy.data_ptr(), C_, out_len, out_len, mix.data_ptr())
+    torch.cuda.synchronize()
+    m = mix.cpu().numpy()
+    want = np.zeros((2, out_len))
+    for c in range(C_):
+        want[c % 2] += O.OverlapSave(ir[c % 2], 0).process(x[c])
+    for s in range(2):
+        assert rms(m[s], want[s]) < FFT_RMS_TOL * 4
+        assert np.max(np.abs(m[s] - want[s])) < 4e-9
 
 
 @pytest.mark.parametrize("hop,nseg", [(1024, 3), (8192, 4)])
@@ -326,3 +408,38 @@ def test_multi_segments_equal_one_call(gpu, hop, nseg):
         eng.process_device_segment(dx.data_ptr(), n, n, dy.data_ptr(), out_len, out_len, cuts[2], cuts[3])
     with pytest.raises(Exception):
         eng.process_device_segment(dx.data_ptr(), n, n, dy.data_ptr(), out_len, out_len, 1, cuts[1])
+
+
+def test_comm_mixdown_reduce_world1(gpu):
+    """ad_comm_* / ad_mixdown_reduce (the C-ABI RCCL mixdown) at
+    world size 1: the reduce to root 0 leaves k_mixdown's partial mix, both for
+    a contiguous [2][len] mix (one reduce) and a strided segment (two grouped
+    reduces), and a stereo group reduces its output rows in place."""
+    import torch
+
+    from algodsp import shard
+
+    comm = shard.Comm(0, 1, 0)
+    x = torch.from_numpy(np.stack([signals.white_noise(3000, c) for c in range(8)])).cuda()
+    xn = x.cpu().numpy()
+    mix = torch.full((2, 3000), np.nan, dtype=torch.float64, device="cuda")
+    s = torch.cuda.current_stream()
+    comm.mixdown_reduce(x.data_ptr(), 8, 3000, 3000, mix.data_ptr(), 3000, 0, 0, s.cuda_stream)
+    s.synchronize()
+    m = mix.cpu().numpy()
+    np.testing.assert_allclose(m[0], xn[0::2].sum(0), atol=1e-14)
+    np.testing.assert_allclose(m[1], xn[1::2].sum(0), atol=1e-14)
+    seg = torch.zeros((2, 3000), dtype=torch.float64, device="cuda")
+    comm.mixdown_reduce(x.data_ptr() + 8 * 1000, 3, 3000, 500, seg.data_ptr() + 8 * 1000, 3000, 1, 0, s.cuda_stream)
+    s.synchronize()
+    sg = seg.cpu().numpy()
+    np.testing.assert_allclose(sg[1, 1000:1500], (xn[0] + xn[2])[1000:1500], atol=1e-14)
+    np.testing.assert_allclose(sg[0, 1000:1500], xn[1][1000:1500], atol=1e-14)
+    assert not sg[:, :1000].any() and not sg[:, 1500:].any()
+    st = x[:2].clone()
+    comm.mixdown_reduce(0, 0, 3000, 3000, st.data_ptr(), 3000, 0, 0, s.cuda_stream)
+    s.synchronize()
+    np.testing.assert_array_equal(st.cpu().numpy(), xn[:2])
+    with pytest.raises(conv.ADError):
+        comm.mixdown_reduce(x.data_ptr(), 8, 3000, 3000, mix.data_ptr(), 3000, 0, 1, s.cuda_stream)  # root >= world
+    comm.close()

@@ -369,6 +369,35 @@ def test_fir_device_paths(gpu, taps):
     assert rms(dy.cpu().numpy()[1], O.Fir(h).process_block(x[1])) <= RMS_TOL
 
 
+def test_fir_mixed_streams(gpu):
+    """Calls on the NULL stream, a side stream and the host-buffer path, then
+    Reset, then more calls: the shared delay line is ordered across streams
+    (each call waits for the previous call's last operation), so the result
+    equals one sequential filter."""
+    import torch
+
+    h = signals.make_test_kernel(300)
+    C, n = 2, 4000
+    x = np.stack([signals.white_noise(n, 90 + c) for c in range(C)])
+    dx = torch.from_numpy(x).cuda()
+    dy = torch.zeros_like(dx)
+    side = torch.cuda.Stream()
+    f = P.Filter(h, channels=C)
+    for rep in range(2):
+        f.process_device(dx.data_ptr(), n, dy.data_ptr(), n, 1000, 0)
+        f.process_device(dx.data_ptr() + 8 * 1000, n, dy.data_ptr() + 8 * 1000, n, 1000, side.cuda_stream)
+        blk = x[:, 2000:2500].copy()
+        f.ProcessBlock(blk)
+        f.process_device(dx.data_ptr() + 8 * 2500, n, dy.data_ptr() + 8 * 2500, n, 1500, 0)
+        torch.cuda.synchronize()
+        got = dy.cpu().numpy()
+        got[:, 2000:2500] = blk
+        for c in range(C):
+            assert rms(got[c], O.Fir(h).process_block(x[c])) <= RMS_TOL
+        f.process_device(dx.data_ptr(), n, dy.data_ptr(), n, 700, side.cuda_stream)
+        f.Reset()
+
+
 def test_fir_block_to_and_reset(gpu):
     h = signals.make_test_kernel(40)
     x = signals.white_noise(500, 3)
