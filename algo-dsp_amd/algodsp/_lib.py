@@ -178,6 +178,12 @@ def _declare(L: C.CDLL) -> None:
         "ad_comm_rank": (C.c_int, [vp]),
         "ad_comm_size": (C.c_int, [vp]),
         "ad_mixdown_reduce": (C.c_int, [vp, vp, C.c_int, i64, i64, C.c_int, vp, i64, C.c_int, vp]),
+        "ad_conv_ols_process_multi": (C.c_int, [vp, C.POINTER(c_double_p), C.POINTER(c_double_p), C.c_int, i64]),
+        "ad_conv_multi_stream_create": (C.c_int, [c_double_p, C.c_int, i64, i64, C.c_int, C.POINTER(C.c_int32),
+                                                  C.c_int, C.POINTER(vp)]),
+        "ad_conv_multi_stream_process_block": (C.c_int, [vp, C.POINTER(c_double_p), C.POINTER(c_double_p), C.c_int,
+                                                         i64]),
+        "ad_conv_multi_stream_process_block_device": (C.c_int, [vp, vp, i64, vp, i64, vp]),
         "ad_conv_profile_enable": (C.c_int, [vp, C.c_int]),
         "ad_conv_profile_read": (C.c_int, [vp, c_double_p, c_int64_p, c_double_p]),
         "ad_compressor_default_config": (None, [C.POINTER(CompressorConfig), C.c_double]),

@@ -25,6 +25,7 @@ __all__ = [
     "Direct", "DirectCircular", "Convolve", "ConvolveMode",
     "NewStreamingOverlapSave", "NewStreamingOverlapAdd", "NewOverlapSave", "NewOverlapAdd",
     "NewPartitionedConvolution", "OverlapAddConvolve", "OverlapSaveConvolve", "MultiChannelConvolver",
+    "MultiChannelStreamingConvolver",
     "ErrDivisionByZero", "Correlate", "CorrelateDirect", "CorrelateMode", "AutoCorrelate", "AutoCorrelateNormalized",
     "CorrelateNormalized", "CorrelateFFT", "FindPeak", "LagFromIndex", "IndexFromLag",
     "DeconvNaive", "DeconvRegularized", "DeconvWiener", "DeconvOptions", "DefaultDeconvOptions", "Deconvolve",
@@ -270,6 +271,67 @@ class MultiChannelConvolver(_Handle):
         check(lib().ad_conv_multi_process_device_segment(self._h, C.c_void_p(d_in), in_stride, in_len,
                                                          C.c_void_p(d_out), out_stride, out_len, out_begin,
                                                          out_end, C.c_void_p(stream)))
+
+
+def _row_ptrs(a: np.ndarray):
+    """(c_double_p * rows) of a C-contiguous 2-D float64 array."""
+    rows = a.shape[0]
+    arr = (C.POINTER(C.c_double) * rows)()
+    base = a.ctypes.data
+    for r in range(rows):
+        arr[r] = C.cast(C.c_void_p(base + r * a.strides[0]), C.POINTER(C.c_double))
+    return arr
+
+
+def _process_host_multi(self, x) -> np.ndarray:
+    """OverlapSave.Process of every channel on host buffers
+    (ad_conv_ols_process_multi: chunked, PCIe overlapped with the compute)."""
+    xs = np.ascontiguousarray(np.asarray(x, dtype=np.float64))
+    if xs.ndim == 1:
+        xs = xs.reshape(1, -1)
+    out = np.empty((xs.shape[0], xs.shape[1] + self.kernel_len - 1), dtype=np.float64)
+    check(lib().ad_conv_ols_process_multi(self._h, _row_ptrs(xs), _row_ptrs(out), int(xs.shape[0]),
+                                          int(xs.shape[1])))
+    return out
+
+
+MultiChannelConvolver.process_host = _process_host_multi
+
+
+class MultiChannelStreamingConvolver(_Handle):
+    """`channels` StreamingOverlapSave instances in one handle (one launch per
+    engine kernel per block for all channels; the frequency-domain delay line
+    stays on the device): ad_conv_multi_stream_*."""
+
+    def __init__(self, kernels, block_size: int, channels: int, ir_index=None, device: int = DEVICE):
+        k = f64(kernels)
+        if k.ndim == 1:
+            k = k.reshape(1, -1)
+        n_ir, K = k.shape
+        irx = None
+        if ir_index is not None:
+            arr = (C.c_int32 * channels)(*[int(v) for v in ir_index])
+            irx = C.cast(arr, C.POINTER(C.c_int32))
+        h = C.c_void_p()
+        check(lib().ad_conv_multi_stream_create(ptr(k), int(n_ir), int(K), int(block_size), int(channels), irx,
+                                                int(device), C.byref(h)))
+        super().__init__(h)
+        self.channels = channels
+
+    def BlockSize(self) -> int:
+        return int(lib().ad_conv_block_size(self._h))
+
+    def ProcessBlock(self, x) -> np.ndarray:
+        """x: [channels][block] -> [channels][block] (host buffers)."""
+        xs = np.ascontiguousarray(np.asarray(x, dtype=np.float64))
+        out = np.empty_like(xs)
+        check(lib().ad_conv_multi_stream_process_block(self._h, _row_ptrs(xs), _row_ptrs(out), int(xs.shape[0]),
+                                                       int(xs.shape[1])))
+        return out
+
+    def process_block_device(self, d_in: int, in_stride: int, d_out: int, out_stride: int, stream: int = 0) -> None:
+        check(lib().ad_conv_multi_stream_process_block_device(self._h, C.c_void_p(d_in), int(in_stride),
+                                                              C.c_void_p(d_out), int(out_stride), C.c_void_p(stream)))
 
 
 def mixdown_device(d_chan: int, channels: int, stride: int, length: int, d_mix: int, stream: int = 0,

@@ -13,6 +13,7 @@
 
 #include "ad_common.hpp"
 #include "conv_kernels.hpp"
+#include "host_pipeline.hpp"
 #include "nupols_engine.hpp"
 #include "upols_engine.hpp"
 
@@ -20,7 +21,7 @@ using namespace adsp;
 
 namespace {
 
-enum class Kind { StreamOLS, StreamOLA, BatchOLS, BatchOLA, Partitioned, Multi };
+enum class Kind { StreamOLS, StreamOLA, BatchOLS, BatchOLA, Partitioned, Multi, MultiStream };
 
 struct StageDesc {
   int64_t part_size;
@@ -84,6 +85,8 @@ struct ad_conv {
   std::vector<StageDesc> stages;
 
   std::unique_ptr<Upols> eng;  // FFT path
+  std::unique_ptr<HostPipeline> pipe;  // overlapped host-buffer offline calls
+  int channels = 1;
   int64_t hop = 0;
   int64_t seg_next = -1;  // next out_begin of a segmented offline call (-1: none open)
 
@@ -120,6 +123,7 @@ struct ad_conv {
   int64_t ylin_base = 0;         // linear-conv index of ylin.front()
 
   ~ad_conv() {
+    pipe.reset();
     if (done) {
       (void)hipEventSynchronize(done);
       (void)hipEventDestroy(done);
@@ -253,16 +257,17 @@ void stream_convolve(ad_conv* h, const double* in, int64_t n, double* out) {
   std::memcpy(out, h->pin_out, n * sizeof(double));
 }
 
-// Offline full convolution of one channel with the handle's kernel.
+// Offline full convolution of host channels with the handle's kernel(s):
+// chunked and overlapped across PCIe (host_pipeline.hpp).
+void batch_convolve_multi(ad_conv* h, const double* const* in, int C, int64_t n, double* const* out,
+                          int64_t out_len) {
+  if (!h->pipe) h->pipe.reset(new HostPipeline(h->device));
+  order_after_last(h, h->stream);
+  h->pipe->offline(*h->eng, in, C, n, out, out_len, h->stream);
+  mark_last(h, h->stream);
+}
 void batch_convolve(ad_conv* h, const double* in, int64_t n, double* out, int64_t out_len) {
-  hipStream_t s = h->stream;
-  h->din.reserve((size_t)n);
-  h->dout.reserve((size_t)out_len);
-  AD_HIP(hipMemcpyAsync(h->din.p, in, n * sizeof(double), hipMemcpyHostToDevice, s));
-  h->eng->begin_offline(s);
-  h->eng->run(h->din.p, n, n, h->dout.p, out_len, out_len, /*use_hist=*/false, s);
-  AD_HIP(hipMemcpyAsync(out, h->dout.p, out_len * sizeof(double), hipMemcpyDeviceToHost, s));
-  AD_HIP(hipStreamSynchronize(s));
+  batch_convolve_multi(h, &in, 1, n, &out, out_len);
 }
 
 int64_t batch_hop(int64_t K) {
@@ -682,6 +687,7 @@ int ad_conv_multi_create(const double* kernels, int n_ir, int64_t K, int64_t hop
     h->hop = hop;
     h->block_size = hop;
     h->fft_size = 2 * hop;
+    h->channels = channels;
     h->eng.reset(new Upols(dev, kernels, n_ir, K, (int)hop, channels, ir_index, (int)max_chunk_blocks, h->stream));
     return h.release();
   });
@@ -726,6 +732,117 @@ int ad_conv_multi_process_device_segment(ad_conv* h, const double* d_in, int64_t
                 (out_end + L - 1) / L);
     mark_last(h, s);
     h->seg_next = out_end < out_len ? out_end : -1;
+  });
+}
+
+int ad_conv_ols_process_multi(ad_conv* h, const double* const* in, double* const* out, int channels, int64_t n) {
+  // OverlapSave.Process (overlap_save.go:126-254) of every channel of a
+  // multi-channel handle, host buffers in and out (n + K - 1 samples each)
+  return guard([&] {
+    if (!h || h->kind != Kind::Multi) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "not a multi-channel convolver");
+    if (channels != h->channels)
+      AD_FAIL(AD_ERR_LENGTH_MISMATCH, "conv: channel count mismatch: handle has " + std::to_string(h->channels) +
+                                          ", got " + std::to_string(channels));
+    if (n <= 0) AD_FAIL(AD_ERR_EMPTY_INPUT, "conv: empty input");
+    if (!in || !out) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "null channel pointer array");
+    for (int c = 0; c < channels; ++c)
+      if (!in[c] || !out[c]) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "null channel buffer");
+    DeviceScope ds(h->device);
+    h->seg_next = -1;
+    batch_convolve_multi(h, in, channels, n, out, n + h->K - 1);
+  });
+}
+
+// --- multi-channel streaming (persistent frequency-domain delay line) --------
+
+int ad_conv_multi_stream_create(const double* kernels, int n_ir, int64_t K, int64_t block_size, int channels,
+                                const int32_t* ir_index, int device, ad_conv** out) {
+  // NewStreamingOverlapSave (streaming_overlap_save.go:45-84) for `channels`
+  // channels sharing n_ir kernels: one handle, one launch per kernel per block
+  return create_guarded(out, [&]() -> ad_conv* {
+    if (K <= 0 || !kernels || n_ir <= 0) AD_FAIL(AD_ERR_EMPTY_KERNEL, "conv: empty kernel");
+    if (block_size <= 0)
+      AD_FAIL(AD_ERR_INVALID_ARGUMENT, "conv: blockSize must be positive, got " + std::to_string(block_size));
+    if (channels <= 0) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "channels must be positive");
+    const int64_t hop = largest_pow2_divisor(block_size, 8192);
+    if (hop < 64)
+      AD_FAIL(AD_ERR_INVALID_BLOCK_SIZE, "multi-channel streaming needs a block size with a power-of-two divisor "
+                                         ">= 64, got " + std::to_string(block_size));
+    const int dev = pick_device(device);
+    DeviceScope ds(dev);
+    std::unique_ptr<ad_conv> h(new_handle(Kind::MultiStream, dev));
+    h->K = K;
+    h->hop = hop;
+    h->block_size = block_size;
+    h->fft_size = next_pow2(block_size + K - 1);  // FFTSize() of the reference streaming convolver
+    h->channels = channels;
+    const int jc = (int)std::max<int64_t>(1, std::min<int64_t>(block_size / hop, 4096));
+    h->eng.reset(new Upols(dev, kernels, n_ir, K, (int)hop, channels, ir_index, jc, h->stream));
+    h->eng->reset_stream(h->stream);
+    AD_HIP(hipStreamSynchronize(h->stream));
+    return h.release();
+  });
+}
+
+int ad_conv_multi_stream_process_block_device(ad_conv* h, const double* d_in, int64_t in_stride, double* d_out,
+                                              int64_t out_stride, void* stream) {
+  // ProcessBlockTo (streaming_overlap_save.go:152-164) for every channel;
+  // device buffers [channels][stride], block_size samples each
+  return guard([&] {
+    if (!h || h->kind != Kind::MultiStream)
+      AD_FAIL(AD_ERR_INVALID_ARGUMENT, "not a multi-channel streaming convolver");
+    if (!d_in || !d_out) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "null device buffer");
+    const int64_t B = h->block_size;
+    if (in_stride < B || out_stride < B) AD_FAIL(AD_ERR_LENGTH_MISMATCH, "conv: stride shorter than the block");
+    DeviceScope ds(h->device);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    order_after_last(h, s);
+    h->eng->run(d_in, in_stride, B, d_out, out_stride, B, /*use_hist=*/true, s);
+    mark_last(h, s);
+  });
+}
+
+int ad_conv_multi_stream_process_block(ad_conv* h, const double* const* in, double* const* out, int channels,
+                                       int64_t n) {
+  // ProcessBlockTo for every channel, host buffers (copied through pinned
+  // staging inside the call; returns when the output is on the host)
+  return guard([&] {
+    if (!h || h->kind != Kind::MultiStream)
+      AD_FAIL(AD_ERR_INVALID_ARGUMENT, "not a multi-channel streaming convolver");
+    if (channels != h->channels)
+      AD_FAIL(AD_ERR_LENGTH_MISMATCH, "conv: channel count mismatch: handle has " + std::to_string(h->channels) +
+                                          ", got " + std::to_string(channels));
+    if (n != h->block_size)
+      AD_FAIL(AD_ERR_LENGTH_MISMATCH, "conv: buffer length mismatch: expected " + std::to_string(h->block_size) +
+                                          " input samples, got " + std::to_string(n));
+    if (!in || !out) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "null channel pointer array");
+    for (int c = 0; c < channels; ++c)
+      if (!in[c] || !out[c]) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "null channel buffer");
+    DeviceScope ds(h->device);
+    const size_t cnt = (size_t)channels * n;
+    if (h->pin_n < cnt) {
+      if (h->pin_in) AD_HIP(hipHostFree(h->pin_in));
+      if (h->pin_out) AD_HIP(hipHostFree(h->pin_out));
+      h->pin_in = h->pin_out = nullptr;
+      h->pin_n = 0;
+      AD_HIP(hipHostMalloc(reinterpret_cast<void**>(&h->pin_in), cnt * sizeof(double), hipHostMallocDefault));
+      AD_HIP(hipHostMalloc(reinterpret_cast<void**>(&h->pin_out), cnt * sizeof(double), hipHostMallocDefault));
+      h->pin_n = cnt;
+    }
+    h->din.reserve(cnt);
+    h->dout.reserve(cnt);
+    hipStream_t s = h->stream;
+    order_after_last(h, s);
+    const int workers = cnt >= ((size_t)1 << 16) ? 8 : 0;
+    parallel_for(channels, [&](int64_t c) { std::memcpy(h->pin_in + c * n, in[c], (size_t)n * sizeof(double)); },
+                 workers);
+    AD_HIP(hipMemcpyAsync(h->din.p, h->pin_in, cnt * sizeof(double), hipMemcpyHostToDevice, s));
+    h->eng->run(h->din.p, n, n, h->dout.p, n, n, /*use_hist=*/true, s);
+    AD_HIP(hipMemcpyAsync(h->pin_out, h->dout.p, cnt * sizeof(double), hipMemcpyDeviceToHost, s));
+    mark_last(h, s);
+    AD_HIP(hipStreamSynchronize(s));
+    parallel_for(channels, [&](int64_t c) { std::memcpy(out[c], h->pin_out + c * n, (size_t)n * sizeof(double)); },
+                 workers);
   });
 }
 

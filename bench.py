@@ -40,6 +40,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-sample", type=int, default=1 << 24, help="samples per channel (per host thread) for the CPU leg")
     p.add_argument("--mixdown", choices=["auto", "on", "off"], default="auto")
+    p.add_argument("--host-io", choices=["on", "off"], default="on",
+                   help="N = 1: also time the same step host buffer -> host buffer (PCIe included)")
     p.add_argument("--pipeline", choices=["on", "off"], default="on",
                    help="N > 1: overlap step i's mixdown reduce with step i+1's convolution (two output buffers)")
     p.add_argument("--segments", type=int, default=1,
@@ -335,6 +337,24 @@ def main():
                   "tolerance_rms": 1e-7}
         if parity["rms"] > 1e-7:
             print(f"bench.py: PARITY FAILURE {parity}", file=sys.stderr)
+        host_io = None
+        if world == 1 and args.host_io == "on":
+            # the same step from HOST buffers to HOST buffers through the C ABI
+            # (ad_conv_ols_process_multi: chunked pinned staging, H2D || UPOLS ||
+            # D2H on three streams) -- PCIe included, not the metric
+            eng.process_host(x_host)  # warm-up (pinned buffers, device scratch)
+            reps = 3
+            th = time.perf_counter()
+            for _ in range(reps):
+                yh = eng.process_host(x_host)
+            dth = (time.perf_counter() - th) / reps
+            hd = ys[last].cpu().numpy() if not mixdown else None
+            host_io = {"value": round(C * n / dth / 1e6, 3), "unit": "Msamples/s", "ms_per_call": round(dth * 1e3, 3),
+                       "bytes_per_sample_pcie": 8 + 8 * out_len / n,
+                       "equals_device_result": bool(hd is not None and np.array_equal(yh, hd)),
+                       "note": "host buffer in -> host buffer out per call (ad_conv_ols_process_multi), "
+                               "PCIe + host copies included; wall time"}
+            del yh, hd
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(ir, args.cpu_sample)
@@ -390,6 +410,7 @@ def main():
             "kernels": {k: {kk: (round(vv, 3) if isinstance(vv, float) else vv) for kk, vv in v.items()}
                         for k, v in kernels.items()},
             "parity": parity,
+            "host_io": host_io,
             "cpu_baseline": cpu,
         }
         if cpu:

@@ -158,6 +158,31 @@ int ad_conv_multi_process_device(ad_conv* h, const double* d_in, int64_t in_stri
 int ad_conv_multi_process_device_segment(ad_conv* h, const double* d_in, int64_t in_stride, int64_t in_len,
                                          double* d_out, int64_t out_stride, int64_t out_len, int64_t out_begin,
                                          int64_t out_end, void* stream);
+/* OverlapSave.Process / ProcessTo (overlap_save.go:126-272) of every channel
+ * of a multi-channel handle on HOST buffers: in[c] holds n samples, out[c]
+ * receives n + kernel_len - 1.  The signal crosses PCIe in chunks through
+ * pinned double buffers, overlapping H2D of chunk i+1, the convolution of
+ * chunk i and D2H of chunk i-1 (three streams); bit-identical to the device
+ * call.  channels must equal the handle's (else AD_ERR_LENGTH_MISMATCH).    */
+int ad_conv_ols_process_multi(ad_conv* h, const double* const* in, double* const* out, int channels, int64_t n);
+
+/* ---- multi-channel streaming convolver ----------------------------------
+ * `channels` StreamingOverlapSave instances (streaming_overlap_save.go:45-184)
+ * sharing n_ir kernels (ir_index[c], NULL: c % n_ir) in one handle: each
+ * block call runs every channel with ONE launch per engine kernel, the
+ * frequency-domain delay line and input history stay on the device between
+ * calls (config 4 real-time form: 64 reverb channels, block by block).
+ * block_size needs a power-of-two divisor >= 64 (the hop).  Zero latency:
+ * out = the newest block_size samples of each channel's linear convolution.
+ * Reset / getters: ad_conv_reset, ad_conv_block_size, ad_conv_fft_size.   */
+int ad_conv_multi_stream_create(const double* kernels, int n_ir, int64_t kernel_len, int64_t block_size,
+                                int channels, const int32_t* ir_index, int device, ad_conv** out);
+/* host buffers: in[c], out[c] of n == block_size samples (else AD_ERR_LENGTH_MISMATCH) */
+int ad_conv_multi_stream_process_block(ad_conv* h, const double* const* in, double* const* out, int channels,
+                                       int64_t n);
+/* device buffers [channels][stride]; asynchronous on `stream` */
+int ad_conv_multi_stream_process_block_device(ad_conv* h, const double* d_in, int64_t in_stride, double* d_out,
+                                              int64_t out_stride, void* stream);
 /* Live kernel timing (HIP events recorded around every launch on the launch
  * stream) for the FFT engine of a handle.  Kernel index: 0 window rFFT,
  * 1 frequency-domain delay-line MAC, 2 inverse rFFT + overlap-save store.

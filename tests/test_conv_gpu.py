@@ -443,3 +443,74 @@ def test_comm_mixdown_reduce_world1(gpu):
     with pytest.raises(conv.ADError):
         comm.mixdown_reduce(x.data_ptr(), 8, 3000, 3000, mix.data_ptr(), 3000, 0, 1, s.cuda_stream)  # root >= world
     comm.close()
+
+
+# ------------------------------------------------- host-buffer multichannel
+def test_process_host_multi_chunked(gpu):
+    """ad_conv_ols_process_multi (host buffers, chunked PCIe pipeline): several
+    16 MiB chunks per call, bit-identical to the device-resident call and
+    within the FFT tolerance of the oracle's OverlapSave.Process."""
+    ir = irlib.large_church()
+    K = ir.shape[1]
+    n = 2_500_000  # > 2 chunks of 2^20 samples per channel at 2 channels
+    x = np.stack([signals.white_noise(n, 0x5EED + c) for c in range(2)])
+    eng = conv.MultiChannelConvolver(ir, hop=8192, channels=2)
+    got = eng.process_host(x)
+    assert got.shape == (2, n + K - 1)
+    dev, _ = _multi_run(ir, x, hop=8192)
+    np.testing.assert_array_equal(got, dev)
+    want = O.OverlapSave(ir[1], 0).process(x[1])
+    assert rms(got[1], want) < FFT_RMS_TOL and np.max(np.abs(got[1] - want)) < 1e-9
+    # second call on the same handle, shorter signal (one chunk)
+    got2 = eng.process_host(x[:, :50_000])
+    np.testing.assert_allclose(got2[0], O.OverlapSave(ir[0], 0).process(x[0, :50_000]), atol=1e-9)
+    with pytest.raises(conv.ErrLengthMismatch):
+        eng.process_host(x[:1, :1000])
+
+
+def test_batch_process_many_chunks(gpu):
+    """OverlapSave.Process on a host buffer longer than several pipeline chunks
+    (C = 1: 2^21 samples per chunk) against the oracle."""
+    h = irlib.large_church()[0, :16384]
+    n = 5_000_000
+    x = signals.white_noise(n, 11)
+    got = conv.NewOverlapSave(h, 0).Process(x)
+    want = O.OverlapSave(h, 0).process(x)
+    assert rms(got, want) < FFT_RMS_TOL and np.max(np.abs(got - want)) < 1e-9
+
+
+@pytest.mark.parametrize("K,B", [(16384, 4096), (3000, 512), (131072, 8192)])
+def test_multi_stream_vs_oracle(gpu, K, B):
+    """ad_conv_multi_stream_*: 5 channels x n_ir kernels, block by block, host
+    and device calls interleaved, Reset; each channel against the oracle's
+    StreamingOverlapSave (streaming_overlap_save.go:100-164)."""
+    import torch
+
+    irs = np.stack([signals.make_test_kernel(K), irlib.large_church()[1, :K]])
+    ir_index = [1, 0, 0, 1, 1]
+    C_, nb = 5, 5
+    x = np.stack([signals.white_noise(B * nb, 70 + c) for c in range(C_)])
+    s = conv.MultiChannelStreamingConvolver(irs, B, C_, ir_index=ir_index)
+    assert s.BlockSize() == B and s.FFTSize() == O.Streaming(irs[0], B).fft_size()
+    dx = torch.from_numpy(x).cuda()
+    dy = torch.zeros_like(dx)
+    for rep in range(2):
+        got = np.empty_like(x)
+        for i in range(nb):
+            if i % 2:
+                st = torch.cuda.current_stream()
+                s.process_block_device(dx.data_ptr() + 8 * i * B, B * nb, dy.data_ptr() + 8 * i * B, B * nb,
+                                       st.cuda_stream)
+                st.synchronize()
+                got[:, i * B:(i + 1) * B] = dy.cpu().numpy()[:, i * B:(i + 1) * B]
+            else:
+                got[:, i * B:(i + 1) * B] = s.ProcessBlock(x[:, i * B:(i + 1) * B])
+        for c in range(C_):
+            o = O.Streaming(irs[ir_index[c]], B)
+            want = np.concatenate([o.process_block(x[c, i * B:(i + 1) * B]) for i in range(nb)])
+            assert rms(got[c], want) < FFT_RMS_TOL and np.max(np.abs(got[c] - want)) < 1e-9
+        s.Reset()
+    with pytest.raises(conv.ErrLengthMismatch):
+        s.ProcessBlock(x[:, :B - 1])
+    with pytest.raises(conv.ErrLengthMismatch):
+        s.ProcessBlock(x[:4, :B])
