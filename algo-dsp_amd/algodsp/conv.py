@@ -283,13 +283,18 @@ def _row_ptrs(a: np.ndarray):
     return arr
 
 
-def _process_host_multi(self, x) -> np.ndarray:
+def _process_host_multi(self, x, out: np.ndarray | None = None) -> np.ndarray:
     """OverlapSave.Process of every channel on host buffers
-    (ad_conv_ols_process_multi: chunked, PCIe overlapped with the compute)."""
+    (ad_conv_ols_process_multi: chunked, PCIe overlapped with the compute);
+    `out` ([C][n+K-1] float64, C-contiguous) is reused when given (ProcessTo)."""
     xs = np.ascontiguousarray(np.asarray(x, dtype=np.float64))
     if xs.ndim == 1:
         xs = xs.reshape(1, -1)
-    out = np.empty((xs.shape[0], xs.shape[1] + self.kernel_len - 1), dtype=np.float64)
+    shape = (xs.shape[0], xs.shape[1] + self.kernel_len - 1)
+    if out is None:
+        out = np.empty(shape, dtype=np.float64)
+    elif out.shape != shape or out.dtype != np.float64 or not out.flags.c_contiguous:
+        raise ErrLengthMismatch(3, f"conv: output must be a C-contiguous float64 array of shape {shape}")
     check(lib().ad_conv_ols_process_multi(self._h, _row_ptrs(xs), _row_ptrs(out), int(xs.shape[0]),
                                           int(xs.shape[1])))
     return out

@@ -5,6 +5,7 @@
 #include "host_pipeline.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 #include <condition_variable>
 #include <cstring>
 #include <deque>
@@ -93,6 +94,14 @@ class Pool {
   bool stop_ = false;
 };
 
+int copy_workers() {
+  static const int w = [] {
+    const char* v = std::getenv("AD_PIPE_WORKERS");
+    return v && *v ? std::max(0, std::atoi(v)) : 8;
+  }();
+  return w;
+}
+
 // Copies a [C][len] column range between the caller's per-channel buffers and
 // a packed [C][len] pinned buffer, split into ~1 MiB pieces over the pool.
 void copy_in(double* pin, const double* const* in, int C, int64_t col0, int64_t len) {
@@ -102,7 +111,7 @@ void copy_in(double* pin, const double* const* in, int C, int64_t col0, int64_t 
     const int c = (int)(k / per);
     const int64_t a = (k % per) * piece, b = std::min(len, a + piece);
     std::memcpy(pin + (int64_t)c * len + a, in[c] + col0 + a, (size_t)(b - a) * sizeof(double));
-  });
+  }, copy_workers());
 }
 void copy_out(double* const* out, const double* pin, int C, int64_t col0, int64_t len) {
   const int64_t piece = int64_t(1) << 17;
@@ -111,7 +120,7 @@ void copy_out(double* const* out, const double* pin, int C, int64_t col0, int64_
     const int c = (int)(k / per);
     const int64_t a = (k % per) * piece, b = std::min(len, a + piece);
     std::memcpy(out[c] + col0 + a, pin + (int64_t)c * len + a, (size_t)(b - a) * sizeof(double));
-  });
+  }, copy_workers());
 }
 
 }  // namespace
@@ -159,10 +168,58 @@ void HostPipeline::ensure_pinned(int64_t doubles) {
   pin_cap_ = doubles;
 }
 
+namespace {
+// AD_PIPE_MODE: "stage" (pinned staging + host memcpy), "register" (page-lock
+// the caller's buffers for the call and DMA straight from / to them), or
+// "auto" (register calls of >= 64 MiB, stage smaller ones).
+int pipe_mode() {
+  static const int m = [] {
+    const char* v = std::getenv("AD_PIPE_MODE");
+    if (v && !std::strcmp(v, "stage")) return 0;
+    if (v && !std::strcmp(v, "register")) return 1;
+    return 2;
+  }();
+  return m;
+}
+
+// Page-locks [p, p + bytes) for the scope of one call (hipHostRegister);
+// `ok` is false when the runtime refuses, and the caller then stages.
+struct Registration {
+  std::vector<void*> ptrs;
+  bool ok = true;
+  void add(const void* p, size_t bytes) {
+    if (!ok) return;
+    if (hipHostRegister(const_cast<void*>(p), bytes, hipHostRegisterDefault) != hipSuccess) {
+      (void)hipGetLastError();
+      ok = false;
+      return;
+    }
+    ptrs.push_back(const_cast<void*>(p));
+  }
+  ~Registration() {
+    for (void* p : ptrs) (void)hipHostUnregister(p);
+  }
+};
+}  // namespace
+
 void HostPipeline::offline(Upols& eng, const double* const* in, int C, int64_t n, double* const* out,
                            int64_t out_len, hipStream_t s) {
   const int64_t L = eng.hop();
   if (C != eng.channels()) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "channel count differs from the engine's");
+  const int mode = pipe_mode();
+  const int64_t bytes = (int64_t)C * (n + out_len) * 8;
+  if (mode == 1 || (mode == 2 && bytes >= (int64_t(64) << 20))) {
+    Registration reg;
+    for (int c = 0; c < C && reg.ok; ++c) {
+      reg.add(in[c], (size_t)n * sizeof(double));
+      if (static_cast<const void*>(out[c]) != static_cast<const void*>(in[c]))
+        reg.add(out[c], (size_t)out_len * sizeof(double));
+    }
+    if (reg.ok) {
+      offline_direct(eng, in, C, n, out, out_len, s);
+      return;
+    }
+  }
   // chunk: S input samples per channel (a multiple of L), C*S doubles <= kChunkBytes
   int64_t S = std::max<int64_t>(L, (kChunkBytes / 8 / C) / L * L);
   S = std::min(S, (n + L - 1) / L * L);  // small calls: small pinned buffers
@@ -232,6 +289,44 @@ void HostPipeline::offline(Upols& eng, const double* const* in, int C, int64_t n
   }
   while (!pending.empty()) drain_one();
   // nothing of this call may still read din_/dout_ when the next call starts
+  AD_HIP(hipStreamSynchronize(s_in_));
+}
+
+// Registered form: the caller's pages are locked for this call, so the chunks
+// go straight between them and the device (no host memcpy).  Same chunking
+// and stream overlap as the staged form.
+void HostPipeline::offline_direct(Upols& eng, const double* const* in, int C, int64_t n, double* const* out,
+                                  int64_t out_len, hipStream_t s) {
+  const int64_t L = eng.hop();
+  int64_t S = std::max<int64_t>(L, (kChunkBytes / 8 / C) / L * L);
+  S = std::min(S, (n + L - 1) / L * L);
+  const int64_t nblocks = (out_len + L - 1) / L;
+  din_.reserve((size_t)C * n);
+  dout_.reserve((size_t)C * out_len);
+  eng.begin_offline(s);
+  const int64_t nin = (n + S - 1) / S;
+  int64_t jdone = 0, out_issued = 0;
+  for (int64_t i = 0; i < nin; ++i) {
+    const int64_t c0 = i * S, len = std::min(S, n - c0);
+    for (int c = 0; c < C; ++c)
+      AD_HIP(hipMemcpyAsync(din_.p + (int64_t)c * n + c0, in[c] + c0, (size_t)len * sizeof(double),
+                            hipMemcpyHostToDevice, s_in_));
+    AD_HIP(hipEventRecord(ev_in_[0], s_in_));
+    const int64_t je = (i == nin - 1) ? nblocks : std::min(nblocks, (c0 + len) / L);
+    if (je > jdone) {
+      AD_HIP(hipStreamWaitEvent(s, ev_in_[0], 0));
+      eng.run(din_.p, n, n, dout_.p, out_len, out_len, /*use_hist=*/false, s, jdone, je);
+      AD_HIP(hipEventRecord(ev_comp_, s));
+      jdone = je;
+      const int64_t upto = std::min(out_len, je * L);
+      AD_HIP(hipStreamWaitEvent(s_out_, ev_comp_, 0));
+      for (int c = 0; c < C; ++c)
+        AD_HIP(hipMemcpyAsync(out[c] + out_issued, dout_.p + (int64_t)c * out_len + out_issued,
+                              (size_t)(upto - out_issued) * sizeof(double), hipMemcpyDeviceToHost, s_out_));
+      out_issued = upto;
+    }
+  }
+  AD_HIP(hipStreamSynchronize(s_out_));
   AD_HIP(hipStreamSynchronize(s_in_));
 }
 

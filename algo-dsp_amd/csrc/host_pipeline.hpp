@@ -55,6 +55,8 @@ class HostPipeline {
   hipEvent_t ev_out_[2] = {nullptr, nullptr};   // D2H of slot done (pin_out filled)
   DevBuf<double> din_, dout_;
   void ensure_pinned(int64_t doubles);
+  void offline_direct(Upols& eng, const double* const* in, int C, int64_t n, double* const* out, int64_t out_len,
+                      hipStream_t s_comp);
 };
 
 }  // namespace adsp

@@ -6,8 +6,10 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 if [ "${SKIP_TESTS:-0}" != "1" ]; then
+  KARGS=()
+  if [ -n "${PYTEST_K:-}" ]; then KARGS=(-k "$PYTEST_K"); fi
   timeout -k 10 ${PYTEST_TIMEOUT:-600} python -u -m pytest tests -m gpu -x -q -p no:cacheprovider \
-    --timeout 180 --timeout-method thread ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1
+    --timeout 180 --timeout-method thread "${KARGS[@]}" > gpurun_out/pytest_gpu.log 2>&1
   rc=$?
   echo "pytest rc=$rc"; tail -30 gpurun_out/pytest_gpu.log
   if [ $rc -ne 0 ]; then exit $rc; fi
