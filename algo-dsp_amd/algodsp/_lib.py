@@ -184,6 +184,11 @@ def _declare(L: C.CDLL) -> None:
         "ad_conv_multi_stream_process_block": (C.c_int, [vp, C.POINTER(c_double_p), C.POINTER(c_double_p), C.c_int,
                                                          i64]),
         "ad_conv_multi_stream_process_block_device": (C.c_int, [vp, vp, i64, vp, i64, vp]),
+        "ad_conv_pc_multi_create": (C.c_int, [c_double_p, i64, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(vp)]),
+        "ad_conv_pc_multi_process_device": (C.c_int, [vp, vp, i64, vp, i64, i64, vp]),
+        "ad_conv_reverb_multi_create": (C.c_int, [c_double_p, i64, C.c_int, C.c_int, C.c_int, C.POINTER(vp)]),
+        "ad_conv_reverb_multi_process_device": (C.c_int, [vp, vp, i64, i64, vp]),
+        "ad_conv_reverb_multi_process": (C.c_int, [vp, c_double_p, i64]),
         "ad_conv_profile_enable": (C.c_int, [vp, C.c_int]),
         "ad_conv_profile_read": (C.c_int, [vp, c_double_p, c_int64_p, c_double_p]),
         "ad_compressor_default_config": (None, [C.POINTER(CompressorConfig), C.c_double]),

@@ -25,7 +25,7 @@ __all__ = [
     "Direct", "DirectCircular", "Convolve", "ConvolveMode",
     "NewStreamingOverlapSave", "NewStreamingOverlapAdd", "NewOverlapSave", "NewOverlapAdd",
     "NewPartitionedConvolution", "OverlapAddConvolve", "OverlapSaveConvolve", "MultiChannelConvolver",
-    "MultiChannelStreamingConvolver",
+    "MultiChannelStreamingConvolver", "PartitionedConvolutionMulti", "NewConvolutionReverbMulti",
     "ErrDivisionByZero", "Correlate", "CorrelateDirect", "CorrelateMode", "AutoCorrelate", "AutoCorrelateNormalized",
     "CorrelateNormalized", "CorrelateFFT", "FindPeak", "LagFromIndex", "IndexFromLag",
     "DeconvNaive", "DeconvRegularized", "DeconvWiener", "DeconvOptions", "DefaultDeconvOptions", "Deconvolve",
@@ -186,6 +186,54 @@ def NewConvolutionReverb(kernel, minBlockOrder: int) -> ConvolutionReverb:
     """convolution.go:28-44 (maxBlockOrder fixed at 13, wet = dry = 1)"""
     k = f64(kernel)
     return ConvolutionReverb(_create(lib().ad_conv_reverb_create, ptr(k), k.size, int(minBlockOrder), DEVICE))
+
+
+class PartitionedConvolutionMulti(_Handle):
+    """`channels` PartitionedConvolution instances sharing one IR, device
+    resident (ad_conv_pc_multi_*): one launch per engine kernel per stage
+    per call for all channels."""
+
+    def __init__(self, kernel, minBlockOrder: int, maxBlockOrder: int, channels: int, device: int = DEVICE,
+                 reverb: bool = False):
+        k = f64(kernel)
+        h = C.c_void_p()
+        if reverb:
+            check(lib().ad_conv_reverb_multi_create(ptr(k), k.size, int(minBlockOrder), int(channels), int(device),
+                                                    C.byref(h)))
+        else:
+            check(lib().ad_conv_pc_multi_create(ptr(k), k.size, int(minBlockOrder), int(maxBlockOrder), int(channels),
+                                                int(device), C.byref(h)))
+        super().__init__(h)
+        self.channels = channels
+
+    def Latency(self) -> int:
+        return int(lib().ad_conv_latency(self._h))
+
+    def StageCount(self) -> int:
+        return int(lib().ad_conv_stage_count(self._h))
+
+    def process_device(self, d_in: int, in_stride: int, d_out: int, out_stride: int, n: int, stream: int = 0):
+        check(lib().ad_conv_pc_multi_process_device(self._h, C.c_void_p(d_in), int(in_stride), C.c_void_p(d_out),
+                                                    int(out_stride), int(n), C.c_void_p(stream)))
+
+    # ConvolutionReverb form
+    def SetWetDry(self, wet: float, dry: float) -> None:
+        check(lib().ad_conv_reverb_set_wet_dry(self._h, float(wet), float(dry)))
+
+    def ProcessInPlace(self, block: np.ndarray) -> None:
+        """block [channels][n] float64 (host), dry*block + wet*reverb in place."""
+        if not (isinstance(block, np.ndarray) and block.dtype == np.float64 and block.flags.c_contiguous):
+            raise TypeError("block must be a C-contiguous float64 array")
+        check(lib().ad_conv_reverb_multi_process(self._h, ptr(block), block.shape[-1]))
+
+    def process_inplace_device(self, d_buf: int, stride: int, n: int, stream: int = 0) -> None:
+        check(lib().ad_conv_reverb_multi_process_device(self._h, C.c_void_p(d_buf), int(stride), int(n),
+                                                        C.c_void_p(stream)))
+
+
+def NewConvolutionReverbMulti(kernel, minBlockOrder: int, channels: int) -> PartitionedConvolutionMulti:
+    """NewConvolutionReverb (convolution.go:28-44) x channels, one handle."""
+    return PartitionedConvolutionMulti(kernel, minBlockOrder, 13, channels, reverb=True)
 
 
 def Direct(a, b) -> np.ndarray:

@@ -33,7 +33,7 @@ INPUT_NODE_ID = "_input"  # graph.go:10-13
 OUTPUT_NODE_ID = "_output"
 NODE_TYPE_SPLIT_FREQ = "split-freq"
 
-FXN_INPUT, FXN_OUTPUT, FXN_PASS, FXN_SPLIT_FREQ, FXN_BIQUAD, FXN_COMPRESSOR, FXN_FREEVERB = range(7)
+FXN_INPUT, FXN_OUTPUT, FXN_PASS, FXN_SPLIT_FREQ, FXN_BIQUAD, FXN_COMPRESSOR, FXN_FREEVERB, FXN_CONV_REVERB = range(8)
 MAX_PARENTS = 8
 
 FILTER_TYPES = ("filter", "filter-lowpass", "filter-highpass", "filter-bandpass", "filter-notch",
@@ -54,7 +54,9 @@ class _Node(C.Structure):
                 ("sections", C.POINTER(C.c_double)), ("nsec", C.c_int),
                 ("sections2", C.POINTER(C.c_double)), ("nsec2", C.c_int),
                 ("comp", C.POINTER(CompressorConfig)), ("verb", C.c_double * 5),
-                ("dyn_mode", C.c_int), ("dyn_range_db", C.c_double), ("dyn_hold_ms", C.c_double)]
+                ("dyn_mode", C.c_int), ("dyn_range_db", C.c_double), ("dyn_hold_ms", C.c_double),
+                ("ir", C.POINTER(C.c_double)), ("ir_len", C.c_int64), ("conv_min_order", C.c_int),
+                ("conv_wet", C.c_double), ("conv_dry", C.c_double)]
 
 
 def clamp(v, lo, hi):  # core.Clamp
@@ -249,13 +251,41 @@ def split_freq_sections(p: Params, fs: float):
     return xo
 
 
-class Chain:
-    """effectchain.Chain for `channels` independent channels of one graph."""
+def conv_reverb_kernel(p: Params, provider):
+    """convReverbRuntime.Configure (runtime_misc.go:18-58): the IR at irIndex
+    (default 0), stereo averaged to mono ((ch0 + ch1) * 0.5 over the shorter
+    length, ch0's tail kept), and the wet level (default 0.35; dry 1.0).
+    None when there is no provider or no such IR: the runtime then has no
+    engine and Process leaves the block untouched (a pass-through node)."""
+    ir_index = int(p.GetNum("irIndex", 0))
+    wet = p.GetNum("wet", 0.35)
+    if provider is None:
+        return None
+    samples, _fs, ok = provider.GetIR(ir_index)
+    if not ok or samples is None or len(samples) == 0:
+        return None
+    ch0 = np.asarray(samples[0], dtype=np.float64)
+    kernel = ch0.copy()
+    if len(samples) > 1:
+        ch1 = np.asarray(samples[1], dtype=np.float64)
+        n = min(ch0.size, ch1.size)
+        kernel[:n] = (ch0[:n] + ch1[:n]) * 0.5
+    if kernel.size == 0:  # NewConvolutionReverb: "reverb: empty impulse response kernel"
+        raise ValueError("effectchain: create convolution reverb: reverb: empty impulse response kernel")
+    return kernel, wet
 
-    def __init__(self, sample_rate: float = 48000.0, channels: int = 1, designer=None, device: int = 0):
+
+class Chain:
+    """effectchain.Chain for `channels` independent channels of one graph.
+    `ir_provider` is effectchain.WithIRProvider's IRProvider (GetIR(index) ->
+    (samples [ch][n], sample_rate, ok)) for reverb-conv nodes."""
+
+    def __init__(self, sample_rate: float = 48000.0, channels: int = 1, designer=None, device: int = 0,
+                 ir_provider=None):
         self.sample_rate = float(sample_rate)
         self.channels = int(channels)
         self.designer = designer
+        self.ir_provider = ir_provider
         self.device = int(device)
         self.graph = CompiledGraph({}, {}, {}, [])
         self._h = None
@@ -351,6 +381,19 @@ class Chain:
                 for j, v in enumerate(freeverb_params(p)):
                     d.verb[j] = v
                 sd.update(type="verb", verb=freeverb_params(p))
+            elif t == "reverb-conv":
+                kw = None if p.Bypassed else conv_reverb_kernel(p, self.ir_provider)
+                if kw is None:
+                    d.type = FXN_PASS  # no engine: Process is a no-op (runtime_misc.go:61-64)
+                    sd["type"] = "pass"
+                else:
+                    kern, wet = kw
+                    kern = np.ascontiguousarray(kern)
+                    keep.append(kern)
+                    d.type = FXN_CONV_REVERB
+                    d.ir, d.ir_len = ptr(kern), kern.size
+                    d.conv_min_order, d.conv_wet, d.conv_dry = 7, wet, 1.0  # NewConvolutionReverb(kernel, 7)
+                    sd.update(type="conv", kernel=kern, min_order=7, wet=wet, dry=1.0)
             else:
                 raise UnknownEffect(f"effect type {t!r} is not run by the GPU graph runtime")
             spec.append(sd)

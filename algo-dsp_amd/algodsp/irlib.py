@@ -147,3 +147,23 @@ def large_church(path=DEFAULT_IRLIB, pad_to: int | None = 131072) -> np.ndarray:
                 s = np.pad(s, ((0, 0), (0, pad_to - s.shape[1])))
             return s
     raise KeyError("Large Church not found in IR library")
+
+
+class LibraryProvider:
+    """effectchain.IRProvider over an IR library (internal/webdemo
+    effects_chain_adapter.go:12-23 + irlib.go:59-65): GetIR(index) returns
+    (samples [ch][n], sample_rate, ok); ok is False out of range."""
+
+    def __init__(self, path=DEFAULT_IRLIB, gpu: bool = False):
+        self.irs = read_irlib(path, gpu=gpu)
+
+    def GetIR(self, index: int):
+        if index < 0 or index >= len(self.irs):
+            return None, 0.0, False
+        ir = self.irs[index]
+        if ir["samples"] is None or len(ir["samples"]) == 0:
+            return None, 0.0, False
+        return ir["samples"], ir["sample_rate"], True
+
+    def IRNames(self):
+        return [ir["name"] for ir in self.irs]

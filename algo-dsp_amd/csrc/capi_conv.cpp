@@ -21,7 +21,7 @@ using namespace adsp;
 
 namespace {
 
-enum class Kind { StreamOLS, StreamOLA, BatchOLS, BatchOLA, Partitioned, Multi, MultiStream };
+enum class Kind { StreamOLS, StreamOLA, BatchOLS, BatchOLA, Partitioned, Multi, MultiStream, PartitionedMulti };
 
 struct StageDesc {
   int64_t part_size;
@@ -115,6 +115,7 @@ struct ad_conv {
 
   // partitioned: non-uniform multi-stage engine (latency >= 64)
   std::unique_ptr<Nupols> nup;
+  std::unique_ptr<NupolsDev> nupd;  // many-channel device-resident form
 
   // partitioned FIFO state (latency < 64: time-domain streaming fallback shape)
   std::vector<double> pending;   // input samples not yet convolved (< hop)
@@ -129,6 +130,7 @@ struct ad_conv {
       (void)hipEventDestroy(done);
     }
     nup.reset();
+    nupd.reset();
     eng.reset();
     if (stream) (void)hipStreamSynchronize(stream);
     if (pin_in) (void)hipHostFree(pin_in);
@@ -503,7 +505,8 @@ int ad_conv_reverb_create(const double* kernel, int64_t K, int min_order, int de
 
 int ad_conv_reverb_set_wet_dry(ad_conv* h, double wet, double dry) {
   return guard([&] {
-    if (!h || h->kind != Kind::Partitioned) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "not a convolution reverb");
+    if (!h || (h->kind != Kind::Partitioned && h->kind != Kind::PartitionedMulti))
+      AD_FAIL(AD_ERR_INVALID_ARGUMENT, "not a convolution reverb");
     h->wet = wet;
     h->dry = dry;
   });
@@ -544,6 +547,7 @@ int ad_conv_reset(ad_conv* h) {
     DeviceScope ds(h->device);
     if (h->has_last) AD_HIP(hipStreamWaitEvent(h->stream, h->done, 0));  // after the last device call
     if (h->nup) h->nup->reset();
+    if (h->nupd) h->nupd->reset(h->stream);
     stream_reset(h);
     h->has_last = false;
   });
@@ -843,6 +847,106 @@ int ad_conv_multi_stream_process_block(ad_conv* h, const double* const* in, doub
     AD_HIP(hipStreamSynchronize(s));
     parallel_for(channels, [&](int64_t c) { std::memcpy(out[c], h->pin_out + c * n, (size_t)n * sizeof(double)); },
                  workers);
+  });
+}
+
+// --- many-channel partitioned convolution / convolution reverb (device) --------
+
+int ad_conv_pc_multi_create(const double* kernel, int64_t K, int min_order, int max_order, int channels, int device,
+                            ad_conv** out) {
+  // `channels` NewPartitionedConvolution(kernel, minOrder, maxOrder)
+  // instances (partitioned.go:212-266) sharing one IR, run together
+  return create_guarded(out, [&]() -> ad_conv* {
+    if (K <= 0 || !kernel) AD_FAIL(AD_ERR_EMPTY_IMPULSE_RESPONSE, "conv: empty impulse response");
+    if (min_order < 1)
+      AD_FAIL(AD_ERR_INVALID_BLOCK_ORDER,
+              "conv: invalid block order: minBlockOrder must be >= 1, got " + std::to_string(min_order));
+    if (max_order < min_order)
+      AD_FAIL(AD_ERR_INVALID_BLOCK_ORDER, "conv: invalid block order: maxBlockOrder (" + std::to_string(max_order) +
+                                              ") must be >= minBlockOrder (" + std::to_string(min_order) + ")");
+    if (min_order < 6 || min_order > 13)
+      AD_FAIL(AD_ERR_INVALID_ARGUMENT, "many-channel partitioned engine: latency 2^minBlockOrder must be 64..8192");
+    if (channels <= 0) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "channels must be positive");
+    const int dev = pick_device(device);
+    DeviceScope ds(dev);
+    std::unique_ptr<ad_conv> h(new_handle(Kind::PartitionedMulti, dev));
+    const int64_t latency = int64_t(1) << min_order;
+    const int64_t padded = ((K + latency - 1) / latency) * latency;
+    h->K = K;
+    h->latency = latency;
+    h->block_size = latency;
+    h->channels = channels;
+    h->stages = partition_ir(padded, min_order, max_order);
+    int64_t cover = 0;
+    for (const auto& st : h->stages) cover = std::max(cover, st.start + st.count * st.part_size);
+    const int64_t keff = std::min<int64_t>(K, cover);
+    h->conv_len = keff;
+    h->fft_size = 2 * h->stages.back().part_size;
+    const int64_t pmax = std::min<int64_t>(8192, std::max<int64_t>(latency, int64_t(1) << std::min(max_order, 13)));
+    h->nupd.reset(new NupolsDev(dev, kernel, keff, latency, pmax, channels, h->stream));
+    AD_HIP(hipStreamSynchronize(h->stream));
+    return h.release();
+  });
+}
+
+int ad_conv_reverb_multi_create(const double* kernel, int64_t K, int min_order, int channels, int device,
+                                ad_conv** out) {
+  // NewConvolutionReverb (reverb/convolution.go:28-44) x channels: maxBlockOrder 13, wet = dry = 1
+  if (out) *out = nullptr;
+  if (K <= 0 || !kernel) {
+    set_last_error("reverb: empty impulse response kernel");
+    return AD_ERR_EMPTY_IMPULSE_RESPONSE;
+  }
+  return ad_conv_pc_multi_create(kernel, K, min_order, 13, channels, device, out);
+}
+
+int ad_conv_pc_multi_process_device(ad_conv* h, const double* d_in, int64_t in_stride, double* d_out,
+                                    int64_t out_stride, int64_t n, void* stream) {
+  // PartitionedConvolutionT.ProcessBlock (partitioned.go:348-396) of every channel
+  return guard([&] {
+    if (!h || h->kind != Kind::PartitionedMulti) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "not a many-channel partitioned convolver");
+    if (n == 0) return;
+    if (n < 0 || in_stride < n || out_stride < n || !d_in || !d_out)
+      AD_FAIL(AD_ERR_LENGTH_MISMATCH, "conv: bad buffer geometry");
+    DeviceScope ds(h->device);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    order_after_last(h, s);
+    h->nupd->process(d_in, in_stride, d_out, out_stride, n, /*mix=*/false, 1.0, 0.0, s);
+    mark_last(h, s);
+  });
+}
+
+int ad_conv_reverb_multi_process_device(ad_conv* h, double* d_buf, int64_t stride, int64_t n, void* stream) {
+  // ConvolutionReverb.ProcessInPlace (convolution.go:60-85) of every channel:
+  // buf = dry*buf + wet*PartitionedConvolution(buf)
+  return guard([&] {
+    if (!h || h->kind != Kind::PartitionedMulti) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "not a many-channel convolution reverb");
+    if (n == 0) return;
+    if (n < 0 || stride < n || !d_buf) AD_FAIL(AD_ERR_LENGTH_MISMATCH, "conv: bad buffer geometry");
+    DeviceScope ds(h->device);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    order_after_last(h, s);
+    h->nupd->process(d_buf, stride, d_buf, stride, n, /*mix=*/true, h->wet, h->dry, s);
+    mark_last(h, s);
+  });
+}
+
+int ad_conv_reverb_multi_process(ad_conv* h, double* buf, int64_t n) {
+  // host buffer [channels][n], in place; returns when the block is back on the host
+  return guard([&] {
+    if (!h || h->kind != Kind::PartitionedMulti) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "not a many-channel convolution reverb");
+    if (n == 0) return;
+    if (n < 0 || !buf) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "bad buffer");
+    DeviceScope ds(h->device);
+    const size_t cnt = (size_t)h->channels * n;
+    h->din.reserve(cnt);
+    hipStream_t s = h->stream;
+    order_after_last(h, s);
+    AD_HIP(hipMemcpyAsync(h->din.p, buf, cnt * sizeof(double), hipMemcpyHostToDevice, s));
+    h->nupd->process(h->din.p, n, h->din.p, n, n, /*mix=*/true, h->wet, h->dry, s);
+    AD_HIP(hipMemcpyAsync(buf, h->din.p, cnt * sizeof(double), hipMemcpyDeviceToHost, s));
+    mark_last(h, s);
+    AD_HIP(hipStreamSynchronize(s));
   });
 }
 

@@ -51,11 +51,17 @@ struct ChainDel {
 };
 using ChainPtr = std::unique_ptr<ad_fx_chain, ChainDel>;
 
+struct ConvDel {
+  void operator()(ad_conv* c) const { ad_conv_destroy(c); }
+};
+using ConvPtr = std::unique_ptr<ad_conv, ConvDel>;
+
 struct FxOp {
-  enum Kind { ZERO, COPY, MIX, CHAIN } kind;
-  int dst = -1;                 // buffer id (written; CHAIN: read and written in place)
+  enum Kind { ZERO, COPY, MIX, CHAIN, CONV } kind;
+  int dst = -1;                 // buffer id (written; CHAIN / CONV: read and written in place)
   std::vector<int> srcs;        // COPY / MIX: buffers read
   ad_fx_chain* chain = nullptr;   // CHAIN
+  ad_conv* conv = nullptr;        // CONV (many-channel convolution reverb)
   // schedule (see schedule()): lane 0 is the caller's stream
   int lane = 0;
   std::vector<int> waits;  // ops on other lanes this op waits for
@@ -81,6 +87,7 @@ struct ad_fx_graph {
   int out_buf = 0;
   std::vector<FxOp> ops;
   std::vector<ChainPtr> chains;
+  std::vector<ConvPtr> convs;
   DevBuf<double> pool;   // buffers 1..nbuf-1, [nbuf-1][channels][cap]
   int64_t cap = 0;
   DevBuf<double> work;   // host-call staging
@@ -99,6 +106,7 @@ struct ad_fx_graph {
         (void)hipStreamDestroy(l);
       }
     chains.clear();
+    convs.clear();
     if (stream) {
       (void)hipStreamSynchronize(stream);
       (void)hipStreamDestroy(stream);
@@ -143,7 +151,7 @@ void compile(ad_fx_graph* g, const ad_fx_node* nodes, int n) {
   int out_node = -1;
   for (int i = 0; i < n; ++i) {
     const ad_fx_node& d = nodes[i];
-    if (d.type < AD_FXN_INPUT || d.type > AD_FXN_FREEVERB)
+    if (d.type < AD_FXN_INPUT || d.type > AD_FXN_CONV_REVERB)
       AD_FAIL(AD_ERR_UNKNOWN_EFFECT, "fx graph: node type not supported by the GPU runtime");
     if (d.type == AD_FXN_INPUT && i != 0) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "fx graph: more than one input node");
     if (d.type == AD_FXN_OUTPUT) {
@@ -165,6 +173,8 @@ void compile(ad_fx_graph* g, const ad_fx_node* nodes, int n) {
     if (d.type == AD_FXN_SPLIT_FREQ && (d.nsec <= 0 || !d.sections || d.nsec2 <= 0 || !d.sections2))
       AD_FAIL(AD_ERR_INVALID_ARGUMENT, "fx graph: split-freq node needs LP and HP sections");
     if (d.type == AD_FXN_COMPRESSOR && !d.comp) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "fx graph: compressor without config");
+    if (d.type == AD_FXN_CONV_REVERB && !d.bypassed && (!d.ir || d.ir_len <= 0))
+      AD_FAIL(AD_ERR_EMPTY_IMPULSE_RESPONSE, "fx graph: reverb-conv node without an impulse response");
     if (d.type == AD_FXN_COMPRESSOR && (d.dyn_mode < 0 || d.dyn_mode > 2))
       AD_FAIL(AD_ERR_INVALID_ARGUMENT, "fx graph: bad dynamics mode");
   }
@@ -215,6 +225,18 @@ void compile(ad_fx_graph* g, const ad_fx_node* nodes, int n) {
       continue;
     }
     if (d.type == AD_FXN_OUTPUT || d.type == AD_FXN_PASS || d.bypassed) continue;
+    if (d.type == AD_FXN_CONV_REVERB) {
+      flush(g, gr);
+      ad_conv* cr = nullptr;
+      ck(ad_conv_reverb_multi_create(d.ir, d.ir_len, d.conv_min_order, g->channels, g->device, &cr));
+      g->convs.emplace_back(cr);
+      ck(ad_conv_reverb_set_wet_dry(cr, d.conv_wet, d.conv_dry));
+      FxOp op{FxOp::CONV};
+      op.dst = b;
+      op.conv = cr;
+      g->ops.push_back(op);
+      continue;
+    }
     const int lvl = d.type == AD_FXN_BIQUAD ? 1 : (d.type == AD_FXN_COMPRESSOR ? 2 : 3);
     if (gr.open && (lvl < gr.level() || (lvl == gr.level() && lvl > 1))) flush(g, gr);
     gr.open = true;
@@ -254,7 +276,7 @@ void schedule(ad_fx_graph* g) {
   for (int i = 0; i < (int)g->ops.size(); ++i) {
     FxOp& op = g->ops[i];
     std::vector<int> reads = op.srcs;
-    if (op.kind == FxOp::CHAIN) reads.push_back(op.dst);
+    if (op.kind == FxOp::CHAIN || op.kind == FxOp::CONV) reads.push_back(op.dst);
     std::vector<int> deps;
     for (int b : reads)
       if (last_writer[b] >= 0) deps.push_back(last_writer[b]);
@@ -345,6 +367,9 @@ void run(ad_fx_graph* g, double* d0, int64_t stride0, int64_t n, hipStream_t s) 
       case FxOp::CHAIN:
         ck(ad_fx_chain_process_device(op.chain, dst, st(op.dst), n, ls));
         break;
+      case FxOp::CONV:
+        ck(ad_conv_reverb_multi_process_device(op.conv, dst, st(op.dst), n, ls));
+        break;
     }
     if (op.signal) AD_HIP(hipEventRecord(g->op_ev[i], ls));
   }
@@ -420,6 +445,7 @@ int ad_fx_graph_process(ad_fx_graph* g, double* buf, int64_t n) {
 int ad_fx_graph_reset(ad_fx_graph* g) {
   return graph_guard(g, [&] {
     for (auto& c : g->chains) ck(ad_fx_chain_reset(c.get()));
+    for (auto& c : g->convs) ck(ad_conv_reset(c.get()));
   });
 }
 

@@ -718,6 +718,38 @@ __global__ __launch_bounds__(256) void k_mixdown(const double* __restrict__ ch, 
   mix[mix_stride + t] = first_parity ? e : o;
 }
 
+// Column shift with zero fill (accumulator / FIFO compaction of the
+// multichannel partitioned engine).
+__global__ __launch_bounds__(256) void k_shift_cols(const double* __restrict__ src, int64_t src_stride,
+                                                    double* __restrict__ dst, int64_t dst_stride, int64_t ncopy,
+                                                    int64_t ncols) {
+  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int c = blockIdx.y;
+  if (j >= ncols) return;
+  dst[(int64_t)c * dst_stride + j] = j < ncopy ? src[(int64_t)c * src_stride + j] : 0.0;
+}
+
+// Emit of the partitioned convolution / ConvolutionReverb mix
+// (reverb/convolution.go:60-85: block[i] = dry*block[i] + wet*reverbOut[i]).
+__global__ __launch_bounds__(256) void k_pc_emit(const double* in, int64_t in_stride, double* out,
+                                                 int64_t out_stride, const double* __restrict__ acc,
+                                                 int64_t acc_stride, int64_t off, int64_t first, int64_t n, int mix,
+                                                 double wet, double dry) {
+#pragma clang fp contract(off)
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int c = blockIdx.y;
+  if (i >= n) return;
+  const double r = i < first ? 0.0 : acc[(int64_t)c * acc_stride + off + i];
+  if (mix) {
+    const double x = in[(int64_t)c * in_stride + i];
+    const double a = dry * x;
+    const double b = wet * r;
+    out[(int64_t)c * out_stride + i] = a + b;
+  } else {
+    out[(int64_t)c * out_stride + i] = r;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Launchers
 // ---------------------------------------------------------------------------
@@ -891,6 +923,21 @@ void launch_mixdown(const double* ch, int channels, int64_t stride, int64_t len,
                     int first_parity, hipStream_t s) {
   hipLaunchKernelGGL(k_mixdown, dim3((unsigned)((len + 255) / 256)), dim3(256), 0, s, ch, channels, stride, len, mix,
                      mix_stride, first_parity & 1);
+}
+
+void launch_shift_cols(const double* src, int64_t src_stride, double* dst, int64_t dst_stride, int channels,
+                       int64_t ncopy, int64_t ncols, hipStream_t s) {
+  if (channels <= 0 || ncols <= 0) return;
+  hipLaunchKernelGGL(k_shift_cols, dim3((unsigned)((ncols + 255) / 256), (unsigned)channels), dim3(256), 0, s, src,
+                     src_stride, dst, dst_stride, ncopy, ncols);
+}
+
+void launch_pc_emit(const double* in, int64_t in_stride, double* out, int64_t out_stride, const double* acc,
+                    int64_t acc_stride, int64_t off, int64_t first, int64_t n, int channels, int mix, double wet,
+                    double dry, hipStream_t s) {
+  if (channels <= 0 || n <= 0) return;
+  hipLaunchKernelGGL(k_pc_emit, dim3((unsigned)((n + 255) / 256), (unsigned)channels), dim3(256), 0, s, in, in_stride,
+                     out, out_stride, acc, acc_stride, off, first, n, mix, wet, dry);
 }
 
 }  // namespace adsp

@@ -76,6 +76,7 @@ struct IrfftArgs {
   int jc;
   int channels;
   int aligned;
+  int accumulate;       // 1: add into out (partitioned stages sharing one accumulator)
   const double2* twM;
   const double2* twN;
 };
@@ -89,5 +90,13 @@ void launch_direct_circular(const double* a, const double* b, int64_t n, double*
 void launch_stream_direct(const double* h, int64_t K, const double* buf, int64_t B, double* y, hipStream_t s);
 void launch_mixdown(const double* ch, int channels, int64_t stride, int64_t len, double* mix, int64_t mix_stride,
                     int first_parity, hipStream_t s);
+// dst[c][j] = j < ncopy ? src[c][j] : 0 for j < ncols (channel strides differ)
+void launch_shift_cols(const double* src, int64_t src_stride, double* dst, int64_t dst_stride, int channels,
+                       int64_t ncopy, int64_t ncols, hipStream_t s);
+// Partitioned-convolution emit: out[c][i] = (i < first ? 0 : acc[c][off + i]) or, with mix,
+// dry * in[c][i] + wet * that (ConvolutionReverb.ProcessInPlace, no contraction).
+void launch_pc_emit(const double* in, int64_t in_stride, double* out, int64_t out_stride, const double* acc,
+                    int64_t acc_stride, int64_t off, int64_t first, int64_t n, int channels, int mix, double wet,
+                    double dry, hipStream_t s);
 
 }  // namespace adsp

@@ -44,17 +44,22 @@ __device__ __forceinline__ double2 fetch_pair(const double* xc, const double* hc
 // Inverse store: the upper half of the time window (m >= M/2) to y.
 template <int M, int V>
 __device__ __forceinline__ void irfft_store_out(const double2* v, int tid, double* yc, int64_t ob, int64_t out_len,
-                                                bool aligned) {
+                                                bool aligned, bool acc) {
 #pragma unroll
   for (int s = 0; s < V; ++s) {
     const int m = last_pass_index<M, V>(tid, s);
     if (m < M / 2) continue;
     const int64_t o = ob + 2 * m;
     if (o + 1 < out_len && aligned) {
-      *reinterpret_cast<double2*>(yc + o) = v[s];
+      double2 r = v[s];
+      if (acc) {
+        const double2 q = *reinterpret_cast<const double2*>(yc + o);
+        r = make_double2(q.x + r.x, q.y + r.y);
+      }
+      *reinterpret_cast<double2*>(yc + o) = r;
     } else {
-      if (o < out_len) yc[o] = v[s].x;
-      if (o + 1 < out_len) yc[o + 1] = v[s].y;
+      if (o < out_len) yc[o] = acc ? yc[o] + v[s].x : v[s].x;
+      if (o + 1 < out_len) yc[o + 1] = acc ? yc[o + 1] + v[s].y : v[s].y;
     }
   }
 }
@@ -124,7 +129,8 @@ __global__ __launch_bounds__((FftPlan<M, V>::BLOCK)) void k_irfft_store(IrfftArg
   }
   fft_run<M, V, false>(v, tid, lds, TwGlobal{a.twM});
   if (!active) return;
-  irfft_store_out<M, V>(v, tid, a.out + (int64_t)c * a.out_stride, a.o0 + (int64_t)j * L - M, a.out_len, a.aligned);
+  irfft_store_out<M, V>(v, tid, a.out + (int64_t)c * a.out_stride, a.o0 + (int64_t)j * L - M, a.out_len, a.aligned,
+                        a.accumulate);
 }
 
 // ---------------------------------------------------------------------------
@@ -245,10 +251,15 @@ __global__ __launch_bounds__((SplitPlan<M>::T)) __attribute__((amdgpu_waves_per_
     const double2 r = c_sub(av[s], c_mul(c_conj(twC(m)), bv[s]));
     const int64_t o = ob + 2 * m;
     if (fast) {
-      *reinterpret_cast<double2*>(yc + o) = r;
+      double2 w = r;
+      if (a.accumulate) {
+        const double2 q = *reinterpret_cast<const double2*>(yc + o);
+        w = make_double2(q.x + r.x, q.y + r.y);
+      }
+      *reinterpret_cast<double2*>(yc + o) = w;
     } else {
-      if (o < a.out_len) yc[o] = r.x;
-      if (o + 1 < a.out_len) yc[o + 1] = r.y;
+      if (o < a.out_len) yc[o] = a.accumulate ? yc[o] + r.x : r.x;
+      if (o + 1 < a.out_len) yc[o + 1] = a.accumulate ? yc[o + 1] + r.y : r.y;
     }
   }
 }

@@ -4,6 +4,8 @@
 #include <algorithm>
 #include <cstring>
 
+#include "conv_kernels.hpp"
+
 namespace adsp {
 
 Nupols::Nupols(int device, const double* h, int64_t K, int64_t lambda, int64_t p_max)
@@ -122,6 +124,117 @@ void Nupols::process(const double* in, int64_t n, double* out) {
   const int64_t drop_in = std::min<int64_t>(std::max<int64_t>(min_done - xin_base_, 0), (int64_t)xin_.size());
   xin_.erase(xin_.begin(), xin_.begin() + drop_in);
   xin_base_ += drop_in;
+}
+
+// ---------------------------------------------------------------------------
+// NupolsDev
+// ---------------------------------------------------------------------------
+namespace {
+int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
+}  // namespace
+
+NupolsDev::NupolsDev(int device, const double* h, int64_t K, int64_t lambda, int64_t p_max, int channels,
+                     hipStream_t s)
+    : C_(channels), lambda_(lambda) {
+  if (lambda < 64 || !is_pow2(lambda) || p_max < lambda || !is_pow2(p_max) || p_max > 8192 || channels < 1)
+    AD_FAIL(AD_ERR_INTERNAL, "NupolsDev: bad geometry");
+  // same stage layout as Nupols (two partitions per size, the rest at p_max)
+  int64_t T = 0, p = lambda;
+  while (T < K) {
+    int64_t nparts = 2;
+    if (p >= p_max) nparts = (K - T + p - 1) / p;
+    Stage st;
+    st.p = p;
+    st.T = T;
+    st.taps = std::min<int64_t>(nparts * p, K - T);
+    st_.push_back(std::move(st));
+    T += nparts * p;
+    if (p < p_max) p *= 2;
+  }
+  for (auto& st : st_) {
+    // up to 64 blocks (and >= 8192 samples) per launch chunk: long calls batch
+    const int jc = (int)std::max<int64_t>(64, 8192 / st.p);
+    st.eng.reset(new Upols(device, h + st.T, 1, st.taps, (int)st.p, channels, nullptr, jc, s));
+  }
+  reset(s);
+}
+
+void NupolsDev::reset(hipStream_t s) {
+  for (auto& st : st_) {
+    st.eng->reset_stream(s);
+    st.done = 0;
+  }
+  received_ = emitted_ = 0;
+  xin_base_ = acc_base_ = 0;
+  acc_hi_ = 0;
+  if (acc_[acur_].p) AD_HIP(hipMemsetAsync(acc_[acur_].p, 0, acc_[acur_].n * sizeof(double), s));
+}
+
+void NupolsDev::ensure_xin(int64_t need_hi, hipStream_t s) {
+  if (need_hi - xin_base_ <= xcap_) return;
+  int64_t min_done = received_;
+  for (auto& st : st_) min_done = std::min(min_done, st.done);
+  const int64_t nb = min_done / 64 * 64;  // keep 16-byte alignment of every stage's block start
+  const int64_t keep = received_ - nb;
+  const int64_t cap = std::max<int64_t>(round_up(2 * (need_hi - nb), 8192), xcap_);
+  DevBuf<double>& dst = xin_[xcur_ ^ 1];
+  dst.alloc((size_t)C_ * cap);
+  if (keep > 0 && xin_[xcur_].p)
+    launch_shift_cols(xin_[xcur_].p + (nb - xin_base_), xcap_, dst.p, cap, C_, keep, keep, s);
+  if (cap != xcap_) xin_[xcur_].release();  // same size: kept for the next compaction
+  xcur_ ^= 1;
+  xcap_ = cap;
+  xin_base_ = nb;
+}
+
+void NupolsDev::ensure_acc(int64_t lo_keep, int64_t need_hi, hipStream_t s) {
+  if (need_hi - acc_base_ <= acap_ && acc_[acur_].p) return;
+  const int64_t nb = std::max<int64_t>(acc_base_, lo_keep / 64 * 64);
+  const int64_t keep = std::max<int64_t>(0, acc_hi_ - nb);
+  const int64_t cap = std::max<int64_t>(round_up(2 * (need_hi - nb), 8192), acap_);
+  DevBuf<double>& dst = acc_[acur_ ^ 1];
+  dst.alloc((size_t)C_ * cap);
+  if (acc_[acur_].p)
+    launch_shift_cols(acc_[acur_].p + (nb - acc_base_), acap_, dst.p, cap, C_, keep, cap, s);
+  else
+    AD_HIP(hipMemsetAsync(dst.p, 0, dst.n * sizeof(double), s));
+  if (cap != acap_) acc_[acur_].release();
+  acur_ ^= 1;
+  acap_ = cap;
+  acc_base_ = nb;
+}
+
+void NupolsDev::process(const double* d_in, int64_t in_stride, double* d_out, int64_t out_stride, int64_t n,
+                        bool mix, double wet, double dry, hipStream_t s) {
+  if (n <= 0) return;
+  // 1. append the block to the input FIFO
+  ensure_xin(received_ + n, s);
+  AD_HIP(hipMemcpy2DAsync(xin_[xcur_].p + (received_ - xin_base_), (size_t)xcap_ * sizeof(double), d_in,
+                          (size_t)in_stride * sizeof(double), (size_t)n * sizeof(double), (size_t)C_,
+                          hipMemcpyDeviceToDevice, s));
+  received_ += n;
+  // 2. every complete block of every stage; K3 adds into the accumulator at +T
+  int64_t hi = acc_hi_;
+  for (auto& st : st_) {
+    const int64_t nb = (received_ - st.done) / st.p;
+    if (nb > 0) hi = std::max(hi, st.done + nb * st.p + st.T);
+  }
+  ensure_acc(emitted_ - lambda_, std::max(hi, emitted_ + n), s);
+  for (auto& st : st_) {
+    const int64_t nb = (received_ - st.done) / st.p;
+    if (nb == 0) continue;
+    const int64_t len = nb * st.p;
+    st.eng->run(xin_[xcur_].p + (st.done - xin_base_), xcap_, len, acc_[acur_].p + (st.done + st.T - acc_base_),
+                acap_, len, /*use_hist=*/true, s, 0, -1, /*accumulate=*/true);
+    st.done += len;
+  }
+  acc_hi_ = hi;
+  // 3. emit y[t - lambda] for t in [emitted, emitted + n)
+  const int64_t first = std::max<int64_t>(0, std::min<int64_t>(n, lambda_ - emitted_));
+  launch_pc_emit(d_in, in_stride, d_out, out_stride, acc_[acur_].p, acap_, emitted_ - lambda_ - acc_base_, first, n,
+                 C_, mix ? 1 : 0, wet, dry, s);
+  AD_HIP(hipGetLastError());
+  emitted_ += n;
 }
 
 }  // namespace adsp

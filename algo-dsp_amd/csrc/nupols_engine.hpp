@@ -64,4 +64,46 @@ class Nupols {
   int64_t emitted_ = 0;      // output samples emitted
 };
 
+// Device-resident, many-channel form of the same engine: `channels` copies of
+// PartitionedConvolution sharing one IR (the batched effect-chain runtime's
+// reverb-conv node, one instance per graph copy; ad_conv_pc_multi_*).  Every
+// stage is ONE zero-latency UPOLS engine over all channels (one launch per
+// engine kernel per stage per call, whatever the channel count), its K3 adds
+// straight into a device accumulator [C][acap] at the stage's tap offset T_s,
+// and an emit kernel reads y[t - lambda] (optionally mixed dry/wet as
+// ConvolutionReverb.ProcessInPlace does).  Input and accumulator are linear
+// device buffers compacted in place of a ring, so each stage reads its blocks
+// and writes its outputs as contiguous runs.  All work is enqueued on the
+// caller's stream; nothing synchronises the host.
+class NupolsDev {
+ public:
+  NupolsDev(int device, const double* h, int64_t K, int64_t lambda, int64_t p_max, int channels, hipStream_t s);
+  // out[c][0..n) = (h * x_c)[t - lambda] (mix: dry*in + wet*that) for the next
+  // n samples of every channel; in == out (in place) allowed.
+  void process(const double* d_in, int64_t in_stride, double* d_out, int64_t out_stride, int64_t n, bool mix,
+               double wet, double dry, hipStream_t s);
+  void reset(hipStream_t s);
+  int channels() const { return C_; }
+
+ private:
+  struct Stage {
+    int64_t p = 0, T = 0, taps = 0;
+    std::unique_ptr<Upols> eng;
+    int64_t done = 0;  // input samples consumed
+  };
+  int C_;
+  int64_t lambda_;
+  std::vector<Stage> st_;
+  DevBuf<double> xin_[2];  // [C][xcap], ping-pong for compaction
+  int xcur_ = 0;
+  int64_t xcap_ = 0, xin_base_ = 0;
+  DevBuf<double> acc_[2];  // [C][acap]
+  int acur_ = 0;
+  int64_t acap_ = 0, acc_base_ = 0;
+  int64_t received_ = 0, emitted_ = 0;
+  int64_t acc_hi_ = 0;  // highest accumulator time written + 1 (columns beyond are zero)
+  void ensure_xin(int64_t need_hi, hipStream_t s);
+  void ensure_acc(int64_t lo_keep, int64_t need_hi, hipStream_t s);
+};
+
 }  // namespace adsp

@@ -192,7 +192,7 @@ void Upols::begin_offline(hipStream_t) {
 }
 
 void Upols::run(const double* d_in, int64_t in_stride, int64_t n, double* d_out, int64_t out_stride, int64_t out_len,
-                bool use_hist, hipStream_t s, int64_t jb, int64_t je) {
+                bool use_hist, hipStream_t s, int64_t jb, int64_t je, bool accumulate) {
   if (out_len <= 0) return;
   if (je < 0) je = (out_len + L_ - 1) / L_;
   const int64_t J = je - jb;
@@ -266,6 +266,7 @@ void Upols::run(const double* d_in, int64_t in_stride, int64_t n, double* d_out,
     b.jc = jc;
     b.channels = C_;
     b.aligned = out_aligned;
+    b.accumulate = accumulate ? 1 : 0;
     b.twM = tw_.p;
     b.twN = tw_.p + M_;
     prof_begin(s, &e0);

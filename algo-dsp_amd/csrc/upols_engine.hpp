@@ -39,8 +39,9 @@ class Upols {
   // [jb, je): the output blocks to run (je < 0: through the end of out_len).
   // Offline segments of one signal run in increasing order (the delay line
   // carries from one segment to the next).
+  // accumulate: K3 adds into d_out instead of storing (partitioned stages).
   void run(const double* d_in, int64_t in_stride, int64_t n, double* d_out, int64_t out_stride, int64_t out_len,
-           bool use_hist, hipStream_t s, int64_t jb = 0, int64_t je = -1);
+           bool use_hist, hipStream_t s, int64_t jb = 0, int64_t je = -1, bool accumulate = false);
   // Saves the last L input samples of the call into the streaming history.
   // Streaming calls (use_hist) refresh the history inside K1; kept for API
   // symmetry, a no-op.

@@ -183,6 +183,27 @@ int ad_conv_multi_stream_process_block(ad_conv* h, const double* const* in, doub
 /* device buffers [channels][stride]; asynchronous on `stream` */
 int ad_conv_multi_stream_process_block_device(ad_conv* h, const double* d_in, int64_t in_stride, double* d_out,
                                               int64_t out_stride, void* stream);
+/* ---- many-channel partitioned convolution / convolution reverb ----------
+ * `channels` PartitionedConvolution instances (partitioned.go:212-436) that
+ * share ONE impulse response, device resident: y[c][t] = (h * x_c)[t - 2^minOrder]
+ * for any call length.  Each non-uniform stage is one UPOLS engine over all
+ * channels (one launch per engine kernel per stage per call), accumulating
+ * into a device buffer; latency 2^minOrder must be 64..8192 here.
+ * The reverb form (maxBlockOrder 13, wet = dry = 1 until
+ * ad_conv_reverb_set_wet_dry) processes in place as
+ * ConvolutionReverb.ProcessInPlace (convolution.go:60-85) -- the
+ * effect-chain reverb-conv node.  ad_conv_reset, ad_conv_latency,
+ * ad_conv_stage_count / ad_conv_stage_info apply.                          */
+int ad_conv_pc_multi_create(const double* kernel, int64_t kernel_len, int min_order, int max_order, int channels,
+                            int device, ad_conv** out);
+int ad_conv_pc_multi_process_device(ad_conv* h, const double* d_in, int64_t in_stride, double* d_out,
+                                    int64_t out_stride, int64_t n, void* stream);
+int ad_conv_reverb_multi_create(const double* kernel, int64_t kernel_len, int min_order, int channels, int device,
+                                ad_conv** out);
+int ad_conv_reverb_multi_process_device(ad_conv* h, double* d_buf, int64_t stride, int64_t n, void* stream);
+/* host buffer [channels][n], in place */
+int ad_conv_reverb_multi_process(ad_conv* h, double* buf, int64_t n);
+
 /* Live kernel timing (HIP events recorded around every launch on the launch
  * stream) for the FFT engine of a handle.  Kernel index: 0 window rFFT,
  * 1 frequency-domain delay-line MAC, 2 inverse rFFT + overlap-save store.
@@ -305,7 +326,9 @@ void ad_fx_chain_destroy(ad_fx_chain* h);
  *                      and dyn-limiter = NewLimiter's ratio 100 / attack 0.1 ms /
  *                      hard knee / no makeup config, limiter.go:11-44);
  *   AD_FXN_FREEVERB    reverb.Reverb.ProcessInPlace, verb = {wet, dry,
- *                      room_size, damp, gain} (runtime_filter_pitch_reverb.go:330-345).
+ *                      room_size, damp, gain} (runtime_filter_pitch_reverb.go:330-345);
+ *   AD_FXN_CONV_REVERB reverb.ConvolutionReverb.ProcessInPlace (reverb-conv,
+ *                      runtime_misc.go:61-67) on the many-channel partitioned engine.
  * The result is the output node's buffer.  Linear runs of in-place nodes fuse
  * into one launch (bit-identical, see capi_fxgraph.cpp).  Other node types
  * return AD_ERR_UNKNOWN_EFFECT; the configs are copied at create.          */
@@ -316,6 +339,9 @@ void ad_fx_chain_destroy(ad_fx_chain* h);
 #define AD_FXN_BIQUAD 4
 #define AD_FXN_COMPRESSOR 5
 #define AD_FXN_FREEVERB 6
+#define AD_FXN_CONV_REVERB 7 /* reverb-conv (runtime_misc.go:12-67): ConvolutionReverb(ir, conv_min_order)
+                                with SetWetDry(conv_wet, conv_dry), in place; the caller
+                                mono-averages the provider's IR as Configure does */
 #define AD_FX_MAX_PARENTS 8
 typedef struct ad_fx_node {
   int type;
@@ -332,6 +358,10 @@ typedef struct ad_fx_node {
   int dyn_mode;                     /* COMPRESSOR: 0 compressor / limiter, 1 expander (dyn-expander),
                                        2 gate (dyn-gate); see ad_fx_chain_set_expander */
   double dyn_range_db, dyn_hold_ms; /* expander / gate: SetRange, the gate's SetHold */
+  const double* ir;                 /* CONV_REVERB: impulse response [ir_len] */
+  int64_t ir_len;
+  int conv_min_order;               /* CONV_REVERB: minBlockOrder (reverb-conv uses 7; maxBlockOrder 13) */
+  double conv_wet, conv_dry;        /* CONV_REVERB: SetWetDry(wet, dry) (reverb-conv: wet param, dry 1.0) */
 } ad_fx_node;
 typedef struct ad_fx_graph ad_fx_graph;
 int ad_fx_graph_create(const ad_fx_node* nodes, int n_nodes, int channels, int device, ad_fx_graph** out);

@@ -482,6 +482,8 @@ class FxGraph:
                 v = Freeverb()
                 v.set(*d["verb"])
                 self.rt.append(["verb", v])
+            elif t == "conv":  # ConvolutionReverb(kernel, minOrder) + SetWetDry (convolution.go:28-85)
+                self.rt.append(["conv", Partitioned(d["kernel"], d["min_order"], 13), d["wet"], d["dry"]])
             else:
                 self.rt.append([t])
 
@@ -523,4 +525,7 @@ class FxGraph:
                 buf[i] = r[1].process_in_place(dst)
             elif r[0] == "verb":
                 buf[i] = r[1].process_in_place(dst)
+            elif r[0] == "conv":
+                rev = r[1].process_block(dst)
+                buf[i] = r[3] * dst + r[2] * rev  # block[i] = dry*block[i] + wet*reverbOut[i]
         return buf[[i for i, d in enumerate(self.nodes) if d["type"] == "output"][0]]

@@ -514,3 +514,48 @@ def test_multi_stream_vs_oracle(gpu, K, B):
         s.ProcessBlock(x[:, :B - 1])
     with pytest.raises(conv.ErrLengthMismatch):
         s.ProcessBlock(x[:4, :B])
+
+
+@pytest.mark.parametrize("K,lo,hi", [(95432, 7, 13), (1000, 6, 13), (20000, 10, 11), (5000, 13, 13)])
+def test_partitioned_multi_vs_oracle(gpu, K, lo, hi):
+    """ad_conv_pc_multi_* (many-channel, device-resident partitioned engine):
+    3 channels sharing one IR, device calls of varying length (shorter and
+    longer than every stage, > one accumulator span), each channel against the
+    oracle's PartitionedConvolution; Reset restarts the stream; the reverb form
+    mixes dry/wet in place."""
+    import torch
+
+    h = signals.make_impulse_kernel(K) if K < 90000 else irlib.large_church(pad_to=None)[0]
+    C_ = 3
+    lat = 1 << lo
+    sizes = [lat, 1, 3 * lat + 5, 20011, 7, 40000, lat]
+    n = sum(sizes)
+    x = np.stack([signals.white_noise(n, 300 + c) for c in range(C_)])
+    g = conv.PartitionedConvolutionMulti(h, lo, hi, C_)
+    assert g.Latency() == lat and g.StageCount() == O.Partitioned(h, lo, hi).stage_count()
+    dx = torch.from_numpy(x).cuda()
+    dy = torch.full_like(dx, np.nan)
+    s = torch.cuda.current_stream()
+    for rep in range(2):
+        pos = 0
+        for m in sizes:
+            g.process_device(dx.data_ptr() + 8 * pos, n, dy.data_ptr() + 8 * pos, n, m, s.cuda_stream)
+            pos += m
+        s.synchronize()
+        y = dy.cpu().numpy()
+        for c in range(C_):
+            o = O.Partitioned(h, lo, hi)
+            want = np.concatenate([o.process_block(x[c, a:a + m]) for a, m in
+                                   zip(np.cumsum([0] + sizes[:-1]), sizes)])
+            assert rms(y[c], want) < FFT_RMS_TOL
+            assert np.max(np.abs(y[c] - want)) < 1e-9
+        g.Reset()
+    # reverb form: in place, dry/wet
+    r = conv.NewConvolutionReverbMulti(h, lo, C_)
+    r.SetWetDry(0.3, 0.8)
+    blk = x[:, :5000].copy()
+    r.ProcessInPlace(blk)
+    for c in range(C_):
+        o = O.Partitioned(h, lo, 13)
+        want = 0.8 * x[c, :5000] + 0.3 * o.process_block(x[c, :5000])
+        assert np.max(np.abs(blk[c] - want)) < 1e-9

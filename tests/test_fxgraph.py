@@ -113,10 +113,39 @@ def test_dynamics_gate_expander_clamps():
 
 
 def test_unknown_effects_rejected():
-    for t in ("chorus", "filter-moog", "dyn-lookahead", "vocoder", "reverb-conv"):
+    for t in ("chorus", "filter-moog", "dyn-lookahead", "vocoder"):
         ch = E.Chain(FS, 2, designer=design.RBJDesigner())
         with pytest.raises(E.UnknownEffect):
             ch.LoadGraph(graph([{"id": "n", "type": t}], [("_input", "n"), ("n", "_output")]))
+
+
+class _Prov:
+    def __init__(self, irs):
+        self.irs = irs
+
+    def GetIR(self, i):
+        if 0 <= i < len(self.irs):
+            return self.irs[i], 48000.0, True
+        return None, 0.0, False
+
+
+def test_conv_reverb_configure_semantics():
+    """convReverbRuntime.Configure (runtime_misc.go:18-58): irIndex default 0,
+    stereo -> (ch0 + ch1) * 0.5 over the shorter length with ch0's tail kept,
+    wet default 0.35, no provider / missing IR -> no engine (pass-through)."""
+    a = np.array([1.0, 2.0, 3.0, 4.0])
+    b = np.array([3.0, 0.5])
+    prov = _Prov([[a, b], [b]])
+    k, wet = E.conv_reverb_kernel(E.Params("r", "reverb-conv"), prov)
+    np.testing.assert_array_equal(k, [2.0, 1.25, 3.0, 4.0])
+    assert wet == 0.35
+    k, wet = E.conv_reverb_kernel(E.Params("r", "reverb-conv", num={"irIndex": 1.9, "wet": 0.8}), prov)
+    np.testing.assert_array_equal(k, b)
+    assert wet == 0.8
+    assert E.conv_reverb_kernel(E.Params("r", "reverb-conv", num={"irIndex": 5}), prov) is None
+    assert E.conv_reverb_kernel(E.Params("r", "reverb-conv"), None) is None
+    with pytest.raises(ValueError):
+        E.conv_reverb_kernel(E.Params("r", "reverb-conv"), _Prov([[np.zeros(0)]]))
 
 
 # ------------------------------------------------------------------ GPU tests
@@ -236,3 +265,46 @@ def test_reset_and_device_path(gpu):
     torch.cuda.synchronize()
     np.testing.assert_array_equal(d[:, :2048].cpu().numpy(), first)
     assert not d[:, 2048:].any()
+
+
+def _conv_graph(wet=0.4, with_dry=False, index=0):
+    nodes = [{"id": "cv", "type": "reverb-conv", "params": {"irIndex": index, "wet": wet}}]
+    edges = [("_input", "cv"), ("cv", "_output")]
+    if with_dry:
+        nodes.insert(0, {"id": "comp", "type": "dyn-compressor", "params": {"thresholdDB": -12, "ratio": 3}})
+        edges = [("_input", "comp"), ("comp", "cv"), ("cv", "_output"), ("_input", "_output")]
+    return graph(nodes, edges)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("with_dry", [False, True])
+def test_reverb_conv_node_vs_oracle(gpu, with_dry):
+    """reverb-conv nodes (runtime_misc.go:12-67) on the many-channel
+    partitioned engine: Large Church (stereo, averaged to mono) at latency 128,
+    calls of varying length, against the oracle's Chain.Process restatement
+    (Partitioned(kernel, 7, 13) + dry/wet mix).  FFT tolerance 1e-7 RMS."""
+    from algodsp import irlib
+
+    prov = irlib.LibraryProvider()
+    idx = prov.IRNames().index("Large Church")
+    C = 4
+    ch = E.Chain(FS, C, designer=design.RBJDesigner(), ir_provider=prov)
+    ch.LoadGraph(_conv_graph(0.4, with_dry, idx))
+    kinds = [d["type"] for d in ch.spec]
+    assert "conv" in kinds
+    oracles = [O.FxGraph(ch.spec, FS) for _ in range(C)]
+    for k, n in enumerate([128, 4096, 1000, 20011, 128, 7]):
+        x = np.stack([0.5 * signals.white_noise(n, 500 * k + c) for c in range(C)])
+        y = x.copy()
+        assert ch.Process(y)
+        for c in range(C):
+            want = oracles[c].process(x[c])
+            assert rms(y[c], want) < 1e-7
+            assert np.max(np.abs(y[c] - want)) < 1e-9
+    # without a provider the node passes the block through (no engine)
+    ch2 = E.Chain(FS, 2)
+    ch2.LoadGraph(_conv_graph())
+    x = signals.white_noise(300, 1).reshape(1, -1).repeat(2, 0).copy()
+    y = x.copy()
+    assert ch2.Process(y)
+    np.testing.assert_array_equal(y, x)
