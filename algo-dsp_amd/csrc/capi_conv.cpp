@@ -434,7 +434,15 @@ int ad_conv_partitioned_create(const double* kernel, int64_t K, int min_order, i
     const int64_t keff = std::min<int64_t>(K, cover);
     h->fft_size = 2 * h->stages.back().part_size;
     const char* uni = std::getenv("AD_PC_UNIFORM");
-    if (latency >= 64 && latency <= 8192 && !(uni && *uni == '1')) {
+    const char* eng = std::getenv("AD_PC_ENGINE");  // "host": the per-stage-stream engine with host accumulation
+    if (latency >= 64 && latency <= 8192 && !(uni && *uni == '1') && !(eng && !std::strcmp(eng, "host"))) {
+      // Device-resident non-uniform stages (NupolsDev, one channel): mapped
+      // pinned block I/O, the accumulator on the device, emit-before-convolve.
+      const int64_t pmax = std::min<int64_t>(8192, std::max<int64_t>(latency, int64_t(1) << std::min(max_order, 13)));
+      h->conv_len = keff;
+      h->nupd.reset(new NupolsDev(dev, kernel, keff, latency, pmax, 1, h->stream));
+      AD_HIP(hipStreamSynchronize(h->stream));
+    } else if (latency >= 64 && latency <= 8192 && !(uni && *uni == '1')) {
       // Non-uniform stages: hop lambda for the head of the IR, doubling up to
       // 2^maxBlockOrder (<= 8192) for the tail (nupols_engine.hpp).
       const int64_t pmax = std::min<int64_t>(8192, std::max<int64_t>(latency, int64_t(1) << std::min(max_order, 13)));
@@ -458,6 +466,11 @@ int ad_conv_partitioned_process_block(ad_conv* h, const double* in, int64_t in_l
                                           " != output length " + std::to_string(out_len));
     if (in_len == 0) return;
     DeviceScope ds(h->device);
+    if (h->nupd) {
+      h->nupd->process_host(in, out, in_len, /*mix=*/false, 1.0, 0.0, h->stream);
+      h->emitted += in_len;
+      return;
+    }
     if (h->nup) {
       h->nup->process(in, in_len, out);
       h->emitted += in_len;

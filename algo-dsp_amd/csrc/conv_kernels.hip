@@ -731,15 +731,25 @@ __global__ __launch_bounds__(256) void k_shift_cols(const double* __restrict__ s
 
 // Emit of the partitioned convolution / ConvolutionReverb mix
 // (reverb/convolution.go:60-85: block[i] = dry*block[i] + wet*reverbOut[i]).
+// Optionally also appends the input block to the engine's input FIFO (one
+// launch for a call's I/O).
 __global__ __launch_bounds__(256) void k_pc_emit(const double* in, int64_t in_stride, double* out,
                                                  int64_t out_stride, const double* __restrict__ acc,
                                                  int64_t acc_stride, int64_t off, int64_t first, int64_t n, int mix,
-                                                 double wet, double dry) {
+                                                 double wet, double dry, double* append_to, int64_t append_stride,
+                                                 int emit, int64_t row2) {
 #pragma clang fp contract(off)
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int c = blockIdx.y;
   if (i >= n) return;
-  const double r = i < first ? 0.0 : acc[(int64_t)c * acc_stride + off + i];
+  if (append_to) append_to[(int64_t)c * append_stride + i] = in[(int64_t)c * in_stride + i];
+  if (!emit) return;
+  double r = 0.0;
+  if (i >= first) {
+    const int64_t q = (int64_t)c * acc_stride + off + i;
+    r = acc[q];
+    if (row2) r = r + acc[row2 + q];  // the side-stream stages' accumulator row
+  }
   if (mix) {
     const double x = in[(int64_t)c * in_stride + i];
     const double a = dry * x;
@@ -934,10 +944,131 @@ void launch_shift_cols(const double* src, int64_t src_stride, double* dst, int64
 
 void launch_pc_emit(const double* in, int64_t in_stride, double* out, int64_t out_stride, const double* acc,
                     int64_t acc_stride, int64_t off, int64_t first, int64_t n, int channels, int mix, double wet,
-                    double dry, hipStream_t s) {
+                    double dry, hipStream_t s, double* append_to, int64_t append_stride, bool emit, int64_t row2) {
   if (channels <= 0 || n <= 0) return;
   hipLaunchKernelGGL(k_pc_emit, dim3((unsigned)((n + 255) / 256), (unsigned)channels), dim3(256), 0, s, in, in_stride,
-                     out, out_stride, acc, acc_stride, off, first, n, mix, wet, dry);
+                     out, out_stride, acc, acc_stride, off, first, n, mix, wet, dry, append_to, append_stride,
+                     emit ? 1 : 0, row2);
+}
+
+// ---------------------------------------------------------------------------
+// Fused small partitioned stage (NupolsDev; PartitionedConvolutionT stages of
+// two partitions, partitioned.go:134-183).  Stateless per block: the
+// frequency-domain delay line of two partitions is replaced by transforming
+// the previous window again, so every (block, channel) is independent and a
+// call of any length is one launch per stage.
+//   y[t] (t in [d, d+p)) = IFFT_N( FFT_N(x[d-p, d+p)) . H0 + FFT_N(x[d-2p, d)) . H1 )[p + t - d]
+// Radix-2 Stockham passes in LDS (natural order in and out), 256 threads.
+// ---------------------------------------------------------------------------
+namespace {
+
+// Twiddles W_N^e read from the W_2048 table (e << (11 - log2 N)).
+struct TwStrided {
+  const double2* __restrict__ t;
+  int sh;
+  __device__ __forceinline__ double2 operator()(int e) const { return t[e << sh]; }
+};
+
+// Register FFTs (FftPlan<N, 16>: T = N/16 threads per transform, radix-16
+// passes through LDS): lanes [0, T) transform the previous window, lanes
+// [T, 2T) the current one, concurrently; a 256-thread block repeats the two
+// groups (duplicate lanes compute and store identical values) so every lane
+// reaches the same barriers.  The products meet in LDS, one group inverts.
+template <int N>
+__device__ __forceinline__ void pc_small_body(const PcSmallArgs& a, int blk, int c, double2* lds) {
+  using Plan = FftPlan<N, 16>;
+  constexpr int T = Plan::T, P = N / 2, MP = Plan::MP;
+  const int tid = threadIdx.x;
+  const int lt = tid % T;
+  const int g = (tid / T) & 1;
+  const bool lead = tid < 2 * T;  // the lanes whose results are kept
+  const int64_t d = a.d0 + (int64_t)blk * P;
+  const double* xc = a.xin + (int64_t)c * a.xstride;
+  const TwStrided tw{a.tw, 11 - ilog2c(N)};
+  const int64_t w0 = d - 2 * P + (int64_t)g * P;  // window start: x[d-2p, d) (g = 0), x[d-p, d+p) (g = 1)
+  double2 v[16];
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+    const int64_t t = w0 + pass0_index<N, 16>(lt, s);
+    v[s] = make_double2(t < 0 ? 0.0 : xc[t - a.xbase], 0.0);
+  }
+  double2* img = lds + g * MP;
+  fft_run<N, 16, true>(v, lt, img, tw);
+  // spectra products: g = 0 with the second partition H1, g = 1 with H0
+  const double2* Hg = a.H + (g ? 0 : N);
+#pragma unroll
+  for (int s = 0; s < 16; ++s) v[s] = c_mul(v[s], Hg[last_pass_index<N, 16>(lt, s)]);
+  __syncthreads();  // both transforms' last LDS reads are done
+  if (g == 0) {
+#pragma unroll
+    for (int s = 0; s < 16; ++s) lds[last_pass_index<N, 16>(lt, s)] = v[s];
+  }
+  __syncthreads();
+  if (g == 1) {
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int k = last_pass_index<N, 16>(lt, s);
+      lds[MP + k] = c_add(lds[k], v[s]);
+    }
+  }
+  __syncthreads();
+  // inverse transform of Y (both groups run it on the same data)
+#pragma unroll
+  for (int s = 0; s < 16; ++s) v[s] = lds[MP + pass0_index<N, 16>(lt, s)];
+  __syncthreads();
+  fft_run<N, 16, false>(v, lt, lds + g * MP, tw);
+  if (!lead || g != 1) return;
+  double* out = a.acc + (int64_t)c * a.acc_stride + a.acc_off + (int64_t)blk * P;
+  constexpr double inv = 1.0 / N;
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+    const int m = last_pass_index<N, 16>(lt, s);
+    if (m >= P) out[m - P] += v[s].x * inv;
+  }
+}
+
+template <int N>
+__global__ __launch_bounds__(256) void k_pc_small(PcSmallArgs a) {
+  __shared__ __attribute__((aligned(16))) double2 lds[2 * FftPlan<N, 16>::MP];
+  pc_small_body<N>(a, blockIdx.x, blockIdx.y, lds);
+}
+
+__global__ __launch_bounds__(256) void k_pc_small_multi(PcSmallMulti m) {
+  __shared__ __attribute__((aligned(16))) double2 lds[2 * FftPlan<2048, 16>::MP];
+  int k = 0;
+  while (k + 1 < m.nst && (int)blockIdx.x >= m.first[k + 1]) ++k;
+  const int blk = blockIdx.x - m.first[k];
+  switch (m.N[k]) {
+    case 128: pc_small_body<128>(m.st[k], blk, blockIdx.y, lds); break;
+    case 256: pc_small_body<256>(m.st[k], blk, blockIdx.y, lds); break;
+    case 512: pc_small_body<512>(m.st[k], blk, blockIdx.y, lds); break;
+    case 1024: pc_small_body<1024>(m.st[k], blk, blockIdx.y, lds); break;
+    default: pc_small_body<2048>(m.st[k], blk, blockIdx.y, lds); break;
+  }
+}
+
+template <int N>
+void pc_small_go(const PcSmallArgs& a, int channels, hipStream_t s) {
+  hipLaunchKernelGGL((k_pc_small<N>), dim3((unsigned)a.nb, (unsigned)channels), dim3(256), 0, s, a);
+}
+
+}  // namespace
+
+void launch_pc_small_multi(const PcSmallMulti& m, int channels, hipStream_t s) {
+  if (m.nst <= 0 || channels <= 0 || m.first[m.nst] <= 0) return;
+  hipLaunchKernelGGL(k_pc_small_multi, dim3((unsigned)m.first[m.nst], (unsigned)channels), dim3(256), 0, s, m);
+}
+
+bool launch_pc_small(int N, const PcSmallArgs& a, int channels, hipStream_t s) {
+  if (a.nb <= 0 || channels <= 0) return true;
+  switch (N) {
+    case 128: pc_small_go<128>(a, channels, s); return true;
+    case 256: pc_small_go<256>(a, channels, s); return true;
+    case 512: pc_small_go<512>(a, channels, s); return true;
+    case 1024: pc_small_go<1024>(a, channels, s); return true;
+    case 2048: pc_small_go<2048>(a, channels, s); return true;
+    default: return false;
+  }
 }
 
 }  // namespace adsp

@@ -90,6 +90,34 @@ void launch_direct_circular(const double* a, const double* b, int64_t n, double*
 void launch_stream_direct(const double* h, int64_t K, const double* buf, int64_t B, double* y, hipStream_t s);
 void launch_mixdown(const double* ch, int channels, int64_t stride, int64_t len, double* mix, int64_t mix_stride,
                     int first_parity, hipStream_t s);
+// One small partitioned stage (two partitions of p <= 1024 taps) for nb
+// consecutive blocks of every channel, fused and stateless: a workgroup per
+// (block, channel) transforms both input windows x[d-2p, d) and x[d-p, d+p)
+// (N = 2p points), multiplies by the two partition spectra, inverse
+// transforms and adds the block's p outputs into the accumulator.
+struct PcSmallArgs {
+  const double* xin;     // [C][xstride] input FIFO, column 0 = absolute time xbase
+  int64_t xstride, xbase;
+  int64_t d0;            // absolute time of the first block
+  int nb;                // blocks per channel
+  const double2* H;      // [2][N] full complex spectra of the two partitions (zero padded to N)
+  double* acc;           // [C][acc_stride]; block b adds at acc + (d0 + b*p) - acc_origin
+  int64_t acc_stride;
+  int64_t acc_off;       // accumulator column of absolute time d0 (includes the stage's tap offset)
+  const double2* tw;     // W_2048^m, m < 2048
+};
+bool launch_pc_small(int N, const PcSmallArgs& a, int channels, hipStream_t s);
+// Several fused stages in ONE launch (their accumulator ranges must be
+// disjoint): stage k takes grid columns [first[k], first[k+1]).
+constexpr int kPcMaxFused = 8;
+struct PcSmallMulti {
+  PcSmallArgs st[kPcMaxFused];
+  int N[kPcMaxFused];
+  int first[kPcMaxFused + 1];
+  int nst;
+};
+void launch_pc_small_multi(const PcSmallMulti& m, int channels, hipStream_t s);
+
 // dst[c][j] = j < ncopy ? src[c][j] : 0 for j < ncols (channel strides differ)
 void launch_shift_cols(const double* src, int64_t src_stride, double* dst, int64_t dst_stride, int channels,
                        int64_t ncopy, int64_t ncols, hipStream_t s);
@@ -97,6 +125,7 @@ void launch_shift_cols(const double* src, int64_t src_stride, double* dst, int64
 // dry * in[c][i] + wet * that (ConvolutionReverb.ProcessInPlace, no contraction).
 void launch_pc_emit(const double* in, int64_t in_stride, double* out, int64_t out_stride, const double* acc,
                     int64_t acc_stride, int64_t off, int64_t first, int64_t n, int channels, int mix, double wet,
-                    double dry, hipStream_t s);
+                    double dry, hipStream_t s, double* append_to = nullptr, int64_t append_stride = 0,
+                    bool emit = true, int64_t row2 = 0);
 
 }  // namespace adsp

@@ -2,6 +2,9 @@
 #include "nupols_engine.hpp"
 
 #include <algorithm>
+#include <climits>
+#include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 #include "conv_kernels.hpp"
@@ -131,6 +134,34 @@ void Nupols::process(const double* in, int64_t n, double* out) {
 // ---------------------------------------------------------------------------
 namespace {
 int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
+
+// In-place forward DFT of a power-of-two length in long double (radix-2,
+// bit-reversed input reordering): the fused stages' partition spectra.
+void host_fft_ld(std::vector<long double>& re, std::vector<long double>& im) {
+  const size_t n = re.size();
+  for (size_t i = 1, j = 0; i < n; ++i) {
+    size_t bit = n >> 1;
+    for (; j & bit; bit >>= 1) j ^= bit;
+    j ^= bit;
+    if (i < j) {
+      std::swap(re[i], re[j]);
+      std::swap(im[i], im[j]);
+    }
+  }
+  for (size_t len = 2; len <= n; len <<= 1) {
+    const long double a = -6.283185307179586476925286766559005768L / (long double)len;
+    for (size_t i = 0; i < n; i += len)
+      for (size_t k = 0; k < len / 2; ++k) {
+        const long double wr = cosl(a * k), wi = sinl(a * k);
+        const long double xr = re[i + k + len / 2] * wr - im[i + k + len / 2] * wi;
+        const long double xi = re[i + k + len / 2] * wi + im[i + k + len / 2] * wr;
+        re[i + k + len / 2] = re[i + k] - xr;
+        im[i + k + len / 2] = im[i + k] - xi;
+        re[i + k] += xr;
+        im[i + k] += xi;
+      }
+  }
+}
 }  // namespace
 
 NupolsDev::NupolsDev(int device, const double* h, int64_t K, int64_t lambda, int64_t p_max, int channels,
@@ -151,17 +182,61 @@ NupolsDev::NupolsDev(int device, const double* h, int64_t K, int64_t lambda, int
     T += nparts * p;
     if (p < p_max) p *= 2;
   }
-  for (auto& st : st_) {
-    // up to 64 blocks (and >= 8192 samples) per launch chunk: long calls batch
-    const int jc = (int)std::max<int64_t>(64, 8192 / st.p);
-    st.eng.reset(new Upols(device, h + st.T, 1, st.taps, (int)st.p, channels, nullptr, jc, s));
+  // AD_PC_SIDE=1: the large stages on a stream of their own (measured: no
+  // gain at lambda = 128, slower at 4096-sample calls -- off by default)
+  const char* sd = std::getenv("AD_PC_SIDE");
+  use_side_ = sd && *sd == '1';
+  AD_HIP(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
+  AD_HIP(hipEventCreateWithFlags(&ev_main_, hipEventDisableTiming));
+  AD_HIP(hipEventCreateWithFlags(&ev_side_, hipEventDisableTiming));
+  const char* fz = std::getenv("AD_PC_FUSED");
+  const bool allow_fused = !(fz && *fz == '0');
+  std::vector<double2> tw(2048);
+  for (int m = 0; m < 2048; ++m) {
+    const long double a = -6.283185307179586476925286766559005768L * m / 2048.0L;
+    tw[m] = make_double2((double)cosl(a), (double)sinl(a));
   }
+  tw2048_.alloc(2048);
+  AD_HIP(hipMemcpyAsync(tw2048_.p, tw.data(), 2048 * sizeof(double2), hipMemcpyHostToDevice, s));
+  for (auto& st : st_) {
+    st.fused = allow_fused && st.p <= 1024 && st.taps <= 2 * st.p;
+    if (st.fused) {
+      const int N = (int)(2 * st.p);
+      std::vector<double2> hs(2 * (size_t)N);
+      for (int part = 0; part < 2; ++part) {
+        std::vector<long double> re(N, 0.0L), im(N, 0.0L);
+        for (int64_t k = 0; k < st.p; ++k) {
+          const int64_t tap = st.T + part * st.p + k;
+          if (tap < st.T + st.taps) re[k] = h[tap];
+        }
+        host_fft_ld(re, im);
+        for (int k = 0; k < N; ++k) hs[(size_t)part * N + k] = make_double2((double)re[k], (double)im[k]);
+      }
+      st.H.reset(new DevBuf<double2>());
+      st.H->alloc(hs.size());
+      AD_HIP(hipMemcpyAsync(st.H->p, hs.data(), hs.size() * sizeof(double2), hipMemcpyHostToDevice, s));
+      AD_HIP(hipStreamSynchronize(s));  // hs must outlive the copy
+    } else {
+      // up to 64 blocks (and >= 8192 samples) per launch chunk: long calls batch
+      const int jc = (int)std::max<int64_t>(64, 8192 / st.p);
+      st.eng.reset(new Upols(device, h + st.T, 1, st.taps, (int)st.p, channels, nullptr, jc, s));
+    }
+  }
+  AD_HIP(hipStreamSynchronize(s));
   reset(s);
 }
 
+void NupolsDev::wait_side(hipStream_t s) {
+  if (!side_busy_) return;
+  AD_HIP(hipStreamWaitEvent(s, ev_side_, 0));
+  side_busy_ = false;
+  side_lo_ = INT64_MAX;
+}
+
 void NupolsDev::reset(hipStream_t s) {
+  wait_side(s);
   for (auto& st : st_) {
-    st.eng->reset_stream(s);
+    if (st.eng) st.eng->reset_stream(s);
     st.done = 0;
   }
   received_ = emitted_ = 0;
@@ -172,9 +247,10 @@ void NupolsDev::reset(hipStream_t s) {
 
 void NupolsDev::ensure_xin(int64_t need_hi, hipStream_t s) {
   if (need_hi - xin_base_ <= xcap_) return;
-  int64_t min_done = received_;
-  for (auto& st : st_) min_done = std::min(min_done, st.done);
-  const int64_t nb = min_done / 64 * 64;  // keep 16-byte alignment of every stage's block start
+  wait_side(s);  // side-stream stages may still read either FIFO buffer
+  int64_t min_done = received_;  // fused stages re-read two windows (2p) before their next block
+  for (auto& st : st_) min_done = std::min(min_done, st.fused ? st.done - 2 * st.p : st.done);
+  const int64_t nb = std::max<int64_t>(0, min_done) / 64 * 64;  // 16-byte alignment of every block start
   const int64_t keep = received_ - nb;
   const int64_t cap = std::max<int64_t>(round_up(2 * (need_hi - nb), 8192), xcap_);
   DevBuf<double>& dst = xin_[xcur_ ^ 1];
@@ -189,13 +265,14 @@ void NupolsDev::ensure_xin(int64_t need_hi, hipStream_t s) {
 
 void NupolsDev::ensure_acc(int64_t lo_keep, int64_t need_hi, hipStream_t s) {
   if (need_hi - acc_base_ <= acap_ && acc_[acur_].p) return;
+  wait_side(s);  // no side-stream write may land in a buffer being shifted
   const int64_t nb = std::max<int64_t>(acc_base_, lo_keep / 64 * 64);
   const int64_t keep = std::max<int64_t>(0, acc_hi_ - nb);
   const int64_t cap = std::max<int64_t>(round_up(2 * (need_hi - nb), 8192), acap_);
   DevBuf<double>& dst = acc_[acur_ ^ 1];
-  dst.alloc((size_t)C_ * cap);
+  dst.alloc((size_t)2 * C_ * cap);
   if (acc_[acur_].p)
-    launch_shift_cols(acc_[acur_].p + (nb - acc_base_), acap_, dst.p, cap, C_, keep, cap, s);
+    launch_shift_cols(acc_[acur_].p + (nb - acc_base_), acap_, dst.p, cap, 2 * C_, keep, cap, s);
   else
     AD_HIP(hipMemsetAsync(dst.p, 0, dst.n * sizeof(double), s));
   if (cap != acap_) acc_[acur_].release();
@@ -204,37 +281,202 @@ void NupolsDev::ensure_acc(int64_t lo_keep, int64_t need_hi, hipStream_t s) {
   acc_base_ = nb;
 }
 
-void NupolsDev::process(const double* d_in, int64_t in_stride, double* d_out, int64_t out_stride, int64_t n,
-                        bool mix, double wet, double dry, hipStream_t s) {
-  if (n <= 0) return;
-  // 1. append the block to the input FIFO
+int64_t NupolsDev::complete_upto() const {
+  int64_t c = INT64_MAX;
+  for (auto& st : st_) c = std::min(c, st.done + st.T);
+  return c;
+}
+
+void NupolsDev::append(const double* d_in, int64_t in_stride, int64_t n, bool mapped_src, hipStream_t s) {
   ensure_xin(received_ + n, s);
-  AD_HIP(hipMemcpy2DAsync(xin_[xcur_].p + (received_ - xin_base_), (size_t)xcap_ * sizeof(double), d_in,
-                          (size_t)in_stride * sizeof(double), (size_t)n * sizeof(double), (size_t)C_,
-                          hipMemcpyDeviceToDevice, s));
+  double* dst = xin_[xcur_].p + (received_ - xin_base_);
+  if (mapped_src && C_ == 1) {
+    launch_copy_f64(d_in, dst, n, s);  // a copy kernel reads mapped host memory fastest
+  } else {
+    AD_HIP(hipMemcpy2DAsync(dst, (size_t)xcap_ * sizeof(double), d_in, (size_t)in_stride * sizeof(double),
+                            (size_t)n * sizeof(double), (size_t)C_, hipMemcpyDeviceToDevice, s));
+  }
   received_ += n;
-  // 2. every complete block of every stage; K3 adds into the accumulator at +T
+}
+
+void NupolsDev::run_stages(int64_t emit_hi, hipStream_t s) {
   int64_t hi = acc_hi_;
   for (auto& st : st_) {
     const int64_t nb = (received_ - st.done) / st.p;
     if (nb > 0) hi = std::max(hi, st.done + nb * st.p + st.T);
   }
-  ensure_acc(emitted_ - lambda_, std::max(hi, emitted_ + n), s);
+  ensure_acc(emitted_ - lambda_, std::max(hi, emit_hi), s);
+  // Fused stages whose accumulator ranges are pairwise disjoint (every
+  // lambda-aligned call: the stages firing together tile the time axis) go
+  // in one launch; otherwise one launch each, in stage order.
+  {
+    PcSmallMulti m{};
+    std::vector<std::pair<int64_t, int64_t>> ranges;
+    bool disjoint = true;
+    for (auto& st : st_) {
+      const int64_t nb = (received_ - st.done) / st.p;
+      if (!st.fused || nb == 0) continue;
+      const int64_t lo = st.done + st.T, hi2 = lo + nb * st.p;
+      for (auto& r : ranges)
+        if (lo < r.second && r.first < hi2) disjoint = false;
+      ranges.push_back({lo, hi2});
+      if (m.nst == kPcMaxFused || (int64_t)m.first[m.nst] + nb > (1 << 30)) disjoint = false;
+      if (!disjoint) break;
+      PcSmallArgs& a = m.st[m.nst];
+      a.xin = xin_[xcur_].p;
+      a.xstride = xcap_;
+      a.xbase = xin_base_;
+      a.d0 = st.done;
+      a.nb = (int)nb;
+      a.H = st.H->p;
+      a.acc = acc_[acur_].p;
+      a.acc_stride = acap_;
+      a.acc_off = st.done + st.T - acc_base_;
+      a.tw = tw2048_.p;
+      m.N[m.nst] = (int)(2 * st.p);
+      m.first[m.nst + 1] = m.first[m.nst] + (int)nb;
+      ++m.nst;
+    }
+    if (disjoint && m.nst > 1) {
+      launch_pc_small_multi(m, C_, s);
+      for (auto& st : st_)
+        if (st.fused) st.done += (received_ - st.done) / st.p * st.p;
+    }
+  }
   for (auto& st : st_) {
     const int64_t nb = (received_ - st.done) / st.p;
     if (nb == 0) continue;
     const int64_t len = nb * st.p;
-    st.eng->run(xin_[xcur_].p + (st.done - xin_base_), xcap_, len, acc_[acur_].p + (st.done + st.T - acc_base_),
-                acap_, len, /*use_hist=*/true, s, 0, -1, /*accumulate=*/true);
+    if (st.fused) {
+      PcSmallArgs a{};
+      a.xin = xin_[xcur_].p;
+      a.xstride = xcap_;
+      a.xbase = xin_base_;
+      a.d0 = st.done;
+      a.nb = (int)nb;
+      a.H = st.H->p;
+      a.acc = acc_[acur_].p;
+      a.acc_stride = acap_;
+      a.acc_off = st.done + st.T - acc_base_;
+      a.tw = tw2048_.p;
+      if (!launch_pc_small((int)(2 * st.p), a, C_, s)) AD_FAIL(AD_ERR_INTERNAL, "fused stage size");
+    } else if (!use_side_) {
+      st.eng->run(xin_[xcur_].p + (st.done - xin_base_), xcap_, len, acc_[acur_].p + (st.done + st.T - acc_base_),
+                  acap_, len, /*use_hist=*/true, s, 0, -1, /*accumulate=*/true);
+    } else {
+      // large stage on the side stream, into accumulator row 1: it runs while
+      // the next calls go through; an emit that needs it waits (emit())
+      AD_HIP(hipEventRecord(ev_main_, s));
+      AD_HIP(hipStreamWaitEvent(side_, ev_main_, 0));
+      st.eng->run(xin_[xcur_].p + (st.done - xin_base_), xcap_, len,
+                  acc_[acur_].p + (int64_t)C_ * acap_ + (st.done + st.T - acc_base_), acap_, len, /*use_hist=*/true,
+                  side_, 0, -1, /*accumulate=*/true);
+      AD_HIP(hipEventRecord(ev_side_, side_));
+      side_busy_ = true;
+      side_lo_ = std::min(side_lo_, st.done + st.T);
+    }
     st.done += len;
   }
   acc_hi_ = hi;
-  // 3. emit y[t - lambda] for t in [emitted, emitted + n)
+}
+
+void NupolsDev::emit(const double* d_in, int64_t in_stride, double* d_out, int64_t out_stride, int64_t n, bool mix,
+                     double wet, double dry, hipStream_t s) {
   const int64_t first = std::max<int64_t>(0, std::min<int64_t>(n, lambda_ - emitted_));
+  if (side_lo_ < emitted_ + n - lambda_) wait_side(s);
   launch_pc_emit(d_in, in_stride, d_out, out_stride, acc_[acur_].p, acap_, emitted_ - lambda_ - acc_base_, first, n,
-                 C_, mix ? 1 : 0, wet, dry, s);
+                 C_, mix ? 1 : 0, wet, dry, s, nullptr, 0, true, use_side_ ? (int64_t)C_ * acap_ : 0);
   AD_HIP(hipGetLastError());
   emitted_ += n;
+}
+
+void NupolsDev::process(const double* d_in, int64_t in_stride, double* d_out, int64_t out_stride, int64_t n,
+                        bool mix, double wet, double dry, hipStream_t s) {
+  if (n <= 0) return;
+  append(d_in, in_stride, n, false, s);           // 1. the block joins the input FIFO
+  run_stages(emitted_ + n, s);                    // 2. every complete block of every stage (K3 adds at +T)
+  emit(d_in, in_stride, d_out, out_stride, n, mix, wet, dry, s);  // 3. y[t - lambda]
+}
+
+void NupolsDev::ensure_mapped(int64_t n) {
+  if (n <= map_cap_) return;
+  if (map_cap_) AD_HIP(hipDeviceSynchronize());
+  for (int i = 0; i < 2; ++i) {
+    if (in_h_[i]) AD_HIP(hipHostFree(in_h_[i]));
+    in_h_[i] = nullptr;
+  }
+  if (out_h_) AD_HIP(hipHostFree(out_h_));
+  out_h_ = nullptr;
+  map_cap_ = 0;
+  const size_t bytes = (size_t)n * C_ * sizeof(double);
+  for (int i = 0; i < 2; ++i) {
+    AD_HIP(hipHostMalloc(reinterpret_cast<void**>(&in_h_[i]), bytes, hipHostMallocMapped));
+    AD_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&in_d_[i]), in_h_[i], 0));
+  }
+  AD_HIP(hipHostMalloc(reinterpret_cast<void**>(&out_h_), bytes, hipHostMallocMapped));
+  AD_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&out_d_), out_h_, 0));
+  map_cap_ = n;
+}
+
+void NupolsDev::process_host(const double* in, double* out, int64_t n, bool mix, double wet, double dry,
+                             hipStream_t s) {
+  if (n <= 0) return;
+  if (!ev_emit_) {
+    AD_HIP(hipEventCreateWithFlags(&ev_emit_, hipEventDisableTiming));
+    for (auto& e : ev_in_) AD_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
+  ensure_mapped(n);
+  const int slot = in_slot_;
+  in_slot_ ^= 1;
+  if (in_used_[slot]) AD_HIP(hipEventSynchronize(ev_in_[slot]));  // the append that read this buffer is done
+  std::memcpy(in_h_[slot], in, (size_t)n * C_ * sizeof(double));
+  // The emit needs the accumulator only below emitted + n - lambda.  When the
+  // previous calls' stage work already covers that (every lambda-aligned call
+  // of at most lambda samples), the output goes out first and this call's
+  // stage work runs behind it: the caller gets its block back while the GPU
+  // convolves, and the next call finds that work done.
+  const bool emit_first = emitted_ + n - lambda_ <= complete_upto();
+  if (emit_first) {
+    // one launch: emit from the accumulator + append the block to the FIFO
+    ensure_xin(received_ + n, s);
+    const int64_t first = std::max<int64_t>(0, std::min<int64_t>(n, lambda_ - emitted_));
+    if (side_lo_ < emitted_ + n - lambda_) wait_side(s);
+    launch_pc_emit(in_d_[slot], n, out_d_, n, acc_[acur_].p, acap_, emitted_ - lambda_ - acc_base_, first, n, C_,
+                   mix ? 1 : 0, wet, dry, s, xin_[xcur_].p + (received_ - xin_base_), xcap_, true,
+                   use_side_ ? (int64_t)C_ * acap_ : 0);
+    AD_HIP(hipGetLastError());
+    emitted_ += n;
+    received_ += n;
+    AD_HIP(hipEventRecord(ev_emit_, s));
+    AD_HIP(hipEventRecord(ev_in_[slot], s));
+    run_stages(emitted_, s);
+  } else {
+    append(in_d_[slot], n, n, true, s);
+    AD_HIP(hipEventRecord(ev_in_[slot], s));
+    run_stages(emitted_ + n, s);
+    emit(in_d_[slot], n, out_d_, n, n, mix, wet, dry, s);
+    AD_HIP(hipEventRecord(ev_emit_, s));
+  }
+  in_used_[slot] = true;
+  AD_HIP(hipEventSynchronize(ev_emit_));
+  std::memcpy(out, out_h_, (size_t)n * C_ * sizeof(double));
+}
+
+NupolsDev::~NupolsDev() {
+  if (side_) {
+    (void)hipStreamSynchronize(side_);
+    (void)hipStreamDestroy(side_);
+  }
+  if (ev_main_) (void)hipEventDestroy(ev_main_);
+  if (ev_side_) (void)hipEventDestroy(ev_side_);
+  if (ev_emit_) {
+    (void)hipDeviceSynchronize();
+    (void)hipEventDestroy(ev_emit_);
+    for (auto& e : ev_in_) (void)hipEventDestroy(e);
+  }
+  for (auto& p : in_h_)
+    if (p) (void)hipHostFree(p);
+  if (out_h_) (void)hipHostFree(out_h_);
 }
 
 }  // namespace adsp

@@ -19,6 +19,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <climits>
 #include <cstdint>
 #include <memory>
 #include <vector>
@@ -82,22 +83,51 @@ class NupolsDev {
   // n samples of every channel; in == out (in place) allowed.
   void process(const double* d_in, int64_t in_stride, double* d_out, int64_t out_stride, int64_t n, bool mix,
                double wet, double dry, hipStream_t s);
+  // Host buffers in[C][n] -> out[C][n] through mapped pinned memory; blocks
+  // until out is written.  Emits before this call's stage work when the
+  // accumulator is already complete for the emitted range (see .cpp).
+  void process_host(const double* in, double* out, int64_t n, bool mix, double wet, double dry, hipStream_t s);
   void reset(hipStream_t s);
   int channels() const { return C_; }
+  ~NupolsDev();
 
  private:
+  int64_t complete_upto() const;  // accumulator complete for times below this
+  void append(const double* d_in, int64_t in_stride, int64_t n, bool mapped_src, hipStream_t s);
+  void run_stages(int64_t emit_hi, hipStream_t s);
+  void emit(const double* d_in, int64_t in_stride, double* d_out, int64_t out_stride, int64_t n, bool mix,
+            double wet, double dry, hipStream_t s);
+  void ensure_mapped(int64_t n);
+  double* in_h_[2] = {nullptr, nullptr};
+  double* in_d_[2] = {nullptr, nullptr};
+  double *out_h_ = nullptr, *out_d_ = nullptr;
+  int64_t map_cap_ = 0;
+  int in_slot_ = 0;
+  bool in_used_[2] = {false, false};
+  hipEvent_t ev_emit_ = nullptr;
+  hipEvent_t ev_in_[2] = {nullptr, nullptr};
+
   struct Stage {
     int64_t p = 0, T = 0, taps = 0;
-    std::unique_ptr<Upols> eng;
-    int64_t done = 0;  // input samples consumed
+    bool fused = false;        // two partitions, p <= 1024: k_pc_small (stateless per block)
+    std::unique_ptr<Upols> eng;  // otherwise: a zero-latency UPOLS engine over all channels
+    std::unique_ptr<DevBuf<double2>> H;  // fused: [2][2p] partition spectra
+    int64_t done = 0;          // input samples consumed
   };
+  DevBuf<double2> tw2048_;     // W_2048^m, m < 2048 (fused stages)
   int C_;
   int64_t lambda_;
   std::vector<Stage> st_;
   DevBuf<double> xin_[2];  // [C][xcap], ping-pong for compaction
   int xcur_ = 0;
   int64_t xcap_ = 0, xin_base_ = 0;
-  DevBuf<double> acc_[2];  // [C][acap]
+  DevBuf<double> acc_[2];  // [2][C][acap]: row 0 the caller-stream stages, row 1 the side-stream stages
+  bool use_side_ = false;
+  hipStream_t side_ = nullptr;  // the large (UPOLS) stages: off the per-call critical path
+  hipEvent_t ev_main_ = nullptr, ev_side_ = nullptr;
+  bool side_busy_ = false;      // side work enqueued since the caller's stream last waited for it
+  int64_t side_lo_ = INT64_MAX; // earliest output time that work writes
+  void wait_side(hipStream_t s);
   int acur_ = 0;
   int64_t acap_ = 0, acc_base_ = 0;
   int64_t received_ = 0, emitted_ = 0;
