@@ -199,6 +199,21 @@ __device__ __forceinline__ TwLds<M> tw_lds_fill(double2* ltab, const double2* __
   return TwLds<M>{ltab, ltab + Sp::NLO};
 }
 
+// Same tables computed in the kernel (sincospi; <= 1 ulp from the rounded
+// table, far inside the 1e-7 gate): no global load ahead of a workgroup's
+// data loads, so its first transform waits for one memory round trip only.
+template <int M>
+__device__ __forceinline__ TwLds<M> tw_lds_compute(double2* ltab, int tid, int nthreads) {
+  using Sp = TwSplit<M>;
+  for (int i = tid; i < Sp::N; i += nthreads) {
+    const int e = i < Sp::NLO ? i : ((i - Sp::NLO) << Sp::S);
+    double sn, cs;
+    sincospi(-2.0 * (double)e / (double)M, &sn, &cs);
+    ltab[i < Sp::NLO ? tw_slot(i) : i] = make_double2(cs, sn);
+  }
+  return TwLds<M>{ltab, ltab + Sp::NLO};
+}
+
 // Twiddle multiply for butterfly jb of a pass with stride NS and radix R:
 // v[r] *= W_{NS*R}^{(jb mod NS) * r} = W_M^{e*r}, e = (jb mod NS) * M/(NS*R).
 template <int M, int R, int NS, bool FWD, class TW>

@@ -167,8 +167,6 @@ __global__ __launch_bounds__((SplitPlan<M>::T)) __attribute__((amdgpu_waves_per_
   constexpr int M2 = SP::M2, V = SP::V, T = SP::T, L = M;
   __shared__ __attribute__((aligned(16))) double2 lds[SP::LDS];
   const int tid = threadIdx.x;
-  const TwLds<M2> twS = tw_lds_fill<M2, 2>(lds + FftPlan<M2, V>::MP, a.twM, tid, T);
-  const TwLds<M> twC = tw_lds_fill<M>(lds + FftPlan<M2, V>::MP + TwSplit<M2>::N, a.twM, tid, T);
   const int64_t e = xcd_remap_fft(blockIdx.x, gridDim.x);
   const int c = (int)(e / a.jc);
   const int j = (int)(e % a.jc);
@@ -178,12 +176,13 @@ __global__ __launch_bounds__((SplitPlan<M>::T)) __attribute__((amdgpu_waves_per_
 
   double2 ev[V], ov[V];
   if (a.aligned && t0 >= 0 && t0 + 2 * L <= a.n) {  // wave-uniform fast path
+    // E's inputs first: its transform starts while O's are still in flight
 #pragma unroll
-    for (int s = 0; s < V; ++s) {
-      const double* p = xc + t0 + 4 * pass0_index<M2, V>(tid, s);
-      ev[s] = *reinterpret_cast<const double2*>(p);
-      ov[s] = *reinterpret_cast<const double2*>(p + 2);
-    }
+    for (int s = 0; s < V; ++s)
+      ev[s] = *reinterpret_cast<const double2*>(xc + t0 + 4 * pass0_index<M2, V>(tid, s));
+#pragma unroll
+    for (int s = 0; s < V; ++s)
+      ov[s] = *reinterpret_cast<const double2*>(xc + t0 + 4 * pass0_index<M2, V>(tid, s) + 2);
   } else {
 #pragma unroll
     for (int s = 0; s < V; ++s) {
@@ -205,6 +204,8 @@ __global__ __launch_bounds__((SplitPlan<M>::T)) __attribute__((amdgpu_waves_per_
       }
     }
   }
+  const TwLds<M2> twS = tw_lds_compute<M2>(lds + FftPlan<M2, V>::MP, tid, T);
+  const TwLds<M> twC = tw_lds_compute<M>(lds + FftPlan<M2, V>::MP + TwSplit<M2>::N, tid, T);
   __syncthreads();  // twiddle tables
   fft_run<M2, V, true>(ev, tid, lds, twS);
   __syncthreads();  // E's last LDS reads are done
@@ -225,19 +226,21 @@ __global__ __launch_bounds__((SplitPlan<M>::T)) __attribute__((amdgpu_waves_per_
   constexpr int M2 = SP::M2, V = SP::V, T = SP::T, L = M;
   __shared__ __attribute__((aligned(16))) double2 lds[SP::LDS];
   const int tid = threadIdx.x;
-  const TwLds<M2> twS = tw_lds_fill<M2, 2>(lds + FftPlan<M2, V>::MP, a.twM, tid, T);
-  const TwLds<M> twC = tw_lds_fill<M>(lds + FftPlan<M2, V>::MP + TwSplit<M2>::N, a.twM, tid, T);
   const int64_t e = xcd_remap_fft(blockIdx.x, gridDim.x);
   const int c = (int)(e / a.jc);
   const int j = (int)(e % a.jc);
   const double2* Zb = a.Y + (int64_t)c * a.y_ch_stride + (int64_t)j * a.MS;
   double2 av[V], bv[V];
+  // bins 2k, 2k+1 in wave-lane row order (zrow_pos): one 32-byte pair per
+  // lane and s (loading all of A first measured slower: half-line requests)
 #pragma unroll
   for (int s = 0; s < V; ++s) {
-    const int k = pass0_index<M2, V>(tid, s);  // bins 2k, 2k+1 in wave-lane row order (zrow_pos)
+    const int k = pass0_index<M2, V>(tid, s);
     av[s] = Zb[zrow_pos(2 * k, M)];
     bv[s] = Zb[zrow_pos(2 * k + 1, M)];
   }
+  const TwLds<M2> twS = tw_lds_compute<M2>(lds + FftPlan<M2, V>::MP, tid, T);
+  const TwLds<M> twC = tw_lds_compute<M>(lds + FftPlan<M2, V>::MP + TwSplit<M2>::N, tid, T);
   __syncthreads();  // twiddle tables
   fft_run<M2, V, false>(av, tid, lds, twS);
   __syncthreads();
