@@ -113,6 +113,7 @@ class DeconvOptionsC(C.Structure):
 _lib = None
 
 c_double_p = C.POINTER(C.c_double)
+c_float_p = C.POINTER(C.c_float)
 c_int64_p = C.POINTER(C.c_int64)
 
 
@@ -148,6 +149,11 @@ def _declare(L: C.CDLL) -> None:
         "ad_conv_stream_ols_create": (C.c_int, [c_double_p, i64, i64, C.c_int, C.POINTER(vp)]),
         "ad_conv_stream_ola_create": (C.c_int, [c_double_p, i64, i64, C.c_int, C.POINTER(vp)]),
         "ad_conv_process_block": (C.c_int, [vp, c_double_p, i64, c_double_p, i64]),
+        "ad_conv_stream_ols32_create": (C.c_int, [c_float_p, i64, i64, C.c_int, C.POINTER(vp)]),
+        "ad_conv_stream_ola32_create": (C.c_int, [c_float_p, i64, i64, C.c_int, C.POINTER(vp)]),
+        "ad_conv_process_block32": (C.c_int, [vp, c_float_p, i64, c_float_p, i64]),
+        "ad_conv_partitioned32_create": (C.c_int, [c_float_p, i64, C.c_int, C.c_int, C.c_int, C.POINTER(vp)]),
+        "ad_conv_partitioned_process_block32": (C.c_int, [vp, c_float_p, i64, c_float_p, i64]),
         "ad_conv_ols_create": (C.c_int, [c_double_p, i64, i64, C.c_int, C.POINTER(vp)]),
         "ad_conv_ola_create": (C.c_int, [c_double_p, i64, i64, C.c_int, C.POINTER(vp)]),
         "ad_conv_process": (C.c_int, [vp, c_double_p, i64, c_double_p, i64]),

@@ -24,6 +24,7 @@ __all__ = [
     "ModeFull", "ModeSame", "ModeValid",
     "Direct", "DirectCircular", "Convolve", "ConvolveMode",
     "NewStreamingOverlapSave", "NewStreamingOverlapAdd", "NewOverlapSave", "NewOverlapAdd",
+    "NewStreamingOverlapSave32", "NewStreamingOverlapAdd32", "NewPartitionedConvolution32",
     "NewPartitionedConvolution", "OverlapAddConvolve", "OverlapSaveConvolve", "MultiChannelConvolver",
     "MultiChannelStreamingConvolver", "PartitionedConvolutionMulti", "NewConvolutionReverbMulti",
     "ErrDivisionByZero", "Correlate", "CorrelateDirect", "CorrelateMode", "AutoCorrelate", "AutoCorrelateNormalized",
@@ -97,6 +98,43 @@ def NewStreamingOverlapAdd(kernel, blockSize: int) -> StreamingConvolver:
     return StreamingConvolver(_create(lib().ad_conv_stream_ola_create, ptr(k), k.size, int(blockSize), DEVICE))
 
 
+def _f32(a) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(a, dtype=np.float32))
+
+
+def _fptr(a: np.ndarray):
+    if a.size == 0:
+        return C.cast(C.c_void_p(0), C.POINTER(C.c_float))
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+class StreamingConvolver32(StreamingConvolver):
+    """StreamingConvolverT[float32, complex64] (streaming.go:27-49)."""
+
+    def ProcessBlockTo(self, output: np.ndarray, input) -> None:
+        x = _f32(input)
+        if not (isinstance(output, np.ndarray) and output.dtype == np.float32 and output.flags.c_contiguous):
+            raise TypeError("output must be a contiguous float32 ndarray")
+        check(lib().ad_conv_process_block32(self._h, _fptr(x), x.size, _fptr(output), output.size))
+
+    def ProcessBlock(self, input) -> np.ndarray:
+        out = np.empty(self.BlockSize(), dtype=np.float32)
+        self.ProcessBlockTo(out, input)
+        return out
+
+
+def NewStreamingOverlapSave32(kernel, blockSize: int) -> StreamingConvolver32:
+    """streaming_overlap_save.go:94"""
+    k = _f32(kernel)
+    return StreamingConvolver32(_create(lib().ad_conv_stream_ols32_create, _fptr(k), k.size, int(blockSize), DEVICE))
+
+
+def NewStreamingOverlapAdd32(kernel, blockSize: int) -> StreamingConvolver32:
+    """streaming_overlap_add.go:93"""
+    k = _f32(kernel)
+    return StreamingConvolver32(_create(lib().ad_conv_stream_ola32_create, _fptr(k), k.size, int(blockSize), DEVICE))
+
+
 class BatchConvolver(_Handle):
     """conv.OverlapSave / conv.OverlapAdd batch convolvers."""
 
@@ -164,6 +202,23 @@ def NewPartitionedConvolution(kernel, minBlockOrder: int, maxBlockOrder: int) ->
     k = f64(kernel)
     return PartitionedConvolution(
         _create(lib().ad_conv_partitioned_create, ptr(k), k.size, int(minBlockOrder), int(maxBlockOrder), DEVICE))
+
+
+class PartitionedConvolution32(PartitionedConvolution):
+    """PartitionedConvolutionT[float32, complex64] (partitioned.go:340)."""
+
+    def ProcessBlock(self, input, output: np.ndarray) -> None:
+        x = _f32(input)
+        if not (isinstance(output, np.ndarray) and output.dtype == np.float32 and output.flags.c_contiguous):
+            raise TypeError("output must be a contiguous float32 ndarray")
+        check(lib().ad_conv_partitioned_process_block32(self._h, _fptr(x), x.size, _fptr(output), output.size))
+
+
+def NewPartitionedConvolution32(kernel, minBlockOrder: int, maxBlockOrder: int) -> PartitionedConvolution32:
+    """partitioned.go:340"""
+    k = _f32(kernel)
+    return PartitionedConvolution32(
+        _create(lib().ad_conv_partitioned32_create, _fptr(k), k.size, int(minBlockOrder), int(maxBlockOrder), DEVICE))
 
 
 class ConvolutionReverb(_Handle):

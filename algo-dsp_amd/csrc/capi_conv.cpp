@@ -87,6 +87,8 @@ struct ad_conv {
   std::unique_ptr<Upols> eng;  // FFT path
   std::unique_ptr<HostPipeline> pipe;  // overlapped host-buffer offline calls
   int channels = 1;
+  bool f32 = false;                    // float32 boundary (the *32 constructors)
+  std::vector<double> w_in, w_out;     // float32 calls: widened block
   int64_t hop = 0;
   int64_t seg_next = -1;  // next out_begin of a segmented offline call (-1: none open)
 
@@ -342,6 +344,86 @@ int ad_conv_process_block(ad_conv* h, const double* in, int64_t in_len, double* 
                                           " output samples, got " + std::to_string(out_len));
     DeviceScope ds(h->device);
     stream_convolve(h, in, in_len, out);
+  });
+}
+
+// --- float32 instantiations ---------------------------------------------------
+// NewStreamingOverlapSave32 (streaming_overlap_save.go:94), NewStreamingOverlapAdd32
+// (streaming_overlap_add.go:93), NewPartitionedConvolution32 (partitioned.go:340):
+// float32 kernels and blocks at the boundary.  The samples are widened to
+// float64 (exactly) on the way in and rounded once to float32 on the way out;
+// the convolution itself runs on the float64 engine, so the result is the
+// correctly rounded float32 of a float64 convolution -- within the reference's
+// own complex64 error (its float32 tests allow 1e-4, streaming_test.go:175-265).
+
+namespace {
+std::vector<double> widen(const float* p, int64_t n) {
+  std::vector<double> v((size_t)std::max<int64_t>(n, 0));
+  for (int64_t i = 0; i < n; ++i) v[(size_t)i] = (double)p[i];
+  return v;
+}
+}  // namespace
+
+int ad_conv_stream_ols32_create(const float* kernel, int64_t kernel_len, int64_t block_size, int device,
+                                ad_conv** out) {
+  if (out) *out = nullptr;
+  if (kernel_len <= 0 || !kernel) {
+    set_last_error("conv: empty kernel");
+    return AD_ERR_EMPTY_KERNEL;
+  }
+  const std::vector<double> k = widen(kernel, kernel_len);
+  const int rc = stream_create(Kind::StreamOLS, k.data(), kernel_len, block_size, device, out);
+  if (rc == AD_OK) (*out)->f32 = true;
+  return rc;
+}
+
+int ad_conv_stream_ola32_create(const float* kernel, int64_t kernel_len, int64_t block_size, int device,
+                                ad_conv** out) {
+  if (out) *out = nullptr;
+  if (kernel_len <= 0 || !kernel) {
+    set_last_error("conv: empty kernel");
+    return AD_ERR_EMPTY_KERNEL;
+  }
+  const std::vector<double> k = widen(kernel, kernel_len);
+  const int rc = stream_create(Kind::StreamOLA, k.data(), kernel_len, block_size, device, out);
+  if (rc == AD_OK) (*out)->f32 = true;
+  return rc;
+}
+
+int ad_conv_process_block32(ad_conv* h, const float* in, int64_t in_len, float* out, int64_t out_len) {
+  return guard([&] {
+    if (!h) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "nil handle");
+    if (!h->f32) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "not a float32 convolver");
+    h->w_in = widen(in, in_len);
+    h->w_out.resize((size_t)std::max<int64_t>(out_len, 0));
+    const int rc = ad_conv_process_block(h, h->w_in.data(), in_len, h->w_out.data(), out_len);
+    if (rc != AD_OK) throw Status{rc, ad_last_error()};
+    for (int64_t i = 0; i < out_len; ++i) out[i] = (float)h->w_out[(size_t)i];
+  });
+}
+
+int ad_conv_partitioned32_create(const float* kernel, int64_t kernel_len, int min_block_order, int max_block_order,
+                                 int device, ad_conv** out) {
+  if (out) *out = nullptr;
+  if (kernel_len <= 0 || !kernel) {
+    set_last_error("conv: empty impulse response");
+    return AD_ERR_EMPTY_IMPULSE_RESPONSE;
+  }
+  const std::vector<double> k = widen(kernel, kernel_len);
+  const int rc = ad_conv_partitioned_create(k.data(), kernel_len, min_block_order, max_block_order, device, out);
+  if (rc == AD_OK) (*out)->f32 = true;
+  return rc;
+}
+
+int ad_conv_partitioned_process_block32(ad_conv* h, const float* in, int64_t in_len, float* out, int64_t out_len) {
+  return guard([&] {
+    if (!h) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "nil handle");
+    if (!h->f32) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "not a float32 convolver");
+    h->w_in = widen(in, in_len);
+    h->w_out.resize((size_t)std::max<int64_t>(out_len, 0));
+    const int rc = ad_conv_partitioned_process_block(h, h->w_in.data(), in_len, h->w_out.data(), out_len);
+    if (rc != AD_OK) throw Status{rc, ad_last_error()};
+    for (int64_t i = 0; i < out_len; ++i) out[i] = (float)h->w_out[(size_t)i];
   });
 }
 

@@ -78,6 +78,24 @@ int ad_conv_stream_ola_create(const double* kernel, int64_t kernel_len, int64_t 
  * (AD_ERR_LENGTH_MISMATCH otherwise).  in and out may alias.              */
 int ad_conv_process_block(ad_conv* h, const double* in, int64_t in_len, double* out, int64_t out_len);
 
+/* ---- float32 instantiations (F = float32, C = complex64 in the reference) --
+ * NewStreamingOverlapSave32 streaming_overlap_save.go:94,
+ * NewStreamingOverlapAdd32  streaming_overlap_add.go:93,
+ * NewPartitionedConvolution32 partitioned.go:340 (+ ProcessBlock :348-396).
+ * Same validation, getters, Reset and destroy as the float64 handles; the
+ * *_block32 calls take float32 blocks and refuse float64 handles.  Samples
+ * are widened exactly to float64, convolved by the float64 engine and
+ * rounded once to float32 (never less accurate than the reference's
+ * complex64 path).                                                       */
+int ad_conv_stream_ols32_create(const float* kernel, int64_t kernel_len, int64_t block_size, int device,
+                                ad_conv** out);
+int ad_conv_stream_ola32_create(const float* kernel, int64_t kernel_len, int64_t block_size, int device,
+                                ad_conv** out);
+int ad_conv_process_block32(ad_conv* h, const float* in, int64_t in_len, float* out, int64_t out_len);
+int ad_conv_partitioned32_create(const float* kernel, int64_t kernel_len, int min_block_order, int max_block_order,
+                                 int device, ad_conv** out);
+int ad_conv_partitioned_process_block32(ad_conv* h, const float* in, int64_t in_len, float* out, int64_t out_len);
+
 /* ---- batch conv.OverlapSave / conv.OverlapAdd ---------------------------
  * NewOverlapSave(kernel, fftSize)  overlap_save.go:53-107 (fftSize<=0: auto,
  *   non-power-of-two: AD_ERR_INVALID_BLOCK_SIZE, < 2K: silently raised)

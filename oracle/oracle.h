@@ -82,6 +82,19 @@ int64_t or_ols_fft_size(const or_ols* h);
 int64_t or_ols_step_size(const or_ols* h);
 void or_ols_free(or_ols* h);
 
+/* ---- float32 / complex64 instantiations (or_conv32.c): NewStreamingOverlapSave32
+ * streaming_overlap_save.go:94, NewStreamingOverlapAdd32 streaming_overlap_add.go:93,
+ * NewPartitionedConvolution32 partitioned.go:340 ---- */
+typedef struct or_stream32 or_stream32;
+int or_stream32_new(int is_ola, const float* kernel, int64_t K, int64_t B, or_stream32** out);
+int or_stream32_process_block(or_stream32* h, const float* in, float* out, int64_t n);
+int64_t or_stream32_fft_size(const or_stream32* h);
+void or_stream32_free(or_stream32* h);
+typedef struct or_pc32 or_pc32;
+int or_pc32_new(const float* kernel, int64_t K, int min_order, int max_order, or_pc32** out);
+int or_pc32_process_block(or_pc32* p, const float* input, float* output, int64_t n);
+void or_pc32_free(or_pc32* p);
+
 /* ---- dsp/conv/streaming_overlap_{save,add}.go ---- */
 typedef struct or_stream or_stream;
 int or_sols_new(const double* kernel, int64_t K, int64_t B, or_stream** out);

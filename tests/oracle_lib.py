@@ -16,6 +16,7 @@ ORACLE_DIR = ROOT / "oracle"
 ORACLE_LIB = ORACLE_DIR / "liboracle.so"
 
 dp = C.POINTER(C.c_double)
+fp = C.POINTER(C.c_float)
 i64 = C.c_int64
 vp = C.c_void_p
 
@@ -55,6 +56,13 @@ def lib() -> C.CDLL:
             "or_stream_reset": (None, [vp]),
             "or_stream_fft_size": (i64, [vp]),
             "or_stream_free": (None, [vp]),
+            "or_stream32_new": (C.c_int, [C.c_int, fp, i64, i64, C.POINTER(vp)]),
+            "or_stream32_process_block": (C.c_int, [vp, fp, fp, i64]),
+            "or_stream32_fft_size": (i64, [vp]),
+            "or_stream32_free": (None, [vp]),
+            "or_pc32_new": (C.c_int, [fp, i64, C.c_int, C.c_int, C.POINTER(vp)]),
+            "or_pc32_process_block": (C.c_int, [vp, fp, fp, i64]),
+            "or_pc32_free": (None, [vp]),
             "or_pc_new": (C.c_int, [dp, i64, C.c_int, C.c_int, C.POINTER(vp)]),
             "or_pc_process_block": (C.c_int, [vp, dp, dp, i64]),
             "or_pc_reset": (None, [vp]),
@@ -266,6 +274,52 @@ class Streaming:
     def __del__(self):
         if getattr(self, "h", None):
             lib().or_stream_free(self.h)
+
+
+def _f32(a):
+    return np.ascontiguousarray(np.asarray(a, dtype=np.float32))
+
+
+class Streaming32:
+    """NewStreamingOverlapSave32 / NewStreamingOverlapAdd32 (float32, complex64)."""
+
+    def __init__(self, kernel, block, ola=False):
+        k = _f32(kernel)
+        self._h = C.c_void_p()
+        _ck(lib().or_stream32_new(1 if ola else 0, k.ctypes.data_as(fp), k.size, int(block), C.byref(self._h)))
+        self.block = int(block)
+
+    def process_block(self, x):
+        xi = _f32(x)
+        out = np.empty(self.block, dtype=np.float32)
+        _ck(lib().or_stream32_process_block(self._h, xi.ctypes.data_as(fp), out.ctypes.data_as(fp), xi.size))
+        return out
+
+    def fft_size(self):
+        return int(lib().or_stream32_fft_size(self._h))
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().or_stream32_free(self._h)
+
+
+class Partitioned32:
+    """NewPartitionedConvolution32 (float32, complex64)."""
+
+    def __init__(self, kernel, min_order, max_order):
+        k = _f32(kernel)
+        self._h = C.c_void_p()
+        _ck(lib().or_pc32_new(k.ctypes.data_as(fp), k.size, int(min_order), int(max_order), C.byref(self._h)))
+
+    def process_block(self, x):
+        xi = _f32(x)
+        out = np.empty(xi.size, dtype=np.float32)
+        _ck(lib().or_pc32_process_block(self._h, xi.ctypes.data_as(fp), out.ctypes.data_as(fp), xi.size))
+        return out
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().or_pc32_free(self._h)
 
 
 class Partitioned:

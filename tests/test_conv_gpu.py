@@ -559,3 +559,59 @@ def test_partitioned_multi_vs_oracle(gpu, K, lo, hi):
         o = O.Partitioned(h, lo, 13)
         want = 0.8 * x[c, :5000] + 0.3 * o.process_block(x[c, :5000])
         assert np.max(np.abs(blk[c] - want)) < 1e-9
+
+
+# ------------------------------------------------------------ float32 handles
+F32_TOL = 1e-4  # the reference's float32 tolerance (streaming_test.go:175-234)
+
+
+@pytest.mark.parametrize("ola", [False, True])
+@pytest.mark.parametrize("K,B,nb", [(5, 16, 8), (3, 8, 2), (16384, 4096, 4), (1000, 512, 6)])
+def test_streaming32_vs_oracle(gpu, ola, K, B, nb):
+    """NewStreamingOverlapSave32 / NewStreamingOverlapAdd32: float32 blocks in
+    and out against the float32 (complex64) oracle at the reference's 1e-4,
+    and against the float64 oracle rounded to float32 (one rounding)."""
+    h = signals.make_test_kernel(K).astype(np.float32)
+    x = signals.white_noise(B * nb, K + 3).astype(np.float32)
+    ctor = conv.NewStreamingOverlapAdd32 if ola else conv.NewStreamingOverlapSave32
+    g = ctor(h, B)
+    o32 = O.Streaming32(h, B, ola=ola)
+    o64 = O.Streaming(h.astype(np.float64), B, ola=ola)
+    assert g.FFTSize() == o32.fft_size() and g.BlockSize() == B
+    for i in range(nb):
+        blk = x[i * B:(i + 1) * B]
+        got = g.ProcessBlock(blk)
+        assert got.dtype == np.float32
+        scale = max(1.0, float(np.max(np.abs(got))))
+        assert np.max(np.abs(got.astype(np.float64) - o32.process_block(blk))) <= F32_TOL * scale
+        w64 = o64.process_block(blk.astype(np.float64))
+        assert np.max(np.abs(got - w64.astype(np.float32))) <= 4 * np.finfo(np.float32).eps * scale
+    with pytest.raises(conv.ErrLengthMismatch):
+        g.ProcessBlock(x[:B - 1])
+
+
+@pytest.mark.parametrize("K,lo,hi", [(1000, 6, 9), (95432, 7, 13), (3, 2, 5)])
+def test_partitioned32_vs_oracle(gpu, K, lo, hi):
+    """NewPartitionedConvolution32 against the float32 oracle (1e-4) and the
+    float64 oracle, calls of varying length; latency and stage layout."""
+    h = (signals.make_impulse_kernel(K) if K < 90000 else irlib.large_church(pad_to=None)[1]).astype(np.float32)
+    lat = 1 << lo
+    g = conv.NewPartitionedConvolution32(h, lo, hi)
+    o32 = O.Partitioned32(h, lo, hi)
+    o64 = O.Partitioned(h.astype(np.float64), lo, hi)
+    assert g.Latency() == lat and g.StageCount() == o64.stage_count()
+    x = signals.white_noise(20000, 9).astype(np.float32)
+    pos = 0
+    for m in [lat, 3, 5 * lat + 1, 4000, 1, 20000]:
+        m = min(m, x.size - pos)
+        if m <= 0:
+            break
+        blk = x[pos:pos + m]
+        out = np.empty(m, dtype=np.float32)
+        g.ProcessBlock(blk, out)
+        w32 = o32.process_block(blk)
+        w64 = o64.process_block(blk.astype(np.float64))
+        scale = max(1.0, float(np.max(np.abs(w64))) if m else 1.0)
+        assert np.max(np.abs(out.astype(np.float64) - w32)) <= F32_TOL * scale
+        assert np.max(np.abs(out - w64.astype(np.float32))) <= 4 * np.finfo(np.float32).eps * scale
+        pos += m

@@ -487,3 +487,28 @@ def test_expander_gain_behaviour():
     fb = O.Expander(48000.0, topology=1, **kw).process_in_place(np.full(512, 0.05))[-1]
     ff = O.Expander(48000.0, topology=0, **kw).process_in_place(np.full(512, 0.05))[-1]
     assert fb != ff
+
+
+# ---------------------------------------------------------- float32 variants
+def test_oracle_streaming32_kats():
+    """The float32 restatement (or_conv32.c) against the reference's own float32
+    tests: impulse response (streaming_test.go:236-266) and OLA == OLS within
+    1e-4 (:175-234); plus partitioned32 vs the float64 oracle."""
+    c = KATS["streaming32_impulse"]
+    for ola in (False, True):
+        s = O.Streaming32(c["kernel"], c["block_size"], ola=ola)
+        np.testing.assert_allclose(s.process_block(c["input"]), c["expected"], atol=c["tol"], rtol=0)
+    e = KATS["streaming32_equivalence"]
+    B, nb = e["block_size"], e["num_blocks"]
+    i = np.arange(B * nb)
+    sig = (np.sin(i * 0.1) + 0.5 * np.cos(i * 0.05)).astype(np.float32)
+    a = O.Streaming32(e["kernel"], B, ola=True)
+    b = O.Streaming32(e["kernel"], B, ola=False)
+    ya = np.concatenate([a.process_block(sig[k * B:(k + 1) * B]) for k in range(nb)])
+    yb = np.concatenate([b.process_block(sig[k * B:(k + 1) * B]) for k in range(nb)])
+    assert np.max(np.abs(ya.astype(np.float64) - yb)) <= e["tol"]
+    h = signals.make_impulse_kernel(1000)
+    x = signals.white_noise(3000, 5)
+    p32 = O.Partitioned32(h, 6, 9).process_block(x)
+    p64 = O.Partitioned(h, 6, 9).process_block(x)
+    assert np.max(np.abs(p32 - p64)) < 1e-4
