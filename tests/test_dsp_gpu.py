@@ -255,6 +255,39 @@ def test_effect_chain_config5(gpu):
         assert rms(y[c], v) <= RMS_TOL, rms(y[c], v)
 
 
+def test_effect_chain_config5_bench_shape(gpu):
+    """Config 5 at the shape bench.py --workload fx times: 256 channels, device
+    buffers, the staged engine (default), 2^18 samples = 16 of its 16384-sample
+    chunks, in two calls (the second ends mid-chunk); channels 0, 63, 64 (the
+    first of the second 64-channel group) and 255 against the oracle chain
+    (chain_process.go:11-33: biquad chains -> Compressor -> Freeverb)."""
+    import torch
+
+    fs = 48000.0
+    eq = design.config5_eq(fs)
+    comp_cfg = {"auto_makeup": 0, "makeup_db": 0.0}
+    verb = (0.22, 1.0, 0.72, 0.45, 0.015)
+    C, n = 256, 1 << 18
+    x = np.stack([0.5 * signals.white_noise(n, 0x5EED + c) for c in range(C)])
+    fx = P.EffectChain(C, eq, comp_cfg, verb, fs)
+    dx = torch.from_numpy(x).cuda()
+    s = torch.cuda.current_stream()
+    cut = 5 * 16384 + 1000
+    fx.process_device(dx.data_ptr(), n, cut, s.cuda_stream)
+    fx.process_device(dx.data_ptr() + 8 * cut, n, n - cut, s.cuda_stream)
+    s.synchronize()
+    y = dx.cpu().numpy()
+    for c in (0, 63, 64, 255):
+        v = x[c].copy()
+        for co, g in eq:
+            v, _ = O.biquad_chain_block(np.ravel(co), np.zeros(2 * len(co)), g, v)
+        v = O.Compressor(fs, **comp_cfg).process_in_place(v)
+        o = O.Freeverb()
+        o.set(*verb)
+        v = o.process_in_place(v)
+        assert rms(y[c], v) <= RMS_TOL, (c, rms(y[c], v))
+
+
 # ------------------------------------------------------------------ staged engine == fused kernels
 STAGED_CASES = {
     "eq": dict(eq=True),
