@@ -281,7 +281,10 @@ int64_t batch_hop(int64_t K) {
 
 void make_batch_engine(ad_conv* h, const double* kernel, int64_t K) {
   h->hop = batch_hop(K);
-  h->eng.reset(new Upols(h->device, kernel, 1, K, (int)h->hop, 1, nullptr, 64, h->stream));
+  // up to 512 blocks per launch (a host pipeline segment is <= 2^21 samples):
+  // a mono call then fills the chip with few launches; the delay line and
+  // product rows cost ~2 x 512 x (hop + 8) x 16 B (134 MB at hop 8192)
+  h->eng.reset(new Upols(h->device, kernel, 1, K, (int)h->hop, 1, nullptr, 512, h->stream));
 }
 
 template <class Fn>

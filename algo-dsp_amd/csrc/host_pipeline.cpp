@@ -222,7 +222,9 @@ void HostPipeline::offline(Upols& eng, const double* const* in, int C, int64_t n
   }
   // chunk: S input samples per channel (a multiple of L), C*S doubles <= kChunkBytes
   int64_t S = std::max<int64_t>(L, (kChunkBytes / 8 / C) / L * L);
-  S = std::min(S, (n + L - 1) / L * L);  // small calls: small pinned buffers
+  // at least ~4 chunks when the signal allows (transfers overlap the compute
+  // only across chunks); small calls: small pinned buffers
+  S = std::min(S, std::max<int64_t>(L, ((n + 3) / 4 + L - 1) / L * L));
   const int64_t nblocks = (out_len + L - 1) / L;
   ensure_pinned((int64_t)C * S);
   din_.reserve((size_t)C * n);
@@ -299,7 +301,7 @@ void HostPipeline::offline_direct(Upols& eng, const double* const* in, int C, in
                                   int64_t out_len, hipStream_t s) {
   const int64_t L = eng.hop();
   int64_t S = std::max<int64_t>(L, (kChunkBytes / 8 / C) / L * L);
-  S = std::min(S, (n + L - 1) / L * L);
+  S = std::min(S, std::max<int64_t>(L, ((n + 3) / 4 + L - 1) / L * L));
   const int64_t nblocks = (out_len + L - 1) / L;
   din_.reserve((size_t)C * n);
   dout_.reserve((size_t)C * out_len);

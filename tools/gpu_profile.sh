@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 TAG=${TAG:-r01}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
-BARGS=${BENCH_ARGS:---steps 5 --warmup 2 --no-cpu-baseline}
+BARGS=${BENCH_ARGS:---steps 5 --warmup 2 --no-cpu-baseline --host-io off}
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o bench -- python3 bench.py $BARGS > $OUT/bench_trace.log 2>&1
 rc=$?; echo "trace rc=$rc"; tail -3 $OUT/bench_trace.log
 if [ $rc -ne 0 ]; then exit $rc; fi

@@ -269,6 +269,72 @@ def main():
                         "samples", ms, cs, ncb * lam, f"oracle PartitionedConvolution, {ncb} blocks", None, 0,
                         "latency-bound: mean per-call wall time incl. PCIe"))
 
+    # float32 instantiations (streaming_overlap_save.go:94, streaming_overlap_add.go:93, partitioned.go:340)
+    xs32, ys32 = xs.astype(np.float32), np.empty(nblk * B, dtype=np.float32)
+    k32 = k16.astype(np.float32)
+    for ctor, name, ref in ((conv.NewStreamingOverlapSave32, "a5 (f32)", "NewStreamingOverlapSave32 "
+                             "streaming_overlap_save.go:94"),
+                            (conv.NewStreamingOverlapAdd32, "a6 (f32)", "NewStreamingOverlapAdd32 "
+                             "streaming_overlap_add.go:93")):
+        s = ctor(k32, B)
+        for i in range(16):
+            s.ProcessBlockTo(ys32[i * B:(i + 1) * B], xs32[i * B:(i + 1) * B])
+        t0 = time.perf_counter()
+        for i in range(nblk):
+            s.ProcessBlockTo(ys32[i * B:(i + 1) * B], xs32[i * B:(i + 1) * B])
+        ms = (time.perf_counter() - t0) / nblk * 1e3
+        o = O.Streaming32(k32, B, ola=(name.startswith("a6")))
+        cs = cpu_time(lambda: o.process_block(xs32[:B]), budget_s=1.0)
+        rows.append(row(name, ref, f"config 2 in float32: mono, K=16384, B={B}, host buffers, one block per call",
+                        B, "samples", ms, cs, B, "float32 oracle streaming block (N=32768 complex64 FFT)", None, 0,
+                        "latency-bound; float32 boundary, float64 engine"))
+    pc32 = conv.NewPartitionedConvolution32(kpc.astype(np.float32), 7, 13)
+    xp32 = xp.astype(np.float32)
+    yp32 = np.empty(lam, dtype=np.float32)
+    for i in range(16):
+        pc32.ProcessBlock(xp32[i * lam:(i + 1) * lam], yp32)
+    nb = 256 if q else 2048
+    t0 = time.perf_counter()
+    for i in range(nb):
+        pc32.ProcessBlock(xp32[i * lam:(i + 1) * lam], yp32)
+    ms = (time.perf_counter() - t0) / nb * 1e3
+    op32 = O.Partitioned32(kpc.astype(np.float32), 7, 13)
+    cs = cpu_time(lambda: [op32.process_block(xp32[i * lam:(i + 1) * lam]) for i in range(ncb)], budget_s=1.0,
+                  max_reps=4)
+    rows.append(row("a9 (f32)", "NewPartitionedConvolution32 partitioned.go:340",
+                    f"Large Church L (95432 taps) in float32, latency {lam}, {lam}-sample calls, host buffers", lam,
+                    "samples", ms, cs, ncb * lam, f"float32 oracle PartitionedConvolution, {ncb} blocks", None, 0,
+                    "latency-bound: mean per-call wall time incl. PCIe"))
+
+    # many-channel forms: config 4 block by block (64 reverb channels, IR[c mod 2]),
+    # and the reverb-conv node's engine (64 channels sharing one IR, latency 128)
+    import torch
+
+    C4, B4 = 64, 4096
+    ms4 = conv.MultiChannelStreamingConvolver(ir, B4, C4, ir_index=[c % 2 for c in range(C4)])
+    dx4 = torch.from_numpy(np.stack([signals.white_noise(B4, 0x5EED + c) for c in range(C4)])).cuda()
+    dy4 = torch.empty_like(dx4)
+    ms = dev_time(lambda sp: ms4.process_block_device(dx4.data_ptr(), B4, dy4.data_ptr(), B4, sp), 8 if q else 64)
+    rows.append(row("a5 x64 (config 4 streaming)", "StreamingOverlapSave.ProcessBlockTo x 64 channels "
+                    "streaming_overlap_save.go:152-164", f"64 ch x {B4}-sample blocks, 131072-tap Large Church "
+                    "IR[c mod 2], device buffers, one handle", C4 * B4, "samples", ms, None, 0, "", None, 0,
+                    "one launch per engine kernel per block for all 64 channels (hop 4096, P = 32)"))
+    pcm = conv.PartitionedConvolutionMulti(kpc, 7, 13, C4)
+    dxp = torch.from_numpy(np.stack([signals.white_noise(lam * 64, c) for c in range(C4)])).cuda()
+    dyp = torch.empty_like(dxp)
+    cnt = [0]
+
+    def pc_call(sp):
+        o = (cnt[0] % 64) * lam
+        cnt[0] += 1
+        pcm.process_device(dxp.data_ptr() + 8 * o, lam * 64, dyp.data_ptr() + 8 * o, lam * 64, lam, sp)
+
+    ms = dev_time(pc_call, 128 if q else 1024, warm=64)
+    rows.append(row("a9/f1 x64 (reverb-conv engine)", "PartitionedConvolution.ProcessBlock x 64 channels "
+                    "partitioned.go:348-396", f"64 ch sharing Large Church L (95432 taps), latency {lam}, "
+                    f"{lam}-sample device calls", C4 * lam, "samples", ms, None, 0, "", None, 0,
+                    "device-resident many-channel engine (ad_conv_pc_multi): mean per-call time, all stages"))
+
     nbt = 1 << (18 if q else 22)
     xbt = signals.white_noise(nbt, 3)
     for ctor, name, ref, ocls in ((conv.NewOverlapSave, "a4", "OverlapSave.Process overlap_save.go:126-254",
