@@ -167,9 +167,9 @@ __global__ __launch_bounds__((SplitPlan<M>::T)) __attribute__((amdgpu_waves_per_
   constexpr int M2 = SP::M2, V = SP::V, T = SP::T, L = M;
   __shared__ __attribute__((aligned(16))) double2 lds[SP::LDS];
   const int tid = threadIdx.x;
-  const int64_t e = xcd_remap_fft(blockIdx.x, gridDim.x);
-  const int c = (int)(e / a.jc);
-  const int j = (int)(e % a.jc);
+  const int e = __builtin_amdgcn_readfirstlane(xcd_remap_fft(blockIdx.x, gridDim.x));  // uniform: SGPRs
+  const int c = __builtin_amdgcn_readfirstlane(e / a.jc);
+  const int j = __builtin_amdgcn_readfirstlane(e - c * a.jc);
   const double* xc = a.x + (int64_t)c * a.x_stride;
   const double* hc = a.xhist ? a.xhist + (int64_t)c * a.hist_stride : nullptr;
   const int64_t t0 = a.s0 + (int64_t)j * L - L;  // first sample of the 2L window
@@ -226,9 +226,11 @@ __global__ __launch_bounds__((SplitPlan<M>::T)) __attribute__((amdgpu_waves_per_
   constexpr int M2 = SP::M2, V = SP::V, T = SP::T, L = M;
   __shared__ __attribute__((aligned(16))) double2 lds[SP::LDS];
   const int tid = threadIdx.x;
-  const int64_t e = xcd_remap_fft(blockIdx.x, gridDim.x);
-  const int c = (int)(e / a.jc);
-  const int j = (int)(e % a.jc);
+  // item indices and row bases are wave-uniform: keep them in SGPRs (VGPR
+  // copies of 64-bit bases spilled to scratch at the 128-VGPR cap)
+  const int e = __builtin_amdgcn_readfirstlane(xcd_remap_fft(blockIdx.x, gridDim.x));
+  const int c = __builtin_amdgcn_readfirstlane(e / a.jc);
+  const int j = __builtin_amdgcn_readfirstlane(e - c * a.jc);
   const double2* Zb = a.Y + (int64_t)c * a.y_ch_stride + (int64_t)j * a.MS;
   double2 av[V], bv[V];
   // bins 2k, 2k+1 in wave-lane row order (zrow_pos): one 32-byte pair per
@@ -245,25 +247,34 @@ __global__ __launch_bounds__((SplitPlan<M>::T)) __attribute__((amdgpu_waves_per_
   fft_run<M2, V, false>(av, tid, lds, twS);
   __syncthreads();
   fft_run<M2, V, false>(bv, tid, lds, twS);
-  double* yc = a.out + (int64_t)c * a.out_stride;
   const int64_t ob = a.o0 + (int64_t)j * L;  // output of time index M/2 + m is at ob + 2m
-  const bool fast = a.aligned && ob + 2 * M2 <= a.out_len;
+  double* yb = a.out + (int64_t)c * a.out_stride + ob;
 #pragma unroll
   for (int s = 0; s < V; ++s) {
     const int m = last_pass_index<M2, V>(tid, s);
-    const double2 r = c_sub(av[s], c_mul(c_conj(twC(m)), bv[s]));
-    const int64_t o = ob + 2 * m;
-    if (fast) {
-      double2 w = r;
-      if (a.accumulate) {
-        const double2 q = *reinterpret_cast<const double2*>(yc + o);
-        w = make_double2(q.x + r.x, q.y + r.y);
-      }
-      *reinterpret_cast<double2*>(yc + o) = w;
+    av[s] = c_sub(av[s], c_mul(c_conj(twC(m)), bv[s]));
+  }
+  if (a.aligned && ob + 2 * M2 <= a.out_len) {  // wave-uniform fast paths
+    if (!a.accumulate) {
+#pragma unroll
+      for (int s = 0; s < V; ++s)
+        *reinterpret_cast<double2*>(yb + 2 * last_pass_index<M2, V>(tid, s)) = av[s];
     } else {
-      if (o < a.out_len) yc[o] = a.accumulate ? yc[o] + r.x : r.x;
-      if (o + 1 < a.out_len) yc[o + 1] = a.accumulate ? yc[o + 1] + r.y : r.y;
+#pragma unroll
+      for (int s = 0; s < V; ++s) {
+        double2* p = reinterpret_cast<double2*>(yb + 2 * last_pass_index<M2, V>(tid, s));
+        const double2 q = *p;
+        *p = make_double2(q.x + av[s].x, q.y + av[s].y);
+      }
     }
+    return;
+  }
+  const int64_t left = a.out_len - ob;  // valid outputs from yb on
+#pragma unroll
+  for (int s = 0; s < V; ++s) {
+    const int o = 2 * last_pass_index<M2, V>(tid, s);
+    if (o < left) yb[o] = a.accumulate ? yb[o] + av[s].x : av[s].x;
+    if (o + 1 < left) yb[o + 1] = a.accumulate ? yb[o + 1] + av[s].y : av[s].y;
   }
 }
 
