@@ -81,22 +81,24 @@ __device__ __forceinline__ void cmac(double2& s, const double2 x, const double2 
   s.y = fma(x.y, h.x, s.y);
 }
 
-// Ring-slot walker over this lane's X stream.  Branch-free: spectra before
-// the signal start (logical index < 0) read the ring's zero row (slot Q), and
-// spectra past the run read stale ring rows whose products only reach
-// outputs that are never stored, so every load is a plain global load.
+// Ring-slot walker over this lane's block-spectrum stream.  Branch-free:
+// blocks before the signal start (logical index < 0) and after its last
+// input block (> gend) read the ring's zero row (slot Q), so every load is a
+// plain global load.
 struct XStream {
   const double2* Xc;
   int Q, MS;
-  int64_t lx;  // logical index of row 0 of the current group (wave-uniform, ph = 0)
-  int sl;      // its ring slot (wave-uniform)
-  int dph;     // row offset of the ph = 1 half (-PC)
+  int64_t lx;    // logical index of row 0 of the current group (wave-uniform, ph = 0)
+  int64_t gend;  // last logical block holding input
+  int sl;        // its ring slot (wave-uniform)
+  int dph;       // row offset of the ph = 1 half (-PC)
   bool ph;
   __device__ __forceinline__ int slot(int off) const {  // wave-uniform
     int s = sl + off;
     if (s >= Q) s -= Q;
     if (s < 0) s += Q;
-    return (lx + off >= 0) ? s : Q;
+    const int64_t g = lx + off;
+    return (g >= 0 && g <= gend) ? s : Q;
   }
   __device__ __forceinline__ double2 load(int off) const {  // row lx + off (+ dph for ph = 1)
     const int r0 = slot(off), r1 = slot(off + dph);
@@ -139,7 +141,30 @@ __device__ __forceinline__ void xpair(double2 a, double2& u, double2& v) {
   xpair<B32>(a.y, u.y, v.y);
 }
 
-// Separation of K1's raw packed spectrum into the real-signal spectrum (x2):
+// The window spectrum of output block g from K1's block spectra:
+// Zr[g][k] = P[g-1][k] + (-1)^k P[g][k] (fft_kernels.hip).  A lane walks its
+// stream in block order; the previous row's value waits in a per-lane LDS
+// cell (not in VGPRs: K2 at PC = 16 sits at its register cap), and (-1)^k is
+// a sign bit on the high dword (k's parity is the lane's: mirror partners
+// M-k share it, the middle bin M/2 is even).
+// v * (+1 or -1) as a sign-bit flip of the high dword (m = 0 or 0x80000000):
+// exact, and one 32-bit mask per lane instead of a double or a pre-signed
+// copy of each constant.
+__device__ __forceinline__ double flip(double v, int m) {
+  return __hiloint2double(__double2hiint(v) ^ m, __double2loint(v));
+}
+
+struct BlockPair {
+  double2 prev;  // this lane's P[g-1]
+  int smask;     // 0 or 0x80000000
+  __device__ __forceinline__ double2 next(const double2 cur) {
+    const double2 z = make_double2(prev.x + flip(cur.x, smask), prev.y + flip(cur.y, smask));
+    prev = cur;
+    return z;
+  }
+};
+
+// Separation of the window's packed spectrum Zr into the real-signal spectrum (x2):
 //   X'[k] = (A + B) - i W_2M^k (A - B),  A = Zr[k], B = conj Zr[M-k]   (= 2 X[k])
 // with A, conj(B) the mirror pair (u, v) of xpair:
 //   X'.x = (u.x + v.x) + W.x (u.y + v.y) + s W.y (u.x - v.x)
@@ -149,14 +174,14 @@ __device__ __forceinline__ void xpair(double2 a, double2& u, double2& v) {
 // H' is taken out in the Z epilogue's scale.
 template <int NH>
 struct Unpack {
-  double2 tw;   // W_2M^k (k = M: -1)
-  double2 stw;  // s * tw
-  double s;     // +1 lower mirror lane, -1 upper
+  double2 tw;  // W_2M^k (k = M: -1)
+  int m;       // sign of s: 0 lower mirror lane (+1), 0x80000000 upper (-1)
   __device__ __forceinline__ double2 operator()(const double2 a) const {
     double2 u, v;
     xpair<NH == 1>(a, u, v);
-    const double sx = u.x + v.x, dx = u.x - v.x, sy = u.y + v.y, dy = u.y - v.y;
-    return make_double2(fma(stw.y, dx, fma(tw.x, sy, sx)), fma(-stw.x, dx, fma(tw.y, sy, s * dy)));
+    const double sx = u.x + v.x, sy = u.y + v.y;
+    const double sdx = flip(u.x - v.x, m), sdy = flip(u.y - v.y, m);  // s (u - v), exact
+    return make_double2(fma(tw.y, sdx, fma(tw.x, sy, sx)), fma(-tw.x, sdx, fma(tw.y, sy, sdy)));
   }
 };
 
@@ -171,11 +196,14 @@ struct Unpack {
 //   Z.y = s S (u.y - v.y) + s t.x (u.x - v.x) - t.y (u.y + v.y)
 template <int NH>
 struct ZEpilogue {
-  double2* zc;      // Z row base of this lane's bin (bin M: the row's padding column M)
+  double2* zb;      // Z row 0 of the channel (wave-uniform)
+  unsigned zo;      // this lane's bin position in a row (bin M: the row's padding column M);
+                    // a 32-bit lane offset from a uniform row base keeps the store
+                    // address out of a 64-bit VGPR pair
   int64_t jstride;  // MS
   double2 tw;       // t = conj(W_2M^m) * S
-  double2 stw;      // s * t
-  double S, sS;     // 1/8M, s/8M
+  double S;         // 1/8M (wave-uniform)
+  int m;            // sign of s (see Unpack)
   // Unconditional (branch-free) store: rows past the run land in the spare
   // rows after jc_max (or in rows >= jc that K3 never reads), so the wave's
   // vmcnt bookkeeping stays exact across the group loop.  Lanes that carry
@@ -192,9 +220,10 @@ struct ZEpilogue {
     }
     double2 u, v;
     xpair<NH == 1>(y, u, v);
-    const double sx = u.x + v.x, dx = u.x - v.x, sy = u.y + v.y, dy = u.y - v.y;
-    const double2 z = make_double2(fma(-tw.x, sy, fma(-stw.y, dx, sx * S)), fma(-tw.y, sy, fma(stw.x, dx, sS * dy)));
-    double2* zp = zc + j * jstride;
+    const double sx = u.x + v.x, sy = u.y + v.y;
+    const double sdx = flip(u.x - v.x, m), sdy = flip(u.y - v.y, m);  // s (u - v), exact
+    const double2 z = make_double2(fma(-tw.x, sy, fma(-tw.y, sdx, sx * S)), fma(-tw.y, sy, fma(tw.x, sdx, S * sdy)));
+    double2* zp = (zb + j * jstride) + zo;
     if constexpr (FIRST) {
       *zp = z;
     } else {
@@ -222,9 +251,10 @@ struct Row {
   }
   template <bool FIRST, class UP, class EPI>
   __device__ static __forceinline__ void run(double2 (&acc)[PC], const double2 (&h)[PC], double2 (&xb)[D],
-                                             const XStream& st, const UP& up, const EPI& epi, int i) {
+                                             const XStream& st, BlockPair& bp, const UP& up, const EPI& epi,
+                                             int i) {
     if constexpr (U < PC) {
-      const double2 x = up(xb[U % D]);
+      const double2 x = up(bp.next(xb[U % D]));
       xb[U % D] = st.load(U + D);
       if constexpr (WARM) {
         macs<PC - U>(acc, h, x);
@@ -234,7 +264,7 @@ struct Row {
         acc[U] = make_double2(0.0, 0.0);
       }
       __builtin_amdgcn_sched_barrier(0);
-      Row<PC, D, U + 1, WARM>::template run<FIRST>(acc, h, xb, st, up, epi, i);
+      Row<PC, D, U + 1, WARM>::template run<FIRST>(acc, h, xb, st, bp, up, epi, i);
     }
   }
 };
@@ -279,18 +309,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MacOcc<PC, N
   const double2* Xc = a.X + (int64_t)c * a.x_ch_stride + kz;
   const double sgn = mi ? -1.0 : 1.0;
   Unpack<NH> up;
-  up.s = sgn;
+  up.m = mi ? (int)0x80000000u : 0;
   up.tw = (k < a.M) ? a.twN[k] : make_double2(-1.0, 0.0);
-  up.stw = c_scale(up.tw, sgn);
   ZEpilogue<NH> epi;
   epi.S = 0.125 / (double)a.M;
-  epi.sS = sgn * epi.S;
+  epi.m = up.m;
   // Z rows in wave-lane order (zrow_pos): one aligned 1-KiB run per wave row.
   const int zpos = zrow_pos(k, a.M);
-  epi.zc = a.Y + (int64_t)c * a.y_ch_stride + zpos;
+  epi.zb = a.Y + (int64_t)c * a.y_ch_stride;
+  epi.zo = (unsigned)zpos;
   epi.jstride = a.MS;
   epi.tw = (k < a.M) ? c_scale(c_conj(a.twN[k]), epi.S) : make_double2(0.0, 0.0);
-  epi.stw = c_scale(epi.tw, sgn);
 
   {
     const int pb = a.p0 + (ph ? PC : 0);  // this lane's first partition
@@ -312,17 +341,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MacOcc<PC, N
     st.Xc = Xc;
     st.Q = a.Q;
     st.MS = a.MS;
-    st.lx = a.g0 + j0 - PC - a.p0;  // row 0 of the warm-up group (feeds nothing), ph = 0
+    st.lx = a.g0 + j0 - PC - a.p0;  // row 0 of the warm-up group (only the first row's P[g-1]), ph = 0
+    st.gend = a.gend;
     st.sl = (int)(((st.lx % a.Q) + a.Q) % a.Q);
     st.dph = -PC;
     st.ph = ph;
+    BlockPair bp;
+    bp.smask = (kz & 1) ? (int)0x80000000u : 0;
+    bp.prev = st.load(0);
     double2 xb[D];
 #pragma unroll
     for (int d = 1; d <= D; ++d) xb[d % D] = st.load(d);
-    Row<PC, D, 1, true>::template run<FIRST>(acc, h, xb, st, up, epi, j0);
+    Row<PC, D, 1, true>::template run<FIRST>(acc, h, xb, st, bp, up, epi, j0);
     st.advance<PC>();
     for (int i = j0; i < j1; i += PC) {
-      Row<PC, D, 0, false>::template run<FIRST>(acc, h, xb, st, up, epi, i);
+      Row<PC, D, 0, false>::template run<FIRST>(acc, h, xb, st, bp, up, epi, i);
       st.advance<PC>();
     }
   }
@@ -364,6 +397,10 @@ struct XRing {
     if (s < 0) s += Q;
     const int64_t g = lx + off;
     return (g >= 0 && g <= lend) ? s : Q;
+  }
+  __device__ __forceinline__ double2 load(int off) const {  // plain load of row lx + off (+ dph)
+    const int r0 = slot(off), r1 = slot(off + dph);
+    return Xc[(int64_t)(ph ? r1 : r0) * MS];
   }
   // DMA row lx + off (+ dph for ph = 1) into LDS at byte address lds (+16 B per lane).
   __device__ __forceinline__ void issue(int off, unsigned lds) const {
@@ -407,7 +444,8 @@ struct RowL {
   }
   template <bool FIRST, class UP, class EPI>
   __device__ static __forceinline__ void run(double2 (&acc)[PC], const double2 (&h)[PC], double2* ring,
-                                             const XRing& st, const UP& up, const EPI& epi, int i) {
+                                             const XRing& st, BlockPair& bp, const UP& up, const EPI& epi,
+                                             int i) {
     if constexpr (U < PC) {
       constexpr int S = U % DL;
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(wait_count()) : "memory");
@@ -415,7 +453,7 @@ struct RowL {
       // the fake operand holds the DMA that refills slot S behind this read
       asm volatile("" ::"v"(xr.x), "v"(xr.y));
       st.issue(U + DL, ring_addr<DL>(ring, S));
-      const double2 x = up(xr);
+      const double2 x = up(bp.next(xr));
       if constexpr (GRP == 0) {
         macs<PC - U>(acc, h, x);
       } else {
@@ -424,7 +462,7 @@ struct RowL {
         acc[U] = make_double2(0.0, 0.0);
       }
       __builtin_amdgcn_sched_barrier(0);
-      RowL<PC, DL, U + 1, GRP>::template run<FIRST>(acc, h, ring, st, up, epi, i);
+      RowL<PC, DL, U + 1, GRP>::template run<FIRST>(acc, h, ring, st, bp, up, epi, i);
     }
   }
 };
@@ -466,27 +504,31 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MacOccL<PC, 
   const double2* Xc = a.X + (int64_t)c * a.x_ch_stride + kz;
   const double sgn = mi ? -1.0 : 1.0;
   Unpack<NH> up;
-  up.s = sgn;
+  up.m = mi ? (int)0x80000000u : 0;
   up.tw = (k < a.M) ? a.twN[k] : make_double2(-1.0, 0.0);
-  up.stw = c_scale(up.tw, sgn);
   ZEpilogue<NH> epi;
   epi.S = 0.125 / (double)a.M;
-  epi.sS = sgn * epi.S;
+  epi.m = up.m;
   const int zpos = zrow_pos(k, a.M);
-  epi.zc = a.Y + (int64_t)c * a.y_ch_stride + zpos;
+  epi.zb = a.Y + (int64_t)c * a.y_ch_stride;
+  epi.zo = (unsigned)zpos;
   epi.jstride = a.MS;
   epi.tw = (k < a.M) ? c_scale(c_conj(a.twN[k]), epi.S) : make_double2(0.0, 0.0);
-  epi.stw = c_scale(epi.tw, sgn);
 
   XRing st;
   st.Xc = Xc;
   st.Q = a.Q;
   st.MS = a.MS;
   st.lx = a.g0 + j0 - PC - a.p0;
-  st.lend = a.g0 + j1 - 1 - a.p0;
+  st.lend = min((int64_t)(a.g0 + j1 - 1 - a.p0), a.gend);
   st.sl = (int)(((st.lx % a.Q) + a.Q) % a.Q);
   st.dph = -PC;
   st.ph = ph;
+  // P[g-1] of the first row the run consumes, ahead of the ring DMAs (vmcnt
+  // retires in order, so the counted waits below stay conservative)
+  BlockPair bp;
+  bp.smask = (kz & 1) ? (int)0x80000000u : 0;
+  bp.prev = st.load(0);
   // ring prologue first: its DMAs overlap the H loads
 #pragma unroll
   for (int d = 1; d <= DL; ++d) st.issue(d, ring_addr<DL>(ring, d % DL));
@@ -506,14 +548,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MacOccL<PC, 
 #pragma unroll
   for (int q = 0; q < PC; ++q) acc[q] = make_double2(0.0, 0.0);
 
-  RowL<PC, DL, 1, 0>::template run<FIRST>(acc, h, ring, st, up, epi, j0);
+  RowL<PC, DL, 1, 0>::template run<FIRST>(acc, h, ring, st, bp, up, epi, j0);
   st.advance<PC>();
   if (j0 < j1) {
-    RowL<PC, DL, 0, 1>::template run<FIRST>(acc, h, ring, st, up, epi, j0);
+    RowL<PC, DL, 0, 1>::template run<FIRST>(acc, h, ring, st, bp, up, epi, j0);
     st.advance<PC>();
   }
   for (int i = j0 + PC; i < j1; i += PC) {
-    RowL<PC, DL, 0, 2>::template run<FIRST>(acc, h, ring, st, up, epi, i);
+    RowL<PC, DL, 0, 2>::template run<FIRST>(acc, h, ring, st, bp, up, epi, i);
     st.advance<PC>();
   }
   // drain the tail DMAs before the wave (and its LDS) retires

@@ -24,22 +24,18 @@ struct RfftArgs {
   const double* x;      // input samples, channel c at x + c*x_stride (call-relative index)
   int64_t x_stride;
   int64_t n;            // valid input samples per channel (beyond: zeros)
-  const double* xhist;  // [C][hist_stride]: the L samples preceding the call (nullable -> zeros)
-  double* hist_out;     // [C][hist_stride]: receives the last window's upper half (the next
-                        // call's history) when non-null; must not alias xhist
-  int64_t hist_stride;
-  int64_t s0;           // first output sample of chunk block 0 (call-relative)
+  int64_t s0;           // first sample of chunk block 0 (call-relative)
   int jc;               // blocks per channel in this launch
   int channels;
   int aligned;          // x and x_stride allow 16-byte pair loads
-  double2* X;           // spectra ring [C][Q][MS]
+  double2* X;           // block-spectra ring [C][Q][MS]
   int64_t x_ch_stride;  // Q*MS
   int Q;
   int slot0;            // ring slot of block 0
   int MS;
   const double2* twM;   // W_M^e, e < M
   const double2* twN;   // W_{2M}^k, k < M
-  int per_wg;           // windows per workgroup (set by the launcher, <= the plan's F)
+  int per_wg;           // blocks per workgroup (set by the launcher, <= the plan's F)
 };
 
 struct MacArgs {
@@ -47,6 +43,7 @@ struct MacArgs {
   int64_t x_ch_stride;
   int Q;
   int64_t g0;           // logical spectrum index of chunk block 0 (< 0: zeros)
+  int64_t gend;         // last logical block holding input samples (later blocks: zeros)
   int nx, ny;           // bin-pair waves, output runs (set by the launcher)
   int p0;               // first partition of this launch's chunk (set by the launcher)
   int bx_fast;          // grid order: bin groups fastest (1) or runs fastest (0) (set by the launcher)

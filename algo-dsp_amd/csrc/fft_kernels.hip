@@ -1,10 +1,18 @@
 // Window real-FFT (K1) and inverse real-FFT + overlap-save store (K3) kernels
 // of the UPOLS convolution engine (see conv_kernels.hip for the data flow).
 //
-// K1: Zr[c][g] = FFT_M(z), z[m] = x[(g-1)L + 2m] + i x[(g-1)L + 2m + 1]: the
-//     half-length complex FFT of the 2L-sample window (N = 2L, M = L).  The
-//     raw packed spectrum is stored; k_fdl_mac separates it into the real
-//     spectrum X[k] = (Zr[k] + conj Zr[M-k])/2 - i W_2M^k (Zr[k] - conj Zr[M-k])/2.
+// K1: P[c][g] = FFT_M(z), z[m] = x[gL + 2m] + i x[gL + 2m + 1] for m < M/2 and
+//     z[m] = 0 above: the packed half-length complex FFT of input block g
+//     zero padded to N = 2L (M = L).  The window spectrum overlap-save needs,
+//     the packed FFT of x[(g-1)L .. (g+1)L), is Zr[g][k] = P[g-1][k] +
+//     (-1)^k P[g][k] (a shift by M/2 in an M-point FFT is a factor (-1)^k),
+//     which k_fdl_mac forms on load from consecutive rows of its stream and
+//     then separates into the real spectrum
+//     X[k] = (Zr[k] + conj Zr[M-k])/2 - i W_2M^k (Zr[k] - conj Zr[M-k])/2.
+//     One transform per input block (not per output block): a call of n
+//     samples runs ceil(n/L) K1 items, the convolution tail none, and no
+//     input history is kept between streaming calls (the previous block's P
+//     is in the ring).
 // K3: y[c][jL .. (j+1)L) = last L samples of irFFT_N(Y[c][j]); the input is
 //     the half-length spectrum Z already folded by k_fdl_mac's epilogue, so
 //     K3 is a plain inverse complex FFT + store of the upper half.
@@ -33,12 +41,9 @@ __device__ __forceinline__ int xcd_remap_fft(int b, int G) {
   return (xcd < rem) ? xcd * (q + 1) + r : rem * (q + 1) + (xcd - rem) * q + r;
 }
 
-__device__ __forceinline__ double2 fetch_pair(const double* xc, const double* hc, int64_t t, int64_t n, int L,
-                                              bool aligned) {
-  if (t >= 0 && t + 1 < n && aligned) return *reinterpret_cast<const double2*>(xc + t);
-  const double r0 = (t < 0) ? (hc ? hc[L + t] : 0.0) : (t < n ? xc[t] : 0.0);
-  const double r1 = (t + 1 < 0) ? (hc ? hc[L + t + 1] : 0.0) : (t + 1 < n ? xc[t + 1] : 0.0);
-  return make_double2(r0, r1);
+__device__ __forceinline__ double2 fetch_pair(const double* xc, int64_t t, int64_t n, bool aligned) {
+  if (t + 1 < n && aligned) return *reinterpret_cast<const double2*>(xc + t);
+  return make_double2(t < n ? xc[t] : 0.0, t + 1 < n ? xc[t + 1] : 0.0);
 }
 
 // Inverse store: the upper half of the time window (m >= M/2) to y.
@@ -82,23 +87,13 @@ __global__ __launch_bounds__((FftPlan<M, V>::BLOCK)) void k_window_rfft(RfftArgs
   const int j = active ? (int)(e % a.jc) : 0;
   double2* lds = lds_all + f * Plan::MP;
   const double* xc = a.x + (int64_t)c * a.x_stride;
-  const double* hc = a.xhist ? a.xhist + (int64_t)c * a.hist_stride : nullptr;
-  const int64_t t0 = a.s0 + (int64_t)j * L - L;  // first sample of the 2L window
+  const int64_t t0 = a.s0 + (int64_t)j * L;  // first sample of block j
 
   double2 v[V];
 #pragma unroll
-  for (int s = 0; s < V; ++s)
-    v[s] = active ? fetch_pair(xc, hc, t0 + 2 * pass0_index<M, V>(tid, s), a.n, L, a.aligned) : make_double2(0, 0);
-  if (active && a.hist_out && j == a.jc - 1) {  // streaming: the next call's history
-    double* ho = a.hist_out + (int64_t)c * a.hist_stride;
-#pragma unroll
-    for (int s = 0; s < V; ++s) {
-      const int w = 2 * pass0_index<M, V>(tid, s);
-      if (w >= L) {
-        ho[w - L] = v[s].x;
-        ho[w - L + 1] = v[s].y;
-      }
-    }
+  for (int s = 0; s < V; ++s) {
+    const int m = pass0_index<M, V>(tid, s);
+    v[s] = (active && m < M / 2) ? fetch_pair(xc, t0 + 2 * m, a.n, a.aligned) : make_double2(0, 0);
   }
   fft_run<M, V, true>(v, tid, lds, TwGlobal{a.twM});
   if (!active) return;
@@ -148,9 +143,10 @@ __global__ __launch_bounds__((FftPlan<M, V>::BLOCK)) void k_irfft_store(IrfftArg
 // so two workgroups share a CU and one's HBM phase hides under the other's
 // LDS/VALU phase: a workgroup barriers only with itself.  Twiddles live in LDS
 // (no global load between the loads and stores of an item).
-// K1 stores the raw packed spectrum Zr (M values); k_fdl_mac separates it
-// into the real-signal spectrum on load (Zr[k] and Zr[M-k] sit in partner
-// lanes of its pair waves).
+// K1 stores the packed block spectrum P (M values); k_fdl_mac forms the
+// window spectrum Zr from two consecutive P rows and separates it into the
+// real-signal spectrum on load (Zr[k] and Zr[M-k] sit in partner lanes of
+// its pair waves).  Half of K1's pass-0 inputs are the block's zero padding.
 // ---------------------------------------------------------------------------
 template <int M>
 struct SplitPlan {
@@ -171,37 +167,29 @@ __global__ __launch_bounds__((SplitPlan<M>::T)) __attribute__((amdgpu_waves_per_
   const int c = __builtin_amdgcn_readfirstlane(e / a.jc);
   const int j = __builtin_amdgcn_readfirstlane(e - c * a.jc);
   const double* xc = a.x + (int64_t)c * a.x_stride;
-  const double* hc = a.xhist ? a.xhist + (int64_t)c * a.hist_stride : nullptr;
-  const int64_t t0 = a.s0 + (int64_t)j * L - L;  // first sample of the 2L window
-
+  const int64_t t0 = a.s0 + (int64_t)j * L;  // first sample of block j
+  // E[m] = z[2m], O[m] = z[2m+1] hold samples 4m.. of the block; the upper
+  // half of the padded block is zero, i.e. pass-0 slots s with
+  // s mod R0 >= R0/2 (pass0_index >= M2/2), known at compile time.
+  constexpr int R0 = FftPlan<M2, V>::R0;
   double2 ev[V], ov[V];
-  if (a.aligned && t0 >= 0 && t0 + 2 * L <= a.n) {  // wave-uniform fast path
+  if (a.aligned && t0 + L <= a.n) {  // wave-uniform fast path
     // E's inputs first: its transform starts while O's are still in flight
 #pragma unroll
     for (int s = 0; s < V; ++s)
-      ev[s] = *reinterpret_cast<const double2*>(xc + t0 + 4 * pass0_index<M2, V>(tid, s));
+      ev[s] = (s % R0 < R0 / 2) ? *reinterpret_cast<const double2*>(xc + t0 + 4 * pass0_index<M2, V>(tid, s))
+                                : make_double2(0.0, 0.0);
 #pragma unroll
     for (int s = 0; s < V; ++s)
-      ov[s] = *reinterpret_cast<const double2*>(xc + t0 + 4 * pass0_index<M2, V>(tid, s) + 2);
+      ov[s] = (s % R0 < R0 / 2) ? *reinterpret_cast<const double2*>(xc + t0 + 4 * pass0_index<M2, V>(tid, s) + 2)
+                                : make_double2(0.0, 0.0);
   } else {
 #pragma unroll
     for (int s = 0; s < V; ++s) {
       const int64_t t = t0 + 4 * pass0_index<M2, V>(tid, s);
-      ev[s] = fetch_pair(xc, hc, t, a.n, L, a.aligned);
-      ov[s] = fetch_pair(xc, hc, t + 2, a.n, L, a.aligned);
-    }
-  }
-  if (a.hist_out && j == a.jc - 1) {  // streaming: the next call's history
-    double* ho = a.hist_out + (int64_t)c * a.hist_stride;
-#pragma unroll
-    for (int s = 0; s < V; ++s) {
-      const int w = 4 * pass0_index<M2, V>(tid, s);  // window offset of ev[s]
-      if (w >= L) {
-        ho[w - L] = ev[s].x;
-        ho[w - L + 1] = ev[s].y;
-        ho[w - L + 2] = ov[s].x;
-        ho[w - L + 3] = ov[s].y;
-      }
+      const bool live = s % R0 < R0 / 2;
+      ev[s] = live ? fetch_pair(xc, t, a.n, a.aligned) : make_double2(0.0, 0.0);
+      ov[s] = live ? fetch_pair(xc, t + 2, a.n, a.aligned) : make_double2(0.0, 0.0);
     }
   }
   const TwLds<M2> twS = tw_lds_compute<M2>(lds + FftPlan<M2, V>::MP, tid, T);

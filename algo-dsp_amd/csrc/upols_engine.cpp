@@ -80,9 +80,7 @@ Upols::Upols(int device, const double* kernels, int n_ir, int64_t K, int L, int 
   a.x = dparts.p;
   a.x_stride = L_;
   a.n = L_;
-  a.xhist = nullptr;
-  a.hist_stride = 0;
-  a.s0 = L_;
+  a.s0 = 0;
   a.jc = 1;
   a.channels = (int)nparts;
   a.aligned = 1;
@@ -99,8 +97,6 @@ Upols::Upols(int device, const double* kernels, int n_ir, int64_t K, int L, int 
   X_.alloc((size_t)C_ * (Q_ + 1) * MS_);  // Q ring rows + one zero row per channel
   // Z rows: jc_max outputs + 16 rows of run overshoot (k_fdl_mac)
   Y_.alloc((size_t)C_ * (jc_max_ + 16) * MS_);
-  hist_[0].alloc((size_t)C_ * L_);
-  hist_[1].alloc((size_t)C_ * L_);
   std::vector<int> irm(C_);
   for (int c = 0; c < C_; ++c) irm[c] = ir_map ? ir_map[c] : (c % n_ir_);
   for (int c = 0; c < C_; ++c)
@@ -179,9 +175,6 @@ void Upols::read_profile(double* ms, int64_t* launches, double* alg_bytes) {
 
 void Upols::reset_stream(hipStream_t s) {
   AD_HIP(hipMemsetAsync(X_.p, 0, X_.n * sizeof(double2), s));
-  AD_HIP(hipMemsetAsync(hist_[0].p, 0, hist_[0].n * sizeof(double), s));
-  AD_HIP(hipMemsetAsync(hist_[1].p, 0, hist_[1].n * sizeof(double), s));
-  hcur_ = 0;
   g_next_ = 0;
 }
 
@@ -199,6 +192,9 @@ void Upols::run(const double* d_in, int64_t in_stride, int64_t n, double* d_out,
   if (J <= 0) return;
   const int in_aligned = ((reinterpret_cast<uintptr_t>(d_in) & 15) == 0) && (in_stride % 2 == 0);
   const int out_aligned = ((reinterpret_cast<uintptr_t>(d_out) & 15) == 0) && (out_stride % 2 == 0);
+  // call blocks holding input samples: [0, nb_in); K1 transforms only those,
+  // K2 reads every later block as zeros
+  const int64_t nb_in = (std::max<int64_t>(n, 0) + L_ - 1) / L_;
   // balanced chunks of at most jc_max blocks (no tiny tail launch)
   const int64_t nchunks = (J + jc_max_ - 1) / jc_max_;
   const int64_t jc_even = (J + nchunks - 1) / nchunks;
@@ -206,17 +202,14 @@ void Upols::run(const double* d_in, int64_t in_stride, int64_t n, double* d_out,
     const int jc = (int)std::min<int64_t>(jc_even, J - cr);
     const int64_t cs = jb + cr;  // first output block of this chunk
     const int slot0 = (int)(g_next_ % Q_);
+    const int jin = (int)std::clamp<int64_t>(nb_in - cs, 0, jc);  // K1 items per channel
 
     RfftArgs a{};
     a.x = d_in;
     a.x_stride = in_stride;
     a.n = n;
-    a.xhist = use_hist ? hist_[hcur_].p : nullptr;
-    // the last chunk's last window leaves the next call's history in the other buffer
-    a.hist_out = (use_hist && cr + jc >= J) ? hist_[hcur_ ^ 1].p : nullptr;
-    a.hist_stride = L_;
     a.s0 = cs * L_;
-    a.jc = jc;
+    a.jc = jin;
     a.channels = C_;
     a.aligned = in_aligned;
     a.X = X_.p;
@@ -232,13 +225,14 @@ void Upols::run(const double* d_in, int64_t in_stride, int64_t n, double* d_out,
     hipEvent_t e0;
     prof_begin(s, &e0);
     launch_window_rfft(M_, a, s);
-    prof_end(s, e0, 0, blocks * ((double)L_ * 8 + (double)(M_ + 1) * 16));
+    prof_end(s, e0, 0, (double)C_ * jin * ((double)L_ * 8 + (double)M_ * 16));
 
     MacArgs m{};
     m.X = X_.p;
     m.x_ch_stride = (int64_t)(Q_ + 1) * MS_;
     m.Q = Q_;
     m.g0 = g_next_;
+    m.gend = g_next_ - cs + nb_in - 1;
     m.MS = MS_;
     m.H = H_.p;
     m.h_ir_stride = (int64_t)P_ * MS_;
@@ -275,7 +269,6 @@ void Upols::run(const double* d_in, int64_t in_stride, int64_t n, double* d_out,
     AD_HIP(hipGetLastError());
     g_next_ += jc;
   }
-  if (use_hist) hcur_ ^= 1;
 }
 
 void Upols::save_history(const double*, int64_t, int64_t n, hipStream_t) {

@@ -1,7 +1,8 @@
 // Uniformly partitioned overlap-save engine (host runtime around the HIP
 // kernels of conv_kernels.hip).  One engine owns the IR spectra of n_ir
 // impulse responses, the per-channel frequency-domain delay line (X ring),
-// the per-chunk product spectra (Y) and the input history for streaming.
+// the per-chunk product spectra (Y).  The ring holds one spectrum per input
+// block (K1's block spectra), so streaming needs no separate input history.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -28,23 +29,24 @@ class Upols {
   int64_t kernel_len() const { return K_; }
   hipStream_t stream() const { return stream_; }
 
-  // Streaming state: zero the delay line and input history.
+  // Streaming state: zero the delay line.
   void reset_stream(hipStream_t s);
   // Offline call start: only the delay-line slots preceding block 0 are zeroed.
   void begin_offline(hipStream_t s);
 
   // Runs ceil(out_len/L) blocks for all channels.  d_in: [C][in_stride],
   // n valid samples.  d_out: [C][out_stride], out_len samples written.
-  // use_hist: the L samples before the call come from the streaming history.
+  // use_hist: the call continues the stream (the blocks before it are the
+  // previous calls' blocks, already in the ring); offline calls that start a
+  // signal call begin_offline first, so the blocks before it read as zeros.
   // [jb, je): the output blocks to run (je < 0: through the end of out_len).
   // Offline segments of one signal run in increasing order (the delay line
   // carries from one segment to the next).
   // accumulate: K3 adds into d_out instead of storing (partitioned stages).
   void run(const double* d_in, int64_t in_stride, int64_t n, double* d_out, int64_t out_stride, int64_t out_len,
            bool use_hist, hipStream_t s, int64_t jb = 0, int64_t je = -1, bool accumulate = false);
-  // Saves the last L input samples of the call into the streaming history.
-  // Streaming calls (use_hist) refresh the history inside K1; kept for API
-  // symmetry, a no-op.
+  // Kept for API symmetry: the ring already holds the last block's spectrum
+  // (checks that a streaming call covers at least one hop).
   void save_history(const double* d_in, int64_t in_stride, int64_t n, hipStream_t s);
 
   // Live kernel timing with HIP events on the launch stream (kernel k:
@@ -63,8 +65,6 @@ class Upols {
   DevBuf<double2> H_;    // [n_ir][P][MS]
   DevBuf<double2> X_;    // [C][Q][MS]
   DevBuf<double2> Y_;    // [C][jc_max][MS]
-  DevBuf<double> hist_[2];  // [C][L] ping-pong: K1 reads one and writes the next call's into the other
-  int hcur_ = 0;
   DevBuf<int> irmap_;    // [C]
 
   struct ProfRec {

@@ -12,7 +12,7 @@ BARGS=${BENCH_ARGS:---steps 3 --warmup 1 --no-cpu-baseline --kernel-timing off}
 i=0
 for grp in ${PMC:-"SQ_WAIT_ANY,SQ_WAVE_CYCLES,SQ_ACTIVE_INST_ANY,SQ_WAIT_INST_ANY"}; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc ${grp//,/ } --output-format csv -d $OUT/p$i -o bench -- python3 bench.py $BARGS > $OUT/p$i.log 2>&1
+  timeout -s KILL 90 rocprofv3 --pmc ${grp//,/ } --output-format csv -d $OUT/p$i -o bench -- python3 bench.py $BARGS > $OUT/p$i.log 2>&1
   rc=$?; echo "pass $i ($grp) rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 $OUT/p$i.log; exit $rc; fi
 done
