@@ -196,6 +196,7 @@ def _declare(L: C.CDLL) -> None:
         "ad_conv_reverb_multi_process_device": (C.c_int, [vp, vp, i64, i64, vp]),
         "ad_conv_reverb_multi_process": (C.c_int, [vp, c_double_p, i64]),
         "ad_conv_profile_enable": (C.c_int, [vp, C.c_int]),
+        "ad_conv_profile_kernels": (C.c_int, [vp, C.c_int]),
         "ad_conv_profile_read": (C.c_int, [vp, c_double_p, c_int64_p, c_double_p]),
         "ad_compressor_default_config": (None, [C.POINTER(CompressorConfig), C.c_double]),
         "ad_fx_chain_create": (C.c_int, [C.c_int, C.c_int, C.POINTER(vp)]),

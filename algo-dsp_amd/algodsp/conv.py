@@ -351,7 +351,9 @@ class MultiChannelConvolver(_Handle):
 
     KERNELS = ("k_window_rfft", "k_fdl_mac", "k_irfft_store")
 
-    def profile_enable(self, on: bool = True) -> None:
+    def profile_enable(self, on: bool = True, kernels: int = 7) -> None:
+        """Event timing of the engine's launches; kernels: bit k = KERNELS[k]."""
+        check(lib().ad_conv_profile_kernels(self._h, kernels))
         check(lib().ad_conv_profile_enable(self._h, 1 if on else 0))
 
     def profile_read(self):

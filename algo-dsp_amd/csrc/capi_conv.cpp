@@ -1055,6 +1055,14 @@ int ad_conv_profile_enable(ad_conv* h, int enable) {
   });
 }
 
+int ad_conv_profile_kernels(ad_conv* h, int mask) {
+  return guard([&] {
+    if (!h || !h->eng) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "handle has no FFT engine");
+    if (mask < 0 || mask > 7) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "kernel mask: bits 0..2");
+    h->eng->set_profile_mask(mask);
+  });
+}
+
 int ad_conv_profile_read(ad_conv* h, double* total_ms, int64_t* launches, double* alg_bytes) {
   return guard([&] {
     if (!h || !h->eng) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "handle has no FFT engine");

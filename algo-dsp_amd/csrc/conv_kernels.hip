@@ -805,6 +805,11 @@ __global__ __launch_bounds__(256) void k_pc_emit(const double* in, int64_t in_st
 // ---------------------------------------------------------------------------
 // Launchers
 // ---------------------------------------------------------------------------
+LaunchTiming& launch_timing() {
+  static thread_local LaunchTiming t;
+  return t;
+}
+
 namespace {
 int mac_depth() {
   static const int d = [] {
@@ -819,9 +824,9 @@ void mac_go_d(const MacArgs& a, dim3 grid, hipStream_t s) {
   MacArgs c = a;
   for (c.p0 = 0; c.p0 < a.P; c.p0 += NH * PC) {
     if (c.p0 == 0)
-      hipLaunchKernelGGL((k_fdl_mac<PC, NH, true, DQ>), grid, dim3(64), 0, s, c);
+      timed_launch(k_fdl_mac<PC, NH, true, DQ>, grid, dim3(64), s, c);
     else
-      hipLaunchKernelGGL((k_fdl_mac<PC, NH, false, DQ>), grid, dim3(64), 0, s, c);
+      timed_launch(k_fdl_mac<PC, NH, false, DQ>, grid, dim3(64), s, c);
   }
 }
 
@@ -847,9 +852,9 @@ void mac_go_l(const MacArgs& a, dim3 grid, hipStream_t s) {
   MacArgs c = a;
   for (c.p0 = 0; c.p0 < a.P; c.p0 += NH * PC) {
     if (c.p0 == 0)
-      hipLaunchKernelGGL((k_fdl_mac_lds<PC, NH, true, DL>), grid, dim3(64), 0, s, c);
+      timed_launch(k_fdl_mac_lds<PC, NH, true, DL>, grid, dim3(64), s, c);
     else
-      hipLaunchKernelGGL((k_fdl_mac_lds<PC, NH, false, DL>), grid, dim3(64), 0, s, c);
+      timed_launch(k_fdl_mac_lds<PC, NH, false, DL>, grid, dim3(64), s, c);
   }
 }
 

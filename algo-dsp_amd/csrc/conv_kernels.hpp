@@ -1,6 +1,7 @@
 // Argument blocks and launchers of the conv kernels (conv_kernels.hip).
 #pragma once
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -18,6 +19,27 @@ __host__ __device__ inline int zrow_pos(int q, int M) {
   if (q == M / 2) return M;
   const int d = M - q;
   return ((d >> 5) << 6) + 32 + (d & 31);
+}
+
+// Kernel timing of the engine launchers: when start/stop are set (Upols
+// profiling), the launch carries them in its dispatch packet
+// (hipExtLaunchKernelGGL), so the recorded interval is the kernel's own
+// execution, with no marker packets between the kernels of a call.  start is
+// consumed by the first launch; every launch re-records stop, so a kernel
+// issued as several launches (K2 partition chunks) spans all of them.
+struct LaunchTiming {
+  hipEvent_t start = nullptr, stop = nullptr;
+};
+LaunchTiming& launch_timing();  // per host thread
+template <class F, class... Args>
+inline void timed_launch(F kernel, dim3 grid, dim3 block, hipStream_t s, Args... args) {
+  LaunchTiming& t = launch_timing();
+  if (t.stop) {
+    hipExtLaunchKernelGGL(kernel, grid, block, 0, s, t.start, t.stop, 0, args...);
+    t.start = nullptr;
+  } else {
+    hipLaunchKernelGGL(kernel, grid, block, 0, s, args...);
+  }
 }
 
 struct RfftArgs {

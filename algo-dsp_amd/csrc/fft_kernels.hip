@@ -280,25 +280,23 @@ void rfft_go(const RfftArgs& a, hipStream_t s) {
   // memory) spreads its windows over up to 256 workgroups instead.
   RfftArgs b = a;
   b.per_wg = (int)std::min<int64_t>(Plan::F, std::max<int64_t>(1, (items + 255) / 256));
-  hipLaunchKernelGGL((k_window_rfft<M, V>), dim3((unsigned)((items + b.per_wg - 1) / b.per_wg)), dim3(Plan::BLOCK), 0,
-                     s, b);
+  timed_launch(k_window_rfft<M, V>, dim3((unsigned)((items + b.per_wg - 1) / b.per_wg)), dim3(Plan::BLOCK), s, b);
 }
 template <int M>
 void rfft_split_go(const RfftArgs& a, hipStream_t s) {
   const int64_t items = (int64_t)a.channels * a.jc;
-  hipLaunchKernelGGL((k_window_rfft_split<M>), dim3((unsigned)items), dim3(SplitPlan<M>::T), 0, s, a);
+  timed_launch(k_window_rfft_split<M>, dim3((unsigned)items), dim3(SplitPlan<M>::T), s, a);
 }
 template <int M, int V>
 void irfft_go(const IrfftArgs& a, hipStream_t s) {
   using Plan = FftPlan<M, V>;
   const int64_t items = (int64_t)a.channels * a.jc;
-  hipLaunchKernelGGL((k_irfft_store<M, V>), dim3((unsigned)((items + Plan::F - 1) / Plan::F)), dim3(Plan::BLOCK), 0,
-                     s, a);
+  timed_launch(k_irfft_store<M, V>, dim3((unsigned)((items + Plan::F - 1) / Plan::F)), dim3(Plan::BLOCK), s, a);
 }
 template <int M>
 void irfft_split_go(const IrfftArgs& a, hipStream_t s) {
   const int64_t items = (int64_t)a.channels * a.jc;
-  hipLaunchKernelGGL((k_irfft_store_split<M>), dim3((unsigned)items), dim3(SplitPlan<M>::T), 0, s, a);
+  timed_launch(k_irfft_store_split<M>, dim3((unsigned)items), dim3(SplitPlan<M>::T), s, a);
 }
 
 }  // namespace

@@ -127,18 +127,28 @@ hipEvent_t Upols::take_event() {
   return e;
 }
 
-void Upols::prof_begin(hipStream_t s, hipEvent_t* e) {
+// The events ride in the kernel's dispatch packet (timed_launch), so the
+// interval is the launch's own execution: no marker packets sit between the
+// kernels of a call (those cost ~5 us per kernel and a cold start).
+void Upols::prof_begin(hipStream_t, hipEvent_t* e, int kernel) {
   *e = nullptr;
-  if (!prof_) return;
+  if (!prof_ || !((prof_mask_ >> kernel) & 1)) return;
   *e = take_event();
-  AD_HIP(hipEventRecord(*e, s));
+  LaunchTiming& t = launch_timing();
+  t.start = *e;
+  t.stop = take_event();
 }
 
-void Upols::prof_end(hipStream_t s, hipEvent_t e0, int kernel, double bytes) {
-  if (!prof_ || !e0) return;
-  hipEvent_t e1 = take_event();
-  AD_HIP(hipEventRecord(e1, s));
-  prof_recs_.push_back({e0, e1, kernel, bytes});
+void Upols::prof_end(hipStream_t, hipEvent_t e0, int kernel, double bytes) {
+  if (!e0) return;
+  LaunchTiming& t = launch_timing();
+  if (t.start) {  // nothing was launched
+    event_pool_.push_back(e0);
+    event_pool_.push_back(t.stop);
+  } else {
+    prof_recs_.push_back({e0, t.stop, kernel, bytes});
+  }
+  t.start = t.stop = nullptr;
 }
 
 void Upols::set_profiling(bool on) {
@@ -223,7 +233,7 @@ void Upols::run(const double* d_in, int64_t in_stride, int64_t n, double* d_out,
     // M+1 complex128 bins out, per (channel, block)
     const double blocks = (double)C_ * jc;
     hipEvent_t e0;
-    prof_begin(s, &e0);
+    prof_begin(s, &e0, 0);
     launch_window_rfft(M_, a, s);
     prof_end(s, e0, 0, (double)C_ * jin * ((double)L_ * 8 + (double)M_ * 16));
 
@@ -245,7 +255,7 @@ void Upols::run(const double* d_in, int64_t in_stride, int64_t n, double* d_out,
     m.P = P_;
     m.M = M_;
     m.twN = tw_.p + M_;
-    prof_begin(s, &e0);
+    prof_begin(s, &e0, 1);
     launch_fdl_mac(PC_, NH_, m, C_, s);
     prof_end(s, e0, 1, blocks * (double)(M_ + 1) * 32 + (double)n_ir_ * P_ * (M_ + 1) * 16);
 
@@ -263,7 +273,7 @@ void Upols::run(const double* d_in, int64_t in_stride, int64_t n, double* d_out,
     b.accumulate = accumulate ? 1 : 0;
     b.twM = tw_.p;
     b.twN = tw_.p + M_;
-    prof_begin(s, &e0);
+    prof_begin(s, &e0, 2);
     launch_irfft_store(M_, b, s);
     prof_end(s, e0, 2, blocks * ((double)(M_ + 1) * 16 + (double)L_ * 8));
     AD_HIP(hipGetLastError());

@@ -54,6 +54,7 @@ class Upols {
   // synchronises, accumulates and clears the recorded launches.
   static constexpr int kKernels = 3;
   void set_profiling(bool on);
+  void set_profile_mask(int mask) { prof_mask_ = mask; }
   void read_profile(double* ms, int64_t* launches, double* alg_bytes);
 
  private:
@@ -73,13 +74,14 @@ class Upols {
     double bytes;
   };
   bool prof_ = false;
+  int prof_mask_ = 7;
   std::vector<ProfRec> prof_recs_;
   std::vector<hipEvent_t> event_pool_;
   double acc_ms_[kKernels] = {0, 0, 0};
   int64_t acc_n_[kKernels] = {0, 0, 0};
   double acc_bytes_[kKernels] = {0, 0, 0};
   hipEvent_t take_event();
-  void prof_begin(hipStream_t s, hipEvent_t* e);
+  void prof_begin(hipStream_t s, hipEvent_t* e, int kernel);
   void prof_end(hipStream_t s, hipEvent_t e0, int kernel, double bytes);
 };
 

@@ -230,6 +230,9 @@ int ad_conv_reverb_multi_process(ad_conv* h, double* buf, int64_t n);
  * (DESIGN.md), then clears the counters.  Arrays have 3 entries.          */
 int ad_conv_profile_enable(ad_conv* h, int enable);
 int ad_conv_profile_read(ad_conv* h, double* total_ms, int64_t* launches, double* alg_bytes);
+/* Which kernels enabled timing records: bit k = kernel k (default 7, all).
+ * Timing one kernel keeps two events per call inside a timed loop.       */
+int ad_conv_profile_kernels(ad_conv* h, int mask);
 /* Stereo mixdown of a channel group (build-defined; the
  * reference defines no mixdown):
  *   d_mix[t]              (L) = sum of the group's channels with an even global index,
