@@ -6,11 +6,12 @@
   python bench.py --gpus N --steps K --warmup W
 
 N > 1 (torchrun, one rank per GPU): config 4's shard (BASELINE.json
-configs[3]): every rank convolves its own group of 8 channels x 2^22 samples
-(ch c with IR[c mod 2]) -- the same 2^25 samples per GPU per step as the N = 1
-stereo config, so per-GPU work is fixed (weak scaling) -- and the per-rank
-stereo partial mixes are summed to rank 0 with one RCCL reduce over xGMI (the
-north star's stereo mixdown), inside the timed step.
+configs[3]): every rank convolves its own group of 8 channels x 2^24 samples
+(ch c with IR[c mod 2]), so per-GPU work is fixed (weak scaling) and N = 8 is
+the 64-channel job, and the per-rank stereo partial mixes are summed to rank 0
+with one RCCL reduce over xGMI (the north star's stereo mixdown), inside the
+timed step.  The channels are as long as the N = 1 stereo config's, so the
+convolution tail and the launch ramps weigh the same per sample at every N.
 Rank 0 prints one JSON line.
 """
 from __future__ import annotations
@@ -36,7 +37,7 @@ def parse():
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--samples", type=int, default=None,
-                   help="samples per channel per step (default 2^24 at N = 1, 2^22 at N > 1)")
+                   help="samples per channel per step (default 2^24)")
     p.add_argument("--hop", type=int, default=8192)
     p.add_argument("--chunk", type=int, default=0, help="blocks per channel per engine chunk (0 = auto)")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -61,7 +62,7 @@ def parse():
                    help="fx workload: run an effectchain graph through the batched graph runtime")
     p.add_argument("--workload", choices=["conv", "shard", "fx", "stream", "corr"], default="conv",
                    help="conv: BASELINE metric (overlap-save conv; config 3 at N = 1, config 4's shard at N > 1); "
-                        "shard: config 4's shard (8 ch x 2^22 per GPU + RCCL stereo mixdown) at any N; "
+                        "shard: config 4's shard (8 ch x 2^24 per GPU + RCCL stereo mixdown) at any N; "
                         "fx: config 5 effect chain (256 ch); "
                         "stream: config 2 streaming OLS (mono, 16384 taps, 4096-sample host blocks); "
                         "corr: CorrelateFFT of two 2^23-sample signals (SURVEY 8(f)3, device buffers)")
@@ -176,7 +177,7 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    # config 4's shard (8 ch x 2^22 per GPU + the stereo mixdown) at N > 1, or
+    # config 4's shard (8 ch x 2^24 per GPU + the stereo mixdown) at N > 1, or
     # at any N with --workload shard; config 3 (stereo x 2^24) at N = 1
     shard_cfg = world > 1 or args.workload == "shard"
     mixdown = shard_cfg if args.mixdown == "auto" else args.mixdown == "on"
@@ -186,7 +187,7 @@ def main():
     if args.channels is None:
         args.channels = 8 if shard_cfg else 2
     if args.samples is None:
-        args.samples = (1 << 22) if shard_cfg else (1 << 24)
+        args.samples = 1 << 24
     ir = irlib.large_church()                       # [2][131072], Large Church zero padded
     K = ir.shape[1]
     n = args.samples

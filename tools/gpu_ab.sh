@@ -14,5 +14,5 @@ for v in ${VARIANTS:-"-"}; do
       ${BENCH_ARGS:-} > gpurun_out/ab_$i.json 2> gpurun_out/ab_$i.err
   rc=$?
   if [ $rc -ne 0 ]; then echo "variant $v rc=$rc"; tail -5 gpurun_out/ab_$i.err; exit $rc; fi
-  python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], d['value'], d['ms_per_step'], d['parity']['rms'], {k:round(x['avg_us'],1) for k,x in d['kernels'].items()})" gpurun_out/ab_$i.json "$v"
+  python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], d['value'], d['ms_per_step'], d['parity']['rms'], {k:round(x['avg_us'],1) for k,x in d['kernels'].items()})" gpurun_out/ab_$i.json "$v"
 done
