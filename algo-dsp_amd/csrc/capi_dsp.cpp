@@ -71,7 +71,7 @@ void check_comp_config(const ad_compressor_config& g) {
 // ---------------------------------------------------------------------------
 // effect chain handle
 // ---------------------------------------------------------------------------
-constexpr int kFxSlots = 3;  // chunk buffers in flight (staged engine)
+constexpr int kFxSlots = 4;  // chunk buffers in flight (staged engine; the split EQ stage lags one chunk)
 struct ad_fx_chain {
   int device = 0, channels = 0, cpad = 0;
   hipStream_t stream = nullptr;
@@ -100,6 +100,7 @@ struct ad_fx_chain {
   hipEvent_t ev_in = nullptr;
   hipEvent_t ev[3][kFxSlots] = {};
   DevBuf<double> xT[kFxSlots], vT[kFxSlots], envT[kFxSlots], inT[kFxSlots], coT[kFxSlots];
+  DevBuf<double> midT[kFxSlots];  // split K_eq: the first part's output rows
   int64_t tmax = 0;
 
   ~ad_fx_chain() {
@@ -170,6 +171,16 @@ bool fx_staged_ok(const ad_fx_chain* h) {
          (h->nsec > 0 || h->comp_on || h->verb_on);
 }
 
+// Split K_eq (sections 0 .. s1-1 of chunk i beside the rest + the detector of
+// chunk i - 1, one launch): the EQ recurrences of a channel group run on two
+// CUs, every wave on a SIMD of its own.  Returns s1, or 0 for one pipeline.
+int fx_eq_split(const ad_fx_chain* h) {
+  const char* v = std::getenv("AD_FX_EQSPLIT");
+  if (v && v[0] == '0') return 0;
+  if (!h->comp_on || h->nsec < 3) return 0;
+  return (h->nsec + 2) / 2;  // part waves (s1 + loader) vs (ns - s1 + detector + loader)
+}
+
 int64_t fx_chunk() {
   const char* v = std::getenv("AD_FX_CHUNK");
   const int64_t t = v ? std::atoll(v) : 0;
@@ -186,8 +197,9 @@ void fx_run_staged(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hip
     AD_HIP(hipEventCreateWithFlags(&h->ev_in, hipEventDisableTiming));
   }
   const bool need_x = eq || comp, need_v = comp || (eq && !verb);
+  const int s1 = fx_eq_split(h);
   if (T > h->tmax || (need_x && !h->xT[0].p) || (need_v && !h->vT[0].p) || (comp && !h->envT[0].p) ||
-      (verb && !h->inT[0].p)) {  // (re)size the chunk buffers once no stage is running
+      (verb && !h->inT[0].p) || (s1 && !h->midT[0].p)) {  // (re)size the chunk buffers once no stage is running
     for (hipStream_t x : h->st) AD_HIP(hipStreamSynchronize(x));
     AD_HIP(hipStreamSynchronize(s));
     const size_t r = (size_t)h->cpad * std::max(T, h->tmax);
@@ -199,6 +211,7 @@ void fx_run_staged(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hip
         h->inT[k].alloc(r);
         h->coT[k].alloc(r * kVerbCombs);
       }
+      if (s1) h->midT[k].alloc(r);
     }
     h->tmax = std::max(T, h->tmax);
   }
@@ -210,6 +223,92 @@ void fx_run_staged(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hip
     AD_HIP(hipEventRecord(h->ev_in, s));
     AD_HIP(hipStreamWaitEvent(sc, h->ev_in, 0));
     AD_HIP(hipStreamWaitEvent(sa, h->ev_in, 0));
+  }
+  // chunk i's stage arguments (slot i % kFxSlots)
+  auto chunk_args = [&](int64_t ci) {
+    const int ks = (int)(ci % kFxSlots);
+    const int64_t t0 = ci * T;
+    FxStageArgs a{};
+    a.channels = h->channels;
+    a.cpad = h->cpad;
+    a.len = std::min(T, n - t0);
+    a.buf = d_buf + t0;
+    a.stride = stride;
+    a.xT = h->xT[ks].p;
+    a.vT = h->vT[ks].p;
+    a.envT = h->envT[ks].p;
+    a.inT = h->inT[ks].p;
+    a.coT = h->coT[ks].p;
+    a.tmax = h->tmax;
+    a.eq.nsec = h->nsec;
+    a.eq.sec = h->sec_dev.p;
+    a.eq.sec_ch_stride = h->eq_uniform ? 0 : (int64_t)h->nsec * kSecStride;
+    a.eq.state = h->eq_state.p;
+    a.cp = h->cp;
+    a.cs = h->cs.p;
+    a.rms_ring = h->ring.p;
+    a.vp = h->vp;
+    a.vs = h->vs.p;
+    a.vbuf = h->vbuf.p;
+    return a;
+  };
+  if (s1) {
+    // Split K_eq: launch i runs part A (sections 0 .. s1-1) of chunk i and
+    // part B (sections s1 .. ns-1 + detector) of chunk i - 1, which read A's
+    // rows of chunk i - 1 from midT; chunk i - 1's later stages follow.  A
+    // slot is rewritten (transpose / part A of chunk i) only after chunk
+    // i - kFxSlots's allpasses, enqueued kFxSlots - 1 iterations earlier.
+    const int64_t nch = (n + T - 1) / T;
+    int kl = 0;
+    for (int64_t ci = 0; ci <= nch; ++ci) {
+      FxStageArgs e{};
+      if (ci < nch) {
+        const int ks = (int)(ci % kFxSlots);
+        FxStageArgs a = chunk_args(ci);
+        if (verb && ci >= kFxSlots) AD_HIP(hipStreamWaitEvent(s, h->ev[EA][ks], 0));
+        launch_fx_transpose_in(a, a.xT, s);
+        e = a;
+        e.part[e.nparts++] = FxEqPart{0, s1, 0, a.len, a.xT, h->midT[ks].p, nullptr};
+      }
+      if (ci > 0) {
+        const FxStageArgs b = chunk_args(ci - 1);
+        if (ci == nch) e = b;
+        e.part[e.nparts++] = FxEqPart{s1, h->nsec - s1, 1, b.len, h->midT[(ci - 1) % kFxSlots].p, b.vT, b.envT};
+        static DevBuf<unsigned long long> sprof;
+        const bool want_prof = std::getenv("AD_FX_PROF") != nullptr && ci == 1;
+        if (want_prof) {
+          sprof.reserve(32);
+          AD_HIP(hipMemsetAsync(sprof.p, 0, 32 * sizeof(unsigned long long), s));
+          e.prof = sprof.p;
+        }
+        launch_fx_eq_parts(e, s);
+        if (want_prof) {
+          unsigned long long v[32];
+          AD_HIP(hipStreamSynchronize(s));
+          AD_HIP(hipMemcpy(v, sprof.p, sizeof(v), hipMemcpyDeviceToHost));
+          for (int w = 0; w < 16; ++w)
+            if (v[2 * w] || v[2 * w + 1])
+              fprintf(stderr, "fx split K_eq section/detector %d: compute %llu, barrier wait %llu ticks\n", w, v[2 * w],
+                      v[2 * w + 1]);
+        }
+        launch_fx_gain(b, !verb, s);
+        if (verb) {
+          kl = (int)((ci - 1) % kFxSlots);
+          AD_HIP(hipEventRecord(h->ev[EE][kl], s));
+          AD_HIP(hipStreamWaitEvent(sc, h->ev[EE][kl], 0));
+          launch_fx_comb(b, sc);
+          AD_HIP(hipEventRecord(h->ev[EC][kl], sc));
+          AD_HIP(hipStreamWaitEvent(sa, h->ev[EC][kl], 0));
+          launch_fx_allpass(b, sa);
+          AD_HIP(hipEventRecord(h->ev[EA][kl], sa));
+        }
+      } else {
+        launch_fx_eq_parts(e, s);
+      }
+    }
+    AD_HIP(hipGetLastError());
+    if (verb) AD_HIP(hipStreamWaitEvent(s, h->ev[EA][kl], 0));
+    return;
   }
   int64_t i = 0;
   int k = 0;

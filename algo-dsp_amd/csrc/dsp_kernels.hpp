@@ -87,6 +87,20 @@ void launch_chain(int stages, const ChainArgs& a, hipStream_t s);
 // Staged effect chain (fx_staged.hip): the chain split by recurrence into
 // kernels that run concurrently on their own streams over time chunks, each
 // stage on its own CUs.  Chunk-local buffers are time-major [t][cpad].
+// One K_eq pipeline: sections [s0, s0 + ns) of the chain, then (det) the
+// compressor's detector/envelope, over one chunk.  A launch runs one part per
+// blockIdx.y: the whole chain, or (split, fx_run_staged) sections 0 .. s1-1
+// of chunk i beside sections s1 .. ns-1 + the detector of chunk i - 1, so the
+// EQ recurrences of a channel group get two CUs.
+struct FxEqPart {
+  int s0, ns;
+  int det;
+  int64_t len;       // samples of this part's chunk
+  const double* in;  // input rows [len][cpad]
+  double* out;       // rows of the last section's output (ns = 0: the input)
+  double* env;       // envelope rows (det)
+};
+
 struct FxStageArgs {
   int channels, cpad;
   int64_t len;           // samples in this chunk
@@ -107,9 +121,12 @@ struct FxStageArgs {
   double* vbuf;
   int dbg;  // diagnostics only (AD_FX_DBG): bit 0 skip K_eq global stores, bit 1 skip its barrier, bit 2 skip its input loads
   unsigned long long* prof;  // diagnostics only (AD_FX_PROF): K_eq per wave {compute, barrier wait} clock ticks
+  FxEqPart part[2];          // K_eq parts (launch_fx_eq_parts)
+  int nparts;
 };
 // stage kernels; `mode` selects where a stage writes (see fx_staged.hip)
 void launch_fx_eq(const FxStageArgs& a, bool comp, int out_mode, hipStream_t s);
+void launch_fx_eq_parts(const FxStageArgs& a, hipStream_t s);  // a.part[0 .. nparts)
 void launch_fx_gain(const FxStageArgs& a, bool to_user, hipStream_t s);
 void launch_fx_transpose_in(const FxStageArgs& a, double* dstT, hipStream_t s);   // user -> dstT
 void launch_fx_transpose_out(const FxStageArgs& a, const double* srcT, hipStream_t s);  // srcT -> user

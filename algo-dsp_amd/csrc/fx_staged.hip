@@ -26,6 +26,9 @@
 // is channel-major [c][stride].
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstdlib>
+
 #include "dsp_device.hpp"
 #include "dsp_kernels.hpp"
 
@@ -87,28 +90,31 @@ __device__ __forceinline__ void eq_section_step(const double (&q)[kSecStride], d
 }
 
 template <bool COMP>
-__global__ __launch_bounds__(64 * (kMaxSecPerPass + 2)) void k_fx_eq(FxStageArgs a, int out_mode) {
+__global__ __launch_bounds__(64 * (kMaxSecPerPass + 2)) void k_fx_eq(FxStageArgs a) {
 #pragma clang fp contract(off)
   __shared__ double ring[kMaxSecPerPass][2][kEqP][64];
   __shared__ double xring[2][kEqP][64];  // input rows, written by the loader wave one step ahead
+  const FxEqPart& P = a.part[blockIdx.y];
   const int wid = wave_id();
   const int l = threadIdx.x & 63;
   const int c = blockIdx.x * 64 + l;
   const bool active = c < a.channels;
   const int cc = active ? c : a.channels - 1;
-  const int ns = a.eq.nsec;
-  const int W = ns + (COMP ? 1 : 0);  // compute waves; wave W is the loader
-  // Pipeline role of this wave: sections 0 .. ns-1, detector ns, loader W.
-  // Waves land on SIMD wid % 4; with three or more sections the detector
-  // (the longest recurrence) takes wave 3 so that its SIMD is its own.
-  const int w = (wid == W || !COMP || ns < 3) ? wid : (wid == 3 ? ns : (wid < 3 ? wid : wid - 1));
-  const int64_t len = a.len;
+  const int ns = P.ns;
+  const bool det = COMP && P.det;
+  const int W = ns + (det ? 1 : 0);  // compute waves; wave W is the loader
+  // Pipeline role of this wave: sections 0 .. ns-1, detector ns, loader W
+  // (waves past W idle through the barriers: the launch's other part is
+  // wider).  Waves land on SIMD wid % 4; with three or more sections the
+  // detector (the longest recurrence) takes wave 3 so that its SIMD is its own.
+  const int w = (wid >= W || !det || ns < 3) ? wid : (wid == 3 ? ns : (wid < 3 ? wid : wid - 1));
+  const int64_t len = P.len;
   const int64_t nst = (len + kEqP - 1) / kEqP;
   const int64_t steps = nst + W - 1;
   const int cp = a.cpad;
   const unsigned uc = (unsigned)c;
-  const double* xin = a.xT;  // uniform row pointers; a lane indexes [uc]
-  double* tmo = out_mode == kFxOutInT ? a.inT : a.vT;
+  const double* xin = P.in;  // uniform row pointers; a lane indexes [uc]
+  double* tmo = P.out;
 
   // Wave 0's input comes from xring, filled by the loader wave (wave W):
   // it loads each step's rows kEqPF steps before it writes them to LDS, in
@@ -136,7 +142,10 @@ __global__ __launch_bounds__(64 * (kMaxSecPerPass + 2)) void k_fx_eq(FxStageArgs
   };
   auto emit = [&](int64_t my, const double (&y)[kEqP], int nreal) { put_rows(tmo, my, y, nreal); };
 
-  if (w == W) {
+  if (w > W) {
+    // ---- idle: the barrier count of the part's waves (prologue + one per step)
+    for (int64_t k = 0; k <= steps; ++k) lds_barrier();
+  } else if (w == W) {
     // ---- loader
     double buf[kEqPF][kEqP];
     auto fetch = [&](double (&dst)[kEqP], int64_t step) {
@@ -176,14 +185,15 @@ __global__ __launch_bounds__(64 * (kMaxSecPerPass + 2)) void k_fx_eq(FxStageArgs
       }
     }
   } else if (w < ns) {
-    // ---- EQ section w (section.go:47-53 with the chain gain as pre-gain)
-    const double* sec = a.eq.sec + (int64_t)cc * a.eq.sec_ch_stride + w * kSecStride;
+    // ---- EQ section P.s0 + w (section.go:47-53 with the chain gain as pre-gain)
+    const int gs = P.s0 + w;  // the section's index in the chain
+    const double* sec = a.eq.sec + (int64_t)cc * a.eq.sec_ch_stride + gs * kSecStride;
     double q[kSecStride];
 #pragma unroll
     for (int k = 0; k < kSecStride; ++k) q[k] = sec[k];
-    double* st = a.eq.state + ((int64_t)cc * ns + w) * 2;
+    double* st = a.eq.state + ((int64_t)cc * a.eq.nsec + gs) * 2;
     double d0 = st[0], d1 = st[1];
-    const bool to_ring = w < ns - 1 || COMP;
+    const bool to_ring = w < ns - 1 || det;
     const bool last = w == ns - 1;
     unsigned long long tc = 0, tb = 0;
     lds_barrier();  // the loader's prologue (step 0 in xring)
@@ -217,19 +227,19 @@ __global__ __launch_bounds__(64 * (kMaxSecPerPass + 2)) void k_fx_eq(FxStageArgs
       }
     }
     if (a.prof && l == 0 && blockIdx.x == 0) {
-      a.prof[2 * w] = tc;
-      a.prof[2 * w + 1] = tb;
+      a.prof[2 * gs] = tc;
+      a.prof[2 * gs + 1] = tb;
     }
     if (active) {
       st[0] = d0;
       st[1] = d1;
     }
-  } else if constexpr (COMP) {
+  } else if (det) {
     // ---- detector + envelope (core.go:274-286, 331-400)
     const CompParams& p = a.cp;
     CompChState cs = a.cs[cc];
     double* rring = a.rms_ring + (int64_t)cc * p.rms_n;
-    double* eo = a.envT;
+    double* eo = P.env;
     lds_barrier();  // the loader's prologue (step 0 in xring)
     unsigned long long tc = 0, tb = 0;
     for (int64_t k = 0; k < steps; ++k) {
@@ -298,8 +308,8 @@ __global__ __launch_bounds__(64 * (kMaxSecPerPass + 2)) void k_fx_eq(FxStageArgs
       }
     }
     if (a.prof && l == 0 && blockIdx.x == 0) {
-      a.prof[2 * w] = tc;
-      a.prof[2 * w + 1] = tb;
+      a.prof[2 * (P.s0 + ns)] = tc;
+      a.prof[2 * (P.s0 + ns) + 1] = tb;
     }
     if (active) {  // only the fields this stage owns
       CompChState* o = a.cs + c;
@@ -647,14 +657,40 @@ __global__ __launch_bounds__(64 * kApW) void k_fx_allpass(FxStageArgs a) {
 
 }  // namespace
 
-void launch_fx_eq(const FxStageArgs& a, bool comp, int out_mode, hipStream_t s) {
-  const int W = a.eq.nsec + (comp ? 1 : 0);
-  if (W == 0 || a.len <= 0) return;
-  const dim3 grid((unsigned)((a.channels + 63) / 64)), block((unsigned)(64 * (W + 1)));  // + the loader
-  if (comp)
-    hipLaunchKernelGGL(k_fx_eq<true>, grid, block, 0, s, a, out_mode);
+// The serial stages (K_eq, K_comb, K_ap) are issue/latency bound per wave:
+// their workgroups claim over half a CU's LDS so that no two of them share a
+// CU (config 5: +1.5 %; AD_FX_EXCL=0 turns it off).
+int fx_excl_lds(int own) {
+  static const int on = [] {
+    const char* v = std::getenv("AD_FX_EXCL");
+    return !(v && v[0] == '0');
+  }();
+  if (!on) return 0;
+  return std::max(0, 82 * 1024 - own);
+}
+
+void launch_fx_eq_parts(const FxStageArgs& a, hipStream_t s) {
+  int waves = 0;
+  bool det = false;
+  for (int i = 0; i < a.nparts; ++i) {
+    waves = std::max(waves, a.part[i].ns + (a.part[i].det ? 1 : 0) + 1);  // + the loader
+    det = det || a.part[i].det;
+  }
+  if (a.nparts <= 0 || waves <= 1) return;
+  const dim3 grid((unsigned)((a.channels + 63) / 64), (unsigned)a.nparts), block((unsigned)(64 * waves));
+  const int dyn = fx_excl_lds(72 * 1024);
+  if (det)
+    hipLaunchKernelGGL(k_fx_eq<true>, grid, block, dyn, s, a);
   else
-    hipLaunchKernelGGL(k_fx_eq<false>, grid, block, 0, s, a, out_mode);
+    hipLaunchKernelGGL(k_fx_eq<false>, grid, block, dyn, s, a);
+}
+
+void launch_fx_eq(const FxStageArgs& a, bool comp, int out_mode, hipStream_t s) {
+  if (a.len <= 0) return;
+  FxStageArgs b = a;
+  b.nparts = 1;
+  b.part[0] = FxEqPart{0, a.eq.nsec, comp ? 1 : 0, a.len, a.xT, out_mode == kFxOutInT ? a.inT : a.vT, a.envT};
+  launch_fx_eq_parts(b, s);
 }
 
 void launch_fx_gain(const FxStageArgs& a, bool to_user, hipStream_t s) {
@@ -680,12 +716,13 @@ void launch_fx_transpose_out(const FxStageArgs& a, const double* srcT, hipStream
 
 void launch_fx_comb(const FxStageArgs& a, hipStream_t s) {
   if (a.len <= 0) return;
-  hipLaunchKernelGGL(k_fx_comb, dim3((unsigned)((a.channels + 63) / 64), kVerbCombs), dim3(64), 0, s, a);
+  hipLaunchKernelGGL(k_fx_comb, dim3((unsigned)((a.channels + 63) / 64), kVerbCombs), dim3(64), fx_excl_lds(0), s, a);
 }
 
 void launch_fx_allpass(const FxStageArgs& a, hipStream_t s) {
   if (a.len <= 0) return;
-  hipLaunchKernelGGL(k_fx_allpass, dim3((unsigned)((a.channels + kApCh - 1) / kApCh)), dim3(64 * kApW), 0, s, a);
+  hipLaunchKernelGGL(k_fx_allpass, dim3((unsigned)((a.channels + kApCh - 1) / kApCh)), dim3(64 * kApW),
+                     fx_excl_lds(kApCh * (kApB + 1) * 8), s, a);
 }
 
 }  // namespace adsp

@@ -315,8 +315,11 @@ def test_staged_engine_matches_fused(gpu, case, monkeypatch):
     C, n = 70, 3000
     x = np.stack([0.5 * signals.white_noise(n, 900 + c) * (1 + 0.02 * c) for c in range(C)])
     outs = {}
-    for staged in ("1", "0"):
-        monkeypatch.setenv("AD_FX_STAGED", staged)
+    # "2": staged with the split EQ/detector stage (the default where it
+    # applies), "1": staged, one EQ pipeline per channel group, "0": fused
+    for staged in ("2", "1", "0"):
+        monkeypatch.setenv("AD_FX_STAGED", "0" if staged == "0" else "1")
+        monkeypatch.setenv("AD_FX_EQSPLIT", "0" if staged == "1" else "1")
         monkeypatch.setenv("AD_FX_CHUNK", "256")
         fx = P.EffectChain(C, eq, comp, verb, fs)
         y = x.copy()
@@ -326,19 +329,21 @@ def test_staged_engine_matches_fused(gpu, case, monkeypatch):
             fx.Process(b)
             parts.append(b)
         outs[staged] = (np.concatenate(parts, axis=1), fx)
-    a, b = outs["1"][0], outs["0"][0]
-    assert np.array_equal(a, b), float(np.max(np.abs(a - b)))
+    b = outs["0"][0]
+    for k in ("2", "1"):
+        a = outs[k][0]
+        assert np.array_equal(a, b), (k, float(np.max(np.abs(a - b))))
     if comp is not None:
         from algodsp._lib import lib
         import ctypes as Cc
 
         for c in (0, 33, 69):
             m = []
-            for k in ("1", "0"):
+            for k in ("2", "1", "0"):
                 v = [Cc.c_double() for _ in range(3)]
                 lib().ad_fx_chain_compressor_metrics(outs[k][1]._h, c, *[Cc.byref(t) for t in v])
                 m.append([t.value for t in v])
-            assert m[0] == m[1], (c, m)
+            assert m[0] == m[1] == m[2], (c, m)
 
 
 # ------------------------------------------------------------------ FIR
