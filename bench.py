@@ -386,8 +386,10 @@ def main():
         if tfile.exists():
             try:
                 tab = json.loads(tfile.read_text())
+                # only for the per-GPU workload the PMC passes ran
+                same = tab.get("_config") == {"channels": C, "samples": n, "hop": args.hop}
                 key = next((k for k in tab if k == dom or k.startswith(dom)), None)
-                traffic = tab[key]["hbm_bytes_per_launch"] if key else None
+                traffic = tab[key]["hbm_bytes_per_launch"] if key and same else None
             except Exception:
                 traffic = None
         workload = ("OverlapSave partitioned conv, stereo, 131072-tap IR, full linear convolution "

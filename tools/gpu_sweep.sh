@@ -5,7 +5,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-OUT=gpurun_out/sweep_${TAG:-r01}.jsonl
+OUT=gpurun_out/sweep_${TAG:-r02}.jsonl
 : > $OUT
 CFGS=${SWEEP:-"4096:0:128 8192:0:64"}
 for cfg in $CFGS; do

@@ -1,6 +1,10 @@
 """Per-kernel HBM traffic per launch from rocprofv3 FETCH_SIZE / WRITE_SIZE passes.
 
-Usage: python tools/pmc_traffic.py <prof_dir> > profiles/pmc_traffic.json
+Usage: python tools/pmc_traffic.py <prof_dir> [channels samples hop] > profiles/pmc_traffic.json
+
+The per-GPU workload the passes ran (default: bench.py's N = 1 config, 2
+channels x 2^24 samples, hop 8192) is recorded under "_config"; bench.py
+quotes the traffic only for a run of that same workload.
 
 Corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE on gfx950 reports
 half the bytes of wide (16 B/lane) coalesced streaming reads, so it is
@@ -49,4 +53,6 @@ for k in fetch:
         "launches": len(f),
         "note": "FETCH_SIZE x2 (gfx950 wide-read correction) + WRITE_SIZE, KiB -> bytes",
     }
+cfg = [int(v) for v in sys.argv[2:5]] if len(sys.argv) >= 5 else [2, 1 << 24, 8192]
+out["_config"] = {"channels": cfg[0], "samples": cfg[1], "hop": cfg[2]}
 print(json.dumps(out, indent=1))
