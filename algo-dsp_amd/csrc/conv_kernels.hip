@@ -896,7 +896,7 @@ bool launch_fdl_mac(int PC, int NH, const MacArgs& in, int channels, hipStream_t
   MacArgs a = in;
   const int BW = 32 / NH;
   if (a.M < 2 * BW) return false;  // a pair wave needs M/2 >= BW bins
-  a.nx = a.M / (2 * BW) + 1;        // pair waves + the middle-bin wave
+  a.nx = a.M / (2 * BW) + (a.mid_in_k3 ? 0 : 1);  // pair waves (+ the middle-bin wave)
   if (a.R <= 0) {
     // Auto run length: the fewest runs that still fill every SIMD to its
     // resident-wave limit in ONE round.  A second, partial round leaves a

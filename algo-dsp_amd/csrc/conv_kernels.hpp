@@ -82,6 +82,27 @@ struct MacArgs {
   int R;                // output blocks per wave run (0: auto, one resident round of waves)
   int P;                // partitions
   int M;                // bins 0..M
+  int mid_in_k3;        // 1: no middle-bin wave (K3 computes Z[M/2], MidBin)
+};
+
+// The middle bin M/2 of an output block's Z row, computed by K3 itself
+// (launch_fdl_mac then runs no middle-bin wave: at C channels the K2 grid is
+// 128·C·runs pair waves, which fills the resident slots exactly, where one
+// extra wave per (channel, run) pushed a second round).  Same quantities as
+// K2's middle wave: Y = sum_p X'[g-p] H'[p] over the block-spectrum ring,
+// then the Z fold.  on = 0: Z[M/2] comes from the row (K2 wrote it).
+struct MidBin {
+  int on;
+  const double2* X;     // block-spectrum ring [C][Q+1][MS] (row Q: zeros)
+  int64_t x_ch_stride;
+  int Q;
+  int64_t g0;           // logical block of chunk block 0
+  int64_t gend;         // last logical block holding input
+  const double2* H;     // [n_ir][P][MS] raw partition spectra
+  int64_t h_ir_stride;
+  const int* ir_index;  // [C] (nullable -> c % n_ir)
+  int n_ir;
+  int P;
 };
 
 struct IrfftArgs {
@@ -98,6 +119,7 @@ struct IrfftArgs {
   int accumulate;       // 1: add into out (partitioned stages sharing one accumulator)
   const double2* twM;
   const double2* twN;
+  MidBin mid;
 };
 
 bool launch_window_rfft(int M, const RfftArgs& a, hipStream_t s);

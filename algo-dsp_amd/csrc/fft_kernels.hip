@@ -148,6 +148,53 @@ __global__ __launch_bounds__((FftPlan<M, V>::BLOCK)) void k_irfft_store(IrfftArg
 // real-signal spectrum on load (Zr[k] and Zr[M-k] sit in partner lanes of
 // its pair waves).  Half of K1's pass-0 inputs are the block's zero padding.
 // ---------------------------------------------------------------------------
+// Z[M/2] of output block j of channel c (MidBin; K2's middle-bin wave, in one
+// wave here): lane p takes partition p (and p + 64, ...), forms the window
+// spectrum's middle bin from two block-spectrum rows, separates it and the
+// partition's H the way K2 does for a self-mirrored bin (u = v), multiplies,
+// and the wave sums the products (fixed xor-tree order, so deterministic);
+// then K2's Z fold.  Every lane returns the value.
+template <int M>
+__device__ double2 mid_bin_z(const IrfftArgs& a, int c, int j) {
+  const MidBin& m = a.mid;
+  const int lane = threadIdx.x & 63;
+  const double2 tu = a.twN[M / 2];  // W_2M^(M/2), as K2's unpack
+  const int64_t G = m.g0 + j;       // logical block of this output
+  const double2* Xc = m.X + (int64_t)c * m.x_ch_stride + M / 2;
+  const int ir = m.ir_index ? m.ir_index[c] : (c % m.n_ir);
+  const double2* Hc = m.H + (int64_t)ir * m.h_ir_stride + M / 2;
+  auto row = [&](int64_t g) {
+    const int64_t r = (g < 0 || g > m.gend) ? m.Q : g % m.Q;
+    return Xc[r * a.MS];
+  };
+  // separation of a self-mirrored bin: X' = (fma(W.x, 2a.y, 2a.x), W.y 2a.y)
+  auto unpack = [&](double2 v) {
+    const double sx = v.x + v.x, sy = v.y + v.y;
+    return make_double2(fma(tu.x, sy, sx), tu.y * sy);
+  };
+  double2 t = make_double2(0.0, 0.0);
+  for (int p = lane; p < m.P; p += 64) {
+    const int64_t g = G - p;
+    const double2 pp = row(g - 1), pc = row(g);  // Zr = P[g-1] + (-1)^(M/2) P[g], M/2 even
+    const double2 x = unpack(make_double2(pp.x + pc.x, pp.y + pc.y));
+    const double2 h = unpack(Hc[(int64_t)p * a.MS]);
+    t.x = fma(x.x, h.x, t.x);
+    t.x = fma(-x.y, h.y, t.x);
+    t.y = fma(x.x, h.y, t.y);
+    t.y = fma(x.y, h.x, t.y);
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    t.x += __shfl_xor(t.x, o);
+    t.y += __shfl_xor(t.y, o);
+  }
+  // K2's fold for u = v = Y: Z = (S sx - t.x sy, -t.y sy), t = conj(W) S
+  const double S = 0.125 / (double)M;
+  const double2 te = make_double2(tu.x * S, -tu.y * S);
+  const double sx = t.x + t.x, sy = t.y + t.y;
+  return make_double2(fma(-te.x, sy, sx * S), -te.y * sy);
+}
+
 template <int M>
 struct SplitPlan {
   static constexpr int M2 = M / 2;
@@ -228,6 +275,11 @@ __global__ __launch_bounds__((SplitPlan<M>::T)) __attribute__((amdgpu_waves_per_
     const int k = pass0_index<M2, V>(tid, s);
     av[s] = Zb[zrow_pos(2 * k, M)];
     bv[s] = Zb[zrow_pos(2 * k + 1, M)];
+  }
+  // bin M/2 = 2k at k = M2/2: thread 0, pass-0 slot R0/2
+  if (a.mid.on && tid < 64) {
+    const double2 z = mid_bin_z<M>(a, c, j);
+    if (tid == 0) av[FftPlan<M2, V>::R0 / 2] = z;
   }
   const TwLds<M2> twS = tw_lds_compute<M2>(lds + FftPlan<M2, V>::MP, tid, T);
   const TwLds<M> twC = tw_lds_compute<M>(lds + FftPlan<M2, V>::MP + TwSplit<M2>::N, tid, T);

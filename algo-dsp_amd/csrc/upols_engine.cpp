@@ -255,6 +255,9 @@ void Upols::run(const double* d_in, int64_t in_stride, int64_t n, double* d_out,
     m.P = P_;
     m.M = M_;
     m.twN = tw_.p + M_;
+    // Z[M/2] from K3 (split sizes, few partitions): K2 then runs pair waves only
+    const bool mid_k3 = M_ >= 2048 && P_ <= 256;
+    m.mid_in_k3 = mid_k3 ? 1 : 0;
     prof_begin(s, &e0, 1);
     launch_fdl_mac(PC_, NH_, m, C_, s);
     prof_end(s, e0, 1, blocks * (double)(M_ + 1) * 32 + (double)n_ir_ * P_ * (M_ + 1) * 16);
@@ -273,6 +276,19 @@ void Upols::run(const double* d_in, int64_t in_stride, int64_t n, double* d_out,
     b.accumulate = accumulate ? 1 : 0;
     b.twM = tw_.p;
     b.twN = tw_.p + M_;
+    if (mid_k3) {
+      b.mid.on = 1;
+      b.mid.X = X_.p;
+      b.mid.x_ch_stride = (int64_t)(Q_ + 1) * MS_;
+      b.mid.Q = Q_;
+      b.mid.g0 = m.g0;
+      b.mid.gend = m.gend;
+      b.mid.H = H_.p;
+      b.mid.h_ir_stride = (int64_t)P_ * MS_;
+      b.mid.ir_index = irmap_.p;
+      b.mid.n_ir = n_ir_;
+      b.mid.P = P_;
+    }
     prof_begin(s, &e0, 2);
     launch_irfft_store(M_, b, s);
     prof_end(s, e0, 2, blocks * ((double)(M_ + 1) * 16 + (double)L_ * 8));
