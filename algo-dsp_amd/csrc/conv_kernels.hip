@@ -194,7 +194,7 @@ struct Unpack {
 // mirror pair of Y, t = conj(W_2M^m) * S and S = 1/8M:
 //   Z.x = (u.x + v.x) S - s t.y (u.x - v.x) - t.x (u.y + v.y)
 //   Z.y = s S (u.y - v.y) + s t.x (u.x - v.x) - t.y (u.y + v.y)
-template <int NH>
+template <int NH, bool NTZ = false>
 struct ZEpilogue {
   double2* zb;      // Z row 0 of the channel (wave-uniform)
   unsigned zo;      // this lane's bin position in a row (bin M: the row's padding column M);
@@ -225,7 +225,7 @@ struct ZEpilogue {
     const double2 z = make_double2(fma(-tw.x, sy, fma(-tw.y, sdx, sx * S)), fma(-tw.y, sy, fma(tw.x, sdx, S * sdy)));
     double2* zp = (zb + j * jstride) + zo;
     if constexpr (FIRST) {
-      *zp = z;
+      st2<NTZ>(zp, z);
     } else {
       const double2 o = *zp;
       *zp = make_double2(o.x + z.x, o.y + z.y);
@@ -472,7 +472,8 @@ template <int PC, int NH>
 struct MacOccL {
   static constexpr int W = PC <= 8 ? 4 : 3;
 };
-template <int PC, int NH, bool FIRST, int DL>
+// NTZ (AD_K2_NT=1): non-temporal Z stores.
+template <int PC, int NH, bool FIRST, int DL, bool NTZ = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MacOccL<PC, NH>::W))) void k_fdl_mac_lds(MacArgs a) {
   static_assert(DL <= 16 && PC % DL == 0, "ring depth: slots must repeat every group");
   __shared__ double2 ring[DL * 64];
@@ -506,7 +507,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MacOccL<PC, 
   Unpack<NH> up;
   up.m = mi ? (int)0x80000000u : 0;
   up.tw = (k < a.M) ? a.twN[k] : make_double2(-1.0, 0.0);
-  ZEpilogue<NH> epi;
+  ZEpilogue<NH, NTZ> epi;
   epi.S = 0.125 / (double)a.M;
   epi.m = up.m;
   const int zpos = zrow_pos(k, a.M);
@@ -847,11 +848,21 @@ int mac_lds_depth() {
   return d;
 }
 
+int mac_nt() {
+  static const int v = [] {
+    const char* e = std::getenv("AD_K2_NT");
+    return e ? std::atoi(e) : 0;
+  }();
+  return v;
+}
+
 template <int PC, int NH, int DL>
 void mac_go_l(const MacArgs& a, dim3 grid, hipStream_t s) {
   MacArgs c = a;
   for (c.p0 = 0; c.p0 < a.P; c.p0 += NH * PC) {
-    if (c.p0 == 0)
+    if (c.p0 == 0 && mac_nt() == 1)
+      timed_launch(k_fdl_mac_lds<PC, NH, true, DL, true>, grid, dim3(64), s, c);
+    else if (c.p0 == 0)
       timed_launch(k_fdl_mac_lds<PC, NH, true, DL>, grid, dim3(64), s, c);
     else
       timed_launch(k_fdl_mac_lds<PC, NH, false, DL>, grid, dim3(64), s, c);

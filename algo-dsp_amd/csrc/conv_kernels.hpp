@@ -9,16 +9,20 @@
 namespace adsp {
 
 // Position of bin q (0..M) in a Z row (k_fdl_mac output, K3 input), M >= 64.
-// Wave-lane order: the bins of K2's pair wave bx, 32bx + l and their mirrors
-// M - (32bx + l), sit at 64bx + l and 64bx + 32 + l, so every K2 row store is
-// one aligned 1-KiB line run per wave (a partial 128-B line shared by two
-// waves would reach HBM as a read-modify-write); bin M/2 sits at M, and bin M
-// (only a separation partner) at 32, which K3 never reads.
+// Wave-lane order, parity split: the bins of K2's pair wave bx, 32bx + l, sit
+// at 64bx + 16(l & 1) + (l >> 1), and their mirrors M - (32bx + l) at 32 more,
+// so every K2 row store is one aligned 1-KiB line run per wave (a partial
+// 128-B line shared by two waves would reach HBM as a read-modify-write).
+// K3's split transform reads the even bins (A) and the odd bins (B) as two
+// separate streams: with even and odd bins in separate 256-B runs, each of
+// its load instructions covers whole lines, so all of A can be requested
+// before B and A's transform starts while B is in flight.  Bin M/2 sits at M,
+// and bin M (only a separation partner) at 32, which K3 never reads.
 __host__ __device__ inline int zrow_pos(int q, int M) {
-  if (q < M / 2) return ((q >> 5) << 6) + (q & 31);
   if (q == M / 2) return M;
-  const int d = M - q;
-  return ((d >> 5) << 6) + 32 + (d & 31);
+  const bool mir = q > M / 2;
+  const int d = mir ? M - q : q;
+  return ((d >> 5) << 6) + (mir ? 32 : 0) + ((d & 1) << 4) + ((d & 31) >> 1);
 }
 
 // Kernel timing of the engine launchers: when start/stop are set (Upols

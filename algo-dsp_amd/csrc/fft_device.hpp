@@ -32,6 +32,26 @@ struct cplx {
   double x, y;
 };
 
+// Non-temporal 16-byte load/store (streams touched once: nt keeps them from
+// displacing lines another kernel is about to reuse).
+typedef double d2v_t __attribute__((ext_vector_type(2)));
+template <bool NT>
+__device__ __forceinline__ double2 ld2(const double2* p) {
+  if constexpr (NT) {
+    const d2v_t t = __builtin_nontemporal_load(reinterpret_cast<const d2v_t*>(p));
+    return make_double2(t.x, t.y);
+  } else {
+    return *p;
+  }
+}
+template <bool NT>
+__device__ __forceinline__ void st2(double2* p, double2 v) {
+  if constexpr (NT)
+    __builtin_nontemporal_store(d2v_t{v.x, v.y}, reinterpret_cast<d2v_t*>(p));
+  else
+    *p = v;
+}
+
 __device__ __forceinline__ double2 c_add(double2 a, double2 b) { return make_double2(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ double2 c_sub(double2 a, double2 b) { return make_double2(a.x - b.x, a.y - b.y); }
 __device__ __forceinline__ double2 c_mul(double2 a, double2 b) {

@@ -154,30 +154,56 @@ __global__ __launch_bounds__((FftPlan<M, V>::BLOCK)) void k_irfft_store(IrfftArg
 // partition's H the way K2 does for a self-mirrored bin (u = v), multiplies,
 // and the wave sums the products (fixed xor-tree order, so deterministic);
 // then K2's Z fold.  Every lane returns the value.
+// Split in two so that the loads of the first partitions (p = lane) go out
+// ahead of the item's Z loads: mid_bin_issue loads them, mid_bin_z (after
+// the Z loads are issued) waits for those alone -- vmcnt retires in order --
+// and finishes; partitions p >= 64 (P > 64) are loaded and summed there.
+struct MidLoads {
+  double2 pp, pc, h;  // P[g-1], P[g], H[p] of partition p = lane (zeros past P)
+};
 template <int M>
-__device__ double2 mid_bin_z(const IrfftArgs& a, int c, int j) {
-  const MidBin& m = a.mid;
+struct MidRows {
+  const double2* Xc;
+  const double2* Hc;
+  int64_t G;     // logical block of this output
+  int64_t gend;  // last logical block holding input
+  int Q, P, MS;
+  __device__ __forceinline__ MidRows(const IrfftArgs& a, int c, int j)
+      : G(a.mid.g0 + j), gend(a.mid.gend), Q(a.mid.Q), P(a.mid.P), MS(a.MS) {
+    Xc = a.mid.X + (int64_t)c * a.mid.x_ch_stride + M / 2;
+    const int ir = a.mid.ir_index ? a.mid.ir_index[c] : (c % a.mid.n_ir);
+    Hc = a.mid.H + (int64_t)ir * a.mid.h_ir_stride + M / 2;
+  }
+  __device__ __forceinline__ double2 row(int64_t g) const {
+    const int64_t r = (g < 0 || g > gend) ? Q : g % Q;
+    return Xc[r * MS];
+  }
+  __device__ __forceinline__ MidLoads load(int p) const {
+    if (p >= P) return MidLoads{make_double2(0, 0), make_double2(0, 0), make_double2(0, 0)};
+    const int64_t g = G - p;
+    return MidLoads{row(g - 1), row(g), Hc[(int64_t)p * MS]};
+  }
+};
+template <int M>
+__device__ __forceinline__ MidLoads mid_bin_issue(const IrfftArgs& a, int c, int j) {
+  return MidRows<M>(a, c, j).load(threadIdx.x & 63);
+}
+template <int M>
+__device__ double2 mid_bin_z(const IrfftArgs& a, int c, int j, MidLoads first) {
   const int lane = threadIdx.x & 63;
   const double2 tu = a.twN[M / 2];  // W_2M^(M/2), as K2's unpack
-  const int64_t G = m.g0 + j;       // logical block of this output
-  const double2* Xc = m.X + (int64_t)c * m.x_ch_stride + M / 2;
-  const int ir = m.ir_index ? m.ir_index[c] : (c % m.n_ir);
-  const double2* Hc = m.H + (int64_t)ir * m.h_ir_stride + M / 2;
-  auto row = [&](int64_t g) {
-    const int64_t r = (g < 0 || g > m.gend) ? m.Q : g % m.Q;
-    return Xc[r * a.MS];
-  };
+  const MidRows<M> rows(a, c, j);
   // separation of a self-mirrored bin: X' = (fma(W.x, 2a.y, 2a.x), W.y 2a.y)
   auto unpack = [&](double2 v) {
     const double sx = v.x + v.x, sy = v.y + v.y;
     return make_double2(fma(tu.x, sy, sx), tu.y * sy);
   };
   double2 t = make_double2(0.0, 0.0);
-  for (int p = lane; p < m.P; p += 64) {
-    const int64_t g = G - p;
-    const double2 pp = row(g - 1), pc = row(g);  // Zr = P[g-1] + (-1)^(M/2) P[g], M/2 even
-    const double2 x = unpack(make_double2(pp.x + pc.x, pp.y + pc.y));
-    const double2 h = unpack(Hc[(int64_t)p * a.MS]);
+  for (int p = lane; p < rows.P; p += 64) {
+    const MidLoads ld = p == lane ? first : rows.load(p);
+    // Zr = P[g-1] + (-1)^(M/2) P[g], M/2 even
+    const double2 x = unpack(make_double2(ld.pp.x + ld.pc.x, ld.pp.y + ld.pc.y));
+    const double2 h = unpack(ld.h);
     t.x = fma(x.x, h.x, t.x);
     t.x = fma(-x.y, h.y, t.x);
     t.y = fma(x.x, h.y, t.y);
@@ -204,7 +230,8 @@ struct SplitPlan {
   static constexpr int LDS = Sub::MP + TwSplit<M2>::N + TwSplit<M>::N;  // double2 elements
 };
 
-template <int M>
+// NTF (AD_K1_NT): bit 0 non-temporal input loads, bit 1 non-temporal spectrum stores.
+template <int M, int NTF = 0>
 __global__ __launch_bounds__((SplitPlan<M>::T)) __attribute__((amdgpu_waves_per_eu(4))) void k_window_rfft_split(RfftArgs a) {
   using SP = SplitPlan<M>;
   constexpr int M2 = SP::M2, V = SP::V, T = SP::T, L = M;
@@ -224,11 +251,11 @@ __global__ __launch_bounds__((SplitPlan<M>::T)) __attribute__((amdgpu_waves_per_
     // E's inputs first: its transform starts while O's are still in flight
 #pragma unroll
     for (int s = 0; s < V; ++s)
-      ev[s] = (s % R0 < R0 / 2) ? *reinterpret_cast<const double2*>(xc + t0 + 4 * pass0_index<M2, V>(tid, s))
+      ev[s] = (s % R0 < R0 / 2) ? ld2<NTF & 1>(reinterpret_cast<const double2*>(xc + t0 + 4 * pass0_index<M2, V>(tid, s)))
                                 : make_double2(0.0, 0.0);
 #pragma unroll
     for (int s = 0; s < V; ++s)
-      ov[s] = (s % R0 < R0 / 2) ? *reinterpret_cast<const double2*>(xc + t0 + 4 * pass0_index<M2, V>(tid, s) + 2)
+      ov[s] = (s % R0 < R0 / 2) ? ld2<NTF & 1>(reinterpret_cast<const double2*>(xc + t0 + 4 * pass0_index<M2, V>(tid, s) + 2))
                                 : make_double2(0.0, 0.0);
   } else {
 #pragma unroll
@@ -250,12 +277,16 @@ __global__ __launch_bounds__((SplitPlan<M>::T)) __attribute__((amdgpu_waves_per_
   for (int s = 0; s < V; ++s) {
     const int k = last_pass_index<M2, V>(tid, s);
     const double2 wo = c_mul(twC(k), ov[s]);
-    Xo[k] = c_add(ev[s], wo);
-    Xo[k + M2] = c_sub(ev[s], wo);
+    st2<(NTF & 2) != 0>(Xo + k, c_add(ev[s], wo));
+    st2<(NTF & 2) != 0>(Xo + k + M2, c_sub(ev[s], wo));
   }
 }
 
-template <int M>
+// EXP (diagnostics, AD_K3_EXP; results are wrong for EXP != 0): 1 loads and
+// stores only, 2 transforms and stores without loads, 3 loads and transforms
+// without stores.
+// NTF (AD_K3_NT): bit 0 non-temporal Z loads, bit 1 non-temporal output stores.
+template <int M, int EXP = 0, int NTF = 0>
 __global__ __launch_bounds__((SplitPlan<M>::T)) __attribute__((amdgpu_waves_per_eu(4))) void k_irfft_store_split(IrfftArgs a) {
   using SP = SplitPlan<M>;
   constexpr int M2 = SP::M2, V = SP::V, T = SP::T, L = M;
@@ -268,25 +299,32 @@ __global__ __launch_bounds__((SplitPlan<M>::T)) __attribute__((amdgpu_waves_per_
   const int j = __builtin_amdgcn_readfirstlane(e - c * a.jc);
   const double2* Zb = a.Y + (int64_t)c * a.y_ch_stride + (int64_t)j * a.MS;
   double2 av[V], bv[V];
-  // bins 2k, 2k+1 in wave-lane row order (zrow_pos): one 32-byte pair per
-  // lane and s (loading all of A first measured slower: half-line requests)
+  // wave 0: the middle bin's first partition loads, ahead of the Z loads
+  const bool mid = a.mid.on && tid < 64;
+  MidLoads ml{};
+  if (mid) ml = mid_bin_issue<M>(a, c, j);
+  // all of A (even bins), then all of B (odd bins): zrow_pos keeps each
+  // stream in whole lines, so A's transform starts while B is in flight
 #pragma unroll
-  for (int s = 0; s < V; ++s) {
-    const int k = pass0_index<M2, V>(tid, s);
-    av[s] = Zb[zrow_pos(2 * k, M)];
-    bv[s] = Zb[zrow_pos(2 * k + 1, M)];
-  }
+  for (int s = 0; s < V; ++s)
+    av[s] = EXP == 2 ? make_double2(tid * 1e-3, s) : ld2<NTF & 1>(Zb + zrow_pos(2 * pass0_index<M2, V>(tid, s), M));
+  __builtin_amdgcn_sched_barrier(0);  // keep B's loads behind A's
+#pragma unroll
+  for (int s = 0; s < V; ++s)
+    bv[s] = EXP == 2 ? make_double2(s, tid * 1e-3) : ld2<NTF & 1>(Zb + zrow_pos(2 * pass0_index<M2, V>(tid, s) + 1, M));
   // bin M/2 = 2k at k = M2/2: thread 0, pass-0 slot R0/2
-  if (a.mid.on && tid < 64) {
-    const double2 z = mid_bin_z<M>(a, c, j);
+  if (mid) {
+    const double2 z = mid_bin_z<M>(a, c, j, ml);
     if (tid == 0) av[FftPlan<M2, V>::R0 / 2] = z;
   }
   const TwLds<M2> twS = tw_lds_compute<M2>(lds + FftPlan<M2, V>::MP, tid, T);
   const TwLds<M> twC = tw_lds_compute<M>(lds + FftPlan<M2, V>::MP + TwSplit<M2>::N, tid, T);
   __syncthreads();  // twiddle tables
-  fft_run<M2, V, false>(av, tid, lds, twS);
-  __syncthreads();
-  fft_run<M2, V, false>(bv, tid, lds, twS);
+  if constexpr (EXP != 1) {
+    fft_run<M2, V, false>(av, tid, lds, twS);
+    __syncthreads();
+    fft_run<M2, V, false>(bv, tid, lds, twS);
+  }
   const int64_t ob = a.o0 + (int64_t)j * L;  // output of time index M/2 + m is at ob + 2m
   double* yb = a.out + (int64_t)c * a.out_stride + ob;
 #pragma unroll
@@ -294,11 +332,17 @@ __global__ __launch_bounds__((SplitPlan<M>::T)) __attribute__((amdgpu_waves_per_
     const int m = last_pass_index<M2, V>(tid, s);
     av[s] = c_sub(av[s], c_mul(c_conj(twC(m)), bv[s]));
   }
+  if constexpr (EXP == 3) {
+    bool odd = false;
+#pragma unroll
+    for (int s = 0; s < V; ++s) odd |= av[s].x == 1.2345e300;
+    if (!odd) return;
+  }
   if (a.aligned && ob + 2 * M2 <= a.out_len) {  // wave-uniform fast paths
     if (!a.accumulate) {
 #pragma unroll
       for (int s = 0; s < V; ++s)
-        *reinterpret_cast<double2*>(yb + 2 * last_pass_index<M2, V>(tid, s)) = av[s];
+        st2<(NTF & 2) != 0>(reinterpret_cast<double2*>(yb + 2 * last_pass_index<M2, V>(tid, s)), av[s]);
     } else {
 #pragma unroll
       for (int s = 0; s < V; ++s) {
@@ -323,6 +367,25 @@ __global__ __launch_bounds__((SplitPlan<M>::T)) __attribute__((amdgpu_waves_per_
 // ---------------------------------------------------------------------------
 namespace {
 
+int env_knob(const char* name, int dflt = 0) {
+  const char* e = std::getenv(name);
+  return e ? std::atoi(e) : dflt;
+}
+int k3_exp() {
+  static const int v = env_knob("AD_K3_EXP");
+  return v;
+}
+// K3 default: non-temporal Z loads and output stores (both streams are
+// touched once; A/B on one box: step -1 ... -2.6 %, K3 187 -> 152-157 us, part
+// of which reappears in the next kernel as deferred write-back).
+int k3_nt() {
+  static const int v = env_knob("AD_K3_NT", 3);
+  return v;
+}
+int k1_nt() {
+  static const int v = env_knob("AD_K1_NT");
+  return v;
+}
 template <int M, int V>
 void rfft_go(const RfftArgs& a, hipStream_t s) {
   using Plan = FftPlan<M, V>;
@@ -337,7 +400,16 @@ void rfft_go(const RfftArgs& a, hipStream_t s) {
 template <int M>
 void rfft_split_go(const RfftArgs& a, hipStream_t s) {
   const int64_t items = (int64_t)a.channels * a.jc;
-  timed_launch(k_window_rfft_split<M>, dim3((unsigned)items), dim3(SplitPlan<M>::T), s, a);
+  const dim3 g((unsigned)items), b(SplitPlan<M>::T);
+  if constexpr (M == 8192) {
+    switch (k1_nt()) {
+      case 1: return timed_launch(k_window_rfft_split<M, 1>, g, b, s, a);
+      case 2: return timed_launch(k_window_rfft_split<M, 2>, g, b, s, a);
+      case 3: return timed_launch(k_window_rfft_split<M, 3>, g, b, s, a);
+      default: break;
+    }
+  }
+  timed_launch(k_window_rfft_split<M>, g, b, s, a);
 }
 template <int M, int V>
 void irfft_go(const IrfftArgs& a, hipStream_t s) {
@@ -348,7 +420,21 @@ void irfft_go(const IrfftArgs& a, hipStream_t s) {
 template <int M>
 void irfft_split_go(const IrfftArgs& a, hipStream_t s) {
   const int64_t items = (int64_t)a.channels * a.jc;
-  timed_launch(k_irfft_store_split<M>, dim3((unsigned)items), dim3(SplitPlan<M>::T), s, a);
+  const dim3 g((unsigned)items), b(SplitPlan<M>::T);
+  if constexpr (M == 8192) {
+    switch (k3_exp()) {
+      case 1: return timed_launch(k_irfft_store_split<M, 1>, g, b, s, a);
+      case 2: return timed_launch(k_irfft_store_split<M, 2>, g, b, s, a);
+      case 3: return timed_launch(k_irfft_store_split<M, 3>, g, b, s, a);
+      default: break;
+    }
+  }
+  switch (k3_nt()) {
+    case 1: return timed_launch(k_irfft_store_split<M, 0, 1>, g, b, s, a);
+    case 2: return timed_launch(k_irfft_store_split<M, 0, 2>, g, b, s, a);
+    case 3: return timed_launch(k_irfft_store_split<M, 0, 3>, g, b, s, a);
+    default: return timed_launch(k_irfft_store_split<M>, g, b, s, a);
+  }
 }
 
 }  // namespace
