@@ -305,8 +305,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MacOcc<PC, N
   const int j1 = min(j0 + a.R, a.jc);
   const int ir = a.ir_index ? a.ir_index[c] : (c % a.n_ir);
   const int kz = k & (a.M - 1);  // raw spectrum index: bin M reads Zr[0]
-  const double2* Hc = a.H + (int64_t)ir * a.h_ir_stride + kz;
-  const double2* Xc = a.X + (int64_t)c * a.x_ch_stride + kz;
+  const double2* Hc = a.H + (int64_t)ir * a.h_ir_stride + xrow_pos(kz, a.M);
+  const double2* Xc = a.X + (int64_t)c * a.x_ch_stride + xrow_pos(kz, a.M);
   const double sgn = mi ? -1.0 : 1.0;
   Unpack<NH> up;
   up.m = mi ? (int)0x80000000u : 0;
@@ -501,8 +501,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MacOccL<PC, 
   const int j1 = min(j0 + a.R, a.jc);
   const int ir = a.ir_index ? a.ir_index[c] : (c % a.n_ir);
   const int kz = k & (a.M - 1);
-  const double2* Hc = a.H + (int64_t)ir * a.h_ir_stride + kz;
-  const double2* Xc = a.X + (int64_t)c * a.x_ch_stride + kz;
+  const double2* Hc = a.H + (int64_t)ir * a.h_ir_stride + xrow_pos(kz, a.M);
+  const double2* Xc = a.X + (int64_t)c * a.x_ch_stride + xrow_pos(kz, a.M);
   const double sgn = mi ? -1.0 : 1.0;
   Unpack<NH> up;
   up.m = mi ? (int)0x80000000u : 0;

@@ -25,6 +25,18 @@ __host__ __device__ inline int zrow_pos(int q, int M) {
   return ((d >> 5) << 6) + (mir ? 32 : 0) + ((d & 1) << 4) + ((d & 31) >> 1);
 }
 
+// Position of raw bin q (0..M-1) in a block-spectrum row (K1 output: the X
+// ring and the partition spectra H; K2 and K3's middle bin read it).  A K2
+// pair wave bx reads bins 32bx + l (l < 32) and their mirrors M - (32bx + l),
+// i.e. the runs [32bx, 32bx + 31] and [M - 32bx - 31, M - 32bx]: in natural
+// order the mirror run starts 16 B past a 128-B line and touches five lines
+// for four lines of data.  Bins above M/2 therefore sit one slot lower
+// (q - 1), which puts every mirror run on line boundaries, and bin M/2 moves
+// to the padding column M.  K1's row stores stay contiguous.
+__host__ __device__ inline int xrow_pos(int q, int M) {
+  return q < M / 2 ? q : (q == M / 2 ? M : q - 1);
+}
+
 // Kernel timing of the engine launchers: when start/stop are set (Upols
 // profiling), the launch carries them in its dispatch packet
 // (hipExtLaunchKernelGGL), so the recorded interval is the kernel's own

@@ -99,7 +99,7 @@ __global__ __launch_bounds__((FftPlan<M, V>::BLOCK)) void k_window_rfft(RfftArgs
   if (!active) return;
   double2* Xo = a.X + (int64_t)c * a.x_ch_stride + (int64_t)((a.slot0 + j) % a.Q) * a.MS;
 #pragma unroll
-  for (int s = 0; s < V; ++s) Xo[last_pass_index<M, V>(tid, s)] = v[s];
+  for (int s = 0; s < V; ++s) Xo[xrow_pos(last_pass_index<M, V>(tid, s), M)] = v[s];
 }
 
 template <int M, int V>
@@ -170,9 +170,9 @@ struct MidRows {
   int Q, P, MS;
   __device__ __forceinline__ MidRows(const IrfftArgs& a, int c, int j)
       : G(a.mid.g0 + j), gend(a.mid.gend), Q(a.mid.Q), P(a.mid.P), MS(a.MS) {
-    Xc = a.mid.X + (int64_t)c * a.mid.x_ch_stride + M / 2;
+    Xc = a.mid.X + (int64_t)c * a.mid.x_ch_stride + xrow_pos(M / 2, M);
     const int ir = a.mid.ir_index ? a.mid.ir_index[c] : (c % a.mid.n_ir);
-    Hc = a.mid.H + (int64_t)ir * a.mid.h_ir_stride + M / 2;
+    Hc = a.mid.H + (int64_t)ir * a.mid.h_ir_stride + xrow_pos(M / 2, M);
   }
   __device__ __forceinline__ double2 row(int64_t g) const {
     const int64_t r = (g < 0 || g > gend) ? Q : g % Q;
@@ -277,8 +277,8 @@ __global__ __launch_bounds__((SplitPlan<M>::T)) __attribute__((amdgpu_waves_per_
   for (int s = 0; s < V; ++s) {
     const int k = last_pass_index<M2, V>(tid, s);
     const double2 wo = c_mul(twC(k), ov[s]);
-    st2<(NTF & 2) != 0>(Xo + k, c_add(ev[s], wo));
-    st2<(NTF & 2) != 0>(Xo + k + M2, c_sub(ev[s], wo));
+    st2<(NTF & 2) != 0>(Xo + k, c_add(ev[s], wo));  // k < M/2: xrow_pos(k) = k
+    st2<(NTF & 2) != 0>(Xo + xrow_pos(k + M2, M), c_sub(ev[s], wo));
   }
 }
 
