@@ -375,12 +375,15 @@ int k3_exp() {
   static const int v = env_knob("AD_K3_EXP");
   return v;
 }
-// K3 default: non-temporal Z loads and output stores (both streams are
-// touched once; A/B on one box: step -1 ... -2.6 %, K3 187 -> 152-157 us, part
-// of which reappears in the next kernel as deferred write-back).
-int k3_nt() {
-  static const int v = env_knob("AD_K3_NT", 3);
-  return v;
+// K3 default for launches of two or more resident rounds (>= 1024 items):
+// non-temporal Z loads and output stores (both streams are touched once; A/B
+// on one box: step -1 ... -2.6 %, K3 187 -> 152-157 us, part of which
+// reappears in the next kernel as deferred write-back).  Small launches (a
+// streaming block, a host-pipeline segment) keep the cached path: their Z
+// rows were just written by K2 and their output is read back right after.
+int k3_nt(int64_t items) {
+  static const int v = env_knob("AD_K3_NT", -1);
+  return v >= 0 ? v : (items >= 1024 ? 3 : 0);
 }
 int k1_nt() {
   static const int v = env_knob("AD_K1_NT");
@@ -429,7 +432,7 @@ void irfft_split_go(const IrfftArgs& a, hipStream_t s) {
       default: break;
     }
   }
-  switch (k3_nt()) {
+  switch (k3_nt(items)) {
     case 1: return timed_launch(k_irfft_store_split<M, 0, 1>, g, b, s, a);
     case 2: return timed_launch(k_irfft_store_split<M, 0, 2>, g, b, s, a);
     case 3: return timed_launch(k_irfft_store_split<M, 0, 3>, g, b, s, a);
