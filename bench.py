@@ -472,6 +472,16 @@ def main_stream(args):
     for i in range(nblk):
         s.ProcessBlockTo(y[i * B:(i + 1) * B], x[i * B:(i + 1) * B])
     dt = time.perf_counter() - t0
+    # parity: the measured output's first blocks against exact float64 dot
+    # products (numpy) of the same input (zero history before block 0)
+    nchk = min(nblk, 4) * B
+    ref = np.convolve(x[:nchk], ir)[:nchk]
+    err = y[:nchk] - ref
+    parity = {"rms": float(np.sqrt(np.mean(err ** 2))), "max_abs": float(np.max(np.abs(err))),
+              "outputs_checked": int(nchk), "against": "exact float64 convolution (numpy) of the first blocks",
+              "tolerance_rms": 1e-7}
+    if parity["rms"] > 1e-7:
+        print(f"bench.py: PARITY FAILURE {parity}", file=sys.stderr)
     cpu = None
     if not args.no_cpu_baseline:
         sys.path.insert(0, str(ROOT / "tests"))
@@ -494,6 +504,7 @@ def main_stream(args):
         "config": {"workload": "StreamingOverlapSave mono K=16384 B=4096, host buffers, one block per step",
                    "block": B, "kernel_taps": 16384},
         "note": "latency-bound: each block = H2D copy + 3 kernels + D2H copy + sync",
+        "parity": parity,
         "cpu_baseline": cpu,
     }
     print(json.dumps(line), flush=True)
