@@ -43,6 +43,12 @@ def child():
         for _ in range(6):
             e.Process(xbt)
         out[name + " Msamples/s"] = round(6 * len(xbt) / (time.perf_counter() - t0) / 1e6, 1)
+        yb = np.empty(len(xbt) + len(k16) - 1)
+        e.ProcessTo(yb, xbt)
+        t0 = time.perf_counter()
+        for _ in range(6):
+            e.ProcessTo(yb, xbt)
+        out[name + " ProcessTo Msamples/s"] = round(6 * len(xbt) / (time.perf_counter() - t0) / 1e6, 1)
     print(json.dumps(out))
 
 
