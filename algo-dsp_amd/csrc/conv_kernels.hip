@@ -307,7 +307,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MacOcc<PC, N
   const int kz = k & (a.M - 1);  // raw spectrum index: bin M reads Zr[0]
   const double2* Hc = a.H + (int64_t)ir * a.h_ir_stride + xrow_pos(kz, a.M);
   const double2* Xc = a.X + (int64_t)c * a.x_ch_stride + xrow_pos(kz, a.M);
-  const double sgn = mi ? -1.0 : 1.0;
   Unpack<NH> up;
   up.m = mi ? (int)0x80000000u : 0;
   up.tw = (k < a.M) ? a.twN[k] : make_double2(-1.0, 0.0);
@@ -503,7 +502,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MacOccL<PC, 
   const int kz = k & (a.M - 1);
   const double2* Hc = a.H + (int64_t)ir * a.h_ir_stride + xrow_pos(kz, a.M);
   const double2* Xc = a.X + (int64_t)c * a.x_ch_stride + xrow_pos(kz, a.M);
-  const double sgn = mi ? -1.0 : 1.0;
   Unpack<NH> up;
   up.m = mi ? (int)0x80000000u : 0;
   up.tw = (k < a.M) ? a.twN[k] : make_double2(-1.0, 0.0);
@@ -561,6 +559,82 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MacOccL<PC, 
   }
   // drain the tail DMAs before the wave (and its LDS) retires
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// ---------------------------------------------------------------------------
+// K2 for calls of one or two output blocks per channel (a streaming block, a
+// partitioned stage firing once): one wave per (channel, output block, bin
+// group), all P partitions in one launch.  The run-based kernels above keep
+// PC partitions of H in VGPRs to reuse them over a run of R outputs; with a
+// single output there is no reuse, so this form streams H and X rows
+// instead: no H registers, no rotating accumulators, so many more waves (and
+// loads) per SIMD, and no second launch with a Z read-modify-write when
+// P > 16.  Bit-identical to k_fdl_mac_lds: the same products in the same
+// order -- per chunk of PC partitions p descending, each chunk folded to Z,
+// the chunks' Z summed in launch order -- so a call gives the same outputs
+// whichever form ran.
+// ---------------------------------------------------------------------------
+template <int PC>
+__global__ __launch_bounds__(256) void k_fdl_mac_row(MacArgs a) {
+  const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (w >= a.ny) return;  // ny = waves in this launch (set by the launcher)
+  const int lane = threadIdx.x & 63;
+  const int bx = w % a.nx;
+  const int t = w / a.nx;
+  const int j = t % a.jc;
+  const int c = t / a.jc;
+  const bool mi = lane >> 5;
+  const int l = lane & 31;
+  const bool paired = bx < a.M / 64;
+  const int k = paired ? (mi ? a.M - (bx * 32 + l) : bx * 32 + l) : a.M / 2;
+  const int ir = a.ir_index ? a.ir_index[c] : (c % a.n_ir);
+  const int kz = k & (a.M - 1);
+  const double2* Hc = a.H + (int64_t)ir * a.h_ir_stride + xrow_pos(kz, a.M);
+  const double2* Xc = a.X + (int64_t)c * a.x_ch_stride + xrow_pos(kz, a.M);
+  Unpack<1> up;
+  up.m = mi ? (int)0x80000000u : 0;
+  up.tw = (k < a.M) ? a.twN[k] : make_double2(-1.0, 0.0);
+  ZEpilogue<1> epi;
+  epi.S = 0.125 / (double)a.M;
+  epi.m = up.m;
+  epi.zb = a.Y + (int64_t)c * a.y_ch_stride;
+  epi.zo = (unsigned)zrow_pos(k, a.M);
+  epi.jstride = a.MS;
+  epi.tw = (k < a.M) ? c_scale(c_conj(a.twN[k]), epi.S) : make_double2(0.0, 0.0);
+  const int smask = (kz & 1) ? (int)0x80000000u : 0;
+  const int64_t G = a.g0 + j;  // logical block of this output
+  auto row = [&](int64_t g) {  // block-spectrum row of logical block g (zero row outside the signal)
+    const int64_t r = (g < 0 || g > a.gend) ? a.Q : g % a.Q;
+    return Xc[r * a.MS];
+  };
+  double2 zt = make_double2(0.0, 0.0);
+  for (int p0 = 0; p0 < a.P; p0 += PC) {
+    double2 xr[PC + 1], h[PC];
+    // rows G - p0 - PC .. G - p0 (oldest first) and H[p0 .. p0 + PC)
+#pragma unroll
+    for (int u = 0; u <= PC; ++u) xr[u] = row(G - p0 - PC + u);
+#pragma unroll
+    for (int q = 0; q < PC; ++q) h[q] = Hc[(int64_t)min(p0 + q, a.P - 1) * a.MS];
+    double2 acc = make_double2(0.0, 0.0);
+#pragma unroll
+    for (int u = 1; u <= PC; ++u) {  // window G - p, p = p0 + PC - u (descending)
+      const double2 pp = xr[u - 1], pc = xr[u];
+      const double2 x = up(make_double2(pp.x + flip(pc.x, smask), pp.y + flip(pc.y, smask)));
+      const int q = PC - u;
+      double2 hq = up(h[q]);
+      if (p0 + q >= a.P) hq = make_double2(0.0, 0.0);
+      cmac(acc, x, hq);
+    }
+    // the epilogue's fold, summed over the chunks as the RMW launches do
+    double2 u2, v2;
+    xpair<true>(acc, u2, v2);
+    const double sx = u2.x + v2.x, sy = u2.y + v2.y;
+    const double sdx = flip(u2.x - v2.x, epi.m), sdy = flip(u2.y - v2.y, epi.m);
+    const double2 z = make_double2(fma(-epi.tw.x, sy, fma(-epi.tw.y, sdx, sx * epi.S)),
+                                   fma(-epi.tw.y, sy, fma(epi.tw.x, sdx, epi.S * sdy)));
+    zt = p0 == 0 ? z : make_double2(zt.x + z.x, zt.y + z.y);
+  }
+  epi.zb[(int64_t)j * epi.jstride + epi.zo] = zt;
 }
 
 // ---------------------------------------------------------------------------
@@ -908,6 +982,23 @@ bool launch_fdl_mac(int PC, int NH, const MacArgs& in, int channels, hipStream_t
   const int BW = 32 / NH;
   if (a.M < 2 * BW) return false;  // a pair wave needs M/2 >= BW bins
   a.nx = a.M / (2 * BW) + (a.mid_in_k3 ? 0 : 1);  // pair waves (+ the middle-bin wave)
+  static const bool row_form = [] {  // AD_MAC_ROW=0: run-based kernels for every call
+    const char* v = std::getenv("AD_MAC_ROW");
+    return !(v && v[0] == '0');
+  }();
+  if (NH == 1 && a.jc <= 2 && row_form) {
+    const int64_t waves = (int64_t)channels * a.nx * a.jc;
+    a.ny = (int)waves;
+    const dim3 grid((unsigned)((waves + 3) / 4)), blk(256);
+    switch (PC) {
+      case 1: timed_launch(k_fdl_mac_row<1>, grid, blk, s, a); return true;
+      case 2: timed_launch(k_fdl_mac_row<2>, grid, blk, s, a); return true;
+      case 4: timed_launch(k_fdl_mac_row<4>, grid, blk, s, a); return true;
+      case 8: timed_launch(k_fdl_mac_row<8>, grid, blk, s, a); return true;
+      case 16: timed_launch(k_fdl_mac_row<16>, grid, blk, s, a); return true;
+      default: return false;
+    }
+  }
   if (a.R <= 0) {
     // Auto run length: the fewest runs that still fill every SIMD to its
     // resident-wave limit in ONE round.  A second, partial round leaves a

@@ -516,6 +516,24 @@ def test_multi_stream_vs_oracle(gpu, K, B):
         s.ProcessBlock(x[:4, :B])
 
 
+@pytest.mark.parametrize("K,B", [(131072, 4096), (16384, 8192), (3000, 1024), (40000, 2048)])
+def test_stream_blocks_bit_identical_to_offline(gpu, K, B):
+    """A streaming call (one output block per channel: K2's single-row form,
+    k_fdl_mac_row, all partitions in one launch) gives bit for bit what the
+    offline engine at the same hop gives (the run-based K2, one launch per
+    chunk of 16 partitions with a Z read-modify-write when P > 16): the same
+    products in the same order.  P = 32, 2, 3 and 20."""
+    irs = irlib.large_church()[:, :K]
+    ir_index = [0, 1, 0]
+    C_, nb = 3, 6
+    n = nb * B
+    x = np.stack([signals.white_noise(n, 90 + c) for c in range(C_)])
+    s = conv.MultiChannelStreamingConvolver(irs, B, C_, ir_index=ir_index)
+    got = np.concatenate([s.ProcessBlock(x[:, i * B:(i + 1) * B]) for i in range(nb)], axis=1)
+    want, _ = _multi_run(irs, x, hop=B, ir_index=ir_index)
+    assert np.array_equal(got, want[:, :n])
+
+
 @pytest.mark.parametrize("K,lo,hi", [(95432, 7, 13), (1000, 6, 13), (20000, 10, 11), (5000, 13, 13)])
 def test_partitioned_multi_vs_oracle(gpu, K, lo, hi):
     """ad_conv_pc_multi_* (many-channel, device-resident partitioned engine):
