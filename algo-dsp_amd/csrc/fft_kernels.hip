@@ -136,7 +136,8 @@ __global__ __launch_bounds__((FftPlan<M, V>::BLOCK)) void k_irfft_store(IrfftArg
 //       E = FFT(z[2m]), O = FFT(z[2m+1]), z[m] = x[2m] + i x[2m+1];
 //   K3: z[M/2+m] = A[m] - W_M^-m B[m] (only the upper half is kept),
 //       A = IFFT(Z[2k]), B = IFFT(Z[2k+1]); k_fdl_mac stores Z rows in
-//       wave-lane order (zrow_pos), where bins 2k and 2k+1 are neighbours.
+//       wave-lane order with even and odd bins in separate 256-B runs
+//       (zrow_pos), so A and B are two whole-line load streams.
 // Each thread's E/O inputs are 32 contiguous bytes, and its outputs of
 // both halves are the same last-pass indices, so the radix-2 step needs no
 // exchange.  The LDS image is that of an M/2 transform (69.6 KiB at M = 8192),
