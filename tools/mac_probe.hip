@@ -8,6 +8,7 @@
 //   2: workgroups of 4 waves (bin groups 4g..4g+3 of one run) with a barrier
 //      per row, so a workgroup reads two 2-KiB runs per row together
 //   3: shape 0 without the stores (read side alone)
+//   4: shape 0 with Z stored transposed ([bin group][row]: contiguous per wave)
 //   hipcc --offload-arch=gfx950 -O3 tools/mac_probe.hip -o tools/mac_probe
 #include <hip/hip_runtime.h>
 
@@ -59,7 +60,10 @@ __global__ __launch_bounds__(64 * WPG) void k_probe(Args a) {
       ring[d] = Xc[(r0 + r + d + 8) * MS + off];
       acc.x += v.x;
       acc.y += v.y;
-      if (SHAPE != 3) Zc[(r0 + r + d) * MS + 64 * bx + lane] = acc;
+      if (SHAPE == 4)  // transposed Z: [bin group][row], each wave a contiguous stream
+        Zc[((long)bx * rows_per_ch + r0 + r + d) * 64 + lane] = acc;
+      else if (SHAPE != 3)
+        Zc[(r0 + r + d) * MS + 64 * bx + lane] = acc;
       if (SHAPE == 2) __syncthreads();
     }
   }
@@ -104,6 +108,7 @@ int main() {
   run<1, 1>("shape 1: 1 KiB per wave-row", a);
   run<2, 4>("shape 2: 4-wave lockstep, 2 x 2 KiB per WG-row", a);
   run<3, 1>("shape 3: shape 0 reads only", a);
+  run<4, 1>("shape 4: shape 0 with transposed Z writes", a);
   run<0, 1>("shape 0 again", a);
   return 0;
 }
