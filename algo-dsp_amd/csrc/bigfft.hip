@@ -60,15 +60,29 @@ __global__ __launch_bounds__((PassShape<R, FW>::BLOCK)) void k_fft_pass(FftPassA
 #pragma unroll
   for (int s = 0; s < V; ++s) v[s] = lds[lds_slot(pass0_index<R, V>(tid, s))];
   if (a.Ns > 1) {  // pre-twiddle W_{Ns R}^{(j mod Ns) r} = W_N^{(j mod Ns) r N/(Ns R)}
+    // With u = W_N^{(j mod Ns) N/(Ns R)}, slot s holds r = tid + T k_s, where
+    // k_s = b + r0 V/R0 (pass0_index) runs over 0..V-1: w_s = u^tid (u^T)^k_s.
+    // Two table lookups per thread and a power recurrence in registers, not
+    // one lookup pair per value (the lookups are L2 round trips after the
+    // staging loads); <= V roundings, far inside the 1e-10 parity bars.
     const int64_t jm = j & (a.Ns - 1);
     const int64_t step = a.N / (a.Ns * R);
     const int64_t mask = ((int64_t)1 << a.S) - 1;
+    auto tw = [&](int64_t e) {
+      e &= a.N - 1;
+      return c_mul(a.tw_lo[e & mask], a.tw_hi[e >> a.S]);
+    };
+    double2 base = tw(jm * step * tid);  // u^tid
+    const double2 cT = tw(jm * step * T);  // u^T
+    if (!FWD) base = c_conj(base);
+    const double2 c = FWD ? cT : c_conj(cT);
+    constexpr int R0 = Plan::R0;
 #pragma unroll
-    for (int s = 0; s < V; ++s) {
-      const int64_t e = jm * pass0_index<R, V>(tid, s) * step;
-      double2 w = c_mul(a.tw_lo[e & mask], a.tw_hi[e >> a.S]);
-      if (!FWD) w = c_conj(w);
-      v[s] = c_mul(v[s], w);
+    for (int k = 0; k < V; ++k) {  // base = u^tid (u^T)^k
+#pragma unroll
+      for (int s = 0; s < V; ++s)
+        if ((s / R0) + (s % R0) * (V / R0) == k) v[s] = c_mul(v[s], base);
+      if (k + 1 < V) base = c_mul(base, c);
     }
   }
   __syncthreads();
