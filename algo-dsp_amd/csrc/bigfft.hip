@@ -11,6 +11,14 @@
 
 namespace adsp {
 
+// Go complex128 product (a*b as (ac - bd, ad + bc), no contraction): the
+// correlation's pointwise step, also fused into the inverse's first pass.
+#pragma clang fp contract(off)
+__device__ __forceinline__ double2 go_cmul(double2 a, double2 b) {
+  return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+#pragma clang fp contract(fast)  // the HIP default again for the transforms below
+
 // ---------------------------------------------------------------------------
 // One global Stockham pass of radix R (16 <= R <= 4096): F = BLOCK*16/R
 // butterflies per workgroup.
@@ -43,10 +51,10 @@ __global__ __launch_bounds__((PassShape<R, FW>::BLOCK)) void k_fft_pass(FftPassA
     if (j < nb) {
       const int64_t g = j + (int64_t)r * nb;
       if constexpr (REALIN) {
-        const double* x = a.xr + bt * a.in_batch;
-        v.x = g < a.n_real ? x[g] : 0.0;
+        v.x = g < a.nr[bt] ? a.xb[bt][g] : 0.0;
       } else {
         v = a.in[bt * a.in_batch + g];
+        if (a.in_conj) v = go_cmul(v, c_conj(a.in_conj[g]));
       }
     }
     lds_all[jj * MP + lds_slot(r)] = v;
@@ -109,10 +117,18 @@ __global__ __launch_bounds__((PassShape<R, FW>::BLOCK)) void k_fft_pass(FftPassA
     if (jo >= nb) continue;
     const double2 val = lds_all[jj * MP + lds_slot(rr)];
     const int64_t o = (jo & ~(Ns - 1)) * R + (jo & (Ns - 1)) + (int64_t)rr * Ns;
-    if constexpr (REALOUT)
-      a.out_real[bt * a.out_batch + o] = val.x * a.scale;
-    else
+    if constexpr (REALOUT) {
+      if (a.remap) {
+        if (o < a.n_front)
+          a.out_real[a.front_off + o] = val.x * a.scale;
+        else if (o >= a.back_from)
+          a.out_real[o - a.back_from] = val.x * a.scale;
+      } else {
+        a.out_real[bt * a.out_batch + o] = val.x * a.scale;
+      }
+    } else {
       a.out[bt * a.out_batch + o] = val;
+    }
   }
 }
 
@@ -253,7 +269,42 @@ void BigFft::run(bool forward, const double2* in, const double* xr, int64_t n_re
   a.tw_hi = tw_hi_;
   a.S = S_;
   a.scale = scale;
-  if (radix_.empty()) {  // N <= 8
+  for (int b = 0; b < 2; ++b) {
+    a.xb[b] = xr ? xr + b * in_batch : nullptr;
+    a.nr[b] = n_real;
+  }
+  run_passes(forward, a, in, xr, in_batch, out, out_real, out_batch, batch, scratch, s);
+}
+
+void BigFft::correlate(const double* a_, int64_t n, const double* b_, int64_t m, double2* spec, double* out,
+                       double2* scratch, hipStream_t s) const {
+  FftPassArgs a{};
+  a.N = N_;
+  a.tw_lo = tw_lo_;
+  a.tw_hi = tw_hi_;
+  a.S = S_;
+  a.scale = 1.0;
+  a.xb[0] = a_;
+  a.nr[0] = n;
+  a.xb[1] = b_;
+  a.nr[1] = m;
+  run_passes(true, a, nullptr, a_, 0, spec, nullptr, N_, 2, scratch, s);
+  FftPassArgs i = a;
+  i.scale = 1.0 / (double)N_;
+  i.in_conj = spec + N_;  // the first inverse pass loads spec[0] * conj(spec[1])
+  i.remap = 1;
+  i.n_front = n;  // lags 0..n-1 from the front, -(m-1)..-1 from the back (correlate.go:165-171)
+  i.front_off = m - 1;
+  i.back_from = N_ - m + 1;
+  run_passes(false, i, spec, nullptr, N_, nullptr, out, 0, 1, scratch, s);
+}
+
+void BigFft::run_passes(bool forward, FftPassArgs a, const double2* in, const double* xr, int64_t in_batch,
+                        double2* out, double* out_real, int64_t out_batch, int batch, double2* scratch,
+                        hipStream_t s) const {
+  const int64_t n_real = a.nr[0];
+  const double2* in_conj = a.in_conj;  // first pass only
+  if (radix_.empty()) {  // N <= 8 (no fused edges: callers check fused_ok())
     a.in = in;
     a.xr = xr;
     a.n_real = n_real;
@@ -275,6 +326,7 @@ void BigFft::run(bool forward, const double2* in, const double* xr, int64_t n_re
     const int R = radix_[(size_t)p];
     const bool first = p == 0, last = p == P - 1;
     a.in = first ? in : cur;
+    a.in_conj = first ? in_conj : nullptr;
     a.xr = first ? xr : nullptr;
     a.n_real = n_real;
     a.in_batch = first ? in_batch : N_;
@@ -302,9 +354,6 @@ void BigFft::run(bool forward, const double2* in, const double* xr, int64_t n_re
 // complex128div (Smith's algorithm), magnitudes by math.Hypot.
 // ---------------------------------------------------------------------------
 #pragma clang fp contract(off)
-__device__ __forceinline__ double2 go_cmul(double2 a, double2 b) {
-  return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
-}
 __device__ __forceinline__ double2 go_cdiv(double2 n, double2 m) {
   double e, f;
   if (fabs(m.x) >= fabs(m.y)) {

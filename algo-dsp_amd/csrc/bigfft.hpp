@@ -37,6 +37,16 @@ struct FftPassArgs {
   const double2* tw_lo; // W_N^e, e < 2^S          (pre-twiddles W_N^e = lo[e & (2^S-1)] * hi[e >> S])
   const double2* tw_hi; // W_N^(e 2^S), e < N/2^S
   int S;
+  // Fused edges (CorrelateFFT): per-batch real inputs (first pass, zero past
+  // nr[b]: no staging buffer), the product with conj(in_conj) on the first
+  // pass's load, and the last pass's real output scattered to the caller's
+  // lag order (o < n_front -> out_real[front_off + o], o >= back_from ->
+  // out_real[o - back_from], the rest dropped).
+  const double* xb[2];
+  int64_t nr[2];
+  const double2* in_conj;
+  int remap;
+  int64_t n_front, front_off, back_from;
 };
 
 // Device-resident plan and twiddle tables of one size.
@@ -54,6 +64,13 @@ class BigFft {
   // scratch: N*batch complex; in/out may alias each other and scratch must not.
   void run(bool forward, const double2* in, const double* xr, int64_t n_real, int64_t in_batch, double2* out,
            double* out_real, int64_t out_batch, double scale, int batch, double2* scratch, hipStream_t s) const;
+  // CorrelateFFT's transforms with their edges fused (FftPassArgs): forward
+  // of a (n) and b (m), zero padded, straight from the caller's arrays into
+  // spec [2][N]; then the inverse of spec[0] * conj(spec[1]), written in lag
+  // order to out (n + m - 1 values, correlate.go:165-171).
+  void correlate(const double* a, int64_t n, const double* b, int64_t m, double2* spec, double* out,
+                 double2* scratch, hipStream_t s) const;
+  bool fused_ok() const { return !radix_.empty(); }  // N > 8 (the naive DFT has no fused edges)
 
  private:
   int64_t N_;
@@ -62,6 +79,8 @@ class BigFft {
   std::vector<double2*> twR_;  // per pass
   double2* tw_lo_ = nullptr;
   double2* tw_hi_ = nullptr;
+  void run_passes(bool forward, FftPassArgs a, const double2* in, const double* xr, int64_t in_batch, double2* out,
+                  double* out_real, int64_t out_batch, int batch, double2* scratch, hipStream_t s) const;
 };
 
 // Pointwise spectral operations (contraction off: Go complex128 arithmetic).

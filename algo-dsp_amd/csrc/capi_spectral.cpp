@@ -116,6 +116,20 @@ int ad_correlate_fft(const double* a, int64_t n, const double* b, int64_t m, dou
     hipStream_t s = nullptr;
     const int64_t N = next_pow2(n + m - 1);  // correlate.go:119
     SpectralRun run(dc, N);
+    if (run.fft->fused_ok()) {
+      // a and b to the device unpadded, the fused transforms (see the device
+      // form below), the n + m - 1 lags back in one copy
+      dc.xr.reserve((size_t)(n + m));
+      dc.res.reserve((size_t)(n + m - 1));
+      dc.spec.reserve((size_t)(2 * N));
+      dc.scratch.reserve((size_t)(4 * N));
+      AD_HIP(hipMemcpyAsync(dc.xr.p, a, (size_t)n * sizeof(double), hipMemcpyHostToDevice, s));
+      AD_HIP(hipMemcpyAsync(dc.xr.p + n, b, (size_t)m * sizeof(double), hipMemcpyHostToDevice, s));
+      run.fft->correlate(dc.xr.p, n, dc.xr.p + n, m, dc.spec.p, dc.res.p, dc.scratch.p, s);
+      AD_HIP(hipMemcpyAsync(out, dc.res.p, (size_t)(n + m - 1) * sizeof(double), hipMemcpyDeviceToHost, s));
+      AD_HIP(hipStreamSynchronize(s));
+      return;
+    }
     const double* src[2] = {a, b};
     const int64_t len[2] = {n, m};
     stage_real(dc.xr, N, src, len, 2, s);
@@ -143,6 +157,14 @@ int ad_correlate_fft_device(const double* a, int64_t n, const double* b, int64_t
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const int64_t N = next_pow2(n + m - 1);
     SpectralRun run(dc, N);
+    if (run.fft->fused_ok()) {
+      // transforms straight from the caller's arrays, the product fused into
+      // the inverse's first pass and the lag reordering into its last
+      dc.spec.reserve((size_t)(2 * N));
+      dc.scratch.reserve((size_t)(4 * N));
+      run.fft->correlate(a, n, b, m, dc.spec.p, out, dc.scratch.p, s);
+      return;
+    }
     dc.xr.reserve((size_t)(2 * N));
     AD_HIP(hipMemsetAsync(dc.xr.p, 0, (size_t)(2 * N) * sizeof(double), s));
     AD_HIP(hipMemcpyAsync(dc.xr.p, a, (size_t)n * sizeof(double), hipMemcpyDeviceToDevice, s));

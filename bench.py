@@ -546,14 +546,15 @@ def main_corr(args):
     dt = time.perf_counter() - t0
     ms = e0.elapsed_time(e1) / args.steps
     N = 1 << (2 * n - 2).bit_length()
-    # algorithmic bytes per call: staging (memset + 2 copies), forward passes
-    # (batch 2: real in 8 B, complex 16 B), A*conj(B), inverse passes (real out),
-    # output copies -- see DESIGN.md "spectral row"
+    # algorithmic bytes per call (DESIGN.md "spectral row"): forward passes of
+    # both inputs (the first reads the n + m real samples, zero padding is not
+    # read, and writes 16 B per bin), the inverse's first pass reading both
+    # spectra (A * conj(B) fused), its last pass writing the n + m - 1 kept lags
     from algodsp.conv import _fft_pass_count
     P = _fft_pass_count(N)
-    fwd = 2 * N * (8 + 16) + 2 * N * 32 * (P - 1)
-    inv = N * 32 * (P - 1) + N * (16 + 8)
-    alg = 2 * N * 8 + 2 * n * 16 + fwd + N * 48 + inv + (2 * n - 1) * 16
+    fwd = 2 * n * 8 + 2 * N * 16 + 2 * N * 32 * (P - 1)
+    inv = N * 32 + (2 * n - 1) * 8 if P == 1 else N * 48 + N * 32 * (P - 2) + N * 16 + (2 * n - 1) * 8
+    alg = fwd + inv
     gbs = alg / (ms * 1e-3) / 1e9
     cpu = None
     if not args.no_cpu_baseline:
@@ -576,7 +577,7 @@ def main_corr(args):
                    "fft_size": N},
         "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
-                     "note": "whole call: algorithmic bytes of all passes, pointwise op and copies / event time"},
+                     "note": "whole call: algorithmic bytes of all passes (pointwise op and lag order fused) / event time"},
         "cpu_baseline": cpu,
         "wall_ms_per_step": round(dt / args.steps * 1e3, 4),
     }

@@ -45,6 +45,29 @@ def test_correlate_fft_matches_oracle(gpu, n, m):
     close(conv.CorrelateFFT(a, b), O.correlate_fft(a, b))
 
 
+@pytest.mark.parametrize("n,m", [(3, 3), (5, 3), (1000, 37), (40000, 25000), (1 << 17, 3)])
+def test_correlate_fft_device_matches_host(gpu, n, m):
+    """ad_correlate_fft_device (device arrays on the caller's stream; the
+    product and the lag order fused into the transforms' passes) against the
+    host-buffer entry point, bit for bit, and against the oracle."""
+    import ctypes as C
+
+    import torch
+
+    from algodsp._lib import check, lib
+
+    a, b = signals.white_noise(n, 5 + n), signals.white_noise(m, 9 + m)
+    da, db = torch.from_numpy(a).cuda(), torch.from_numpy(b).cuda()
+    dout = torch.full((n + m - 1,), np.nan, dtype=torch.float64, device="cuda")
+    st = torch.cuda.current_stream()
+    check(lib().ad_correlate_fft_device(C.c_void_p(da.data_ptr()), n, C.c_void_p(db.data_ptr()), m,
+                                        C.c_void_p(dout.data_ptr()), 0, C.c_void_p(st.cuda_stream)))
+    st.synchronize()
+    got = dout.cpu().numpy()
+    assert np.array_equal(got, conv.CorrelateFFT(a, b))
+    close(got, O.correlate_fft(a, b))
+
+
 def test_correlate_fft_empty(gpu):
     with pytest.raises(conv.ErrEmptyInput):
         conv.CorrelateFFT([], [1.0, 2.0])
