@@ -243,7 +243,13 @@ BigFft::BigFft(int64_t N) : N_(N) {
     radix_.push_back((int)N);
     S_ = (k + 1) / 2;
   } else {
-    const int np = (k + 8) / 9;
+    // passes of radix <= 2^maxlog (AD_FFT_LOGR, A/B knob; 9 = radix 512)
+    static const int maxlog = [] {
+      const char* e = std::getenv("AD_FFT_LOGR");
+      const int v = e ? std::atoi(e) : 9;
+      return v >= 4 && v <= 9 ? v : 9;
+    }();
+    const int np = (k + maxlog - 1) / maxlog;
     const int base = k / np, extra = k % np;
     for (int p = 0; p < np; ++p) radix_.push_back(1 << (base + (p < extra ? 1 : 0)));
     S_ = (k + 1) / 2;
