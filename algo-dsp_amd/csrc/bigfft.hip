@@ -51,7 +51,18 @@ __global__ __launch_bounds__((PassShape<R, FW>::BLOCK)) void k_fft_pass(FftPassA
     if (j < nb) {
       const int64_t g = j + (int64_t)r * nb;
       if constexpr (REALIN) {
-        v.x = g < a.nr[bt] ? a.xb[bt][g] : 0.0;
+        if (a.pack2) {
+          v.x = g < a.nr[0] ? a.xb[0][g] : 0.0;
+          v.y = g < a.nr[1] ? a.xb[1][g] : 0.0;
+        } else {
+          v.x = g < a.nr[bt] ? a.xb[bt][g] : 0.0;
+        }
+      } else if (a.unpack2) {
+        const double2 zk = a.in[g], zm = a.in[(a.N - g) & (a.N - 1)];
+        const double2 sp = make_double2(zk.x + zm.x, zk.y - zm.y);  // Z[k] + conj Z[-k] = 2 A[k]
+        const double2 dm = make_double2(zk.x - zm.x, zk.y + zm.y);  // Z[k] - conj Z[-k] = 2i B[k]
+        const double2 t = go_cmul(sp, c_conj(dm));
+        v = make_double2(-0.25 * t.y, 0.25 * t.x);  // A conj(B) = (i/4) sp conj(dm)
       } else {
         v = a.in[bt * a.in_batch + g];
         if (a.in_conj) v = go_cmul(v, c_conj(a.in_conj[g]));
@@ -294,10 +305,13 @@ void BigFft::correlate(const double* a_, int64_t n, const double* b_, int64_t m,
   a.nr[0] = n;
   a.xb[1] = b_;
   a.nr[1] = m;
-  run_passes(true, a, nullptr, a_, 0, spec, nullptr, N_, 2, scratch, s);
+  // both real signals in one complex transform, Z = FFT(a + i b)
+  a.pack2 = 1;
+  run_passes(true, a, nullptr, a_, 0, spec, nullptr, N_, 1, scratch, s);
   FftPassArgs i = a;
+  i.pack2 = 0;
   i.scale = 1.0 / (double)N_;
-  i.in_conj = spec + N_;  // the first inverse pass loads spec[0] * conj(spec[1])
+  i.unpack2 = 1;  // the first inverse pass separates A and B from Z's mirror pairs and loads A conj(B)
   i.remap = 1;
   i.n_front = n;  // lags 0..n-1 from the front, -(m-1)..-1 from the back (correlate.go:165-171)
   i.front_off = m - 1;
@@ -310,6 +324,7 @@ void BigFft::run_passes(bool forward, FftPassArgs a, const double2* in, const do
                         hipStream_t s) const {
   const int64_t n_real = a.nr[0];
   const double2* in_conj = a.in_conj;  // first pass only
+  const int pack2 = a.pack2, unpack2 = a.unpack2;
   if (radix_.empty()) {  // N <= 8 (no fused edges: callers check fused_ok())
     a.in = in;
     a.xr = xr;
@@ -333,6 +348,8 @@ void BigFft::run_passes(bool forward, FftPassArgs a, const double2* in, const do
     const bool first = p == 0, last = p == P - 1;
     a.in = first ? in : cur;
     a.in_conj = first ? in_conj : nullptr;
+    a.pack2 = first ? pack2 : 0;
+    a.unpack2 = first ? unpack2 : 0;
     a.xr = first ? xr : nullptr;
     a.n_real = n_real;
     a.in_batch = first ? in_batch : N_;

@@ -45,6 +45,8 @@ struct FftPassArgs {
   const double* xb[2];
   int64_t nr[2];
   const double2* in_conj;
+  int pack2;    // first forward pass: one complex input xb[0] + i xb[1] (both real signals in one transform)
+  int unpack2;  // first inverse pass: Z = FFT(a + i b) -> A conj(B) = (i/4) (Z[k] + conj Z[-k]) conj(Z[k] - conj Z[-k])
   int remap;
   int64_t n_front, front_off, back_from;
 };

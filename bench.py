@@ -546,14 +546,15 @@ def main_corr(args):
     dt = time.perf_counter() - t0
     ms = e0.elapsed_time(e1) / args.steps
     N = 1 << (2 * n - 2).bit_length()
-    # algorithmic bytes per call (DESIGN.md "spectral row"): forward passes of
-    # both inputs (the first reads the n + m real samples, zero padding is not
-    # read, and writes 16 B per bin), the inverse's first pass reading both
-    # spectra (A * conj(B) fused), its last pass writing the n + m - 1 kept lags
+    # algorithmic bytes per call (DESIGN.md "spectral row"): one forward
+    # transform of a + i b (the first pass reads the n + m real samples, zero
+    # padding is not read, and writes 16 B per bin), the inverse's first pass
+    # reading Z once (A conj(B) from Z's mirror pairs; the mirror re-read is
+    # not counted), its last pass writing the n + m - 1 kept lags
     from algodsp.conv import _fft_pass_count
     P = _fft_pass_count(N)
-    fwd = 2 * n * 8 + 2 * N * 16 + 2 * N * 32 * (P - 1)
-    inv = N * 32 + (2 * n - 1) * 8 if P == 1 else N * 48 + N * 32 * (P - 2) + N * 16 + (2 * n - 1) * 8
+    fwd = 2 * n * 8 + N * 16 + N * 32 * (P - 1)
+    inv = N * 16 + (2 * n - 1) * 8 if P == 1 else N * 32 * (P - 1) + N * 16 + (2 * n - 1) * 8
     alg = fwd + inv
     gbs = alg / (ms * 1e-3) / 1e9
     cpu = None
