@@ -57,15 +57,24 @@ __global__ __launch_bounds__((PassShape<R, FW>::BLOCK)) void k_fft_pass(FftPassA
         } else {
           v.x = g < a.nr[bt] ? a.xb[bt][g] : 0.0;
         }
-      } else if (a.unpack2) {
-        const double2 zk = a.in[g], zm = a.in[(a.N - g) & (a.N - 1)];
-        const double2 sp = make_double2(zk.x + zm.x, zk.y - zm.y);  // Z[k] + conj Z[-k] = 2 A[k]
-        const double2 dm = make_double2(zk.x - zm.x, zk.y + zm.y);  // Z[k] - conj Z[-k] = 2i B[k]
-        const double2 t = go_cmul(sp, c_conj(dm));
-        v = make_double2(-0.25 * t.y, 0.25 * t.x);  // A conj(B) = (i/4) sp conj(dm)
+      } else if (a.half) {
+        // X[q] = A[q] conj(B[q]) from the forward spectrum Z = FFT(a + i b)
+        const int64_t NF = a.NF, msk = NF - 1;
+        auto xq = [&](int64_t q) {
+          const double2 zk = a.in[q], zm = a.in[(NF - q) & msk];
+          const double2 sp = make_double2(zk.x + zm.x, zk.y - zm.y);
+          const double2 dm = make_double2(zk.x - zm.x, zk.y + zm.y);
+          const double2 t = go_cmul(sp, c_conj(dm));
+          return make_double2(-0.25 * t.y, 0.25 * t.x);
+        };
+        const double2 x1 = xq(g), x2 = xq(g + NF / 2);
+        const int64_t fm = ((int64_t)1 << a.fS) - 1;
+        const double2 w = c_conj(c_mul(a.ftw_lo[g & fm], a.ftw_hi[g >> a.fS]));  // W_NF^-g
+        const double2 e = make_double2(0.5 * (x1.x + x2.x), 0.5 * (x1.y + x2.y));
+        const double2 o = c_mul(make_double2(0.5 * (x1.x - x2.x), 0.5 * (x1.y - x2.y)), w);
+        v = make_double2(e.x - o.y, e.y + o.x);
       } else {
         v = a.in[bt * a.in_batch + g];
-        if (a.in_conj) v = go_cmul(v, c_conj(a.in_conj[g]));
       }
     }
     lds_all[jj * MP + lds_slot(r)] = v;
@@ -129,13 +138,21 @@ __global__ __launch_bounds__((PassShape<R, FW>::BLOCK)) void k_fft_pass(FftPassA
     const double2 val = lds_all[jj * MP + lds_slot(rr)];
     const int64_t o = (jo & ~(Ns - 1)) * R + (jo & (Ns - 1)) + (int64_t)rr * Ns;
     if constexpr (REALOUT) {
-      if (a.remap) {
-        if (o < a.n_front)
-          a.out_real[a.front_off + o] = val.x * a.scale;
-        else if (o >= a.back_from)
-          a.out_real[o - a.back_from] = val.x * a.scale;
+      auto emit = [&](int64_t q, double x) {
+        if (a.remap) {
+          if (q < a.n_front)
+            a.out_real[a.front_off + q] = x * a.scale;
+          else if (q >= a.back_from)
+            a.out_real[q - a.back_from] = x * a.scale;
+        } else {
+          a.out_real[bt * a.out_batch + q] = x * a.scale;
+        }
+      };
+      if (a.pairs) {
+        emit(2 * o, val.x);
+        emit(2 * o + 1, val.y);
       } else {
-        a.out_real[bt * a.out_batch + o] = val.x * a.scale;
+        emit(o, val.x);
       }
     } else {
       a.out[bt * a.out_batch + o] = val;
@@ -293,8 +310,8 @@ void BigFft::run(bool forward, const double2* in, const double* xr, int64_t n_re
   run_passes(forward, a, in, xr, in_batch, out, out_real, out_batch, batch, scratch, s);
 }
 
-void BigFft::correlate(const double* a_, int64_t n, const double* b_, int64_t m, double2* spec, double* out,
-                       double2* scratch, hipStream_t s) const {
+void BigFft::correlate_half(const BigFft& half, const double* a_, int64_t n, const double* b_, int64_t m,
+                            double2* spec, double* out, double2* scratch, hipStream_t s) const {
   FftPassArgs a{};
   a.N = N_;
   a.tw_lo = tw_lo_;
@@ -305,26 +322,31 @@ void BigFft::correlate(const double* a_, int64_t n, const double* b_, int64_t m,
   a.nr[0] = n;
   a.xb[1] = b_;
   a.nr[1] = m;
-  // both real signals in one complex transform, Z = FFT(a + i b)
-  a.pack2 = 1;
+  a.pack2 = 1;  // Z = FFT(a + i b)
   run_passes(true, a, nullptr, a_, 0, spec, nullptr, N_, 1, scratch, s);
-  FftPassArgs i = a;
-  i.pack2 = 0;
-  i.scale = 1.0 / (double)N_;
-  i.unpack2 = 1;  // the first inverse pass separates A and B from Z's mirror pairs and loads A conj(B)
+  FftPassArgs i{};
+  i.N = half.N_;
+  i.tw_lo = half.tw_lo_;
+  i.tw_hi = half.tw_hi_;
+  i.S = half.S_;
+  i.scale = 1.0 / (double)half.N_;
+  i.half = 1;
+  i.NF = N_;
+  i.ftw_lo = tw_lo_;
+  i.ftw_hi = tw_hi_;
+  i.fS = S_;
   i.remap = 1;
   i.n_front = n;  // lags 0..n-1 from the front, -(m-1)..-1 from the back (correlate.go:165-171)
   i.front_off = m - 1;
   i.back_from = N_ - m + 1;
-  run_passes(false, i, spec, nullptr, N_, nullptr, out, 0, 1, scratch, s);
+  half.run_passes(false, i, spec, nullptr, half.N_, nullptr, out, 0, 1, scratch, s);
 }
 
 void BigFft::run_passes(bool forward, FftPassArgs a, const double2* in, const double* xr, int64_t in_batch,
                         double2* out, double* out_real, int64_t out_batch, int batch, double2* scratch,
                         hipStream_t s) const {
   const int64_t n_real = a.nr[0];
-  const double2* in_conj = a.in_conj;  // first pass only
-  const int pack2 = a.pack2, unpack2 = a.unpack2;
+  const int pack2 = a.pack2, halfz = a.half;  // first / last pass only
   if (radix_.empty()) {  // N <= 8 (no fused edges: callers check fused_ok())
     a.in = in;
     a.xr = xr;
@@ -347,9 +369,9 @@ void BigFft::run_passes(bool forward, FftPassArgs a, const double2* in, const do
     const int R = radix_[(size_t)p];
     const bool first = p == 0, last = p == P - 1;
     a.in = first ? in : cur;
-    a.in_conj = first ? in_conj : nullptr;
     a.pack2 = first ? pack2 : 0;
-    a.unpack2 = first ? unpack2 : 0;
+    a.half = first ? halfz : 0;
+    a.pairs = last ? halfz : 0;
     a.xr = first ? xr : nullptr;
     a.n_real = n_real;
     a.in_batch = first ? in_batch : N_;

@@ -38,15 +38,23 @@ struct FftPassArgs {
   const double2* tw_hi; // W_N^(e 2^S), e < N/2^S
   int S;
   // Fused edges (CorrelateFFT): per-batch real inputs (first pass, zero past
-  // nr[b]: no staging buffer), the product with conj(in_conj) on the first
-  // pass's load, and the last pass's real output scattered to the caller's
-  // lag order (o < n_front -> out_real[front_off + o], o >= back_from ->
-  // out_real[o - back_from], the rest dropped).
+  // nr[b]: no staging buffer), and the last pass's real output scattered to
+  // the caller's lag order (o < n_front -> out_real[front_off + o],
+  // o >= back_from -> out_real[o - back_from], the rest dropped).
   const double* xb[2];
   int64_t nr[2];
-  const double2* in_conj;
   int pack2;    // first forward pass: one complex input xb[0] + i xb[1] (both real signals in one transform)
-  int unpack2;  // first inverse pass: Z = FFT(a + i b) -> A conj(B) = (i/4) (Z[k] + conj Z[-k]) conj(Z[k] - conj Z[-k])
+  // half: the inverse of the Hermitian A conj(B) as an N/2-point transform
+  // (this plan is N/2 = NF/2): its first pass forms z[k] = E[k] + i O[k] from
+  // X[k] and X[k + NF/2] (E = (X[k] + X[k+NF/2])/2, O = (X[k] - X[k+NF/2]) W_NF^-k / 2,
+  // X from the forward spectrum's mirror pairs), its last pass writes Re z[m]
+  // and Im z[m] as the real outputs 2m and 2m + 1.
+  int half;   // first pass: form z from the spectrum
+  int pairs;  // last pass: write Re z[m], Im z[m] as real outputs 2m, 2m + 1
+  int64_t NF;
+  const double2* ftw_lo;  // W_NF tables of the full-size plan
+  const double2* ftw_hi;
+  int fS;
   int remap;
   int64_t n_front, front_off, back_from;
 };
@@ -66,13 +74,13 @@ class BigFft {
   // scratch: N*batch complex; in/out may alias each other and scratch must not.
   void run(bool forward, const double2* in, const double* xr, int64_t n_real, int64_t in_batch, double2* out,
            double* out_real, int64_t out_batch, double scale, int batch, double2* scratch, hipStream_t s) const;
-  // CorrelateFFT's transforms with their edges fused (FftPassArgs): forward
-  // of a (n) and b (m), zero padded, straight from the caller's arrays into
-  // spec [2][N]; then the inverse of spec[0] * conj(spec[1]), written in lag
-  // order to out (n + m - 1 values, correlate.go:165-171).
-  void correlate(const double* a, int64_t n, const double* b, int64_t m, double2* spec, double* out,
-                 double2* scratch, hipStream_t s) const;
-  bool fused_ok() const { return !radix_.empty(); }  // N > 8 (the naive DFT has no fused edges)
+  // CorrelateFFT with its edges fused (FftPassArgs): one forward transform of
+  // a + i b (n and m real samples, zero padded, read straight from the
+  // caller's arrays) into spec [N]; then the inverse of the Hermitian
+  // A conj(B) on the half plan (N/2 points), written in lag order to out
+  // (n + m - 1 values, correlate.go:165-171).  Both plans need passes (N >= 32).
+  void correlate_half(const BigFft& half, const double* a, int64_t n, const double* b, int64_t m, double2* spec,
+                      double* out, double2* scratch, hipStream_t s) const;
 
  private:
   int64_t N_;

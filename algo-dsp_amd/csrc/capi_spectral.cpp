@@ -76,6 +76,17 @@ struct SpectralRun {
     dc.res.reserve((size_t)N);
     fft->run(false, dc.spec.p, nullptr, 0, N, nullptr, dc.res.p, N, 1.0 / (double)N, 1, dc.scratch.p, s);
   }
+  // CorrelateFFT with fused edges: one forward transform of a + i b, the
+  // inverse of the Hermitian product at half length (N >= 32: both plans
+  // have passes)
+  bool fused() const { return N >= 32; }
+  void correlate(const double* a, int64_t n, const double* b, int64_t m, double* out, hipStream_t s) {
+    auto& h = dc.plans[N / 2];
+    if (!h) h.reset(new BigFft(N / 2));
+    dc.spec.reserve((size_t)N);
+    dc.scratch.reserve((size_t)(2 * N));
+    fft->correlate_half(*h, a, n, b, m, dc.spec.p, out, dc.scratch.p, s);
+  }
   double2* spec() const { return dc.spec.p; }
   double* res() const { return dc.res.p; }
 };
@@ -116,16 +127,14 @@ int ad_correlate_fft(const double* a, int64_t n, const double* b, int64_t m, dou
     hipStream_t s = nullptr;
     const int64_t N = next_pow2(n + m - 1);  // correlate.go:119
     SpectralRun run(dc, N);
-    if (run.fft->fused_ok()) {
+    if (run.fused()) {
       // a and b to the device unpadded, the fused transforms (see the device
       // form below), the n + m - 1 lags back in one copy
       dc.xr.reserve((size_t)(n + m));
       dc.res.reserve((size_t)(n + m - 1));
-      dc.spec.reserve((size_t)(2 * N));
-      dc.scratch.reserve((size_t)(4 * N));
       AD_HIP(hipMemcpyAsync(dc.xr.p, a, (size_t)n * sizeof(double), hipMemcpyHostToDevice, s));
       AD_HIP(hipMemcpyAsync(dc.xr.p + n, b, (size_t)m * sizeof(double), hipMemcpyHostToDevice, s));
-      run.fft->correlate(dc.xr.p, n, dc.xr.p + n, m, dc.spec.p, dc.res.p, dc.scratch.p, s);
+      run.correlate(dc.xr.p, n, dc.xr.p + n, m, dc.res.p, s);
       AD_HIP(hipMemcpyAsync(out, dc.res.p, (size_t)(n + m - 1) * sizeof(double), hipMemcpyDeviceToHost, s));
       AD_HIP(hipStreamSynchronize(s));
       return;
@@ -157,12 +166,10 @@ int ad_correlate_fft_device(const double* a, int64_t n, const double* b, int64_t
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const int64_t N = next_pow2(n + m - 1);
     SpectralRun run(dc, N);
-    if (run.fft->fused_ok()) {
-      // transforms straight from the caller's arrays, the product fused into
-      // the inverse's first pass and the lag reordering into its last
-      dc.spec.reserve((size_t)(2 * N));
-      dc.scratch.reserve((size_t)(4 * N));
-      run.fft->correlate(a, n, b, m, dc.spec.p, out, dc.scratch.p, s);
+    if (run.fused()) {
+      // one forward transform of a + i b straight from the caller's arrays, the
+      // inverse of A conj(B) at half length, its outputs written in lag order
+      run.correlate(a, n, b, m, out, s);
       return;
     }
     dc.xr.reserve((size_t)(2 * N));

@@ -548,13 +548,16 @@ def main_corr(args):
     N = 1 << (2 * n - 2).bit_length()
     # algorithmic bytes per call (DESIGN.md "spectral row"): one forward
     # transform of a + i b (the first pass reads the n + m real samples, zero
-    # padding is not read, and writes 16 B per bin), the inverse's first pass
-    # reading Z once (A conj(B) from Z's mirror pairs; the mirror re-read is
-    # not counted), its last pass writing the n + m - 1 kept lags
+    # padding is not read, and writes 16 B per bin); the inverse at half
+    # length, its first pass reading Z once (A conj(B) from Z's mirror pairs;
+    # the mirror re-reads are not counted) and its last pass writing the
+    # n + m - 1 kept lags
     from algodsp.conv import _fft_pass_count
     P = _fft_pass_count(N)
+    Ph = _fft_pass_count(N // 2)
     fwd = 2 * n * 8 + N * 16 + N * 32 * (P - 1)
-    inv = N * 16 + (2 * n - 1) * 8 if P == 1 else N * 32 * (P - 1) + N * 16 + (2 * n - 1) * 8
+    inv = (N * 16 + (2 * n - 1) * 8 if Ph == 1 else
+           N * 16 + (N // 2) * 16 + (N // 2) * 32 * (Ph - 2) + (N // 2) * 16 + (2 * n - 1) * 8)
     alg = fwd + inv
     gbs = alg / (ms * 1e-3) / 1e9
     cpu = None
@@ -574,7 +577,8 @@ def main_corr(args):
         "value": round(2 * n / (ms * 1e-3) / 1e6, 3), "unit": "Msamples/s", "n_gpus": 1, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f64", "data": "synthetic: SplitMix64 white noise",
-        "config": {"workload": f"conv.CorrelateFFT n = m = {n}, FFT size {N} ({P} device passes), device buffers",
+        "config": {"workload": f"conv.CorrelateFFT n = m = {n}, FFT size {N} (forward: {P} device passes over a + i b; "
+                               f"inverse: {Ph} passes at N/2), device buffers",
                    "fft_size": N},
         "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
