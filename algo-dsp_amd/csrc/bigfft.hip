@@ -17,6 +17,56 @@ namespace adsp {
 __device__ __forceinline__ double2 go_cmul(double2 a, double2 b) {
   return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
 }
+__device__ __forceinline__ double2 go_cdiv(double2 n, double2 m) {
+  double e, f;
+  if (fabs(m.x) >= fabs(m.y)) {
+    const double ratio = m.y / m.x;
+    const double denom = m.x + ratio * m.y;
+    e = (n.x + n.y * ratio) / denom;
+    f = (n.y - n.x * ratio) / denom;
+  } else {
+    const double ratio = m.x / m.y;
+    const double denom = m.y + ratio * m.x;
+    e = (n.x * ratio + n.y) / denom;
+    f = (n.y * ratio - n.x) / denom;
+  }
+  return make_double2(e, f);
+}
+__device__ __forceinline__ double go_hypot(double p, double q) {
+  p = fabs(p);
+  q = fabs(q);
+  if (isinf(p) || isinf(q)) return INFINITY;
+  if (isnan(p) || isnan(q)) return NAN;
+  if (p < q) {
+    const double t = p;
+    p = q;
+    q = t;
+  }
+  if (p == 0) return 0;
+  q = q / p;
+  return p * sqrt(1 + q * q);
+}
+// The pointwise step of the spectral row on one bin (see SpecOp): x the
+// signal's (or the only input's) spectrum, h the kernel's; bin index k for
+// the naive method's first-failing-bin report.
+__device__ __forceinline__ double2 spec_op(int op, double2 x, double2 h, double eps, int64_t k,
+                                           unsigned long long* bad) {
+  switch (op) {
+    case kSpecCorr:
+      return go_cmul(x, c_conj(h));
+    case kSpecNaive:
+      if (go_hypot(h.x, h.y) < 1e-15) atomicMin(bad, (unsigned long long)k);
+      return go_cdiv(x, h);
+    case kSpecReg: {
+      const double mag2 = h.x * h.x + h.y * h.y;
+      return go_cdiv(go_cmul(x, c_conj(h)), make_double2(mag2 + eps, 0.0));
+    }
+    default: {  // kSpecInvFilt
+      const double mag2 = x.x * x.x + x.y * x.y;
+      return go_cdiv(c_conj(x), make_double2(mag2 + eps, 0.0));
+    }
+  }
+}
 #pragma clang fp contract(fast)  // the HIP default again for the transforms below
 
 // ---------------------------------------------------------------------------
@@ -30,7 +80,9 @@ struct PassShape {
   static constexpr int T = FftPlan<R, 16>::T;
   static constexpr int BLOCK = FW * T;
 };
-template <int R, int FW, bool FWD, bool REALIN, bool REALOUT>
+// HALF: the first inverse pass of the spectral row's half-length inverse
+// (FftPassArgs::half), instantiated only where it can occur.
+template <int R, int FW, bool FWD, bool REALIN, bool REALOUT, int HALF = 0>
 __global__ __launch_bounds__((PassShape<R, FW>::BLOCK)) void k_fft_pass(FftPassArgs a) {
   using Plan = FftPlan<R, 16>;
   // per-butterfly LDS stride: odd when a 16-lane group stays inside one
@@ -57,15 +109,20 @@ __global__ __launch_bounds__((PassShape<R, FW>::BLOCK)) void k_fft_pass(FftPassA
         } else {
           v.x = g < a.nr[bt] ? a.xb[bt][g] : 0.0;
         }
-      } else if (a.half) {
-        // X[q] = A[q] conj(B[q]) from the forward spectrum Z = FFT(a + i b)
+      } else if constexpr (HALF != 0) {
+        // X[q] = op(A[q], B[q]) from the forward spectrum Z = FFT(a + i b):
+        // A = (Z[q] + conj Z[-q]) / 2, B = (Z[q] - conj Z[-q]) / 2i
         const int64_t NF = a.NF, msk = NF - 1;
+        // (spec2 set: A and B come from two separate transforms, in and spec2 --
+        // the division of Deconvolve must not take B out of a transform that
+        // A dominates)
+        // HALF = 1: the correlation from Z = FFT(a + i b) (op fixed); 2: any op
         auto xq = [&](int64_t q) {
+          if (HALF == 2 && a.spec2) return spec_op(a.op, a.in[q], a.spec2[q], a.eps, q, a.bad);
           const double2 zk = a.in[q], zm = a.in[(NF - q) & msk];
-          const double2 sp = make_double2(zk.x + zm.x, zk.y - zm.y);
-          const double2 dm = make_double2(zk.x - zm.x, zk.y + zm.y);
-          const double2 t = go_cmul(sp, c_conj(dm));
-          return make_double2(-0.25 * t.y, 0.25 * t.x);
+          const double2 A = make_double2(0.5 * (zk.x + zm.x), 0.5 * (zk.y - zm.y));
+          const double2 B = make_double2(0.5 * (zk.y + zm.y), -0.5 * (zk.x - zm.x));
+          return HALF == 1 ? go_cmul(A, c_conj(B)) : spec_op(a.op, A, B, a.eps, q, a.bad);
         };
         const double2 x1 = xq(g), x2 = xq(g + NF / 2);
         const int64_t fm = ((int64_t)1 << a.fS) - 1;
@@ -217,6 +274,17 @@ int fft_wide() {
 
 template <int R, bool FWD, bool RI, bool RO>
 void go_pass(const FftPassArgs& a, int batch, hipStream_t s) {
+  if constexpr (!FWD && !RI) {
+    if (a.half) {
+      constexpr int F1 = FftPlan<R, 16>::F;
+      const dim3 grid((unsigned)((a.N / R + F1 - 1) / F1), (unsigned)batch);
+      if (a.op == kSpecCorr && !a.spec2)
+        hipLaunchKernelGGL((k_fft_pass<R, F1, FWD, RI, RO, 1>), grid, dim3(PassShape<R, F1>::BLOCK), 0, s, a);
+      else
+        hipLaunchKernelGGL((k_fft_pass<R, F1, FWD, RI, RO, 2>), grid, dim3(PassShape<R, F1>::BLOCK), 0, s, a);
+      return;
+    }
+  }
   const int64_t nb = a.N / R;
   constexpr int F1 = FftPlan<R, 16>::F;
   constexpr int F2 = (8192 / R) > F1 ? (8192 / R) : F1;
@@ -312,6 +380,14 @@ void BigFft::run(bool forward, const double2* in, const double* xr, int64_t n_re
 
 void BigFft::correlate_half(const BigFft& half, const double* a_, int64_t n, const double* b_, int64_t m,
                             double2* spec, double* out, double2* scratch, hipStream_t s) const {
+  // lags 0..n-1 from the front, -(m-1)..-1 from the back (correlate.go:165-171)
+  spectral_half(half, kSpecCorr, 0.0, nullptr, true, a_, n, b_, m, n, m - 1, N_ - m + 1, spec, out, scratch, s);
+}
+
+void BigFft::spectral_half(const BigFft& half, int op, double eps, unsigned long long* bad, bool pack,
+                           const double* a_, int64_t n, const double* b_, int64_t m, int64_t n_front,
+                           int64_t front_off, int64_t back_from, double2* spec, double* out, double2* scratch,
+                           hipStream_t s) const {
   FftPassArgs a{};
   a.N = N_;
   a.tw_lo = tw_lo_;
@@ -322,8 +398,12 @@ void BigFft::correlate_half(const BigFft& half, const double* a_, int64_t n, con
   a.nr[0] = n;
   a.xb[1] = b_;
   a.nr[1] = m;
-  a.pack2 = 1;  // Z = FFT(a + i b)
-  run_passes(true, a, nullptr, a_, 0, spec, nullptr, N_, 1, scratch, s);
+  if (pack) {
+    a.pack2 = 1;  // Z = FFT(a + i b)
+    run_passes(true, a, nullptr, a_, 0, spec, nullptr, N_, 1, scratch, s);
+  } else {  // FFT(a) and FFT(b) as a batch of two real inputs: spec [2][N]
+    run_passes(true, a, nullptr, a_, 0, spec, nullptr, N_, 2, scratch, s);
+  }
   FftPassArgs i{};
   i.N = half.N_;
   i.tw_lo = half.tw_lo_;
@@ -335,10 +415,14 @@ void BigFft::correlate_half(const BigFft& half, const double* a_, int64_t n, con
   i.ftw_lo = tw_lo_;
   i.ftw_hi = tw_hi_;
   i.fS = S_;
+  i.spec2 = pack ? nullptr : spec + N_;
+  i.op = op;
+  i.eps = eps;
+  i.bad = bad;
   i.remap = 1;
-  i.n_front = n;  // lags 0..n-1 from the front, -(m-1)..-1 from the back (correlate.go:165-171)
-  i.front_off = m - 1;
-  i.back_from = N_ - m + 1;
+  i.n_front = n_front;
+  i.front_off = front_off;
+  i.back_from = back_from;
   half.run_passes(false, i, spec, nullptr, half.N_, nullptr, out, 0, 1, scratch, s);
 }
 
@@ -399,65 +483,11 @@ void BigFft::run_passes(bool forward, FftPassArgs a, const double2* in, const do
 // complex128div (Smith's algorithm), magnitudes by math.Hypot.
 // ---------------------------------------------------------------------------
 #pragma clang fp contract(off)
-__device__ __forceinline__ double2 go_cdiv(double2 n, double2 m) {
-  double e, f;
-  if (fabs(m.x) >= fabs(m.y)) {
-    const double ratio = m.y / m.x;
-    const double denom = m.x + ratio * m.y;
-    e = (n.x + n.y * ratio) / denom;
-    f = (n.y - n.x * ratio) / denom;
-  } else {
-    const double ratio = m.x / m.y;
-    const double denom = m.y + ratio * m.x;
-    e = (n.x * ratio + n.y) / denom;
-    f = (n.y * ratio - n.x) / denom;
-  }
-  return make_double2(e, f);
-}
-__device__ __forceinline__ double go_hypot(double p, double q) {
-  p = fabs(p);
-  q = fabs(q);
-  if (isinf(p) || isinf(q)) return INFINITY;
-  if (isnan(p) || isnan(q)) return NAN;
-  if (p < q) {
-    const double t = p;
-    p = q;
-    q = t;
-  }
-  if (p == 0) return 0;
-  q = q / p;
-  return p * sqrt(1 + q * q);
-}
-
 __global__ __launch_bounds__(256) void k_spec_op(int op, double2* __restrict__ a, const double2* __restrict__ b,
                                                  int64_t n, double eps, unsigned long long* bad) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
-  const double2 x = a[i];
-  double2 r;
-  switch (op) {
-    case kSpecCorr:
-      r = go_cmul(x, c_conj(b[i]));
-      break;
-    case kSpecNaive: {
-      const double2 h = b[i];
-      if (go_hypot(h.x, h.y) < 1e-15) atomicMin(bad, (unsigned long long)i);
-      r = go_cdiv(x, h);
-      break;
-    }
-    case kSpecReg: {
-      const double2 h = b[i];
-      const double mag2 = h.x * h.x + h.y * h.y;
-      r = go_cdiv(go_cmul(x, c_conj(h)), make_double2(mag2 + eps, 0.0));
-      break;
-    }
-    default: {  // kSpecInvFilt
-      const double mag2 = x.x * x.x + x.y * x.y;
-      r = go_cdiv(c_conj(x), make_double2(mag2 + eps, 0.0));
-      break;
-    }
-  }
-  a[i] = r;
+  a[i] = spec_op(op, a[i], b ? b[i] : make_double2(0.0, 0.0), eps, i, bad);
 }
 
 void launch_spec_op(int op, double2* a, const double2* b, int64_t n, double eps, unsigned long long* bad,

@@ -49,6 +49,10 @@ struct FftPassArgs {
   // X[k] and X[k + NF/2] (E = (X[k] + X[k+NF/2])/2, O = (X[k] - X[k+NF/2]) W_NF^-k / 2,
   // X from the forward spectrum's mirror pairs), its last pass writes Re z[m]
   // and Im z[m] as the real outputs 2m and 2m + 1.
+  const double2* spec2;     // half: B's own spectrum (A in `in`); null: A, B from Z = FFT(a + i b)
+  int op;                   // half: the pointwise step (SpecOp) applied to A, B
+  double eps;
+  unsigned long long* bad;  // kSpecNaive: first bin with |B| < 1e-15 (atomicMin)
   int half;   // first pass: form z from the spectrum
   int pairs;  // last pass: write Re z[m], Im z[m] as real outputs 2m, 2m + 1
   int64_t NF;
@@ -81,6 +85,16 @@ class BigFft {
   // (n + m - 1 values, correlate.go:165-171).  Both plans need passes (N >= 32).
   void correlate_half(const BigFft& half, const double* a, int64_t n, const double* b, int64_t m, double2* spec,
                       double* out, double2* scratch, hipStream_t s) const;
+  // The same structure for any SpecOp: Z = FFT(x + i h) (x: n, h: m real
+  // samples; h may be null), the inverse of op(X, H) at half length, real
+  // outputs o < n_front to out[front_off + o] and o >= back_from to
+  // out[o - back_from].  Deconvolve and InverseFilter (deconvolve.go:104-394).
+  // pack: one transform of x + i h (the correlation; h's spectrum is then
+  // only as exact as x's magnitude allows, which a division cannot afford,
+  // so Deconvolve transforms x and h separately: pack = false, spec [2][N]).
+  void spectral_half(const BigFft& half, int op, double eps, unsigned long long* bad, bool pack, const double* x,
+                     int64_t n, const double* h, int64_t m, int64_t n_front, int64_t front_off, int64_t back_from,
+                     double2* spec, double* out, double2* scratch, hipStream_t s) const;
 
  private:
   int64_t N_;

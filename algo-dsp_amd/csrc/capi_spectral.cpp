@@ -87,6 +87,17 @@ struct SpectralRun {
     dc.scratch.reserve((size_t)(2 * N));
     fft->correlate_half(*h, a, n, b, m, dc.spec.p, out, dc.scratch.p, s);
   }
+  // Deconvolve / InverseFilter through the same structure (x: n, h: m real
+  // samples, h may be null): the first n_front real outputs to out.
+  void spectral(int op, double eps, unsigned long long* bad, const double* x, int64_t n, const double* h, int64_t m,
+                int64_t n_front, double* out, hipStream_t s) {
+    auto& hp = dc.plans[N / 2];
+    if (!hp) hp.reset(new BigFft(N / 2));
+    const bool two = h != nullptr;  // Deconvolve: separate transforms of x and h
+    dc.spec.reserve((size_t)(two ? 2 * N : N));
+    dc.scratch.reserve((size_t)(two ? 4 * N : 2 * N));
+    fft->spectral_half(*hp, op, eps, bad, !two, x, n, h, h ? m : 0, n_front, 0, N, dc.spec.p, out, dc.scratch.p, s);
+  }
   double2* spec() const { return dc.spec.p; }
   double* res() const { return dc.res.p; }
 };
@@ -229,6 +240,30 @@ int ad_deconvolve(const double* signal, int64_t n, const double* kernel, int64_t
     std::lock_guard<std::mutex> g(dc.mu);
     hipStream_t s = nullptr;
     SpectralRun run(dc, N);
+    if (run.fused()) {
+      // one forward transform of signal + i kernel, the division fused into
+      // the inverse's first pass, the inverse at half length, olen outputs
+      dc.xr.reserve((size_t)(n + m));
+      dc.res.reserve((size_t)olen);
+      AD_HIP(hipMemcpyAsync(dc.xr.p, signal, (size_t)n * sizeof(double), hipMemcpyHostToDevice, s));
+      AD_HIP(hipMemcpyAsync(dc.xr.p + n, kernel, (size_t)m * sizeof(double), hipMemcpyHostToDevice, s));
+      if (op == kSpecNaive) {
+        dc.bad.reserve(1);
+        AD_HIP(hipMemsetAsync(dc.bad.p, 0xff, sizeof(unsigned long long), s));
+      }
+      run.spectral(op, eps, op == kSpecNaive ? dc.bad.p : nullptr, dc.xr.p, n, dc.xr.p + n, m, olen, dc.res.p, s);
+      if (op == kSpecNaive) {
+        unsigned long long first = 0;
+        AD_HIP(hipMemcpyAsync(&first, dc.bad.p, sizeof(first), hipMemcpyDeviceToHost, s));
+        AD_HIP(hipStreamSynchronize(s));
+        if (first != ~0ull)
+          AD_FAIL(AD_ERR_DIVISION_BY_ZERO,
+                  "conv: division by zero in deconvolution: at frequency bin " + std::to_string(first));
+      }
+      AD_HIP(hipMemcpyAsync(out, dc.res.p, (size_t)olen * sizeof(double), hipMemcpyDeviceToHost, s));
+      AD_HIP(hipStreamSynchronize(s));
+      return;
+    }
     const double* src[2] = {signal, kernel};
     const int64_t len[2] = {n, m};
     stage_real(dc.xr, N, src, len, 2, s);
@@ -267,8 +302,18 @@ int ad_inverse_filter(const double* kernel, int64_t m, int64_t length, double ep
     std::lock_guard<std::mutex> g(dc.mu);
     hipStream_t s = nullptr;
     SpectralRun run(dc, N);
+    const int64_t mk = m < N ? m : N;  // kernel truncated to the transform (:367)
+    if (run.fused()) {
+      dc.xr.reserve((size_t)mk);
+      dc.res.reserve((size_t)length);
+      AD_HIP(hipMemcpyAsync(dc.xr.p, kernel, (size_t)mk * sizeof(double), hipMemcpyHostToDevice, s));
+      run.spectral(kSpecInvFilt, epsilon, nullptr, dc.xr.p, mk, nullptr, 0, length, dc.res.p, s);
+      AD_HIP(hipMemcpyAsync(out, dc.res.p, (size_t)length * sizeof(double), hipMemcpyDeviceToHost, s));
+      AD_HIP(hipStreamSynchronize(s));
+      return;
+    }
     const double* src[1] = {kernel};
-    const int64_t len[1] = {m < N ? m : N};  // kernel truncated to the transform (:367)
+    const int64_t len[1] = {mk};
     stage_real(dc.xr, N, src, len, 1, s);
     run.forward(dc.xr.p, 1, s);
     launch_spec_op(kSpecInvFilt, run.spec(), nullptr, N, epsilon, nullptr, s);
