@@ -976,6 +976,31 @@ int device_cus() {
   return n;
 }
 
+void mac_run_geometry(int PC, int NH, int M, int mid_in_k3, int channels, int jc, int R_req, int* R_out,
+                      int* ny_out) {
+  const int BW = 32 / NH;
+  const int nx = M / (2 * BW) + (mid_in_k3 ? 0 : 1);
+  int R = R_req;
+  if (R <= 0) {
+    // Auto run length: the fewest runs that still fill every SIMD to its
+    // resident-wave limit in ONE round.  A second, partial round leaves a
+    // tail of idle SIMDs, and longer runs re-read fewer warm-up rows and H
+    // spectra (stereo 2 x 2064 blocks at M = 8192: R = 192, 2838 waves,
+    // K2 237 us vs 285 us at R = 64).
+    const int64_t slots = (int64_t)mac_waves_per_simd(PC, NH) * 4 * device_cus();
+    const int64_t per_run = (int64_t)channels * nx;
+    int64_t ny = std::max<int64_t>(1, slots / per_run);
+    ny = std::min<int64_t>(ny, (jc + 31) / 32);  // runs of at least 32 blocks
+    ny = std::max<int64_t>(ny, 1);
+    R = (int)((jc + ny - 1) / ny);
+  }
+  // runs must be whole groups of PC (<= 16) outputs so the overshoot of a run
+  // never lands in the next run's rows
+  if (jc > R) R = (R + 15) / 16 * 16;
+  *R_out = R;
+  *ny_out = (jc + R - 1) / R;
+}
+
 bool launch_fdl_mac(int PC, int NH, const MacArgs& in, int channels, hipStream_t s) {
   if (channels <= 0 || in.jc <= 0) return true;
   MacArgs a = in;
@@ -999,24 +1024,8 @@ bool launch_fdl_mac(int PC, int NH, const MacArgs& in, int channels, hipStream_t
       default: return false;
     }
   }
-  if (a.R <= 0) {
-    // Auto run length: the fewest runs that still fill every SIMD to its
-    // resident-wave limit in ONE round.  A second, partial round leaves a
-    // tail of idle SIMDs, and longer runs re-read fewer warm-up rows and H
-    // spectra (stereo 2 x 2064 blocks at M = 8192: R = 192, 2838 waves,
-    // K2 237 us vs 285 us at R = 64).
-    const int64_t slots = (int64_t)mac_waves_per_simd(PC, NH) * 4 * device_cus();
-    const int64_t per_run = (int64_t)channels * a.nx;
-    int64_t ny = std::max<int64_t>(1, slots / per_run);
-    ny = std::min<int64_t>(ny, (a.jc + 31) / 32);  // runs of at least 32 blocks
-    ny = std::max<int64_t>(ny, 1);
-    a.R = (int)((a.jc + ny - 1) / ny);
-  }
-  // runs must be whole groups of PC (<= 16) outputs so the overshoot of a run
-  // never lands in the next run's rows
-  if (a.jc > a.R) a.R = (a.R + 15) / 16 * 16;
+  mac_run_geometry(PC, NH, a.M, a.mid_in_k3, channels, a.jc, a.R, &a.R, &a.ny);
   a.bx_fast = mac_bx_fast();
-  a.ny = (a.jc + a.R - 1) / a.R;
   const dim3 grid((unsigned)((int64_t)channels * a.nx * a.ny));
   if (NH == 1) {
     switch (PC) {

@@ -74,6 +74,11 @@ struct RfftArgs {
   const double2* twM;   // W_M^e, e < M
   const double2* twN;   // W_{2M}^k, k < M
   int per_wg;           // blocks per workgroup (set by the launcher, <= the plan's F)
+  // Item order (split kernels; ord_R = 0: XCD-contiguous order).  K2 run ry
+  // reads block row ry*R - ord_pc + t at its step t, so K1 writes the rows
+  // in decreasing t: the rows K2 needs first are the newest in the Infinity
+  // Cache.  Grid: channels * (ord_ny + 1) * ord_R (rows outside [0, jc) idle).
+  int ord_R, ord_ny, ord_pc;
 };
 
 struct MacArgs {
@@ -136,11 +141,18 @@ struct IrfftArgs {
   const double2* twM;
   const double2* twN;
   MidBin mid;
+  // Item order (split kernel; ord_R = 0: XCD-contiguous order): K2 run ry
+  // writes output row ry*R + t at its step t, so K3 reads the rows in
+  // decreasing t, newest first.  Grid: channels * ord_ny * ord_R.
+  int ord_R, ord_ny;
 };
 
 bool launch_window_rfft(int M, const RfftArgs& a, hipStream_t s);
 bool launch_irfft_store(int M, const IrfftArgs& a, hipStream_t s);
 bool launch_fdl_mac(int PC, int NH, const MacArgs& a, int channels, hipStream_t s);
+// K2's run geometry for a launch (run length R: R_req, or auto when <= 0;
+// runs ny), shared with the K1/K3 launches that order their items by it.
+void mac_run_geometry(int PC, int NH, int M, int mid_in_k3, int channels, int jc, int R_req, int* R, int* ny);
 void launch_copy_f64(const double* src, double* dst, int64_t n, hipStream_t s);
 void launch_direct(const double* a, int64_t n, const double* b, int64_t m, double* dst, hipStream_t s);
 void launch_direct_circular(const double* a, const double* b, int64_t n, double* dst, hipStream_t s);

@@ -238,9 +238,18 @@ __global__ __launch_bounds__((SplitPlan<M>::T)) __attribute__((amdgpu_waves_per_
   constexpr int M2 = SP::M2, V = SP::V, T = SP::T, L = M;
   __shared__ __attribute__((aligned(16))) double2 lds[SP::LDS];
   const int tid = threadIdx.x;
-  const int e = __builtin_amdgcn_readfirstlane(xcd_remap_fft(blockIdx.x, gridDim.x));  // uniform: SGPRs
-  const int c = __builtin_amdgcn_readfirstlane(e / a.jc);
-  const int j = __builtin_amdgcn_readfirstlane(e - c * a.jc);
+  int c, j;
+  if (a.ord_R > 0) {  // newest-last for K2's first steps (RfftArgs::ord_R)
+    const int per = a.channels * (a.ord_ny + 1), b = blockIdx.x;
+    const int t = a.ord_R - 1 - b / per, k = b % per;
+    c = __builtin_amdgcn_readfirstlane(k % a.channels);
+    j = __builtin_amdgcn_readfirstlane((k / a.channels) * a.ord_R - a.ord_pc + t);
+    if (j < 0 || j >= a.jc) return;
+  } else {
+    const int e = __builtin_amdgcn_readfirstlane(xcd_remap_fft(blockIdx.x, gridDim.x));  // uniform: SGPRs
+    c = __builtin_amdgcn_readfirstlane(e / a.jc);
+    j = __builtin_amdgcn_readfirstlane(e - c * a.jc);
+  }
   const double* xc = a.x + (int64_t)c * a.x_stride;
   const int64_t t0 = a.s0 + (int64_t)j * L;  // first sample of block j
   // E[m] = z[2m], O[m] = z[2m+1] hold samples 4m.. of the block; the upper
@@ -295,9 +304,18 @@ __global__ __launch_bounds__((SplitPlan<M>::T)) __attribute__((amdgpu_waves_per_
   const int tid = threadIdx.x;
   // item indices and row bases are wave-uniform: keep them in SGPRs (VGPR
   // copies of 64-bit bases spilled to scratch at the 128-VGPR cap)
-  const int e = __builtin_amdgcn_readfirstlane(xcd_remap_fft(blockIdx.x, gridDim.x));
-  const int c = __builtin_amdgcn_readfirstlane(e / a.jc);
-  const int j = __builtin_amdgcn_readfirstlane(e - c * a.jc);
+  int c, j;
+  if (a.ord_R > 0) {  // newest first (IrfftArgs::ord_R)
+    const int per = a.channels * a.ord_ny, b = blockIdx.x;
+    const int t = a.ord_R - 1 - b / per, k = b % per;
+    c = __builtin_amdgcn_readfirstlane(k % a.channels);
+    j = __builtin_amdgcn_readfirstlane((k / a.channels) * a.ord_R + t);
+    if (j >= a.jc) return;
+  } else {
+    const int e = __builtin_amdgcn_readfirstlane(xcd_remap_fft(blockIdx.x, gridDim.x));
+    c = __builtin_amdgcn_readfirstlane(e / a.jc);
+    j = __builtin_amdgcn_readfirstlane(e - c * a.jc);
+  }
   const double2* Zb = a.Y + (int64_t)c * a.y_ch_stride + (int64_t)j * a.MS;
   double2 av[V], bv[V];
   // wave 0: the middle bin's first partition loads, ahead of the Z loads
@@ -403,7 +421,7 @@ void rfft_go(const RfftArgs& a, hipStream_t s) {
 }
 template <int M>
 void rfft_split_go(const RfftArgs& a, hipStream_t s) {
-  const int64_t items = (int64_t)a.channels * a.jc;
+  const int64_t items = a.ord_R > 0 ? (int64_t)a.channels * (a.ord_ny + 1) * a.ord_R : (int64_t)a.channels * a.jc;
   const dim3 g((unsigned)items), b(SplitPlan<M>::T);
   if constexpr (M == 8192) {
     switch (k1_nt()) {
@@ -423,7 +441,7 @@ void irfft_go(const IrfftArgs& a, hipStream_t s) {
 }
 template <int M>
 void irfft_split_go(const IrfftArgs& a, hipStream_t s) {
-  const int64_t items = (int64_t)a.channels * a.jc;
+  const int64_t items = a.ord_R > 0 ? (int64_t)a.channels * a.ord_ny * a.ord_R : (int64_t)a.channels * a.jc;
   const dim3 g((unsigned)items), b(SplitPlan<M>::T);
   if constexpr (M == 8192) {
     switch (k3_exp()) {

@@ -232,6 +232,20 @@ void Upols::run(const double* d_in, int64_t in_stride, int64_t n, double* d_out,
     // algorithmic bytes per launch: unique input samples in,
     // M+1 complex128 bins out, per (channel, block)
     const double blocks = (double)C_ * jc;
+    // K2's run geometry, decided here so K1 and K3 can order their items by it
+    // (newest rows first for the kernel that reads them next; see RfftArgs)
+    int runR = R_, runNy = 0;
+    mac_run_geometry(PC_, NH_, M_, M_ >= 2048 && P_ <= 256 ? 1 : 0, C_, jc, R_, &runR, &runNy);
+    static const bool order_items = [] {
+      const char* v = std::getenv("AD_ITEM_ORDER");
+      return !(v && v[0] == '0');
+    }();
+    const bool ordered = order_items && M_ >= 2048 && !(NH_ == 1 && jc <= 2) && runNy > 1;
+    if (ordered) {
+      a.ord_R = runR;
+      a.ord_ny = runNy;
+      a.ord_pc = PC_;
+    }
     hipEvent_t e0;
     prof_begin(s, &e0, 0);
     launch_window_rfft(M_, a, s);
@@ -251,7 +265,7 @@ void Upols::run(const double* d_in, int64_t in_stride, int64_t n, double* d_out,
     m.Y = Y_.p;
     m.y_ch_stride = (int64_t)(jc_max_ + 16) * MS_;
     m.jc = jc;
-    m.R = R_ > 0 ? std::min(R_, jc) : 0;
+    m.R = runR;
     m.P = P_;
     m.M = M_;
     m.twN = tw_.p + M_;
@@ -276,6 +290,10 @@ void Upols::run(const double* d_in, int64_t in_stride, int64_t n, double* d_out,
     b.accumulate = accumulate ? 1 : 0;
     b.twM = tw_.p;
     b.twN = tw_.p + M_;
+    if (ordered) {
+      b.ord_R = runR;
+      b.ord_ny = runNy;
+    }
     if (mid_k3) {
       b.mid.on = 1;
       b.mid.X = X_.p;
