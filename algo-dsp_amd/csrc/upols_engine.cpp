@@ -240,7 +240,13 @@ void Upols::run(const double* d_in, int64_t in_stride, int64_t n, double* d_out,
       const char* v = std::getenv("AD_ITEM_ORDER");
       return !(v && v[0] == '0');
     }();
-    const bool ordered = order_items && M_ >= 2048 && !(NH_ == 1 && jc <= 2) && runNy > 1;
+    // worth it when the Infinity Cache (256 MiB) holds the rows of a good
+    // part of a run: stereo at hop 8192 ~81 of R = 176 steps (step 0.5751 ->
+    // 0.5686 ms); the 8-channel shard ~81 of R = 688 (no gain, +0.7 %)
+    const int64_t rows_per_step = (int64_t)C_ * runNy;
+    const int64_t steps_cached = (int64_t(256) << 20) / ((int64_t)MS_ * 16 * std::max<int64_t>(1, rows_per_step));
+    const bool ordered = order_items && M_ >= 2048 && !(NH_ == 1 && jc <= 2) && runNy > 1 &&
+                         steps_cached * 4 >= runR;
     if (ordered) {
       a.ord_R = runR;
       a.ord_ny = runNy;
