@@ -362,6 +362,8 @@ int ad_conv_process_block(ad_conv* h, const double* in, int64_t in_len, double* 
 // correctly rounded float32 of a float64 convolution -- within the reference's
 // own complex64 error (its float32 tests allow 1e-4, streaming_test.go:175-265).
 
+}  // extern "C"
+
 namespace {
 std::vector<double> widen(const float* p, int64_t n) {
   std::vector<double> v((size_t)std::max<int64_t>(n, 0));
@@ -369,6 +371,8 @@ std::vector<double> widen(const float* p, int64_t n) {
   return v;
 }
 }  // namespace
+
+extern "C" {
 
 int ad_conv_stream_ols32_create(const float* kernel, int64_t kernel_len, int64_t block_size, int device,
                                 ad_conv** out) {

@@ -129,7 +129,7 @@ void parallel_for(int64_t n, const std::function<void(int64_t)>& fn, int workers
   Pool::get().run(n, fn, workers);
 }
 
-HostPipeline::HostPipeline(int device) : device_(device) {
+HostPipeline::HostPipeline(int) {
   AD_HIP(hipStreamCreateWithFlags(&s_in_, hipStreamNonBlocking));
   AD_HIP(hipStreamCreateWithFlags(&s_out_, hipStreamNonBlocking));
   for (int i = 0; i < 2; ++i) {

@@ -45,7 +45,6 @@ class HostPipeline {
   static constexpr int64_t kChunkBytes = int64_t(16) << 20;
 
  private:
-  int device_;
   hipStream_t s_in_ = nullptr, s_out_ = nullptr;
   double* pin_in_[2] = {nullptr, nullptr};
   double* pin_out_[2] = {nullptr, nullptr};

@@ -12,7 +12,7 @@
 namespace adsp {
 
 Nupols::Nupols(int device, const double* h, int64_t K, int64_t lambda, int64_t p_max)
-    : device_(device), lambda_(lambda) {
+    : lambda_(lambda) {
   if (lambda < 64 || !is_pow2(lambda) || p_max < lambda || !is_pow2(p_max) || p_max > 8192)
     AD_FAIL(AD_ERR_INTERNAL, "Nupols: bad partition sizes");
   // Stage layout: two partitions per size while the size doubles, the rest

@@ -54,7 +54,6 @@ class Nupols {
     int64_t pend_d = 0;                         // its first input sample
     int64_t pend_n = 0;                         // its length (whole blocks)
   };
-  int device_;
   int64_t lambda_;
   std::vector<Stage> st_;
   std::vector<double> xin_;  // input not yet consumed by every stage
