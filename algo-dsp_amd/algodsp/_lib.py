@@ -167,6 +167,8 @@ def _declare(L: C.CDLL) -> None:
         "ad_conv_fft_size": (i64, [vp]),
         "ad_conv_step_size": (i64, [vp]),
         "ad_conv_latency": (i64, [vp]),
+        "ad_conv_set_host_io": (C.c_int, [vp, C.c_int, C.c_int]),
+        "ad_conv_host_io_profile": (C.c_int, [vp, c_double_p, c_double_p, c_double_p]),
         "ad_conv_destroy": (None, [vp]),
         "ad_conv_direct": (C.c_int, [c_double_p, i64, c_double_p, i64, c_double_p, C.c_int]),
         "ad_conv_direct_circular": (C.c_int, [c_double_p, i64, c_double_p, i64, c_double_p, C.c_int]),
@@ -210,6 +212,10 @@ def _declare(L: C.CDLL) -> None:
         "ad_fx_chain_process_device": (C.c_int, [vp, vp, i64, i64, vp]),
         "ad_fx_chain_compressor_metrics": (C.c_int, [vp, C.c_int, c_double_p, c_double_p, c_double_p]),
         "ad_fx_chain_eq_state": (C.c_int, [vp, c_double_p, i64]),
+        "ad_fx_chain_set_eq_state": (C.c_int, [vp, c_double_p, i64]),
+        "ad_fx_chain_set_engine": (C.c_int, [vp, C.c_int, i64]),
+        "ad_fx_chain_set_profiling": (C.c_int, [vp, C.c_int]),
+        "ad_fx_chain_read_profile": (C.c_int, [vp, C.POINTER(C.c_ulonglong), C.c_int, C.POINTER(C.c_int)]),
         "ad_fx_chain_destroy": (None, [vp]),
         "ad_fx_graph_create": (C.c_int, [vp, C.c_int, C.c_int, C.c_int, C.POINTER(vp)]),
         "ad_fx_graph_process": (C.c_int, [vp, c_double_p, i64]),

@@ -60,6 +60,18 @@ class _Handle:
     def FFTSize(self) -> int:
         return int(lib().ad_conv_fft_size(self._h))
 
+    # host-buffer I/O of batch / multi-channel calls (include/algodsp.h ad_conv_set_host_io)
+    HOST_IO_AUTO, HOST_IO_STAGE, HOST_IO_REGISTER = 0, 1, 2
+
+    def set_host_io(self, mode: int, workers: int = 0) -> None:
+        check(lib().ad_conv_set_host_io(self._h, int(mode), int(workers)))
+
+    def host_io_profile(self):
+        """(register_ms, transfer_ms, unregister_ms) of the last host-buffer call."""
+        r, t, u = C.c_double(), C.c_double(), C.c_double()
+        check(lib().ad_conv_host_io_profile(self._h, C.byref(r), C.byref(t), C.byref(u)))
+        return r.value, t.value, u.value
+
 
 class StreamingConvolver(_Handle):
     """conv.StreamingConvolverT (streaming.go:27-49)."""

@@ -61,6 +61,13 @@ class _FxChain:
     def Reset(self):
         check(lib().ad_fx_chain_reset(self._h))
 
+    # engine selection (include/algodsp.h ad_fx_chain_set_engine); results are
+    # identical in every engine
+    ENGINE_AUTO, ENGINE_FUSED, ENGINE_STAGED_NOSPLIT = 0, 1, 2
+
+    def SetEngine(self, engine: int, chunk: int = 0):
+        check(lib().ad_fx_chain_set_engine(self._h, int(engine), int(chunk)))
+
     def close(self):
         if self._h:
             lib().ad_fx_chain_destroy(self._h)
@@ -109,6 +116,10 @@ class Chain(_FxChain):
         out = np.zeros((self.channels, self.NumSections(), 2))
         check(lib().ad_fx_chain_eq_state(self._h, ptr(out), out.size))
         return out
+
+    def SetState(self, states):  # chain.go:130-138: [channels][sections][2] (a [sections][2] list for 1 channel)
+        st = np.ascontiguousarray(np.asarray(states, dtype=np.float64))
+        check(lib().ad_fx_chain_set_eq_state(self._h, ptr(st), st.size))
 
 
 def Section(b0, b1, b2, a1, a2, channels: int = 1, device: int = DEVICE) -> Chain:

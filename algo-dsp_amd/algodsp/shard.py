@@ -53,6 +53,10 @@ class Comm:
 
         from ._lib import check, lib
 
+        if world > 1 and bootstrap is None:
+            # without it, ranks != 0 would hand RCCL an all-zero id and block in
+            # ncclCommInitRank
+            raise ValueError("Comm: world > 1 needs a bootstrap to share rank 0's unique id")
         L = lib()
         uid = (C.c_uint8 * 128)()
         if rank == 0:

@@ -2,6 +2,7 @@
 // operations of CorrelateFFT / Deconvolve / InverseFilter (see bigfft.hpp).
 #include "bigfft.hpp"
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <string>
@@ -69,6 +70,40 @@ __device__ __forceinline__ double2 spec_op(int op, double2 x, double2 h, double 
 }
 #pragma clang fp contract(fast)  // the HIP default again for the transforms below
 
+// The packing scale of a CorrelateFFT (FftPassArgs::amax): 2^e with
+// e = exponent(max|a|) - exponent(max|b|) (inv: 2^-e); 1 when either maximum
+// is zero or not finite.  A power of two, so scaling by it is exact.
+__device__ __forceinline__ double pack_scale(const unsigned long long* amax, bool inv) {
+  if (!amax) return 1.0;
+  const double ma = __longlong_as_double((long long)amax[0]), mb = __longlong_as_double((long long)amax[1]);
+  if (!(ma > 0.0) || !(mb > 0.0) || !__builtin_isfinite(ma) || !__builtin_isfinite(mb)) return 1.0;
+  int ea = 0, eb = 0;
+  (void)frexp(ma, &ea);
+  (void)frexp(mb, &eb);
+  const int e = ea - eb;
+  return ldexp(1.0, inv ? -e : e);
+}
+
+// {max|a[0..n)|, max|b[0..m)|} as bit patterns (non-negative doubles order
+// like their unsigned bit patterns; a NaN sorts above +inf and disables the
+// scale).  out must be zeroed first.
+__global__ __launch_bounds__(256) void k_absmax2(const double* __restrict__ a, int64_t n, const double* __restrict__ b,
+                                                 int64_t m, unsigned long long* out) {
+  const double* x = blockIdx.y ? b : a;
+  const int64_t len = blockIdx.y ? m : n;
+  unsigned long long mx = 0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < len; i += (int64_t)gridDim.x * 256) {
+    const unsigned long long v = (unsigned long long)__double_as_longlong(fabs(x[i]));
+    mx = v > mx ? v : mx;
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const unsigned long long t = __shfl_xor(mx, o);
+    mx = t > mx ? t : mx;
+  }
+  if ((threadIdx.x & 63) == 0) atomicMax(out + blockIdx.y, mx);
+}
+
 // ---------------------------------------------------------------------------
 // One global Stockham pass of radix R (16 <= R <= 4096): F = BLOCK*16/R
 // butterflies per workgroup.
@@ -94,6 +129,7 @@ __global__ __launch_bounds__((PassShape<R, FW>::BLOCK)) void k_fft_pass(FftPassA
   const int64_t j0 = (int64_t)blockIdx.x * F;
 
   // stage in: element r of butterfly j0 + jj is x[j0 + jj + r nb]; jj fastest
+  const double bscale = REALIN ? pack_scale(a.amax, false) : 1.0;
 #pragma unroll
   for (int i = 0; i < V; ++i) {
     const int idx = i * BLOCK + (int)threadIdx.x;
@@ -105,7 +141,7 @@ __global__ __launch_bounds__((PassShape<R, FW>::BLOCK)) void k_fft_pass(FftPassA
       if constexpr (REALIN) {
         if (a.pack2) {
           v.x = g < a.nr[0] ? a.xb[0][g] : 0.0;
-          v.y = g < a.nr[1] ? a.xb[1][g] : 0.0;
+          v.y = g < a.nr[1] ? a.xb[1][g] * bscale : 0.0;
         } else {
           v.x = g < a.nr[bt] ? a.xb[bt][g] : 0.0;
         }
@@ -179,6 +215,7 @@ __global__ __launch_bounds__((PassShape<R, FW>::BLOCK)) void k_fft_pass(FftPassA
 
   // stage out: output rr of butterfly j goes to (j/Ns) Ns R + (j mod Ns) + rr Ns
   const int64_t Ns = a.Ns;
+  const double oscale = REALOUT ? a.scale * pack_scale(a.amax, true) : a.scale;  // powers of two: exact
 #pragma unroll
   for (int i = 0; i < V; ++i) {
     const int idx = i * BLOCK + (int)threadIdx.x;
@@ -198,9 +235,9 @@ __global__ __launch_bounds__((PassShape<R, FW>::BLOCK)) void k_fft_pass(FftPassA
       auto emit = [&](int64_t q, double x) {
         if (a.remap) {
           if (q < a.n_front)
-            a.out_real[a.front_off + q] = x * a.scale;
+            a.out_real[a.front_off + q] = x * oscale;
           else if (q >= a.back_from)
-            a.out_real[q - a.back_from] = x * a.scale;
+            a.out_real[q - a.back_from] = x * oscale;
         } else {
           a.out_real[bt * a.out_batch + q] = x * a.scale;
         }
@@ -264,14 +301,6 @@ double2* upload(const std::vector<double2>& v) {
   return p;
 }
 
-int fft_wide() {
-  static const int v = [] {
-    const char* e = std::getenv("AD_FFT_WIDE");
-    return e ? std::atoi(e) : 0;
-  }();
-  return v;
-}
-
 template <int R, bool FWD, bool RI, bool RO>
 void go_pass(const FftPassArgs& a, int batch, hipStream_t s) {
   if constexpr (!FWD && !RI) {
@@ -287,14 +316,8 @@ void go_pass(const FftPassArgs& a, int batch, hipStream_t s) {
   }
   const int64_t nb = a.N / R;
   constexpr int F1 = FftPlan<R, 16>::F;
-  constexpr int F2 = (8192 / R) > F1 ? (8192 / R) : F1;
-  if (fft_wide() && F2 != F1 && nb >= F2) {
-    const dim3 grid((unsigned)((nb + F2 - 1) / F2), (unsigned)batch);
-    hipLaunchKernelGGL((k_fft_pass<R, F2, FWD, RI, RO>), grid, dim3(PassShape<R, F2>::BLOCK), 0, s, a);
-  } else {
-    const dim3 grid((unsigned)((nb + F1 - 1) / F1), (unsigned)batch);
-    hipLaunchKernelGGL((k_fft_pass<R, F1, FWD, RI, RO>), grid, dim3(PassShape<R, F1>::BLOCK), 0, s, a);
-  }
+  const dim3 grid((unsigned)((nb + F1 - 1) / F1), (unsigned)batch);
+  hipLaunchKernelGGL((k_fft_pass<R, F1, FWD, RI, RO>), grid, dim3(PassShape<R, F1>::BLOCK), 0, s, a);
 }
 
 template <bool FWD, bool RI, bool RO>
@@ -339,12 +362,8 @@ BigFft::BigFft(int64_t N) : N_(N) {
     radix_.push_back((int)N);
     S_ = (k + 1) / 2;
   } else {
-    // passes of radix <= 2^maxlog (AD_FFT_LOGR, A/B knob; 9 = radix 512)
-    static const int maxlog = [] {
-      const char* e = std::getenv("AD_FFT_LOGR");
-      const int v = e ? std::atoi(e) : 9;
-      return v >= 4 && v <= 9 ? v : 9;
-    }();
+    // passes of radix <= 2^maxlog = 512 (F >= 8: 128-B runs)
+    constexpr int maxlog = 9;
     const int np = (k + maxlog - 1) / maxlog;
     const int base = k / np, extra = k % np;
     for (int p = 0; p < np; ++p) radix_.push_back(1 << (base + (p < extra ? 1 : 0)));
@@ -379,15 +398,21 @@ void BigFft::run(bool forward, const double2* in, const double* xr, int64_t n_re
 }
 
 void BigFft::correlate_half(const BigFft& half, const double* a_, int64_t n, const double* b_, int64_t m,
-                            double2* spec, double* out, double2* scratch, hipStream_t s) const {
+                            double2* spec, double* out, double2* scratch, unsigned long long* amax,
+                            hipStream_t s) const {
+  AD_HIP(hipMemsetAsync(amax, 0, 2 * sizeof(unsigned long long), s));
+  const int64_t mx = std::max(n, m);
+  const unsigned gx = (unsigned)std::min<int64_t>(1024, (mx + 255) / 256);
+  hipLaunchKernelGGL(k_absmax2, dim3(gx, 2), dim3(256), 0, s, a_, n, b_, m, amax);
+  AD_HIP(hipGetLastError());
   // lags 0..n-1 from the front, -(m-1)..-1 from the back (correlate.go:165-171)
-  spectral_half(half, kSpecCorr, 0.0, nullptr, true, a_, n, b_, m, n, m - 1, N_ - m + 1, spec, out, scratch, s);
+  spectral_half(half, kSpecCorr, 0.0, nullptr, true, a_, n, b_, m, n, m - 1, N_ - m + 1, spec, out, scratch, s, amax);
 }
 
 void BigFft::spectral_half(const BigFft& half, int op, double eps, unsigned long long* bad, bool pack,
                            const double* a_, int64_t n, const double* b_, int64_t m, int64_t n_front,
                            int64_t front_off, int64_t back_from, double2* spec, double* out, double2* scratch,
-                           hipStream_t s) const {
+                           hipStream_t s, const unsigned long long* amax) const {
   FftPassArgs a{};
   a.N = N_;
   a.tw_lo = tw_lo_;
@@ -400,6 +425,7 @@ void BigFft::spectral_half(const BigFft& half, int op, double eps, unsigned long
   a.nr[1] = m;
   if (pack) {
     a.pack2 = 1;  // Z = FFT(a + i b)
+    a.amax = amax;
     run_passes(true, a, nullptr, a_, 0, spec, nullptr, N_, 1, scratch, s);
   } else {  // FFT(a) and FFT(b) as a batch of two real inputs: spec [2][N]
     run_passes(true, a, nullptr, a_, 0, spec, nullptr, N_, 2, scratch, s);
@@ -420,6 +446,7 @@ void BigFft::spectral_half(const BigFft& half, int op, double eps, unsigned long
   i.eps = eps;
   i.bad = bad;
   i.remap = 1;
+  i.amax = pack ? amax : nullptr;
   i.n_front = n_front;
   i.front_off = front_off;
   i.back_from = back_from;

@@ -44,6 +44,11 @@ struct FftPassArgs {
   const double* xb[2];
   int64_t nr[2];
   int pack2;    // first forward pass: one complex input xb[0] + i xb[1] (both real signals in one transform)
+  // pack2 correlation: {max|a|, max|b|} as IEEE bit patterns (k_absmax2).  The
+  // first pass multiplies b by 2^e (e = exponent(max|a|) - exponent(max|b|)) so
+  // both halves of a + i b have the same scale, and the last pass multiplies
+  // the outputs by 2^-e (both exact).  null: no scaling.
+  const unsigned long long* amax;
   // half: the inverse of the Hermitian A conj(B) as an N/2-point transform
   // (this plan is N/2 = NF/2): its first pass forms z[k] = E[k] + i O[k] from
   // X[k] and X[k + NF/2] (E = (X[k] + X[k+NF/2])/2, O = (X[k] - X[k+NF/2]) W_NF^-k / 2,
@@ -83,8 +88,11 @@ class BigFft {
   // caller's arrays) into spec [N]; then the inverse of the Hermitian
   // A conj(B) on the half plan (N/2 points), written in lag order to out
   // (n + m - 1 values, correlate.go:165-171).  Both plans need passes (N >= 32).
+  // amax: 2 words of device scratch for the packing scale (FftPassArgs::amax):
+  // without it, b's spectrum taken out of FFT(a + i b) would carry rounding
+  // error of order eps |A|, which for |a| >> |b| is far above eps |B|.
   void correlate_half(const BigFft& half, const double* a, int64_t n, const double* b, int64_t m, double2* spec,
-                      double* out, double2* scratch, hipStream_t s) const;
+                      double* out, double2* scratch, unsigned long long* amax, hipStream_t s) const;
   // The same structure for any SpecOp: Z = FFT(x + i h) (x: n, h: m real
   // samples; h may be null), the inverse of op(X, H) at half length, real
   // outputs o < n_front to out[front_off + o] and o >= back_from to
@@ -94,7 +102,8 @@ class BigFft {
   // so Deconvolve transforms x and h separately: pack = false, spec [2][N]).
   void spectral_half(const BigFft& half, int op, double eps, unsigned long long* bad, bool pack, const double* x,
                      int64_t n, const double* h, int64_t m, int64_t n_front, int64_t front_off, int64_t back_from,
-                     double2* spec, double* out, double2* scratch, hipStream_t s) const;
+                     double2* spec, double* out, double2* scratch, hipStream_t s,
+                     const unsigned long long* amax = nullptr) const;
 
  private:
   int64_t N_;

@@ -92,7 +92,12 @@ struct ad_conv {
   int64_t hop = 0;
   int64_t seg_next = -1;  // next out_begin of a segmented offline call (-1: none open)
 
-  // time-domain streaming path (hop too small for the FFT engine)
+  // streaming blocks that are not a whole number of hops: samples of the
+  // unfinished block carried in pin_in (stream_convolve)
+  bool partial = false;
+  int64_t part_fill = 0;
+
+  // time-domain streaming path (blocks of fewer than 64 samples)
   bool direct_stream = false;
   DevBuf<double> hdev;
   DevBuf<double> sbuf[2];
@@ -115,9 +120,8 @@ struct ad_conv {
   bool has_last = false;
   hipEvent_t done = nullptr;
 
-  // partitioned: non-uniform multi-stage engine (latency >= 64)
-  std::unique_ptr<Nupols> nup;
-  std::unique_ptr<NupolsDev> nupd;  // many-channel device-resident form
+  // partitioned: non-uniform multi-stage engine (64 <= latency <= 8192)
+  std::unique_ptr<NupolsDev> nupd;
 
   // partitioned FIFO state (latency < 64: time-domain streaming fallback shape)
   std::vector<double> pending;   // input samples not yet convolved (< hop)
@@ -131,7 +135,6 @@ struct ad_conv {
       (void)hipEventSynchronize(done);
       (void)hipEventDestroy(done);
     }
-    nup.reset();
     nupd.reset();
     eng.reset();
     if (stream) (void)hipStreamSynchronize(stream);
@@ -166,17 +169,30 @@ void mark_last(ad_conv* h, hipStream_t s) {
   h->has_last = true;
 }
 
-// zero-latency streaming convolution state for `hop` sized chunks
+// Zero-latency streaming convolution state for blocks of B samples
+// (StreamingOverlapSaveT / StreamingOverlapAddT, streaming_overlap_save.go:45-164):
+//  - B with a power-of-two divisor >= 256 (or B itself a power of two >= 64):
+//    the hop is that divisor and every call is B/hop whole engine blocks;
+//  - any other B >= 64 (480, 960, 1000, 4800 ...): hop = nextPow2(B) (<= 8192)
+//    and the partial block is carried: a call re-transforms the block it
+//    ends in with the samples not yet received read as zeros.  The output
+//    sample r of a block depends only on inputs <= r, so the zeros never
+//    reach an emitted sample, and once the block is complete its spectrum in
+//    the delay line is final.  A call costs one or two FFT blocks (at most
+//    ceil((hop - 1 + B) / hop)), never an O(K) time-domain sum per sample;
+//  - B < 64: the time-domain kernel.
 void setup_stream_engine(ad_conv* h, const double* kernel, int64_t K, int64_t B, int64_t hop_cap) {
-  if (const char* v = std::getenv("AD_STREAM_HOP_CAP")) {  // A/B override for sweeps
-    const int64_t c = std::atoll(v);
-    if (c >= 64 && is_pow2(c)) hop_cap = std::min(hop_cap, c);
+  int64_t hop = largest_pow2_divisor(B, hop_cap);
+  if (hop < 256 && hop != B && B >= 64) {
+    hop = std::min<int64_t>(hop_cap, next_pow2(B));
+    h->partial = (B % hop) != 0;
   }
-  const int64_t hop = largest_pow2_divisor(B, hop_cap);
   h->hop = hop;
   h->conv_len = K;
+  h->part_fill = 0;
   if (hop >= 64) {
-    const int jc = (int)std::max<int64_t>(1, std::min<int64_t>(B / hop, 256));
+    const int64_t blocks = h->partial ? (hop - 1 + B + hop - 1) / hop : B / hop;
+    const int jc = (int)std::max<int64_t>(1, std::min<int64_t>(blocks, 256));
     h->eng.reset(new Upols(h->device, kernel, 1, K, (int)hop, 1, nullptr, jc, h->stream));
   } else {
     h->direct_stream = true;
@@ -193,6 +209,7 @@ void stream_reset(ad_conv* h) {
   h->ylin.clear();
   h->emitted = 0;
   h->ylin_base = 0;
+  h->part_fill = 0;
   AD_HIP(hipStreamSynchronize(h->stream));
 }
 
@@ -232,36 +249,50 @@ void stream_convolve(ad_conv* h, const double* in, int64_t n, double* out) {
   // kernels and one synchronisation, no DMA round trips.  K1 transforms each
   // input block once and keeps no input history (the previous block's
   // spectrum is in the delay line), so nothing but the block itself crosses
-  // PCIe: config 2 measured 37.8 us per block direct vs 42.4-43.7 staged
-  // through two copy kernels (AD_STREAM_STAGE=1).
-  if (h->pin_n < (size_t)n) {
+  // PCIe (config 2 measured 37.8 us per block direct vs 42.4-43.7 staged
+  // through HBM by two copy kernels).
+  // Partial-block form (h->partial): pin_in holds the samples of the block the
+  // last call ended in (part_fill of them) followed by this call's; K1
+  // transforms every block they touch (zeros past the last sample), K3 writes
+  // those blocks whole to pin_out, and the call's samples are the slice
+  // [part_fill, part_fill + n).  An unfinished last block is not committed:
+  // the engine's block counter steps back so the next call transforms it
+  // again with more samples.
+  const int64_t L = h->hop;
+  const size_t need_in = h->partial ? (size_t)(L + n) : (size_t)n;
+  const size_t need_out = h->partial ? (size_t)(((L - 1 + n + L - 1) / L) * L) : (size_t)n;
+  const size_t need = std::max(need_in, need_out);
+  if (h->pin_n < need) {
+    std::vector<double> keep(h->pin_in, h->pin_in + (h->pin_in ? h->part_fill : 0));
     if (h->pin_in) AD_HIP(hipHostFree(h->pin_in));
     if (h->pin_out) AD_HIP(hipHostFree(h->pin_out));
     h->pin_in = h->pin_out = nullptr;
     h->pin_n = 0;
-    AD_HIP(hipHostMalloc(reinterpret_cast<void**>(&h->pin_in), n * sizeof(double), hipHostMallocMapped));
-    AD_HIP(hipHostMalloc(reinterpret_cast<void**>(&h->pin_out), n * sizeof(double), hipHostMallocMapped));
+    AD_HIP(hipHostMalloc(reinterpret_cast<void**>(&h->pin_in), need * sizeof(double), hipHostMallocMapped));
+    AD_HIP(hipHostMalloc(reinterpret_cast<void**>(&h->pin_out), need * sizeof(double), hipHostMallocMapped));
     AD_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&h->pin_in_dev), h->pin_in, 0));
     AD_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&h->pin_out_dev), h->pin_out, 0));
-    h->pin_n = (size_t)n;
+    h->pin_n = need;
+    if (!keep.empty()) std::memcpy(h->pin_in, keep.data(), keep.size() * sizeof(double));
   }
-  std::memcpy(h->pin_in, in, n * sizeof(double));
-  static const bool staged = [] {  // A/B: AD_STREAM_STAGE=1 stages the block through HBM with copy kernels
-    const char* v = std::getenv("AD_STREAM_STAGE");
-    return v && v[0] == '1';
-  }();
-  if (staged) {
-    // wide copy kernels move the block over PCIe; K1 and K3 then work on HBM
-    h->din.reserve((size_t)n);
-    h->dout.reserve((size_t)n);
-    launch_copy_f64(h->pin_in_dev, h->din.p, n, s);
-    h->eng->run(h->din.p, n, n, h->dout.p, n, n, /*use_hist=*/true, s);
-    launch_copy_f64(h->dout.p, h->pin_out_dev, n, s);
-  } else {
+  if (!h->partial) {
+    std::memcpy(h->pin_in, in, n * sizeof(double));
     h->eng->run(h->pin_in_dev, n, n, h->pin_out_dev, n, n, /*use_hist=*/true, s);
+    AD_HIP(hipStreamSynchronize(s));
+    std::memcpy(out, h->pin_out, n * sizeof(double));
+    return;
   }
+  const int64_t f0 = h->part_fill;
+  const int64_t tot = f0 + n;
+  const int64_t blocks = (tot + L - 1) / L;
+  std::memcpy(h->pin_in + f0, in, n * sizeof(double));
+  h->eng->run(h->pin_in_dev, tot, tot, h->pin_out_dev, blocks * L, blocks * L, /*use_hist=*/true, s);
+  const int64_t full = (tot / L) * L;
+  if (full < tot) h->eng->rewind(1);  // the last block is not complete yet
   AD_HIP(hipStreamSynchronize(s));
-  std::memcpy(out, h->pin_out, n * sizeof(double));
+  std::memcpy(out, h->pin_out + f0, n * sizeof(double));
+  if (full > 0 && full < tot) std::memmove(h->pin_in, h->pin_in + full, (size_t)(tot - full) * sizeof(double));
+  h->part_fill = tot - full;
 }
 
 // Offline full convolution of host channels with the handle's kernel(s):
@@ -370,6 +401,15 @@ std::vector<double> widen(const float* p, int64_t n) {
   for (int64_t i = 0; i < n; ++i) v[(size_t)i] = (double)p[i];
   return v;
 }
+// Per-block float32 calls: validate before touching the buffers, then widen
+// into the handle's reused vector (no allocation on the streaming hot path).
+void widen_block(ad_conv* h, const float* in, int64_t in_len, const float* out, int64_t out_len) {
+  if (in_len < 0 || out_len < 0) AD_FAIL(AD_ERR_LENGTH_MISMATCH, "conv: negative buffer length");
+  if ((in_len > 0 && !in) || (out_len > 0 && !out)) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "null sample buffer");
+  h->w_in.resize((size_t)in_len);
+  for (int64_t i = 0; i < in_len; ++i) h->w_in[(size_t)i] = (double)in[i];
+  h->w_out.resize((size_t)out_len);
+}
 }  // namespace
 
 extern "C" {
@@ -404,8 +444,11 @@ int ad_conv_process_block32(ad_conv* h, const float* in, int64_t in_len, float* 
   return guard([&] {
     if (!h) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "nil handle");
     if (!h->f32) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "not a float32 convolver");
-    h->w_in = widen(in, in_len);
-    h->w_out.resize((size_t)std::max<int64_t>(out_len, 0));
+    if (in_len != h->block_size || out_len != h->block_size)
+      AD_FAIL(AD_ERR_LENGTH_MISMATCH, "conv: buffer length mismatch: expected " + std::to_string(h->block_size) +
+                                          " samples, got " + std::to_string(in_len) + " in / " +
+                                          std::to_string(out_len) + " out");
+    widen_block(h, in, in_len, out, out_len);
     const int rc = ad_conv_process_block(h, h->w_in.data(), in_len, h->w_out.data(), out_len);
     if (rc != AD_OK) throw Status{rc, ad_last_error()};
     for (int64_t i = 0; i < out_len; ++i) out[i] = (float)h->w_out[(size_t)i];
@@ -429,8 +472,10 @@ int ad_conv_partitioned_process_block32(ad_conv* h, const float* in, int64_t in_
   return guard([&] {
     if (!h) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "nil handle");
     if (!h->f32) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "not a float32 convolver");
-    h->w_in = widen(in, in_len);
-    h->w_out.resize((size_t)std::max<int64_t>(out_len, 0));
+    if (in_len != out_len)
+      AD_FAIL(AD_ERR_LENGTH_MISMATCH, "conv: buffer length mismatch: input length " + std::to_string(in_len) +
+                                          " != output length " + std::to_string(out_len));
+    widen_block(h, in, in_len, out, out_len);
     const int rc = ad_conv_partitioned_process_block(h, h->w_in.data(), in_len, h->w_out.data(), out_len);
     if (rc != AD_OK) throw Status{rc, ad_last_error()};
     for (int64_t i = 0; i < out_len; ++i) out[i] = (float)h->w_out[(size_t)i];
@@ -525,21 +570,15 @@ int ad_conv_partitioned_create(const double* kernel, int64_t K, int min_order, i
     for (const auto& s : h->stages) cover = std::max(cover, s.start + s.count * s.part_size);
     const int64_t keff = std::min<int64_t>(K, cover);
     h->fft_size = 2 * h->stages.back().part_size;
-    const char* uni = std::getenv("AD_PC_UNIFORM");
-    const char* eng = std::getenv("AD_PC_ENGINE");  // "host": the per-stage-stream engine with host accumulation
-    if (latency >= 64 && latency <= 8192 && !(uni && *uni == '1') && !(eng && !std::strcmp(eng, "host"))) {
-      // Device-resident non-uniform stages (NupolsDev, one channel): mapped
-      // pinned block I/O, the accumulator on the device, emit-before-convolve.
+    if (latency >= 64 && latency <= 8192) {
+      // Device-resident non-uniform stages (NupolsDev, one channel): hop lambda
+      // for the head of the IR, doubling up to 2^maxBlockOrder (<= 8192) for
+      // the tail; mapped pinned block I/O, the accumulator on the device,
+      // emit-before-convolve.
       const int64_t pmax = std::min<int64_t>(8192, std::max<int64_t>(latency, int64_t(1) << std::min(max_order, 13)));
       h->conv_len = keff;
       h->nupd.reset(new NupolsDev(dev, kernel, keff, latency, pmax, 1, h->stream));
       AD_HIP(hipStreamSynchronize(h->stream));
-    } else if (latency >= 64 && latency <= 8192 && !(uni && *uni == '1')) {
-      // Non-uniform stages: hop lambda for the head of the IR, doubling up to
-      // 2^maxBlockOrder (<= 8192) for the tail (nupols_engine.hpp).
-      const int64_t pmax = std::min<int64_t>(8192, std::max<int64_t>(latency, int64_t(1) << std::min(max_order, 13)));
-      h->conv_len = keff;
-      h->nup.reset(new Nupols(dev, kernel, keff, latency, pmax));
     } else {
       // Zero-latency engine with hop = latency (<= 8192), output delayed by latency.
       setup_stream_engine(h.get(), kernel, keff, latency, 8192);
@@ -560,11 +599,6 @@ int ad_conv_partitioned_process_block(ad_conv* h, const double* in, int64_t in_l
     DeviceScope ds(h->device);
     if (h->nupd) {
       h->nupd->process_host(in, out, in_len, /*mix=*/false, 1.0, 0.0, h->stream);
-      h->emitted += in_len;
-      return;
-    }
-    if (h->nup) {
-      h->nup->process(in, in_len, out);
       h->emitted += in_len;
       return;
     }
@@ -651,10 +685,32 @@ int ad_conv_reset(ad_conv* h) {
     if (!h) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "nil handle");
     DeviceScope ds(h->device);
     if (h->has_last) AD_HIP(hipStreamWaitEvent(h->stream, h->done, 0));  // after the last device call
-    if (h->nup) h->nup->reset();
     if (h->nupd) h->nupd->reset(h->stream);
     stream_reset(h);
     h->has_last = false;
+  });
+}
+
+int ad_conv_set_host_io(ad_conv* h, int mode, int workers) {
+  return guard([&] {
+    if (!h) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "nil handle");
+    if (mode < AD_HOST_IO_AUTO || mode > AD_HOST_IO_REGISTER) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "unknown host I/O mode");
+    if (workers < 0 || workers > 64) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "copy workers must be in [0, 64]");
+    if (h->kind != Kind::BatchOLS && h->kind != Kind::BatchOLA && h->kind != Kind::Multi)
+      AD_FAIL(AD_ERR_INVALID_ARGUMENT, "host I/O mode applies to batch / multi-channel convolvers");
+    DeviceScope ds(h->device);
+    if (!h->pipe) h->pipe.reset(new HostPipeline(h->device));
+    h->pipe->set_mode(mode, workers);
+  });
+}
+
+int ad_conv_host_io_profile(const ad_conv* h, double* register_ms, double* transfer_ms, double* unregister_ms) {
+  return guard([&] {
+    if (!h) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "nil handle");
+    const HostPipeline* p = h->pipe.get();
+    if (register_ms) *register_ms = p ? p->last_register_ms() : 0.0;
+    if (transfer_ms) *transfer_ms = p ? p->last_transfer_ms() : 0.0;
+    if (unregister_ms) *unregister_ms = p ? p->last_unregister_ms() : 0.0;
   });
 }
 

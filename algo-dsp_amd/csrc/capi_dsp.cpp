@@ -66,6 +66,27 @@ void check_comp_config(const ad_compressor_config& g) {
   if (!(g.rms_window_ms > 0)) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "dynamics: rms window must be positive");
 }
 
+// EQ state on the device is kept per pass of <= kMaxSecPerPass sections,
+// each pass a slab [C][ns][2]; the ABI's layout is [C][nsec][2].
+void eq_state_from_slabs(const double* raw, int C, int nsec, double* state) {
+  for (int s0 = 0; s0 < nsec; s0 += kMaxSecPerPass) {
+    const int ns = std::min(kMaxSecPerPass, nsec - s0);
+    for (int c = 0; c < C; ++c)
+      for (int i = 0; i < ns; ++i)
+        for (int k = 0; k < 2; ++k)
+          state[((int64_t)c * nsec + s0 + i) * 2 + k] = raw[(size_t)C * s0 * 2 + ((size_t)c * ns + i) * 2 + k];
+  }
+}
+void eq_state_to_slabs(const double* state, int C, int nsec, double* raw) {
+  for (int s0 = 0; s0 < nsec; s0 += kMaxSecPerPass) {
+    const int ns = std::min(kMaxSecPerPass, nsec - s0);
+    for (int c = 0; c < C; ++c)
+      for (int i = 0; i < ns; ++i)
+        for (int k = 0; k < 2; ++k)
+          raw[(size_t)C * s0 * 2 + ((size_t)c * ns + i) * 2 + k] = state[((int64_t)c * nsec + s0 + i) * 2 + k];
+  }
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -102,6 +123,12 @@ struct ad_fx_chain {
   DevBuf<double> xT[kFxSlots], vT[kFxSlots], envT[kFxSlots], inT[kFxSlots], coT[kFxSlots];
   DevBuf<double> midT[kFxSlots];  // split K_eq: the first part's output rows
   int64_t tmax = 0;
+  // engine selection (ad_fx_chain_set_engine) and per-wave clock counters of
+  // the first chunk of each call (ad_fx_chain_set_profiling)
+  int engine = AD_FX_ENGINE_AUTO;
+  int64_t chunk = 0;  // staged chunk length (0: kFxChunk)
+  bool prof_on = false;
+  DevBuf<unsigned long long> prof;
 
   ~ad_fx_chain() {
     for (hipStream_t x : st)
@@ -160,14 +187,13 @@ void fx_reset_verb(ad_fx_chain* h) {
 // its latest record when chunk i is enqueued.  Feed-forward compressor only
 // (the feedback topology's gain feeds its own detector).
 bool fx_staged_ok(const ad_fx_chain* h) {
-  const char* v = std::getenv("AD_FX_STAGED");  // read per call: tests compare both engines
-  const bool on = !(v && v[0] == '0');
   // With Freeverb, beyond ~8k channels the fused kernels fill the chip on
   // their own and win (tools/fx_crossover.py: 16384 ch config 5 fused 22.2
   // vs staged 11.6 Gsamples/s; 4096 ch staged 9.7 vs fused 8.3).
+  if (h->engine == AD_FX_ENGINE_FUSED) return false;
   if (h->verb_on && h->channels > 8192) return false;
   if (h->comp_on && h->cp.mode == 2) return false;  // the gate's hold counter is serial in its gain
-  return on && h->staged_ok && (!h->comp_on || !h->cp.topology_fb) && h->nsec <= kMaxSecPerPass &&
+  return h->staged_ok && (!h->comp_on || !h->cp.topology_fb) && h->nsec <= kMaxSecPerPass &&
          (h->nsec > 0 || h->comp_on || h->verb_on);
 }
 
@@ -175,21 +201,25 @@ bool fx_staged_ok(const ad_fx_chain* h) {
 // chunk i - 1, one launch): the EQ recurrences of a channel group run on two
 // CUs, every wave on a SIMD of its own.  Returns s1, or 0 for one pipeline.
 int fx_eq_split(const ad_fx_chain* h) {
-  const char* v = std::getenv("AD_FX_EQSPLIT");
-  if (v && v[0] == '0') return 0;
+  if (h->engine == AD_FX_ENGINE_STAGED_NOSPLIT) return 0;
   if (!h->comp_on || h->nsec < 3) return 0;
   return (h->nsec + 2) / 2;  // part waves (s1 + loader) vs (ns - s1 + detector + loader)
 }
 
-int64_t fx_chunk() {
-  const char* v = std::getenv("AD_FX_CHUNK");
-  const int64_t t = v ? std::atoll(v) : 0;
-  return t >= 256 ? t : (int64_t)16384;
+constexpr int64_t kFxChunk = 16384;  // staged engine: samples per stage chunk
+constexpr int kFxProfWords = 32;
+
+// The profile counters of this call's first chunk (or nullptr).
+unsigned long long* fx_prof_begin(ad_fx_chain* h, size_t words, hipStream_t s) {
+  if (!h->prof_on) return nullptr;
+  h->prof.reserve(words);
+  AD_HIP(hipMemsetAsync(h->prof.p, 0, h->prof.n * sizeof(unsigned long long), s));
+  return h->prof.p;
 }
 
 void fx_run_staged(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hipStream_t s) {
   const bool eq = h->nsec > 0, comp = h->comp_on, verb = h->verb_on;
-  const int64_t T = std::min(fx_chunk(), n);
+  const int64_t T = std::min(h->chunk > 0 ? h->chunk : kFxChunk, n);
   if (!h->st[0]) {
     for (auto& x : h->st) AD_HIP(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
     for (auto& e2 : h->ev)
@@ -274,23 +304,8 @@ void fx_run_staged(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hip
         const FxStageArgs b = chunk_args(ci - 1);
         if (ci == nch) e = b;
         e.part[e.nparts++] = FxEqPart{s1, h->nsec - s1, 1, b.len, h->midT[(ci - 1) % kFxSlots].p, b.vT, b.envT};
-        static DevBuf<unsigned long long> sprof;
-        const bool want_prof = std::getenv("AD_FX_PROF") != nullptr && ci == 1;
-        if (want_prof) {
-          sprof.reserve(32);
-          AD_HIP(hipMemsetAsync(sprof.p, 0, 32 * sizeof(unsigned long long), s));
-          e.prof = sprof.p;
-        }
+        if (ci == 1) e.prof = fx_prof_begin(h, kFxProfWords, s);
         launch_fx_eq_parts(e, s);
-        if (want_prof) {
-          unsigned long long v[32];
-          AD_HIP(hipStreamSynchronize(s));
-          AD_HIP(hipMemcpy(v, sprof.p, sizeof(v), hipMemcpyDeviceToHost));
-          for (int w = 0; w < 16; ++w)
-            if (v[2 * w] || v[2 * w + 1])
-              fprintf(stderr, "fx split K_eq section/detector %d: compute %llu, barrier wait %llu ticks\n", w, v[2 * w],
-                      v[2 * w + 1]);
-        }
         launch_fx_gain(b, !verb, s);
         if (verb) {
           kl = (int)((ci - 1) % kFxSlots);
@@ -337,14 +352,7 @@ void fx_run_staged(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hip
     a.vp = h->vp;
     a.vs = h->vs.p;
     a.vbuf = h->vbuf.p;
-    if (const char* dv = std::getenv("AD_FX_DBG")) a.dbg = std::atoi(dv);
-    static DevBuf<unsigned long long> eprof;
-    const bool want_prof = std::getenv("AD_FX_PROF") != nullptr && i == 0;
-    if (want_prof) {
-      eprof.reserve(32);
-      AD_HIP(hipMemsetAsync(eprof.p, 0, 32 * sizeof(unsigned long long), s));
-      a.prof = eprof.p;
-    }
+    if (i == 0) a.prof = fx_prof_begin(h, kFxProfWords, s);
     if (verb && reuse) AD_HIP(hipStreamWaitEvent(s, h->ev[EA][k], 0));  // inT / coT of that chunk consumed
     if (eq || comp) {
       launch_fx_transpose_in(a, a.xT, s);
@@ -353,15 +361,6 @@ void fx_run_staged(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hip
       if (!comp && !verb) launch_fx_transpose_out(a, a.vT, s);
     } else {
       launch_fx_transpose_in(a, a.inT, s);
-    }
-    if (want_prof) {
-      unsigned long long v[32];
-      AD_HIP(hipStreamSynchronize(s));
-      AD_HIP(hipMemcpy(v, eprof.p, sizeof(v), hipMemcpyDeviceToHost));
-      for (int w = 0; w < 9; ++w)
-        if (v[2 * w] || v[2 * w + 1])
-          fprintf(stderr, "fx K_eq wave %d: compute %llu, barrier wait %llu ticks (chunk of %lld)\n", w, v[2 * w],
-                  v[2 * w + 1], (long long)a.len);
     }
     if (verb) {
       AD_HIP(hipEventRecord(h->ev[EE][k], s));
@@ -396,13 +395,7 @@ void fx_run(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hipStream_
   a.vp = h->vp;
   a.vs = h->vs.p;
   a.vbuf = h->vbuf.p;
-  static DevBuf<unsigned long long> prof;
-  const bool want_prof = std::getenv("AD_FX_PROF") != nullptr;
-  if (want_prof) {
-    prof.reserve((size_t)((h->channels + 63) / 64) * 16);
-    AD_HIP(hipMemsetAsync(prof.p, 0, prof.n * sizeof(unsigned long long), s));
-    a.prof = prof.p;
-  }
+  a.prof = fx_prof_begin(h, std::max<size_t>(kFxProfWords, (size_t)((h->channels + 63) / 64) * 16), s);
   const int post = (h->comp_on ? 2 : 0) | (h->verb_on ? 4 : 0);
   // EQ sections in passes of <= kMaxSecPerPass; the last pass fuses the
   // compressor and Freeverb stages (per-sample fusion is exact, see kernels)
@@ -422,14 +415,6 @@ void fx_run(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hipStream_
   } while (s0 < h->nsec);
   AD_HIP(hipGetLastError());
   AD_HIP(hipEventRecord(h->ev_last, s));
-  if (want_prof) {
-    std::vector<unsigned long long> v(prof.n);
-    AD_HIP(hipStreamSynchronize(s));
-    AD_HIP(hipMemcpy(v.data(), prof.p, v.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-    for (int w = 0; w < 8; ++w)
-      if (v[w * 2 + 1]) fprintf(stderr, "fx-pipe wave %d: busy %llu of %llu ticks (%.1f%%)\n", w, v[w * 2], v[w * 2 + 1],
-                                100.0 * v[w * 2] / v[w * 2 + 1]);
-  }
 }
 
 }  // namespace
@@ -641,18 +626,55 @@ int ad_fx_chain_eq_state(ad_fx_chain* h, double* state, int64_t cap) {
   return fx_guard(h, [&] {
     const int64_t need = (int64_t)h->channels * h->nsec * 2;
     if (cap < need) AD_FAIL(AD_ERR_LENGTH_MISMATCH, "state buffer too small");
+    if (need > 0 && !state) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "null state buffer");
     fx_quiesce(h);
-    // device layout: per pass slab [C][ns][2]; return [C][nsec][2]
     std::vector<double> raw((size_t)need);
     if (need) AD_HIP(hipMemcpy(raw.data(), h->eq_state.p, need * sizeof(double), hipMemcpyDeviceToHost));
-    for (int s0 = 0; s0 < h->nsec; s0 += kMaxSecPerPass) {
-      const int ns = std::min(kMaxSecPerPass, h->nsec - s0);
-      for (int c = 0; c < h->channels; ++c)
-        for (int i = 0; i < ns; ++i)
-          for (int k = 0; k < 2; ++k)
-            state[((int64_t)c * h->nsec + s0 + i) * 2 + k] =
-                raw[(size_t)h->channels * s0 * 2 + ((size_t)c * ns + i) * 2 + k];
-    }
+    eq_state_from_slabs(raw.data(), h->channels, h->nsec, state);
+  });
+}
+
+int ad_fx_chain_set_eq_state(ad_fx_chain* h, const double* state, int64_t n) {
+  // Chain.SetState (chain.go:130-138) / Section.SetState (section.go:152-155)
+  // of every channel: state [channels][nsec][2] {d0, d1}, applied between
+  // calls (after the previous call's work, before the next).
+  return fx_guard(h, [&] {
+    const int64_t need = (int64_t)h->channels * h->nsec * 2;
+    if (n < need) AD_FAIL(AD_ERR_LENGTH_MISMATCH, "state buffer too small: need channels*sections*2 values");
+    if (need > 0 && !state) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "null state buffer");
+    fx_quiesce(h);
+    if (need == 0) return;
+    std::vector<double> raw((size_t)need);
+    eq_state_to_slabs(state, h->channels, h->nsec, raw.data());
+    AD_HIP(hipMemcpy(h->eq_state.p, raw.data(), raw.size() * sizeof(double), hipMemcpyHostToDevice));
+  });
+}
+
+int ad_fx_chain_set_engine(ad_fx_chain* h, int engine, int64_t chunk) {
+  return fx_guard(h, [&] {
+    if (engine < AD_FX_ENGINE_AUTO || engine > AD_FX_ENGINE_STAGED_NOSPLIT)
+      AD_FAIL(AD_ERR_INVALID_ARGUMENT, "unknown effect-chain engine");
+    if (chunk != 0 && chunk < 256) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "staged chunk must be 0 (default) or >= 256");
+    fx_quiesce(h);
+    h->engine = engine;
+    h->chunk = chunk;
+  });
+}
+
+int ad_fx_chain_set_profiling(ad_fx_chain* h, int enable) {
+  return fx_guard(h, [&] {
+    fx_quiesce(h);
+    h->prof_on = enable != 0;
+  });
+}
+
+int ad_fx_chain_read_profile(ad_fx_chain* h, unsigned long long* counters, int cap, int* count) {
+  return fx_guard(h, [&] {
+    fx_quiesce(h);
+    const int n = h->prof.p ? (int)std::min<size_t>(h->prof.n, (size_t)std::max(cap, 0)) : 0;
+    if (n > 0 && !counters) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "null counter buffer");
+    if (n > 0) AD_HIP(hipMemcpy(counters, h->prof.p, (size_t)n * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    if (count) *count = n;
   });
 }
 
@@ -680,21 +702,8 @@ int ad_biquad_chain_process(const double* coeffs, double* state, double gain, do
     }
     int r = ad_fx_chain_set_eq(h, tab.data(), sections, 0);
     if (r != AD_OK) throw Status{r, ad_last_error()};
-    {
-      DeviceScope ds(h->device);
-      // load the caller's state into the pass slabs
-      std::vector<double> raw((size_t)channels * sections * 2);
-      for (int s0 = 0; s0 < sections; s0 += kMaxSecPerPass) {
-        const int ns = std::min(kMaxSecPerPass, sections - s0);
-        for (int c = 0; c < channels; ++c)
-          for (int i = 0; i < ns; ++i)
-            for (int k = 0; k < 2; ++k)
-              raw[(size_t)channels * s0 * 2 + ((size_t)c * ns + i) * 2 + k] =
-                  state[((int64_t)c * sections + s0 + i) * 2 + k];
-      }
-      if (!raw.empty())
-        AD_HIP(hipMemcpy(h->eq_state.p, raw.data(), raw.size() * sizeof(double), hipMemcpyHostToDevice));
-    }
+    r = ad_fx_chain_set_eq_state(h, state, (int64_t)channels * sections * 2);
+    if (r != AD_OK) throw Status{r, ad_last_error()};
     r = ad_fx_chain_process(h, buf, n);
     if (r != AD_OK) throw Status{r, ad_last_error()};
     r = ad_fx_chain_eq_state(h, state, (int64_t)channels * sections * 2);

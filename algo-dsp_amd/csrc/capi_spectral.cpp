@@ -45,7 +45,7 @@ struct DeviceCache {
   std::map<int64_t, std::unique_ptr<BigFft>> plans;
   DevBuf<double2> spec, scratch;
   DevBuf<double> xr, res;
-  DevBuf<unsigned long long> bad;
+  DevBuf<unsigned long long> bad, amax;
 };
 DeviceCache& cache(int dev) {
   static std::mutex m;
@@ -85,7 +85,8 @@ struct SpectralRun {
     if (!h) h.reset(new BigFft(N / 2));
     dc.spec.reserve((size_t)N);
     dc.scratch.reserve((size_t)(2 * N));
-    fft->correlate_half(*h, a, n, b, m, dc.spec.p, out, dc.scratch.p, s);
+    dc.amax.reserve(2);
+    fft->correlate_half(*h, a, n, b, m, dc.spec.p, out, dc.scratch.p, dc.amax.p, s);
   }
   // Deconvolve / InverseFilter through the same structure (x: n, h: m real
   // samples, h may be null): the first n_front real outputs to out.

@@ -194,7 +194,7 @@ struct Unpack {
 // mirror pair of Y, t = conj(W_2M^m) * S and S = 1/8M:
 //   Z.x = (u.x + v.x) S - s t.y (u.x - v.x) - t.x (u.y + v.y)
 //   Z.y = s S (u.y - v.y) + s t.x (u.x - v.x) - t.y (u.y + v.y)
-template <int NH, bool NTZ = false>
+template <int NH>
 struct ZEpilogue {
   double2* zb;      // Z row 0 of the channel (wave-uniform)
   unsigned zo;      // this lane's bin position in a row (bin M: the row's padding column M);
@@ -225,7 +225,7 @@ struct ZEpilogue {
     const double2 z = make_double2(fma(-tw.x, sy, fma(-tw.y, sdx, sx * S)), fma(-tw.y, sy, fma(tw.x, sdx, S * sdy)));
     double2* zp = (zb + j * jstride) + zo;
     if constexpr (FIRST) {
-      st2<NTZ>(zp, z);
+      *zp = z;
     } else {
       const double2 o = *zp;
       *zp = make_double2(o.x + z.x, o.y + z.y);
@@ -281,18 +281,11 @@ template <int PC, int NH, bool FIRST, int DQ>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MacOcc<PC, NH>::W))) void k_fdl_mac(MacArgs a) {
   constexpr int BW = 32 / NH;  // bin pairs per wave
   const int lg = xcd_remap(blockIdx.x, gridDim.x);
-  int ry, bx, c;
-  if (a.bx_fast) {  // neighbouring waves: neighbouring bin groups of the same rows
-    bx = lg % a.nx;
-    const int t = lg / a.nx;
-    ry = t % a.ny;
-    c = t / a.ny;
-  } else {  // neighbouring waves: consecutive runs of one bin group
-    ry = lg % a.ny;
-    const int t = lg / a.ny;
-    bx = t % a.nx;
-    c = t / a.nx;
-  }
+  // neighbouring waves: consecutive runs of one bin group (they re-read each
+  // other's warm-up rows)
+  const int ry = lg % a.ny;
+  const int bx = (lg / a.ny) % a.nx;
+  const int c = lg / a.ny / a.nx;
   const int lane = threadIdx.x;
   const bool ph = NH == 2 && lane >= 32;
   const bool mi = NH == 2 ? ((lane >> 4) & 1) : (lane >> 5);
@@ -471,25 +464,17 @@ template <int PC, int NH>
 struct MacOccL {
   static constexpr int W = PC <= 8 ? 4 : 3;
 };
-// NTZ (AD_K2_NT=1): non-temporal Z stores.
-template <int PC, int NH, bool FIRST, int DL, bool NTZ = false>
+template <int PC, int NH, bool FIRST, int DL>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MacOccL<PC, NH>::W))) void k_fdl_mac_lds(MacArgs a) {
   static_assert(DL <= 16 && PC % DL == 0, "ring depth: slots must repeat every group");
   __shared__ double2 ring[DL * 64];
   constexpr int BW = 32 / NH;
   const int lg = xcd_remap(blockIdx.x, gridDim.x);
-  int ry, bx, c;
-  if (a.bx_fast) {  // neighbouring waves: neighbouring bin groups of the same rows
-    bx = lg % a.nx;
-    const int t = lg / a.nx;
-    ry = t % a.ny;
-    c = t / a.ny;
-  } else {  // neighbouring waves: consecutive runs of one bin group
-    ry = lg % a.ny;
-    const int t = lg / a.ny;
-    bx = t % a.nx;
-    c = t / a.nx;
-  }
+  // neighbouring waves: consecutive runs of one bin group (they re-read each
+  // other's warm-up rows)
+  const int ry = lg % a.ny;
+  const int bx = (lg / a.ny) % a.nx;
+  const int c = lg / a.ny / a.nx;
   const int lane = threadIdx.x;
   const bool ph = NH == 2 && lane >= 32;
   const bool mi = NH == 2 ? ((lane >> 4) & 1) : (lane >> 5);
@@ -505,7 +490,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MacOccL<PC, 
   Unpack<NH> up;
   up.m = mi ? (int)0x80000000u : 0;
   up.tw = (k < a.M) ? a.twN[k] : make_double2(-1.0, 0.0);
-  ZEpilogue<NH, NTZ> epi;
+  ZEpilogue<NH> epi;
   epi.S = 0.125 / (double)a.M;
   epi.m = up.m;
   const int zpos = zrow_pos(k, a.M);
@@ -644,82 +629,9 @@ __global__ __launch_bounds__(256) void k_fdl_mac_row(MacArgs a) {
 // Output-stationary: one lane per output sample, so no atomics are needed and
 // the accumulation order is exactly the reference's.
 // ---------------------------------------------------------------------------
-// LDS-tiled form: a workgroup owns 256 consecutive outputs (wave w: k0 +
-// 64 w + lane) and walks the input index i upward in chunks of DC.  The taps
-// b[k - i] a chunk meets sit in LDS (taps outside [0, m) stored as zeros);
-// a[i] is wave-uniform and comes through scalar loads straight into the
-// v_mul's SGPR operand.  Each wave loops only over its own i range
-// [kw - m + 1, kw + 63] (80 % useful at m = 256); a lane whose output does
-// not take term i multiplies a zero tap, and acc + (+-0) == acc exactly (acc
-// starts at +0 and an IEEE sum is never -0 unless both addends are), so the
-// per-output value is still the reference's increasing-i sum of rounded
-// products with rounded adds.  The identity fails only for a non-finite a[i]
-// (inf * 0 = NaN): a chunk holding one takes the per-lane bounds-checked loop.
-constexpr int DC = 1024;
-__global__ __launch_bounds__(256) void k_direct_lds(const double* __restrict__ a, int64_t n,
-                                                    const double* __restrict__ b, int64_t m,
-                                                    double* __restrict__ dst) {
-#pragma clang fp contract(off)
-  constexpr int DT = 256;
-  __shared__ double sb[DT + DC];
-  const int t = threadIdx.x;
-  const int64_t k0 = (int64_t)blockIdx.x * DT;
-  const int64_t kw = k0 + __builtin_amdgcn_readfirstlane(t & ~63);  // first output of this wave
-  const int64_t k = k0 + t;
-  const int64_t out = n + m - 1;
-  // inputs reaching this tile: i in [k0 - m + 1, k0 + DT - 1] and [0, n)
-  const int64_t ilo = k0 - m + 1 > 0 ? k0 - m + 1 : 0;
-  const int64_t ihi = (k0 + DT - 1 < n - 1) ? k0 + DT - 1 : n - 1;
-  const int64_t wlo = kw - m + 1, whi = kw + 63;  // this wave's i range
-  const int64_t lo = k - m + 1, hi = k;           // this lane's
-  double acc = 0.0;
-  for (int64_t i0 = ilo; i0 <= ihi; i0 += DC) {
-    const int cn = (int)(ihi - i0 + 1 < DC ? ihi - i0 + 1 : DC);
-    const int64_t bb = k0 - i0 - (DC - 1);  // sb[u] = b[bb + u]
-    __syncthreads();
-    int bad = 0;
-    for (int u = t; u < cn; u += 256) bad |= !__builtin_isfinite(a[i0 + u]);
-    for (int u = t; u < DT + DC; u += 256) {
-      const int64_t j = bb + u;
-      sb[u] = (j >= 0 && j < m) ? b[j] : 0.0;
-    }
-    bad = __syncthreads_or(bad);
-    const int s0 = __builtin_amdgcn_readfirstlane((int)(wlo > i0 ? wlo - i0 : 0));
-    const int s1 = __builtin_amdgcn_readfirstlane((int)(whi < i0 + cn - 1 ? whi - i0 : cn - 1));
-    const double* sbt = sb + t + (DC - 1);  // sbt[-ii] = b[k - (i0 + ii)]
-    const double* ai = a + i0;
-    if (!bad) {
-      int ii = s0;
-      for (; ii + 7 <= s1; ii += 8) {
-        double av[8], bv[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) av[u] = ai[ii + u];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) bv[u] = sbt[-(ii + u)];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const double p = bv[u] * av[u];
-          acc = acc + p;
-        }
-      }
-      for (; ii <= s1; ++ii) {
-        const double p = sbt[-ii] * ai[ii];
-        acc = acc + p;
-      }
-    } else {
-      for (int ii = s0; ii <= s1; ++ii) {
-        const int64_t i = i0 + ii;
-        if (i >= lo && i <= hi) {
-          const double p = sbt[-ii] * ai[ii];
-          acc = acc + p;
-        }
-      }
-    }
-  }
-  if (k < out) dst[k] = acc;
-}
+constexpr int DC = 1024;  // taps per chunk
 
-// Tap-stationary register-blocked form (the default).  The sum for output k
+// Tap-stationary register-blocked form.  The sum for output k
 // is read the other way round: y[k] = sum over j = m-1 down to 0 of
 // b[j] * a[k-j], which is the same increasing-i order.  b[j] is wave-uniform
 // (scalar loads) and a lane owns R consecutive outputs, so its inputs
@@ -886,83 +798,31 @@ LaunchTiming& launch_timing() {
 }
 
 namespace {
-int mac_depth() {
-  static const int d = [] {
-    const char* v = std::getenv("AD_MAC_D");
-    return (v && std::atoi(v) == 8) ? 8 : 4;
-  }();
-  return d;
-}
-
-template <int PC, int NH, int DQ>
-void mac_go_d(const MacArgs& a, dim3 grid, hipStream_t s) {
-  MacArgs c = a;
-  for (c.p0 = 0; c.p0 < a.P; c.p0 += NH * PC) {
-    if (c.p0 == 0)
-      timed_launch(k_fdl_mac<PC, NH, true, DQ>, grid, dim3(64), s, c);
-    else
-      timed_launch(k_fdl_mac<PC, NH, false, DQ>, grid, dim3(64), s, c);
-  }
-}
-
-int mac_bx_fast() {
-  static const int v = [] {
-    const char* e = std::getenv("AD_MAC_ORDER");
-    return (e && std::atoi(e) == 1) ? 1 : 0;
-  }();
-  return v;
-}
-
-// LDS-ring depth of k_fdl_mac_lds (0 = register prefetch k_fdl_mac).
-int mac_lds_depth() {
-  static const int d = [] {
-    const char* v = std::getenv("AD_MAC_LDS");
-    return v ? std::atoi(v) : 8;
-  }();
-  return d;
-}
-
-int mac_nt() {
-  static const int v = [] {
-    const char* e = std::getenv("AD_K2_NT");
-    return e ? std::atoi(e) : 0;
-  }();
-  return v;
-}
-
-template <int PC, int NH, int DL>
-void mac_go_l(const MacArgs& a, dim3 grid, hipStream_t s) {
-  MacArgs c = a;
-  for (c.p0 = 0; c.p0 < a.P; c.p0 += NH * PC) {
-    if (c.p0 == 0 && mac_nt() == 1)
-      timed_launch(k_fdl_mac_lds<PC, NH, true, DL, true>, grid, dim3(64), s, c);
-    else if (c.p0 == 0)
-      timed_launch(k_fdl_mac_lds<PC, NH, true, DL>, grid, dim3(64), s, c);
-    else
-      timed_launch(k_fdl_mac_lds<PC, NH, false, DL>, grid, dim3(64), s, c);
-  }
-}
-
-template <int PC, int NH>
+// PC < 8: the register-prefetch form (4 rows in flight per lane); PC >= 8: the
+// LDS-DMA ring of 8 rows per wave (its h and accumulator registers leave no
+// room for a register ring at PC = 16).
+template <int PC>
 void mac_go(const MacArgs& a, dim3 grid, hipStream_t s) {
-  if constexpr (PC >= 8) {
-    const int dl = mac_lds_depth();
-    if constexpr (PC >= 16) {
-      if (dl >= 16) return mac_go_l<PC, NH, 16>(a, grid, s);
+  MacArgs c = a;
+  for (c.p0 = 0; c.p0 < a.P; c.p0 += PC) {
+    if constexpr (PC >= 8) {
+      if (c.p0 == 0)
+        timed_launch(k_fdl_mac_lds<PC, 1, true, 8>, grid, dim3(64), s, c);
+      else
+        timed_launch(k_fdl_mac_lds<PC, 1, false, 8>, grid, dim3(64), s, c);
+    } else {
+      if (c.p0 == 0)
+        timed_launch(k_fdl_mac<PC, 1, true, 4>, grid, dim3(64), s, c);
+      else
+        timed_launch(k_fdl_mac<PC, 1, false, 4>, grid, dim3(64), s, c);
     }
-    if (dl >= 8) return mac_go_l<PC, NH, 8>(a, grid, s);
   }
-  if (PC >= 8 && mac_depth() == 8)
-    mac_go_d<PC, NH, 8>(a, grid, s);
-  else
-    mac_go_d<PC, NH, 4>(a, grid, s);
 }
 }  // namespace
 
 // Resident waves per SIMD of the K2 variant that launch_fdl_mac will pick.
 int mac_waves_per_simd(int PC, int NH) {
-  const bool lds = PC >= 8 && mac_lds_depth() >= 8;
-  if (lds) return PC <= 8 ? 4 : 3;  // MacOccL (VGPR-bound; the 8-row ring is 8 KiB per wave)
+  if (PC >= 8) return PC <= 8 ? 4 : 3;    // MacOccL (VGPR-bound; the 8-row ring is 8 KiB per wave)
   return PC <= 4 ? 4 : (PC == 8 ? 3 : 2);  // MacOcc
 }
 
@@ -1003,15 +863,11 @@ void mac_run_geometry(int PC, int NH, int M, int mid_in_k3, int channels, int jc
 
 bool launch_fdl_mac(int PC, int NH, const MacArgs& in, int channels, hipStream_t s) {
   if (channels <= 0 || in.jc <= 0) return true;
+  if (NH != 1) return false;  // one lane holds all of a chunk's partitions
   MacArgs a = in;
-  const int BW = 32 / NH;
-  if (a.M < 2 * BW) return false;  // a pair wave needs M/2 >= BW bins
-  a.nx = a.M / (2 * BW) + (a.mid_in_k3 ? 0 : 1);  // pair waves (+ the middle-bin wave)
-  static const bool row_form = [] {  // AD_MAC_ROW=0: run-based kernels for every call
-    const char* v = std::getenv("AD_MAC_ROW");
-    return !(v && v[0] == '0');
-  }();
-  if (NH == 1 && a.jc <= 2 && row_form) {
+  if (a.M < 64) return false;  // a pair wave needs M/2 >= 32 bins
+  a.nx = a.M / 64 + (a.mid_in_k3 ? 0 : 1);  // pair waves (+ the middle-bin wave)
+  if (a.jc <= 2) {  // one or two outputs per channel: the row form (no H reuse to exploit)
     const int64_t waves = (int64_t)channels * a.nx * a.jc;
     a.ny = (int)waves;
     const dim3 grid((unsigned)((waves + 3) / 4)), blk(256);
@@ -1024,26 +880,14 @@ bool launch_fdl_mac(int PC, int NH, const MacArgs& in, int channels, hipStream_t
       default: return false;
     }
   }
-  mac_run_geometry(PC, NH, a.M, a.mid_in_k3, channels, a.jc, a.R, &a.R, &a.ny);
-  a.bx_fast = mac_bx_fast();
+  mac_run_geometry(PC, 1, a.M, a.mid_in_k3, channels, a.jc, a.R, &a.R, &a.ny);
   const dim3 grid((unsigned)((int64_t)channels * a.nx * a.ny));
-  if (NH == 1) {
-    switch (PC) {
-      case 1: mac_go<1, 1>(a, grid, s); break;
-      case 2: mac_go<2, 1>(a, grid, s); break;
-      case 4: mac_go<4, 1>(a, grid, s); break;
-      case 8: mac_go<8, 1>(a, grid, s); break;
-      case 16: mac_go<16, 1>(a, grid, s); break;
-      default: return false;
-    }
-    return true;
-  }
   switch (PC) {
-    case 1: mac_go<1, 2>(a, grid, s); break;
-    case 2: mac_go<2, 2>(a, grid, s); break;
-    case 4: mac_go<4, 2>(a, grid, s); break;
-    case 8: mac_go<8, 2>(a, grid, s); break;
-    case 16: mac_go<16, 2>(a, grid, s); break;
+    case 1: mac_go<1>(a, grid, s); break;
+    case 2: mac_go<2>(a, grid, s); break;
+    case 4: mac_go<4>(a, grid, s); break;
+    case 8: mac_go<8>(a, grid, s); break;
+    case 16: mac_go<16>(a, grid, s); break;
     default: return false;
   }
   return true;
@@ -1051,17 +895,9 @@ bool launch_fdl_mac(int PC, int NH, const MacArgs& in, int channels, hipStream_t
 
 void launch_direct(const double* a, int64_t n, const double* b, int64_t m, double* dst, hipStream_t s) {
   const int64_t out = n + m - 1;
-  // R = 4 outputs per lane once that still gives >= 2 workgroups per CU;
-  // AD_DIRECT_R=0 selects the input-stationary k_direct_lds (A/B only).
-  static const int forced = [] {
-    const char* e = std::getenv("AD_DIRECT_R");
-    return e ? std::atoi(e) : -1;
-  }();
-  int R = forced >= 0 ? forced : (out >= 512 * 1024 ? 4 : out >= 512 * 512 ? 2 : 1);
+  // R = 4 outputs per lane once that still gives >= 2 workgroups per CU
+  const int R = out >= 512 * 1024 ? 4 : out >= 512 * 512 ? 2 : 1;
   switch (R) {
-    case 0:
-      hipLaunchKernelGGL(k_direct_lds, dim3((unsigned)((out + 255) / 256)), dim3(256), 0, s, a, n, b, m, dst);
-      break;
     case 4:
       hipLaunchKernelGGL(k_direct_reg<4>, dim3((unsigned)((out + 1023) / 1024)), dim3(256), 0, s, a, n, b, m, dst);
       break;

@@ -89,7 +89,6 @@ struct MacArgs {
   int64_t gend;         // last logical block holding input samples (later blocks: zeros)
   int nx, ny;           // bin-pair waves, output runs (set by the launcher)
   int p0;               // first partition of this launch's chunk (set by the launcher)
-  int bx_fast;          // grid order: bin groups fastest (1) or runs fastest (0) (set by the launcher)
   int MS;
   const double2* H;     // [n_ir][P][MS]
   int64_t h_ir_stride;  // P*MS

@@ -746,11 +746,7 @@ bool chain_pipe_ok(int stages, const ChainArgs& a) {
 
 void launch_chain(int stages, const ChainArgs& a, hipStream_t s) {
   if (a.channels <= 0 || a.n <= 0) return;
-  static const bool pipe = [] {
-    const char* v = std::getenv("AD_FX_PIPE");
-    return !(v && *v == '0');
-  }();
-  if (pipe && chain_pipe_ok(stages, a)) {
+  if (chain_pipe_ok(stages, a)) {
     hipLaunchKernelGGL(k_chain_pipe, dim3((unsigned)((a.channels + 63) / 64)), dim3(320), 0, s, a);
     return;
   }

@@ -119,7 +119,6 @@ struct FxStageArgs {
   VerbParams vp;
   VerbChState* vs;
   double* vbuf;
-  int dbg;  // diagnostics only (AD_FX_DBG): bit 0 skip K_eq global stores, bit 1 skip its barrier, bit 2 skip its input loads
   unsigned long long* prof;  // diagnostics only (AD_FX_PROF): K_eq per wave {compute, barrier wait} clock ticks
   FxEqPart part[2];          // K_eq parts (launch_fx_eq_parts)
   int nparts;

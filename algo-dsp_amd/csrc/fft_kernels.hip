@@ -231,8 +231,7 @@ struct SplitPlan {
   static constexpr int LDS = Sub::MP + TwSplit<M2>::N + TwSplit<M>::N;  // double2 elements
 };
 
-// NTF (AD_K1_NT): bit 0 non-temporal input loads, bit 1 non-temporal spectrum stores.
-template <int M, int NTF = 0>
+template <int M>
 __global__ __launch_bounds__((SplitPlan<M>::T)) __attribute__((amdgpu_waves_per_eu(4))) void k_window_rfft_split(RfftArgs a) {
   using SP = SplitPlan<M>;
   constexpr int M2 = SP::M2, V = SP::V, T = SP::T, L = M;
@@ -261,11 +260,11 @@ __global__ __launch_bounds__((SplitPlan<M>::T)) __attribute__((amdgpu_waves_per_
     // E's inputs first: its transform starts while O's are still in flight
 #pragma unroll
     for (int s = 0; s < V; ++s)
-      ev[s] = (s % R0 < R0 / 2) ? ld2<NTF & 1>(reinterpret_cast<const double2*>(xc + t0 + 4 * pass0_index<M2, V>(tid, s)))
+      ev[s] = (s % R0 < R0 / 2) ? *reinterpret_cast<const double2*>(xc + t0 + 4 * pass0_index<M2, V>(tid, s))
                                 : make_double2(0.0, 0.0);
 #pragma unroll
     for (int s = 0; s < V; ++s)
-      ov[s] = (s % R0 < R0 / 2) ? ld2<NTF & 1>(reinterpret_cast<const double2*>(xc + t0 + 4 * pass0_index<M2, V>(tid, s) + 2))
+      ov[s] = (s % R0 < R0 / 2) ? *reinterpret_cast<const double2*>(xc + t0 + 4 * pass0_index<M2, V>(tid, s) + 2)
                                 : make_double2(0.0, 0.0);
   } else {
 #pragma unroll
@@ -287,16 +286,13 @@ __global__ __launch_bounds__((SplitPlan<M>::T)) __attribute__((amdgpu_waves_per_
   for (int s = 0; s < V; ++s) {
     const int k = last_pass_index<M2, V>(tid, s);
     const double2 wo = c_mul(twC(k), ov[s]);
-    st2<(NTF & 2) != 0>(Xo + k, c_add(ev[s], wo));  // k < M/2: xrow_pos(k) = k
-    st2<(NTF & 2) != 0>(Xo + xrow_pos(k + M2, M), c_sub(ev[s], wo));
+    Xo[k] = c_add(ev[s], wo);  // k < M/2: xrow_pos(k) = k
+    Xo[xrow_pos(k + M2, M)] = c_sub(ev[s], wo);
   }
 }
 
-// EXP (diagnostics, AD_K3_EXP; results are wrong for EXP != 0): 1 loads and
-// stores only, 2 transforms and stores without loads, 3 loads and transforms
-// without stores.
-// NTF (AD_K3_NT): bit 0 non-temporal Z loads, bit 1 non-temporal output stores.
-template <int M, int EXP = 0, int NTF = 0>
+// NT: non-temporal Z loads and output stores (large launches, see k3_nt).
+template <int M, bool NT>
 __global__ __launch_bounds__((SplitPlan<M>::T)) __attribute__((amdgpu_waves_per_eu(4))) void k_irfft_store_split(IrfftArgs a) {
   using SP = SplitPlan<M>;
   constexpr int M2 = SP::M2, V = SP::V, T = SP::T, L = M;
@@ -326,11 +322,11 @@ __global__ __launch_bounds__((SplitPlan<M>::T)) __attribute__((amdgpu_waves_per_
   // stream in whole lines, so A's transform starts while B is in flight
 #pragma unroll
   for (int s = 0; s < V; ++s)
-    av[s] = EXP == 2 ? make_double2(tid * 1e-3, s) : ld2<NTF & 1>(Zb + zrow_pos(2 * pass0_index<M2, V>(tid, s), M));
+    av[s] = ld2<NT>(Zb + zrow_pos(2 * pass0_index<M2, V>(tid, s), M));
   __builtin_amdgcn_sched_barrier(0);  // keep B's loads behind A's
 #pragma unroll
   for (int s = 0; s < V; ++s)
-    bv[s] = EXP == 2 ? make_double2(s, tid * 1e-3) : ld2<NTF & 1>(Zb + zrow_pos(2 * pass0_index<M2, V>(tid, s) + 1, M));
+    bv[s] = ld2<NT>(Zb + zrow_pos(2 * pass0_index<M2, V>(tid, s) + 1, M));
   // bin M/2 = 2k at k = M2/2: thread 0, pass-0 slot R0/2
   if (mid) {
     const double2 z = mid_bin_z<M>(a, c, j, ml);
@@ -339,11 +335,9 @@ __global__ __launch_bounds__((SplitPlan<M>::T)) __attribute__((amdgpu_waves_per_
   const TwLds<M2> twS = tw_lds_compute<M2>(lds + FftPlan<M2, V>::MP, tid, T);
   const TwLds<M> twC = tw_lds_compute<M>(lds + FftPlan<M2, V>::MP + TwSplit<M2>::N, tid, T);
   __syncthreads();  // twiddle tables
-  if constexpr (EXP != 1) {
-    fft_run<M2, V, false>(av, tid, lds, twS);
-    __syncthreads();
-    fft_run<M2, V, false>(bv, tid, lds, twS);
-  }
+  fft_run<M2, V, false>(av, tid, lds, twS);
+  __syncthreads();
+  fft_run<M2, V, false>(bv, tid, lds, twS);
   const int64_t ob = a.o0 + (int64_t)j * L;  // output of time index M/2 + m is at ob + 2m
   double* yb = a.out + (int64_t)c * a.out_stride + ob;
 #pragma unroll
@@ -351,17 +345,11 @@ __global__ __launch_bounds__((SplitPlan<M>::T)) __attribute__((amdgpu_waves_per_
     const int m = last_pass_index<M2, V>(tid, s);
     av[s] = c_sub(av[s], c_mul(c_conj(twC(m)), bv[s]));
   }
-  if constexpr (EXP == 3) {
-    bool odd = false;
-#pragma unroll
-    for (int s = 0; s < V; ++s) odd |= av[s].x == 1.2345e300;
-    if (!odd) return;
-  }
   if (a.aligned && ob + 2 * M2 <= a.out_len) {  // wave-uniform fast paths
     if (!a.accumulate) {
 #pragma unroll
       for (int s = 0; s < V; ++s)
-        st2<(NTF & 2) != 0>(reinterpret_cast<double2*>(yb + 2 * last_pass_index<M2, V>(tid, s)), av[s]);
+        st2<NT>(reinterpret_cast<double2*>(yb + 2 * last_pass_index<M2, V>(tid, s)), av[s]);
     } else {
 #pragma unroll
       for (int s = 0; s < V; ++s) {
@@ -386,28 +374,14 @@ __global__ __launch_bounds__((SplitPlan<M>::T)) __attribute__((amdgpu_waves_per_
 // ---------------------------------------------------------------------------
 namespace {
 
-int env_knob(const char* name, int dflt = 0) {
-  const char* e = std::getenv(name);
-  return e ? std::atoi(e) : dflt;
-}
-int k3_exp() {
-  static const int v = env_knob("AD_K3_EXP");
-  return v;
-}
-// K3 default for launches of two or more resident rounds (>= 1024 items):
+// K3 for launches of two or more resident rounds (>= 1024 items):
 // non-temporal Z loads and output stores (both streams are touched once; A/B
 // on one box: step -1 ... -2.6 %, K3 187 -> 152-157 us, part of which
 // reappears in the next kernel as deferred write-back).  Small launches (a
 // streaming block, a host-pipeline segment) keep the cached path: their Z
 // rows were just written by K2 and their output is read back right after.
-int k3_nt(int64_t items) {
-  static const int v = env_knob("AD_K3_NT", -1);
-  return v >= 0 ? v : (items >= 1024 ? 3 : 0);
-}
-int k1_nt() {
-  static const int v = env_knob("AD_K1_NT");
-  return v;
-}
+bool k3_nt(int64_t items) { return items >= 1024; }
+
 template <int M, int V>
 void rfft_go(const RfftArgs& a, hipStream_t s) {
   using Plan = FftPlan<M, V>;
@@ -423,14 +397,6 @@ template <int M>
 void rfft_split_go(const RfftArgs& a, hipStream_t s) {
   const int64_t items = a.ord_R > 0 ? (int64_t)a.channels * (a.ord_ny + 1) * a.ord_R : (int64_t)a.channels * a.jc;
   const dim3 g((unsigned)items), b(SplitPlan<M>::T);
-  if constexpr (M == 8192) {
-    switch (k1_nt()) {
-      case 1: return timed_launch(k_window_rfft_split<M, 1>, g, b, s, a);
-      case 2: return timed_launch(k_window_rfft_split<M, 2>, g, b, s, a);
-      case 3: return timed_launch(k_window_rfft_split<M, 3>, g, b, s, a);
-      default: break;
-    }
-  }
   timed_launch(k_window_rfft_split<M>, g, b, s, a);
 }
 template <int M, int V>
@@ -443,20 +409,10 @@ template <int M>
 void irfft_split_go(const IrfftArgs& a, hipStream_t s) {
   const int64_t items = a.ord_R > 0 ? (int64_t)a.channels * a.ord_ny * a.ord_R : (int64_t)a.channels * a.jc;
   const dim3 g((unsigned)items), b(SplitPlan<M>::T);
-  if constexpr (M == 8192) {
-    switch (k3_exp()) {
-      case 1: return timed_launch(k_irfft_store_split<M, 1>, g, b, s, a);
-      case 2: return timed_launch(k_irfft_store_split<M, 2>, g, b, s, a);
-      case 3: return timed_launch(k_irfft_store_split<M, 3>, g, b, s, a);
-      default: break;
-    }
-  }
-  switch (k3_nt(items)) {
-    case 1: return timed_launch(k_irfft_store_split<M, 0, 1>, g, b, s, a);
-    case 2: return timed_launch(k_irfft_store_split<M, 0, 2>, g, b, s, a);
-    case 3: return timed_launch(k_irfft_store_split<M, 0, 3>, g, b, s, a);
-    default: return timed_launch(k_irfft_store_split<M>, g, b, s, a);
-  }
+  if (k3_nt(items))
+    timed_launch(k_irfft_store_split<M, true>, g, b, s, a);
+  else
+    timed_launch(k_irfft_store_split<M, false>, g, b, s, a);
 }
 
 }  // namespace

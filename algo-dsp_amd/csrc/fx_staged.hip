@@ -659,15 +659,8 @@ __global__ __launch_bounds__(64 * kApW) void k_fx_allpass(FxStageArgs a) {
 
 // The serial stages (K_eq, K_comb, K_ap) are issue/latency bound per wave:
 // their workgroups claim over half a CU's LDS so that no two of them share a
-// CU (config 5: +1.5 %; AD_FX_EXCL=0 turns it off).
-int fx_excl_lds(int own) {
-  static const int on = [] {
-    const char* v = std::getenv("AD_FX_EXCL");
-    return !(v && v[0] == '0');
-  }();
-  if (!on) return 0;
-  return std::max(0, 82 * 1024 - own);
-}
+// CU (config 5: +1.5 %).
+int fx_excl_lds(int own) { return std::max(0, 82 * 1024 - own); }
 
 void launch_fx_eq_parts(const FxStageArgs& a, hipStream_t s) {
   int waves = 0;

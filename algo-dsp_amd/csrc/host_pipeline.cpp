@@ -4,6 +4,8 @@
 // (overlap_add.go:108-182), and the many-channel form of the same.
 #include "host_pipeline.hpp"
 
+#include <chrono>
+
 #include <algorithm>
 #include <cstdlib>
 #include <condition_variable>
@@ -94,33 +96,25 @@ class Pool {
   bool stop_ = false;
 };
 
-int copy_workers() {
-  static const int w = [] {
-    const char* v = std::getenv("AD_PIPE_WORKERS");
-    return v && *v ? std::max(0, std::atoi(v)) : 8;
-  }();
-  return w;
-}
-
 // Copies a [C][len] column range between the caller's per-channel buffers and
 // a packed [C][len] pinned buffer, split into ~1 MiB pieces over the pool.
-void copy_in(double* pin, const double* const* in, int C, int64_t col0, int64_t len) {
+void copy_in(double* pin, const double* const* in, int C, int64_t col0, int64_t len, int workers) {
   const int64_t piece = std::max<int64_t>(1, (int64_t(1) << 17));  // doubles (1 MiB)
   const int64_t per = (len + piece - 1) / piece;
   parallel_for((int64_t)C * per, [&](int64_t k) {
     const int c = (int)(k / per);
     const int64_t a = (k % per) * piece, b = std::min(len, a + piece);
     std::memcpy(pin + (int64_t)c * len + a, in[c] + col0 + a, (size_t)(b - a) * sizeof(double));
-  }, copy_workers());
+  }, workers);
 }
-void copy_out(double* const* out, const double* pin, int C, int64_t col0, int64_t len) {
+void copy_out(double* const* out, const double* pin, int C, int64_t col0, int64_t len, int workers) {
   const int64_t piece = int64_t(1) << 17;
   const int64_t per = (len + piece - 1) / piece;
   parallel_for((int64_t)C * per, [&](int64_t k) {
     const int c = (int)(k / per);
     const int64_t a = (k % per) * piece, b = std::min(len, a + piece);
     std::memcpy(out[c] + col0 + a, pin + (int64_t)c * len + a, (size_t)(b - a) * sizeof(double));
-  }, copy_workers());
+  }, workers);
 }
 
 }  // namespace
@@ -169,19 +163,6 @@ void HostPipeline::ensure_pinned(int64_t doubles) {
 }
 
 namespace {
-// AD_PIPE_MODE: "stage" (pinned staging + host memcpy), "register" (page-lock
-// the caller's buffers for the call and DMA straight from / to them), or
-// "auto" (register calls of >= 64 MiB, stage smaller ones).
-int pipe_mode() {
-  static const int m = [] {
-    const char* v = std::getenv("AD_PIPE_MODE");
-    if (v && !std::strcmp(v, "stage")) return 0;
-    if (v && !std::strcmp(v, "register")) return 1;
-    return 2;
-  }();
-  return m;
-}
-
 // Page-locks [p, p + bytes) for the scope of one call (hipHostRegister);
 // `ok` is false when the runtime refuses, and the caller then stages.
 struct Registration {
@@ -196,30 +177,60 @@ struct Registration {
     }
     ptrs.push_back(const_cast<void*>(p));
   }
-  ~Registration() {
+  void release() {
     for (void* p : ptrs) (void)hipHostUnregister(p);
+    ptrs.clear();
   }
+  ~Registration() { release(); }
 };
+
+double ms_since(std::chrono::steady_clock::time_point t) {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+}
 }  // namespace
 
 void HostPipeline::offline(Upols& eng, const double* const* in, int C, int64_t n, double* const* out,
                            int64_t out_len, hipStream_t s) {
   const int64_t L = eng.hop();
   if (C != eng.channels()) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "channel count differs from the engine's");
-  const int mode = pipe_mode();
+  const int mode = mode_;
   const int64_t bytes = (int64_t)C * (n + out_len) * 8;
-  if (mode == 1 || (mode == 2 && bytes >= (int64_t(64) << 20))) {
+  last_reg_ms_ = last_xfer_ms_ = last_unreg_ms_ = 0;
+  if (mode == kRegister || (mode == kAuto && bytes >= (int64_t(64) << 20))) {
+    auto t0 = std::chrono::steady_clock::now();
     Registration reg;
     for (int c = 0; c < C && reg.ok; ++c) {
       reg.add(in[c], (size_t)n * sizeof(double));
       if (static_cast<const void*>(out[c]) != static_cast<const void*>(in[c]))
         reg.add(out[c], (size_t)out_len * sizeof(double));
     }
+    last_reg_ms_ = ms_since(t0);
     if (reg.ok) {
-      offline_direct(eng, in, C, n, out, out_len, s);
+      t0 = std::chrono::steady_clock::now();
+      try {
+        offline_direct(eng, in, C, n, out, out_len, s);
+      } catch (...) {
+        // DMAs into / out of the caller's pages may still be queued: drain
+        // every stream of the call before ~Registration unlocks those pages
+        // (the caller may free them as soon as the error returns)
+        (void)hipStreamSynchronize(s_in_);
+        (void)hipStreamSynchronize(s_out_);
+        (void)hipStreamSynchronize(s);
+        throw;
+      }
+      last_xfer_ms_ = ms_since(t0);
+      t0 = std::chrono::steady_clock::now();
+      reg.release();
+      last_unreg_ms_ = ms_since(t0);
       return;
     }
   }
+  const auto t_stage = std::chrono::steady_clock::now();
+  struct StageTime {
+    double* dst;
+    std::chrono::steady_clock::time_point t;
+    ~StageTime() { *dst = ms_since(t); }
+  } stage_time{&last_xfer_ms_, t_stage};
   // chunk: S input samples per channel (a multiple of L), C*S doubles <= kChunkBytes
   int64_t S = std::max<int64_t>(L, (kChunkBytes / 8 / C) / L * L);
   // at least ~4 chunks when the signal allows (transfers overlap the compute
@@ -243,7 +254,7 @@ void HostPipeline::offline(Upols& eng, const double* const* in, int C, int64_t n
     const Piece p = pending.front();
     const int slot = (int)((nout - (int64_t)pending.size()) % 2);
     AD_HIP(hipEventSynchronize(ev_out_[slot]));
-    copy_out(out, pin_out_[slot], C, p.o0, p.len);
+    copy_out(out, pin_out_[slot], C, p.o0, p.len, workers_);
     pending.erase(pending.begin());
   };
   auto issue_output = [&](int64_t upto) {  // D2H of output [out_issued, upto), after ev_comp_
@@ -268,7 +279,7 @@ void HostPipeline::offline(Upols& eng, const double* const* in, int C, int64_t n
     const int slot = (int)(i % 2);
     const int64_t c0 = i * S, len = std::min(S, n - c0);
     if (i >= 2) AD_HIP(hipEventSynchronize(ev_in_[slot]));  // pin_in slot free again
-    copy_in(pin_in_[slot], in, C, c0, len);
+    copy_in(pin_in_[slot], in, C, c0, len, workers_);
     AD_HIP(hipMemcpy2DAsync(din_.p + c0, (size_t)n * sizeof(double), pin_in_[slot], (size_t)len * sizeof(double),
                             (size_t)len * sizeof(double), (size_t)C, hipMemcpyHostToDevice, s_in_));
     AD_HIP(hipEventRecord(ev_in_[slot], s_in_));

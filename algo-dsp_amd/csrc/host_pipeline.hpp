@@ -41,8 +41,25 @@ class HostPipeline {
   void offline(Upols& eng, const double* const* in, int C, int64_t n, double* const* out, int64_t out_len,
                hipStream_t s_comp);
 
+  // How host buffers cross PCIe (ad_conv_set_host_io): kAuto registers calls
+  // of >= 64 MiB and stages smaller ones; kStage copies through pinned double
+  // buffers with `workers` host threads; kRegister page-locks the caller's
+  // buffers for the call (falling back to staging if the runtime refuses).
+  enum Mode { kAuto = 0, kStage = 1, kRegister = 2 };
+  void set_mode(int mode, int workers) {
+    mode_ = mode;
+    workers_ = workers > 0 ? workers : 8;
+  }
+
   // Bytes of one pinned staging buffer (two for input, two for output).
   static constexpr int64_t kChunkBytes = int64_t(16) << 20;
+
+  // Wall-time split of the last offline() call (ms): page-locking the
+  // caller's buffers (hipHostRegister, 0 when staged), the transfers and
+  // compute, and unlocking them again (hipHostUnregister).
+  double last_register_ms() const { return last_reg_ms_; }
+  double last_transfer_ms() const { return last_xfer_ms_; }
+  double last_unregister_ms() const { return last_unreg_ms_; }
 
  private:
   hipStream_t s_in_ = nullptr, s_out_ = nullptr;
@@ -53,6 +70,9 @@ class HostPipeline {
   hipEvent_t ev_comp_ = nullptr;                // compute of the latest segment done
   hipEvent_t ev_out_[2] = {nullptr, nullptr};   // D2H of slot done (pin_out filled)
   DevBuf<double> din_, dout_;
+  double last_reg_ms_ = 0, last_xfer_ms_ = 0, last_unreg_ms_ = 0;
+  int mode_ = kAuto;
+  int workers_ = 8;
   void ensure_pinned(int64_t doubles);
   void offline_direct(Upols& eng, const double* const* in, int C, int64_t n, double* const* out, int64_t out_len,
                       hipStream_t s_comp);

@@ -4,17 +4,10 @@
 //
 // Output contract (as the reference): y[t] = (h * x)[t - lambda], lambda =
 // 2^minOrder, for any call length.  The taps are split into stages of
-// doubling partition size p_s = lambda, 2 lambda, ..., p_max, each stage a
-// zero-latency UPOLS engine with hop p_s over its own tap segment
-// [T_s, T_s + n_s p_s).  Stage s runs once per p_s input samples and its
-// block output lands at output times offset by T_s; T_s + lambda >= p_s makes
-// every contribution arrive before it is emitted.  Stages run on their own
-// HIP streams (the small kernels of the short stages overlap the long ones),
-// read their input blocks straight from mapped pinned host memory and write
-// their output there too (an async H2D copy per launch measured slower: 164
-// vs 142 us per 4096-sample call).  All complete blocks of a stage in one call run as
-// one multi-block launch (up to kBatchSamples), so a call costs about one
-// launch per stage and one synchronisation, whatever its length.
+// doubling partition size p_s = lambda, 2 lambda, ..., p_max, each over its
+// own tap segment [T_s, T_s + n_s p_s).  Stage s runs once per p_s input
+// samples and its block output lands at output times offset by T_s;
+// T_s + lambda >= p_s makes every contribution arrive before it is emitted.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -29,42 +22,7 @@
 
 namespace adsp {
 
-class Nupols {
- public:
-  static constexpr int64_t kBatchSamples = 8192;  // input samples per stage launch (at most)
-  // h: host [K] taps (K = the taps the reference convolves), lambda >= 64,
-  // p_max <= 8192 (powers of two).
-  Nupols(int device, const double* h, int64_t K, int64_t lambda, int64_t p_max);
-  ~Nupols();
-
-  void process(const double* in, int64_t n, double* out);
-  void reset();
-  int stage_count() const { return (int)st_.size(); }
-
- private:
-  struct Stage {
-    int64_t p = 0, T = 0, taps = 0;
-    std::unique_ptr<Upols> eng;
-    hipStream_t stream = nullptr;
-    int64_t cap = 1;                            // blocks per launch (at most)
-    double *in_h = nullptr, *in_d = nullptr;    // mapped pinned [cap p]
-    double *out_h = nullptr, *out_d = nullptr;  // mapped pinned [cap p]
-    int64_t done = 0;                           // input samples consumed
-    bool pending = false;                       // a launched run not yet added into acc_
-    int64_t pend_d = 0;                         // its first input sample
-    int64_t pend_n = 0;                         // its length (whole blocks)
-  };
-  int64_t lambda_;
-  std::vector<Stage> st_;
-  std::vector<double> xin_;  // input not yet consumed by every stage
-  int64_t xin_base_ = 0;     // absolute time of xin_.front()
-  int64_t received_ = 0;     // input samples received
-  std::vector<double> acc_;  // linear-conv output accumulator
-  int64_t acc_base_ = 0;     // absolute time of acc_.front()
-  int64_t emitted_ = 0;      // output samples emitted
-};
-
-// Device-resident, many-channel form of the same engine: `channels` copies of
+// Device-resident engine: `channels` copies of
 // PartitionedConvolution sharing one IR (the batched effect-chain runtime's
 // reverb-conv node, one instance per graph copy; ad_conv_pc_multi_*).  Every
 // stage is ONE zero-latency UPOLS engine over all channels (one launch per
@@ -120,13 +78,7 @@ class NupolsDev {
   DevBuf<double> xin_[2];  // [C][xcap], ping-pong for compaction
   int xcur_ = 0;
   int64_t xcap_ = 0, xin_base_ = 0;
-  DevBuf<double> acc_[2];  // [2][C][acap]: row 0 the caller-stream stages, row 1 the side-stream stages
-  bool use_side_ = false;
-  hipStream_t side_ = nullptr;  // the large (UPOLS) stages: off the per-call critical path
-  hipEvent_t ev_main_ = nullptr, ev_side_ = nullptr;
-  bool side_busy_ = false;      // side work enqueued since the caller's stream last waited for it
-  int64_t side_lo_ = INT64_MAX; // earliest output time that work writes
-  void wait_side(hipStream_t s);
+  DevBuf<double> acc_[2];  // [C][acap], ping-pong for compaction
   int acur_ = 0;
   int64_t acap_ = 0, acc_base_ = 0;
   int64_t received_ = 0, emitted_ = 0;

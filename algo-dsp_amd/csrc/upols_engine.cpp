@@ -13,24 +13,12 @@ namespace adsp {
 
 namespace {
 
-int env_int(const char* name, int dflt) {
-  const char* v = std::getenv(name);
-  if (!v || !*v) return dflt;
-  return std::atoi(v);
-}
-
-// K2 lane layout: NH = 2 splits the partitions over two lane halves (half
-// the VGPRs per lane, twice the waves); NH = 1 keeps all of a chunk's
-// partitions in one lane.  PC = partitions per lane: the smallest power of
-// two >= P/NH, capped at 16 (larger P: one launch per chunk of NH*16).
-int pick_nh(int P) {
-  if (P <= 1) return 1;
-  return env_int("AD_MAC_NH", 1) == 2 ? 2 : 1;
-}
-int pick_pc(int P, int NH) {
-  const int per = (P + NH - 1) / NH;
+// K2 lane layout: one lane keeps PC partitions of a chunk in VGPRs, PC = the
+// smallest power of two >= P, capped at 16 (larger P: one launch per chunk of
+// 16 partitions, the later ones read-modify-writing Z).
+int pick_pc(int P) {
   int pc = 1;
-  while (pc < per && pc < 16) pc *= 2;
+  while (pc < P && pc < 16) pc *= 2;
   return pc;
 }
 
@@ -44,10 +32,10 @@ Upols::Upols(int device, const double* kernels, int n_ir, int64_t K, int L, int 
   M_ = L;
   MS_ = M_ + 8;
   P_ = (int)((K + L - 1) / L);
-  NH_ = pick_nh(P_);
-  PC_ = pick_pc(P_, NH_);
+  NH_ = 1;
+  PC_ = pick_pc(P_);
   Q_ = jc_max_ + P_ + 2 * PC_ + 1;
-  R_ = env_int("AD_MAC_R", 0);  // 0: the launcher sizes runs to one resident round of waves
+  R_ = 0;  // the launcher sizes runs to one resident round of waves
 
   // Twiddle tables, computed in long double on the host.
   std::vector<double2> tw(2 * (size_t)M_);
@@ -236,16 +224,12 @@ void Upols::run(const double* d_in, int64_t in_stride, int64_t n, double* d_out,
     // (newest rows first for the kernel that reads them next; see RfftArgs)
     int runR = R_, runNy = 0;
     mac_run_geometry(PC_, NH_, M_, M_ >= 2048 && P_ <= 256 ? 1 : 0, C_, jc, R_, &runR, &runNy);
-    static const bool order_items = [] {
-      const char* v = std::getenv("AD_ITEM_ORDER");
-      return !(v && v[0] == '0');
-    }();
     // worth it when the Infinity Cache (256 MiB) holds the rows of a good
     // part of a run: stereo at hop 8192 ~81 of R = 176 steps (step 0.5751 ->
     // 0.5686 ms); the 8-channel shard ~81 of R = 688 (no gain, +0.7 %)
     const int64_t rows_per_step = (int64_t)C_ * runNy;
     const int64_t steps_cached = (int64_t(256) << 20) / ((int64_t)MS_ * 16 * std::max<int64_t>(1, rows_per_step));
-    const bool ordered = order_items && M_ >= 2048 && !(NH_ == 1 && jc <= 2) && runNy > 1 &&
+    const bool ordered = M_ >= 2048 && !(NH_ == 1 && jc <= 2) && runNy > 1 &&
                          steps_cached * 4 >= runR;
     if (ordered) {
       a.ord_R = runR;

@@ -31,6 +31,10 @@ class Upols {
 
   // Streaming state: zero the delay line.
   void reset_stream(hipStream_t s);
+  // Steps the block counter back by `blocks`: the next run re-transforms
+  // those blocks into the same delay-line slots (a streaming call that ended
+  // inside a block; its spectrum was provisional).
+  void rewind(int64_t blocks) { g_next_ -= blocks; }
   // Offline call start: only the delay-line slots preceding block 0 are zeroed.
   void begin_offline(hipStream_t s);
 

@@ -125,6 +125,24 @@ int ad_conv_reverb_create(const double* kernel, int64_t kernel_len, int min_bloc
 int ad_conv_reverb_set_wet_dry(ad_conv* h, double wet, double dry);
 int ad_conv_reverb_process_inplace(ad_conv* h, double* block, int64_t n);
 
+/* ---- host-buffer I/O of the batch / multi-channel calls ------------------
+ * ad_conv_process and ad_conv_ols_process_multi move host buffers over PCIe
+ * in overlapped chunks (no reference counterpart: OverlapSave.Process /
+ * ProcessTo, overlap_save.go:126-272, on host memory).  Mode AUTO page-locks
+ * the caller's buffers for the call (hipHostRegister; nothing is retained
+ * after it returns) when the call moves >= 64 MiB and stages smaller calls
+ * through pinned double buffers with `workers` copy threads (0: 8); STAGE and
+ * REGISTER force one form (REGISTER falls back to staging if the runtime
+ * refuses to lock the pages).  Results are identical in every mode.
+ * host_io_profile: wall-time split (ms) of the handle's last host call:
+ * page-locking, transfers + compute, unlocking (0 for the staged form's
+ * first and last).                                                          */
+#define AD_HOST_IO_AUTO 0
+#define AD_HOST_IO_STAGE 1
+#define AD_HOST_IO_REGISTER 2
+int ad_conv_set_host_io(ad_conv* h, int mode, int workers);
+int ad_conv_host_io_profile(const ad_conv* h, double* register_ms, double* transfer_ms, double* unregister_ms);
+
 /* ---- common handle API -------------------------------------------------- */
 int ad_conv_reset(ad_conv* h);   /* Reset(): clears history/tail/FDL state */
 int64_t ad_conv_block_size(const ad_conv* h);
@@ -325,6 +343,29 @@ int ad_fx_chain_compressor_metrics(ad_fx_chain* h, int channel, double* input_pe
                                    double* gain_reduction);
 /* EQ section state [channels][nsec][2] {d0, d1} (Chain.State, chain.go:122-130). */
 int ad_fx_chain_eq_state(ad_fx_chain* h, double* state, int64_t cap);
+/* Chain.SetState (chain.go:130-138) / Section.SetState (section.go:152-155)
+ * of every channel, between calls: state [channels][nsec][2] {d0, d1};
+ * n < channels*nsec*2 -> AD_ERR_LENGTH_MISMATCH (the reference indexes
+ * states[i] for every section).  With ad_fx_chain_eq_state this is the
+ * reference's checkpoint / resume surface for the EQ.                       */
+int ad_fx_chain_set_eq_state(ad_fx_chain* h, const double* state, int64_t n);
+/* Which engine runs the chain (results are identical in every engine):
+ *   AUTO            the staged engine (stage kernels over time chunks on three
+ *                   streams, fx_staged.hip) where it applies -- feed-forward
+ *                   dynamics, <= 8 EQ sections, <= 8192 channels with
+ *                   Freeverb -- with the EQ split over two CUs when a
+ *                   compressor and >= 3 sections are on; else FUSED;
+ *   FUSED           the fused per-sample kernels (dsp_kernels.hip k_chain*);
+ *   STAGED_NOSPLIT  staged, one EQ pipeline per channel group.
+ * chunk: samples per staged chunk (0: 16384; otherwise >= 256).           */
+#define AD_FX_ENGINE_AUTO 0
+#define AD_FX_ENGINE_FUSED 1
+#define AD_FX_ENGINE_STAGED_NOSPLIT 2
+int ad_fx_chain_set_engine(ad_fx_chain* h, int engine, int64_t chunk);
+/* Per-wave clock counters (s_memtime ticks) of the first chunk of each call,
+ * for profiling the serial stages: {compute, barrier wait} pairs per wave. */
+int ad_fx_chain_set_profiling(ad_fx_chain* h, int enable);
+int ad_fx_chain_read_profile(ad_fx_chain* h, unsigned long long* counters, int cap, int* count);
 void ad_fx_chain_destroy(ad_fx_chain* h);
 
 /* ---- batched effectchain graph (dsp/effectchain, 8(f)4) -------------------

@@ -126,6 +126,51 @@ def test_streaming_matches_oracle(gpu, ola, K, B, nb):
     assert np.max(np.abs(got - want)) < 1e-9 * max(1.0, math.sqrt(K) / 8)
 
 
+@pytest.mark.parametrize("ola", [False, True])
+@pytest.mark.parametrize("K", [16384, 131072])
+@pytest.mark.parametrize("B", [480, 960, 1000, 4800, 12000])
+def test_streaming_non_pow2_blocks(gpu, ola, K, B):
+    """Blocks with no power-of-two divisor >= 256 (10 ms audio blocks at 48 kHz
+    and friends): the engine runs at hop nextPow2(B) (<= 8192) and carries the
+    unfinished block, re-transforming it with more samples on the next call.
+    Zero latency, so the concatenated output is the linear convolution
+    (streaming_overlap_save.go:100-164): checked against the oracle's batch
+    OverlapSave.Process over enough calls to cross several hop boundaries, then
+    a Reset and the first calls again."""
+    h = irlib.large_church()[0, :K].copy() if K == 131072 else signals.make_test_kernel(K)
+    L = min(8192, 1 << (B - 1).bit_length())
+    nb = max(4, (3 * L) // B + 2)
+    x = signals.white_noise(B * nb, K + B)
+    g = (conv.NewStreamingOverlapAdd if ola else conv.NewStreamingOverlapSave)(h, B)
+    assert g.FFTSize() == 1 << (B + K - 2).bit_length()
+    got = []
+    for i in range(nb):
+        out = np.empty(B)
+        g.ProcessBlockTo(out, x[i * B:(i + 1) * B])
+        got.append(out)
+    got = np.concatenate(got)
+    want = O.OverlapSave(h, 0).process(x)[:got.size]
+    assert rms(got, want) < FFT_RMS_TOL
+    assert np.max(np.abs(got - want)) < 1e-9
+    g.Reset()
+    again = np.concatenate([g.ProcessBlock(x[i * B:(i + 1) * B]) for i in range(2)])
+    np.testing.assert_array_equal(again, got[:2 * B])
+
+
+def test_streaming_non_pow2_vs_streaming_oracle(gpu):
+    """B = 1000 on a 16384-tap kernel against the oracle's StreamingOverlapSave
+    restatement block by block (fftSize nextPow2(B + K - 1) = 32768)."""
+    K, B, nb = 16384, 1000, 12
+    h = signals.make_test_kernel(K)
+    x = signals.white_noise(B * nb, 77)
+    g = conv.NewStreamingOverlapSave(h, B)
+    o = O.Streaming(h, B)
+    for i in range(nb):
+        blk = x[i * B:(i + 1) * B]
+        got, want = g.ProcessBlock(blk), o.process_block(blk)
+        assert rms(got, want) < FFT_RMS_TOL and np.max(np.abs(got - want)) < 1e-9, i
+
+
 def test_streaming_reset_and_errors(gpu):
     h = signals.make_test_kernel(257)
     s = conv.NewStreamingOverlapSave(h, 256)
@@ -322,63 +367,8 @@ def _exact_window(x, h, t0, w):
     return np.convolve(seg, h, mode="valid")
 
 
-def test_bench_instance_vs_oracle(gpu):
-    """BASELINE config 3 exactly as bench.py runs it (bench.py: hop 8192, auto
-    chunk, auto run length -> P = 16, one k_fdl_mac_lds<16,1,true,8> launch,
-    R = 192 on 256 CUs, stereo x 2^24 samples, one chunk): the whole output of
-    both channels against the oracle's batch OverlapSave.Process
-    (overlap_save.go:126-254), plus exact dot products on windows across the
-    K2 run boundaries and the signal ends."""
-    ir = irlib.large_church()
-    K = ir.shape[1]
-    n = 1 << 24
-    x = np.stack([signals.white_noise(n, 0x5EED + c) for c in range(2)])
-    y, eng = _multi_run(ir, x, hop=8192)
-    assert eng.FFTSize() == 16384
-    out_len = n + K - 1
-    for c in range(2):
-        want = O.OverlapSave(ir[c], 0).process(x[c])
-        assert want.size == out_len
-        assert rms(y[c], want) < FFT_RMS_TOL
-        assert np.max(np.abs(y[c] - want)) < 1e-9
-        del want
-    # run boundaries of the auto run length (multiples of 16 blocks around
-    # 192 blocks) and the chunk's first/last blocks
-    L = 8192
-    for c in range(2):
-        for t0 in [0, K - 64, 16 * L - 32, 192 * L - 32, 384 * L - 32, 193 * L - 7, n - 40, out_len - 64]:
-            got = y[c][t0:t0 + 64]
-            ref = _exact_window(x[c], ir[c], t0, got.size)
-            assert np.max(np.abs(got - ref)) < 1e-9, (c, t0)
-
-
-def test_config4_shard_mixdown_vs_oracle(gpu):
-    """BASELINE config 4's per-GPU shard exactly as bench.py --workload shard runs
-    it: 8 channels x 2^22 samples, channel c with IR[c mod 2] (131072 taps),
-    hop 8192, auto chunk / run length, then k_mixdown (L = even channels,
-    R = odd).  The mix is compared with the oracle's per-channel OverlapSave
-    outputs summed by parity."""
-    import torch
-
-    ir = irlib.large_church()
-    K = ir.shape[1]
-    C_, n = 8, 1 << 22
-    out_len = n + K - 1
-    x = np.stack([signals.white_noise(n, 0x5EED + c) for c in range(C_)])
-    eng = conv.MultiChannelConvolver(ir, hop=8192, channels=C_, ir_index=[c % 2 for c in range(C_)])
-    dx = torch.from_numpy(x).cuda()
-    dy = torch.empty((C_, out_len), dtype=torch.float64, device="cuda")
-    mix = torch.empty((2, out_len), dtype=torch.float64, device="cuda")
-    eng.process_device(dx.data_ptr(), n, n, dy.data_ptr(), out_len, out_len)
-    conv.mixdown_device(dy.data_ptr(), C_, out_len, out_len, mix.data_ptr())
-    torch.cuda.synchronize()
-    m = mix.cpu().numpy()
-    want = np.zeros((2, out_len))
-    for c in range(C_):
-        want[c % 2] += O.OverlapSave(ir[c % 2], 0).process(x[c])
-    for s in range(2):
-        assert rms(m[s], want[s]) < FFT_RMS_TOL * 4
-        assert np.max(np.abs(m[s] - want[s])) < 4e-9
+# test_bench_instance_vs_oracle and the config-4 shard test live in
+# test_configs_gpu.py (test_config3_bench_instance, test_config4_shard).
 
 
 @pytest.mark.parametrize("hop,nseg", [(1024, 3), (8192, 4)])
@@ -461,6 +451,18 @@ def test_process_host_multi_chunked(gpu):
     np.testing.assert_array_equal(got, dev)
     want = O.OverlapSave(ir[1], 0).process(x[1])
     assert rms(got[1], want) < FFT_RMS_TOL and np.max(np.abs(got[1] - want)) < 1e-9
+    reg_ms, xfer_ms, unreg_ms = eng.host_io_profile()
+    assert reg_ms > 0 and xfer_ms > 0 and unreg_ms >= 0  # 2 x 2.6 M samples > 64 MiB: registered
+    # every host I/O form gives the same bits (ad_conv_set_host_io)
+    for mode, workers in [(conv.MultiChannelConvolver.HOST_IO_STAGE, 1), (conv.MultiChannelConvolver.HOST_IO_STAGE, 8),
+                          (conv.MultiChannelConvolver.HOST_IO_REGISTER, 0)]:
+        eng.set_host_io(mode, workers)
+        np.testing.assert_array_equal(eng.process_host(x), dev)
+        r, t, _ = eng.host_io_profile()
+        assert (r > 0) == (mode == conv.MultiChannelConvolver.HOST_IO_REGISTER) and t > 0
+    eng.set_host_io(conv.MultiChannelConvolver.HOST_IO_AUTO)
+    with pytest.raises(conv.ErrInvalidArgument):
+        eng.set_host_io(7)
     # second call on the same handle, shorter signal (one chunk)
     got2 = eng.process_host(x[:, :50_000])
     np.testing.assert_allclose(got2[0], O.OverlapSave(ir[0], 0).process(x[0, :50_000]), atol=1e-9)

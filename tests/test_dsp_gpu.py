@@ -110,6 +110,34 @@ def test_chain_one_shot_state_io(gpu):
         np.testing.assert_array_equal(state[c].ravel(), st)
 
 
+@pytest.mark.parametrize("sections", [3, 11])
+def test_chain_set_state_round_trip(gpu, sections):
+    """Chain.State / Chain.SetState (chain.go:122-138) as a checkpoint at a call
+    boundary: run A, save the state, run B; a second chain restored from the
+    saved state produces B's block bit for bit, and both equal the oracle run
+    over A + B in one pass.  Covers > 8 sections (several EQ passes)."""
+    coeffs = stable_sections(sections, 40 + sections)
+    C, n1, n2 = 5, 1500, 2200
+    x = np.stack([signals.white_noise(n1 + n2, 600 + c) for c in range(C)])
+    ch = P.Chain(coeffs, 0.9, channels=C)
+    a, b = x[:, :n1].copy(), x[:, n1:].copy()
+    ch.ProcessBlock(a)
+    saved = ch.State().copy()
+    ch.ProcessBlock(b)
+    ch2 = P.Chain(coeffs, 0.9, channels=C)
+    ch2.SetState(saved)
+    np.testing.assert_array_equal(ch2.State(), saved)
+    b2 = x[:, n1:].copy()
+    ch2.ProcessBlock(b2)
+    assert np.array_equal(b2, b)
+    for c in (0, C - 1):
+        want, st = O.biquad_chain_block(coeffs.ravel(), np.zeros(2 * sections), 0.9, x[c])
+        assert np.array_equal(np.concatenate([a[c], b[c]]), want)
+        np.testing.assert_array_equal(ch.State()[c].ravel(), st)
+    with pytest.raises(Exception):
+        ch2.SetState(saved[:, :1])  # too short: the reference indexes every section
+
+
 def test_chain_reset(gpu):
     coeffs = stable_sections(2, 5)
     ch = P.Chain(coeffs)
@@ -162,16 +190,16 @@ def test_compressor_vs_oracle(gpu, cfg):
     ("gate", {"threshold_db": -20.0, "attack_ms": 0.1, "release_ms": 1.0, "hold_ms": 10.0, "knee_db": 0.0}),
     ("gate", {"hold_ms": 0.0, "range_db": -120.0, "ratio": 100.0}),
 ], ids=lambda v: v if isinstance(v, str) else (",".join(f"{k}={x}" for k, x in v.items()) or "defaults"))
-def test_expander_gate_vs_oracle(gpu, kind, cfg, monkeypatch):
+def test_expander_gate_vs_oracle(gpu, kind, cfg):
     """dynamics.Expander / dynamics.Gate (expander.go:358-440, gate.go:360-450)
     on a bursty signal that opens and closes them, over a call boundary: the
     output within 1e-12 RMS of the oracle and the metrics to 1e-13."""
     C, n = 3, 6000
     env = np.where((np.arange(n) // 900) % 2 == 0, 0.5, 0.003)
     x = np.stack([env * signals.white_noise(n, 60 + c) for c in range(C)])
-    for staged in ("1", "0"):
-        monkeypatch.setenv("AD_FX_STAGED", staged)
+    for engine in (P.EffectChain.ENGINE_AUTO, P.EffectChain.ENGINE_FUSED):
         ex = (P.Gate if kind == "gate" else P.Expander)(48000.0, channels=C, **cfg)
+        ex.SetEngine(engine)
         a, b = x[:, :2500].copy(), x[:, 2500:].copy()
         ex.ProcessInPlace(a)
         ex.ProcessInPlace(b)
@@ -255,37 +283,7 @@ def test_effect_chain_config5(gpu):
         assert rms(y[c], v) <= RMS_TOL, rms(y[c], v)
 
 
-def test_effect_chain_config5_bench_shape(gpu):
-    """Config 5 at the shape bench.py --workload fx times: 256 channels, device
-    buffers, the staged engine (default), 2^18 samples = 16 of its 16384-sample
-    chunks, in two calls (the second ends mid-chunk); channels 0, 63, 64 (the
-    first of the second 64-channel group) and 255 against the oracle chain
-    (chain_process.go:11-33: biquad chains -> Compressor -> Freeverb)."""
-    import torch
-
-    fs = 48000.0
-    eq = design.config5_eq(fs)
-    comp_cfg = {"auto_makeup": 0, "makeup_db": 0.0}
-    verb = (0.22, 1.0, 0.72, 0.45, 0.015)
-    C, n = 256, 1 << 18
-    x = np.stack([0.5 * signals.white_noise(n, 0x5EED + c) for c in range(C)])
-    fx = P.EffectChain(C, eq, comp_cfg, verb, fs)
-    dx = torch.from_numpy(x).cuda()
-    s = torch.cuda.current_stream()
-    cut = 5 * 16384 + 1000
-    fx.process_device(dx.data_ptr(), n, cut, s.cuda_stream)
-    fx.process_device(dx.data_ptr() + 8 * cut, n, n - cut, s.cuda_stream)
-    s.synchronize()
-    y = dx.cpu().numpy()
-    for c in (0, 63, 64, 255):
-        v = x[c].copy()
-        for co, g in eq:
-            v, _ = O.biquad_chain_block(np.ravel(co), np.zeros(2 * len(co)), g, v)
-        v = O.Compressor(fs, **comp_cfg).process_in_place(v)
-        o = O.Freeverb()
-        o.set(*verb)
-        v = o.process_in_place(v)
-        assert rms(y[c], v) <= RMS_TOL, (c, rms(y[c], v))
+# the 256-channel bench-shape test lives in test_configs_gpu.py (test_config5_chain)
 
 
 # ------------------------------------------------------------------ staged engine == fused kernels
@@ -302,11 +300,12 @@ STAGED_CASES = {
 
 
 @pytest.mark.parametrize("case", list(STAGED_CASES), ids=list(STAGED_CASES))
-def test_staged_engine_matches_fused(gpu, case, monkeypatch):
-    """The staged engine (stage kernels over time chunks on four streams)
+def test_staged_engine_matches_fused(gpu, case):
+    """The staged engine (stage kernels over time chunks on three streams)
     computes every value with the fused kernels' operations: outputs, EQ
     state and compressor metrics are identical, over chunk boundaries
-    (AD_FX_CHUNK=256), calls that end mid-chunk, and a partial channel group."""
+    (ad_fx_chain_set_engine chunk 256), calls that end mid-chunk, and a
+    partial channel group."""
     fs = 48000.0
     cfg = STAGED_CASES[case]
     eq = design.config5_eq(fs) if cfg.get("eq") else ()
@@ -317,11 +316,11 @@ def test_staged_engine_matches_fused(gpu, case, monkeypatch):
     outs = {}
     # "2": staged with the split EQ/detector stage (the default where it
     # applies), "1": staged, one EQ pipeline per channel group, "0": fused
+    engines = {"2": P.EffectChain.ENGINE_AUTO, "1": P.EffectChain.ENGINE_STAGED_NOSPLIT,
+               "0": P.EffectChain.ENGINE_FUSED}
     for staged in ("2", "1", "0"):
-        monkeypatch.setenv("AD_FX_STAGED", "0" if staged == "0" else "1")
-        monkeypatch.setenv("AD_FX_EQSPLIT", "0" if staged == "1" else "1")
-        monkeypatch.setenv("AD_FX_CHUNK", "256")
         fx = P.EffectChain(C, eq, comp, verb, fs)
+        fx.SetEngine(engines[staged], 256)
         y = x.copy()
         parts = []
         for lo, hi in [(0, 700), (700, 701), (701, 3000)]:

@@ -68,6 +68,19 @@ def test_correlate_fft_device_matches_host(gpu, n, m):
     close(got, O.correlate_fft(a, b))
 
 
+@pytest.mark.parametrize("sa,sb", [(3.0e4, 3.0e-3), (1.0e-4, 2.0e3), (1.0, 1.0e-9)])
+@pytest.mark.parametrize("n,m", [(40000, 25000), (1 << 17, 4096)])
+def test_correlate_fft_unequal_scales(gpu, n, m, sa, sb):
+    """Signals whose magnitudes differ by 1e6 .. 1e9 (an int16-scale recording
+    against a normalised template): the device packs both into one transform of
+    a + i b, so without its power-of-two rescaling of b, B's spectrum would
+    carry rounding of order eps |A| and the correlation's error would grow by
+    |a| / |b|.  The reference transforms a and b separately (correlate.go:122-147);
+    the result must stay within the same relative bar as equal-scale inputs."""
+    a, b = sa * signals.white_noise(n, 3 + n), sb * signals.white_noise(m, 4 + m)
+    close(conv.CorrelateFFT(a, b), O.correlate_fft(a, b))
+
+
 def test_correlate_fft_empty(gpu):
     with pytest.raises(conv.ErrEmptyInput):
         conv.CorrelateFFT([], [1.0, 2.0])

@@ -19,8 +19,8 @@ for C in (256, 1024, 4096, 16384):
     for name, kw in cases.items():
         res = {}
         for st in ("1", "0"):
-            os.environ["AD_FX_STAGED"] = st
             fx = processors.EffectChain(C, sample_rate=fs, **kw)
+            fx.SetEngine(fx.ENGINE_AUTO if st == "1" else fx.ENGINE_FUSED)
             fx.process_device(x.data_ptr(), n, n, s)
             torch.cuda.synchronize()
             t = time.perf_counter()
