@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
@@ -97,6 +98,22 @@ struct ad_conv {
   bool partial = false;
   int64_t part_fill = 0;
 
+  // pre-enqueued block chains (StreamGate, conv_kernels.hpp): one block of
+  // hop >= 2048 per call.  ctl lives in coherent mapped host memory: go
+  // (host -> K1), k1_state (K1 -> host), done (K3 -> host), a line each.
+  struct GateCtl {
+    uint64_t go, pad0[15];
+    uint64_t k1_state, pad1[15];
+    uint64_t done, pad2[15];
+  };
+  bool gated = false;
+  GateCtl* ctl = nullptr;      // host view
+  GateCtl* ctl_dev = nullptr;  // device view
+  DevBuf<uint64_t> gate_word;
+  uint64_t seq = 0;            // last block sequence number issued
+  uint64_t chain_pending = 0;  // sequence number of the pre-enqueued chain (0: none)
+  uint64_t gate_timeout = 0;   // K1's wait, ticks of the device's real-time counter
+
   // time-domain streaming path (blocks of fewer than 64 samples)
   bool direct_stream = false;
   DevBuf<double> hdev;
@@ -130,6 +147,10 @@ struct ad_conv {
   int64_t ylin_base = 0;         // linear-conv index of ylin.front()
 
   ~ad_conv() {
+    if (chain_pending && ctl) {  // release a pre-enqueued chain's K1 at once (gate_cancel without errors)
+      __atomic_store_n(&ctl->go, kGateAbort, __ATOMIC_RELEASE);
+      if (stream) (void)hipStreamSynchronize(stream);
+    }
     pipe.reset();
     if (done) {
       (void)hipEventSynchronize(done);
@@ -140,6 +161,7 @@ struct ad_conv {
     if (stream) (void)hipStreamSynchronize(stream);
     if (pin_in) (void)hipHostFree(pin_in);
     if (pin_out) (void)hipHostFree(pin_out);
+    if (ctl) (void)hipHostFree(ctl);
     if (stream) (void)hipStreamDestroy(stream);
   }
 };
@@ -184,7 +206,11 @@ void mark_last(ad_conv* h, hipStream_t s) {
 void setup_stream_engine(ad_conv* h, const double* kernel, int64_t K, int64_t B, int64_t hop_cap) {
   int64_t hop = largest_pow2_divisor(B, hop_cap);
   if (hop < 256 && hop != B && B >= 64) {
-    hop = std::min<int64_t>(hop_cap, next_pow2(B));
+    // nextPow2(B), and at least K/64 so that a call's K2 (one output block per
+    // touched block, k_fdl_mac_row) keeps <= 64 partitions per wave: with
+    // K = 131072 and B = 480 a hop of 512 would give each of only 8 waves
+    // 256 partitions in series
+    hop = std::min<int64_t>(hop_cap, std::max(next_pow2(B), next_pow2((K + 63) / 64)));
     h->partial = (B % hop) != 0;
   }
   h->hop = hop;
@@ -201,7 +227,98 @@ void setup_stream_engine(ad_conv* h, const double* kernel, int64_t K, int64_t B,
   }
 }
 
+// ---- pre-enqueued streaming chains (StreamGate) ----------------------------
+// Host side of the protocol in conv_kernels.hpp.  A call publishes its block
+// (go = seq), enqueues the next block's chain behind the running one, and
+// spins on the done word; the launches of block i+1 thus overlap block i's
+// kernels and the wait is a load of host memory, not a HIP call.
+using Clock = std::chrono::steady_clock;
+
+void gate_setup(ad_conv* h) {
+  h->gated = !h->partial && !h->direct_stream && h->hop >= 2048 && h->block_size == h->hop;
+  if (!h->gated) return;
+  AD_HIP(hipHostMalloc(reinterpret_cast<void**>(&h->ctl), sizeof(ad_conv::GateCtl),
+                       hipHostMallocMapped | hipHostMallocCoherent));
+  std::memset(h->ctl, 0, sizeof(ad_conv::GateCtl));
+  AD_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&h->ctl_dev), h->ctl, 0));
+  h->gate_word.alloc(1);
+  AD_HIP(hipMemsetAsync(h->gate_word.p, 0, sizeof(uint64_t), h->stream));
+  int khz = 0;
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, h->device) != hipSuccess || khz <= 0) khz = 100000;
+  h->gate_timeout = (uint64_t)khz * 20;  // 20 ms: a later block runs through ordinary launches
+}
+
+// Spins until pred() holds (acquire loads of the ctl words); gives up after
+// 2 s (then the stream is synchronised so that a device fault surfaces).
+template <class Pred>
+void gate_spin(ad_conv* h, Pred&& pred) {
+  const auto t0 = Clock::now();
+  for (uint32_t i = 0;; ++i) {
+    if (pred()) return;
+    if ((i & 1023) == 1023 && Clock::now() - t0 > std::chrono::seconds(2)) {
+      AD_HIP(hipStreamSynchronize(h->stream));
+      if (pred()) return;
+      AD_FAIL(AD_ERR_INTERNAL, "streaming block: completion word never written");
+    }
+    __builtin_ia32_pause();
+  }
+}
+uint64_t ctl_load(const uint64_t* w) { return __atomic_load_n(w, __ATOMIC_ACQUIRE); }
+
+void gate_enqueue(ad_conv* h, uint64_t sq, bool wait_for_go, int64_t n) {
+  StreamGate g{};
+  g.seq = sq;
+  g.done = &h->ctl_dev->done;
+  if (wait_for_go) {
+    g.go = &h->ctl_dev->go;
+    g.k1_state = &h->ctl_dev->k1_state;
+    g.gate = h->gate_word.p;
+    g.timeout = h->gate_timeout;
+  }
+  h->eng->set_gate(g);
+  h->eng->run(h->pin_in_dev, n, n, h->pin_out_dev, n, n, /*use_hist=*/true, h->stream);
+}
+
+// Drops the pre-enqueued chain (its K1 exits at once, K2 / K3 skip) and
+// steps the engine back over its block; the stream is idle afterwards.
+void gate_cancel(ad_conv* h) {
+  if (!h->chain_pending) return;
+  const uint64_t p = h->chain_pending;
+  __atomic_store_n(&h->ctl->go, kGateAbort, __ATOMIC_RELEASE);
+  gate_spin(h, [&] {
+    const uint64_t v = ctl_load(&h->ctl->k1_state);
+    return v == (p | kGateSkipped) || v == p;
+  });
+  AD_HIP(hipStreamSynchronize(h->stream));
+  if (ctl_load(&h->ctl->k1_state) != p) h->eng->rewind(1);
+  __atomic_store_n(&h->ctl->go, 0, __ATOMIC_RELEASE);
+  h->chain_pending = 0;
+}
+
+// One block of n = hop samples (already in pin_in) through the chains.
+void gate_block(ad_conv* h, int64_t n) {
+  const uint64_t sq = ++h->seq;
+  if (h->chain_pending == sq) {
+    __atomic_store_n(&h->ctl->go, sq, __ATOMIC_RELEASE);  // the waiting K1 takes the block
+    gate_enqueue(h, sq + 1, true, n);                      // the next block's chain, behind this one
+    h->chain_pending = sq + 1;
+    // done, or this chain's K1 gave up before go (the caller came late)
+    gate_spin(h, [&] { return ctl_load(&h->ctl->done) == sq || ctl_load(&h->ctl->k1_state) == (sq | kGateSkipped); });
+    if (ctl_load(&h->ctl->done) == sq) return;
+    gate_cancel(h);       // the chain behind it
+    h->eng->rewind(1);    // this block's skipped chain
+    gate_enqueue(h, sq, false, n);
+    gate_spin(h, [&] { return ctl_load(&h->ctl->done) == sq; });
+    return;
+  }
+  gate_enqueue(h, sq, false, n);  // ordinary launches, completion through done
+  gate_enqueue(h, sq + 1, true, n);
+  h->chain_pending = sq + 1;
+  gate_spin(h, [&] { return ctl_load(&h->ctl->done) == sq; });
+}
+
 void stream_reset(ad_conv* h) {
+  gate_cancel(h);
   if (h->eng) h->eng->reset_stream(h->stream);
   for (auto& b : h->sbuf)
     if (b.p) AD_HIP(hipMemsetAsync(b.p, 0, b.n * sizeof(double), h->stream));
@@ -277,8 +394,12 @@ void stream_convolve(ad_conv* h, const double* in, int64_t n, double* out) {
   }
   if (!h->partial) {
     std::memcpy(h->pin_in, in, n * sizeof(double));
-    h->eng->run(h->pin_in_dev, n, n, h->pin_out_dev, n, n, /*use_hist=*/true, s);
-    AD_HIP(hipStreamSynchronize(s));
+    if (h->gated) {
+      gate_block(h, n);
+    } else {
+      h->eng->run(h->pin_in_dev, n, n, h->pin_out_dev, n, n, /*use_hist=*/true, s);
+      AD_HIP(hipStreamSynchronize(s));
+    }
     std::memcpy(out, h->pin_out, n * sizeof(double));
     return;
   }
@@ -353,6 +474,7 @@ static int stream_create(Kind kind, const double* kernel, int64_t K, int64_t B, 
     h->block_size = B;
     h->fft_size = next_pow2(B + K - 1);
     setup_stream_engine(h.get(), kernel, K, B, 8192);
+    gate_setup(h.get());
     stream_reset(h.get());
     return h.release();
   });

@@ -563,6 +563,8 @@ template <int PC>
 __global__ __launch_bounds__(256) void k_fdl_mac_row(MacArgs a) {
   const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (w >= a.ny) return;  // ny = waves in this launch (set by the launcher)
+  // a pre-enqueued chain whose K1 did not run (StreamGate)
+  if (a.sg.gate && __hip_atomic_load(a.sg.gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != a.sg.seq) return;
   const int lane = threadIdx.x & 63;
   const int bx = w % a.nx;
   const int t = w / a.nx;

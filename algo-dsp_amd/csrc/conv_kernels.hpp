@@ -58,6 +58,30 @@ inline void timed_launch(F kernel, dim3 grid, dim3 block, hipStream_t s, Args...
   }
 }
 
+// Pre-enqueued streaming block (the host-buffer streaming call, one block of
+// hop >= 2048 per call; capi_conv.cpp stream_convolve).  The K1 -> K2 -> K3
+// chain of the NEXT block is enqueued while the current one runs; its K1
+// waits in the GPU for the host to publish the block's samples (`go` ==
+// seq in mapped host memory) instead of the host launching after them, so the
+// launches leave the per-block critical path.  K1 gives up after `timeout`
+// ticks of the 100 MHz real-time counter, or at once when go == kGateAbort
+// (Reset / destroy / a late block), and reports its decision in `k1_state`
+// (seq, or seq | kGateSkipped) and in the device word `gate`; K2 and K3 of
+// the chain run only when gate == seq.  K3 publishes the block's completion
+// by writing seq to `done` (mapped host memory) after its output stores, so
+// the host waits on that word, not on a stream.  All pointers null: an
+// ordinary launch.
+constexpr uint64_t kGateAbort = ~0ull;
+constexpr uint64_t kGateSkipped = 1ull << 63;
+struct StreamGate {
+  const uint64_t* go;     // K1: host-written (mapped)
+  uint64_t* k1_state;     // K1: device-written (mapped)
+  uint64_t* gate;         // K1 writes, K2 / K3 read (device memory)
+  uint64_t* done;         // K3: device-written (mapped)
+  uint64_t seq;
+  uint64_t timeout;       // K1's wait, 100 MHz ticks
+};
+
 struct RfftArgs {
   const double* x;      // input samples, channel c at x + c*x_stride (call-relative index)
   int64_t x_stride;
@@ -79,6 +103,7 @@ struct RfftArgs {
   // in decreasing t: the rows K2 needs first are the newest in the Infinity
   // Cache.  Grid: channels * (ord_ny + 1) * ord_R (rows outside [0, jc) idle).
   int ord_R, ord_ny, ord_pc;
+  StreamGate sg;        // split kernels, one item: wait for the block (see StreamGate)
 };
 
 struct MacArgs {
@@ -103,6 +128,7 @@ struct MacArgs {
   int P;                // partitions
   int M;                // bins 0..M
   int mid_in_k3;        // 1: no middle-bin wave (K3 computes Z[M/2], MidBin)
+  StreamGate sg;        // row form: run only if the chain's K1 ran (see StreamGate)
 };
 
 // The middle bin M/2 of an output block's Z row, computed by K3 itself
@@ -144,6 +170,7 @@ struct IrfftArgs {
   // writes output row ry*R + t at its step t, so K3 reads the rows in
   // decreasing t, newest first.  Grid: channels * ord_ny * ord_R.
   int ord_R, ord_ny;
+  StreamGate sg;        // split kernel, one item: run only if K1 ran; publish completion
 };
 
 bool launch_window_rfft(int M, const RfftArgs& a, hipStream_t s);

@@ -73,6 +73,47 @@ __device__ __forceinline__ void irfft_store_out(const double2* v, int tid, doubl
 // One-shot forms (M <= 1024): F = BLOCK/T FFTs per workgroup, one
 // (channel, block) item each.
 // ---------------------------------------------------------------------------
+// StreamGate (conv_kernels.hpp): K1's wait for the host's go word.  Thread 0
+// polls (system-scope acquire loads of mapped host memory, s_sleep between
+// polls) until go == seq, go == kGateAbort or the timeout; it records the
+// decision for K2 / K3 (gate) and the host (k1_state).  Returns false when
+// the workgroup must not run.
+__device__ __forceinline__ bool gate_wait(const StreamGate& g) {
+  if (!g.go) return true;
+  __shared__ int ok;
+  if (threadIdx.x == 0) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    int run = 0;
+    for (;;) {
+      const uint64_t v = __hip_atomic_load(g.go, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (v == g.seq) {
+        run = 1;
+        break;
+      }
+      if (v == kGateAbort || __builtin_amdgcn_s_memrealtime() - t0 > g.timeout) break;
+      __builtin_amdgcn_s_sleep(4);
+    }
+    __hip_atomic_store(g.gate, run ? g.seq : 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(g.k1_state, run ? g.seq : (g.seq | kGateSkipped), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    ok = run;
+  }
+  __syncthreads();
+  return ok != 0;
+}
+// K2 / K3 of a gated chain: did its K1 run?  (K1 finished before this launch
+// started: stream order.)
+__device__ __forceinline__ bool gate_open(const StreamGate& g) {
+  return !g.gate || __hip_atomic_load(g.gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g.seq;
+}
+// K3 of a gated chain: every thread's output stores are complete and visible
+// system-wide, then one lane publishes seq.
+__device__ __forceinline__ void gate_done(const StreamGate& g) {
+  if (!g.done) return;
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(g.done, g.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 template <int M, int V>
 __global__ __launch_bounds__((FftPlan<M, V>::BLOCK)) void k_window_rfft(RfftArgs a) {
   using Plan = FftPlan<M, V>;
@@ -237,6 +278,7 @@ __global__ __launch_bounds__((SplitPlan<M>::T)) __attribute__((amdgpu_waves_per_
   constexpr int M2 = SP::M2, V = SP::V, T = SP::T, L = M;
   __shared__ __attribute__((aligned(16))) double2 lds[SP::LDS];
   const int tid = threadIdx.x;
+  if (!gate_wait(a.sg)) return;
   int c, j;
   if (a.ord_R > 0) {  // newest-last for K2's first steps (RfftArgs::ord_R)
     const int per = a.channels * (a.ord_ny + 1), b = blockIdx.x;
@@ -298,6 +340,7 @@ __global__ __launch_bounds__((SplitPlan<M>::T)) __attribute__((amdgpu_waves_per_
   constexpr int M2 = SP::M2, V = SP::V, T = SP::T, L = M;
   __shared__ __attribute__((aligned(16))) double2 lds[SP::LDS];
   const int tid = threadIdx.x;
+  if (!gate_open(a.sg)) return;
   // item indices and row bases are wave-uniform: keep them in SGPRs (VGPR
   // copies of 64-bit bases spilled to scratch at the 128-VGPR cap)
   int c, j;
@@ -358,15 +401,16 @@ __global__ __launch_bounds__((SplitPlan<M>::T)) __attribute__((amdgpu_waves_per_
         *p = make_double2(q.x + av[s].x, q.y + av[s].y);
       }
     }
-    return;
-  }
-  const int64_t left = a.out_len - ob;  // valid outputs from yb on
+  } else {
+    const int64_t left = a.out_len - ob;  // valid outputs from yb on
 #pragma unroll
-  for (int s = 0; s < V; ++s) {
-    const int o = 2 * last_pass_index<M2, V>(tid, s);
-    if (o < left) yb[o] = a.accumulate ? yb[o] + av[s].x : av[s].x;
-    if (o + 1 < left) yb[o + 1] = a.accumulate ? yb[o + 1] + av[s].y : av[s].y;
+    for (int s = 0; s < V; ++s) {
+      const int o = 2 * last_pass_index<M2, V>(tid, s);
+      if (o < left) yb[o] = a.accumulate ? yb[o] + av[s].x : av[s].x;
+      if (o + 1 < left) yb[o + 1] = a.accumulate ? yb[o + 1] + av[s].y : av[s].y;
+    }
   }
+  gate_done(a.sg);
 }
 
 // ---------------------------------------------------------------------------

@@ -194,6 +194,12 @@ void Upols::run(const double* d_in, int64_t in_stride, int64_t n, double* d_out,
   // K2 reads every later block as zeros
   const int64_t nb_in = (std::max<int64_t>(n, 0) + L_ - 1) / L_;
   // balanced chunks of at most jc_max blocks (no tiny tail launch)
+  StreamGate sg{};
+  if (gate_on_) {
+    if (J != 1 || C_ != 1 || M_ < 2048) AD_FAIL(AD_ERR_INTERNAL, "gated run: one block of one channel, hop >= 2048");
+    sg = gate_;
+    gate_on_ = false;
+  }
   const int64_t nchunks = (J + jc_max_ - 1) / jc_max_;
   const int64_t jc_even = (J + nchunks - 1) / nchunks;
   for (int64_t cr = 0; cr < J; cr += jc_even) {
@@ -236,6 +242,7 @@ void Upols::run(const double* d_in, int64_t in_stride, int64_t n, double* d_out,
       a.ord_ny = runNy;
       a.ord_pc = PC_;
     }
+    a.sg = sg;
     hipEvent_t e0;
     prof_begin(s, &e0, 0);
     launch_window_rfft(M_, a, s);
@@ -262,6 +269,7 @@ void Upols::run(const double* d_in, int64_t in_stride, int64_t n, double* d_out,
     // Z[M/2] from K3 (split sizes, few partitions): K2 then runs pair waves only
     const bool mid_k3 = M_ >= 2048 && P_ <= 256;
     m.mid_in_k3 = mid_k3 ? 1 : 0;
+    m.sg = sg;
     prof_begin(s, &e0, 1);
     launch_fdl_mac(PC_, NH_, m, C_, s);
     prof_end(s, e0, 1, blocks * (double)(M_ + 1) * 32 + (double)n_ir_ * P_ * (M_ + 1) * 16);
@@ -297,6 +305,7 @@ void Upols::run(const double* d_in, int64_t in_stride, int64_t n, double* d_out,
       b.mid.n_ir = n_ir_;
       b.mid.P = P_;
     }
+    b.sg = sg;
     prof_begin(s, &e0, 2);
     launch_irfft_store(M_, b, s);
     prof_end(s, e0, 2, blocks * ((double)(M_ + 1) * 16 + (double)L_ * 8));

@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "ad_common.hpp"
+#include "conv_kernels.hpp"
 
 namespace adsp {
 
@@ -35,6 +36,12 @@ class Upols {
   // those blocks into the same delay-line slots (a streaming call that ended
   // inside a block; its spectrum was provisional).
   void rewind(int64_t blocks) { g_next_ -= blocks; }
+  // The next run() launches its K1 / K2 / K3 as a gated chain (StreamGate,
+  // conv_kernels.hpp); applies to that one run only.
+  void set_gate(const StreamGate& g) {
+    gate_ = g;
+    gate_on_ = true;
+  }
   // Offline call start: only the delay-line slots preceding block 0 are zeroed.
   void begin_offline(hipStream_t s);
 
@@ -65,6 +72,8 @@ class Upols {
   int64_t K_;
   int L_, M_, MS_, P_, PC_, NH_, C_, n_ir_, jc_max_, Q_, R_;
   int64_t g_next_ = 0;  // logical index of the next spectrum block
+  StreamGate gate_{};
+  bool gate_on_ = false;
   hipStream_t stream_;
   DevBuf<double2> tw_;   // [twM (M) | twN (M)]
   DevBuf<double2> H_;    // [n_ir][P][MS]

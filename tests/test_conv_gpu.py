@@ -131,14 +131,15 @@ def test_streaming_matches_oracle(gpu, ola, K, B, nb):
 @pytest.mark.parametrize("B", [480, 960, 1000, 4800, 12000])
 def test_streaming_non_pow2_blocks(gpu, ola, K, B):
     """Blocks with no power-of-two divisor >= 256 (10 ms audio blocks at 48 kHz
-    and friends): the engine runs at hop nextPow2(B) (<= 8192) and carries the
+    and friends): the engine runs at hop max(nextPow2(B), nextPow2(K/64))
+    (<= 8192) and carries the
     unfinished block, re-transforming it with more samples on the next call.
     Zero latency, so the concatenated output is the linear convolution
     (streaming_overlap_save.go:100-164): checked against the oracle's batch
     OverlapSave.Process over enough calls to cross several hop boundaries, then
     a Reset and the first calls again."""
     h = irlib.large_church()[0, :K].copy() if K == 131072 else signals.make_test_kernel(K)
-    L = min(8192, 1 << (B - 1).bit_length())
+    L = min(8192, max(1 << (B - 1).bit_length(), 1 << (-(-K // 64) - 1).bit_length()))
     nb = max(4, (3 * L) // B + 2)
     x = signals.white_noise(B * nb, K + B)
     g = (conv.NewStreamingOverlapAdd if ola else conv.NewStreamingOverlapSave)(h, B)
@@ -155,6 +156,39 @@ def test_streaming_non_pow2_blocks(gpu, ola, K, B):
     g.Reset()
     again = np.concatenate([g.ProcessBlock(x[i * B:(i + 1) * B]) for i in range(2)])
     np.testing.assert_array_equal(again, got[:2 * B])
+
+
+def test_streaming_preenqueued_chain_paths(gpu):
+    """Blocks of one hop >= 2048 run as pre-enqueued K1 -> K2 -> K3 chains whose
+    K1 waits in the GPU for the host's go word (StreamGate, conv_kernels.hpp).
+    Every path of that protocol against the oracle: back-to-back calls (the
+    chain takes the block), a pause longer than K1's 20 ms wait (the chain
+    gives up; the call cancels the chain behind it and runs the block with
+    ordinary launches), Reset with a chain pending, two handles interleaved,
+    and destroy with a chain pending."""
+    import time
+
+    K, B = 16384, 4096
+    h = signals.make_test_kernel(K)
+    x = signals.white_noise(B * 10, 11)
+    g = conv.NewStreamingOverlapSave(h, B)
+    g2 = conv.NewStreamingOverlapAdd(h[::-1].copy(), B)
+    o = O.Streaming(h, B)
+    o2 = O.Streaming(h[::-1].copy(), B, ola=True)
+    for i in range(10):
+        if i in (3, 7):
+            time.sleep(0.05)  # K1 of the pending chain times out
+        blk = x[i * B:(i + 1) * B]
+        got, want = g.ProcessBlock(blk), o.process_block(blk)
+        assert rms(got, want) < FFT_RMS_TOL and np.max(np.abs(got - want)) < 1e-9, i
+        got2, want2 = g2.ProcessBlock(blk), o2.process_block(blk)
+        assert rms(got2, want2) < FFT_RMS_TOL, i
+    g.Reset()
+    o = O.Streaming(h, B)
+    for i in range(3):
+        blk = x[i * B:(i + 1) * B]
+        assert rms(g.ProcessBlock(blk), o.process_block(blk)) < FFT_RMS_TOL, i
+    del g, g2  # destroy with a chain pending (its K1 released at once)
 
 
 def test_streaming_non_pow2_vs_streaming_oracle(gpu):

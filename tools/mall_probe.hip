@@ -115,6 +115,20 @@ int main(int argc, char** argv) {
                   rb >> 20, regions, tw, total / (tw * 1e-6) / 1e12, tr, total / (tr * 1e-6) / 1e12);
     }
   }
+  // one fresh pass (each launch a region untouched for >= 3 GiB of traffic)
+  // of S bytes: does the launch's own footprint set the rate?
+  for (long S : {128L << 20, 256L << 20, 512L << 20, 1L << 30}) {
+    const long it = S / (ITEM * 16);
+    const long regions = alloc / S;
+    const double tw = timeit([&](int r) {
+      hipLaunchKernelGGL(k_write, dim3(grid), dim3(256), 0, 0, ring + (r % regions) * it * ITEM, it, it);
+    });
+    const double tr = timeit([&](int r) {
+      hipLaunchKernelGGL(k_read, dim3(grid), dim3(256), 0, 0, ring + (r % regions) * it * ITEM, it, it, sink);
+    });
+    std::printf("fresh single pass %5ld MiB: write %7.1f us (%5.2f TB/s)  read %7.1f us (%5.2f TB/s)\n", S >> 20, tw,
+                S / (tw * 1e-6) / 1e12, tr, S / (tr * 1e-6) / 1e12);
+  }
   // translation test: a single fresh pass over 1 GiB (regions rotate over 4 GiB),
   // optionally preceded (same stream, not timed separately) by a sparse touch of
   // that region: one load per 64 KiB or per 2 MiB
