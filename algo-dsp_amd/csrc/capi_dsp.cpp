@@ -36,6 +36,12 @@ CompParams comp_params(const ad_compressor_config& g) {
   }
   p.attack = attack;
   p.release = release;
+  {
+    const double b = 1.0 - release;
+    p.env_c1 = 0.5 * (attack + b);
+    p.env_c2 = 0.5 * (attack - b);
+    p.env_k1 = 1.0 - p.env_c1;
+  }
   p.threshold_log2 = g.threshold_db * kLog2Of10Div20;
   p.knee_width_log2 = g.knee_db * kLog2Of10Div20;
   p.inv_knee_width_log2 = g.knee_db > 0 ? 1.0 / p.knee_width_log2 : 0.0;

@@ -9,6 +9,23 @@
 namespace adsp {
 
 // Go math.Log2 (frexp split + Log(frac)*(1/Ln2) + exp), core.go via compressor_math.go:8-20.
+// One envelope-follower step of dynamicsCore.detectorLevel (core.go:351-355):
+//   src > env: env + (src - env) * attack      else: src + (env - src) * release
+// Both branches are env + k (src - env) with k = attack or b = 1 - release, so
+// the step is env + c1 (src - env) + c2 |src - env|, written as
+//   fma(c2, |src - env|, fma(1 - c1, env, c1 src))
+// with c1 = (attack + b)/2, c2 = (attack - b)/2 (CompParams::env_*).  The map
+// is the reference's; the rounding is not (a few ulps on the envelope, which
+// the gain's log2 / exp2 already make a tolerance).  The
+// reference's form is a compare, a select and three dependent operations on
+// the envelope, 109 clocks per sample for one wave on gfx950; this one has no
+// compare or select (|.| is a source modifier) and two dependent FMAs: 24.5
+// clocks (tools/chain_latency.hip).  The detector is config 5's longest
+// recurrence, so its chain is the engine's floor.
+__device__ __forceinline__ double env_step(const CompParams& p, double env, double src) {
+  return __builtin_fma(p.env_c2, fabs(src - env), __builtin_fma(p.env_k1, env, p.env_c1 * src));
+}
+
 __device__ __forceinline__ double go_log2(double x) {
 #pragma clang fp contract(off)
   int e;

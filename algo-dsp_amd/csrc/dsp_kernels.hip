@@ -147,10 +147,7 @@ __global__ __launch_bounds__(64) void k_chain(ChainArgs a) {
           const double mean = cs.rms_sum / (double)p.rms_n;
           src = mean <= 0.0 ? 0.0 : sqrt(mean);
         }
-        if (src > cs.env)
-          cs.env += (src - cs.env) * p.attack;
-        else
-          cs.env = src + (cs.env - src) * p.release;
+        cs.env = env_step(p, cs.env, src);
         double g = gain_for_level(p, cs.env);
         if (p.mode == 2) {  // gate hold (gate.go:361-366)
           if (g >= 1.0) {
@@ -346,12 +343,7 @@ __global__ __launch_bounds__(320) void k_chain_pipe(ChainArgs a) {
               src = mean <= 0.0 ? 0.0 : sqrt(mean);
             }
           }
-          if (real) {
-            if (src > cs.env)
-              cs.env += (src - cs.env) * p.attack;
-            else
-              cs.env = src + (cs.env - src) * p.release;
-          }
+          if (real) cs.env = env_step(p, cs.env, src);
           ring_v[r][d][l] = v;
           ring_env[r][d][l] = cs.env;
         }

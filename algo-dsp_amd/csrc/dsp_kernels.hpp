@@ -30,6 +30,10 @@ struct CompParams {
   double cf;  // 1 - 1/ratio, or ratio - 1 (feedback topology with ratio scaling)
   double makeup_lin;
   double attack, release;  // already the feedback pair when that topology is scaled
+  // the envelope step as env' = c2 |src - env| + (k1 env + c1 src) (env_step,
+  // dsp_device.hpp): c1 = (attack + b) / 2, c2 = (attack - b) / 2, k1 = 1 - c1,
+  // b = 1 - release
+  double env_c1, env_c2, env_k1;
   double lp_alpha, hp_alpha;
   int knee_on, topology_fb, detector_rms, lp_on, hp_on, rms_n;
   // dynamics.Expander / dynamics.Gate (expander.go, gate.go): mode 1 / 2 use

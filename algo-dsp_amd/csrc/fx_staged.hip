@@ -260,8 +260,7 @@ __global__ __launch_bounds__(64 * (kMaxSecPerPass + 2)) void k_fx_eq(FxStageArgs
 #pragma unroll
           for (int d = 0; d < kEqP; ++d) {
             const double src = fabs(x[d]);
-            const double ne =
-                src > cs.env ? cs.env + (src - cs.env) * p.attack : src + (cs.env - src) * p.release;
+            const double ne = env_step(p, cs.env, src);
             cs.env = ne;
             e[d] = ne;
           }
@@ -293,7 +292,7 @@ __global__ __launch_bounds__(64 * (kMaxSecPerPass + 2)) void k_fx_eq(FxStageArgs
             const double mean = cs.rms_sum / (double)p.rms_n;
             src = mean <= 0.0 ? 0.0 : sqrt(mean);
           }
-          const double ne = src > cs.env ? cs.env + (src - cs.env) * p.attack : src + (cs.env - src) * p.release;
+          const double ne = env_step(p, cs.env, src);
           if (real) cs.env = ne;
           e[d] = ne;
         }

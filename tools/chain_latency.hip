@@ -1,0 +1,98 @@
+// Microbenchmark: cycles per sample of the serial recurrences of config 5's
+// compressor detector and Freeverb comb, one wave, in the forms a kernel can
+// write them:
+//  env/ref    env' = src > env ? env + (src-env)*a : src + (env-src)*r  (core.go:351-355)
+//  env/abs    env' = fma(c2, |src-env|, fma(1-c1, env, c1*src)),
+//             c1 = (a + b)/2, c2 = (a - b)/2, b = 1 - r  (the same map, other rounding)
+//  comb/ref   fs' = flush(out*d2 + fs*d1), flush: |v| < 1e-23 -> 0   (reverb.go:101-117)
+//  comb/int   the same with the flush as integer ops on the bit pattern (bit-exact)
+//   hipcc --offload-arch=gfx950 -O3 tools/chain_latency.hip -o tools/chain_latency
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+
+template <int V>
+__global__ void k_env(double* out, const double* in, int iters, double a, double r, long long* cyc) {
+#pragma clang fp contract(off)
+  double x[8];
+  for (int d = 0; d < 8; ++d) x[d] = in[d * 64 + threadIdx.x];
+  const double b = 1.0 - r, c1 = 0.5 * (a + b), c2 = 0.5 * (a - b), k1 = 1.0 - c1;
+  double env = 0.0, acc = 0.0;
+  const long long t0 = clock64();
+  for (int i = 0; i < iters; ++i) {
+#pragma unroll
+    for (int d = 0; d < 8; ++d) {
+      const double src = fabs(x[d]);
+      double ne;
+      if constexpr (V == 0) {
+        ne = src > env ? env + (src - env) * a : src + (env - src) * r;
+      } else {
+        ne = __builtin_fma(c2, fabs(src - env), __builtin_fma(k1, env, c1 * src));
+      }
+      env = ne;
+      acc += ne;
+    }
+  }
+  const long long t1 = clock64();
+  out[threadIdx.x] = acc + env;
+  if (threadIdx.x == 0) *cyc = t1 - t0;
+}
+
+__device__ __forceinline__ double flush_int(double v) {
+  // |v| < 1e-23 -> +0 (v itself otherwise), from the bit pattern: the
+  // magnitude bits compare like the magnitudes (non-negative, non-NaN)
+  const long long bits = __double_as_longlong(v);
+  const long long mag = bits & 0x7fffffffffffffffLL;
+  const long long thr = __double_as_longlong(1e-23);
+  const long long keep = (thr - 1 - mag) >> 63;  // all ones when mag >= thr
+  return __longlong_as_double(bits & keep);
+}
+
+template <int V>
+__global__ void k_comb(double* out, const double* in, int iters, double d1, double d2, long long* cyc) {
+#pragma clang fp contract(off)
+  double x[8];
+  for (int d = 0; d < 8; ++d) x[d] = in[d * 64 + threadIdx.x];
+  double fs = 0.0, acc = 0.0;
+  const long long t0 = clock64();
+  for (int i = 0; i < iters; ++i) {
+#pragma unroll
+    for (int d = 0; d < 8; ++d) {
+      const double o = x[d];
+      double v = o * d2 + fs * d1;
+      if constexpr (V == 0)
+        v = fabs(v) < 1e-23 ? 0.0 : v;
+      else
+        v = flush_int(v);
+      fs = v;
+      acc += v;
+    }
+  }
+  const long long t1 = clock64();
+  out[threadIdx.x] = acc + fs;
+  if (threadIdx.x == 0) *cyc = t1 - t0;
+}
+
+int main() {
+  double *d, *in;
+  long long* cy;
+  if (hipMalloc(&d, 64 * 8) || hipMalloc(&in, 512 * 8) || hipMalloc(&cy, 8)) return 1;
+  double h[512];
+  for (int i = 0; i < 512; ++i) h[i] = ((i * 7919) % 1000) / 1000.0 - 0.5;
+  if (hipMemcpy(in, h, sizeof(h), hipMemcpyHostToDevice)) return 1;
+  const int iters = 20000;
+  long long v;
+  auto report = [&](const char* name) {
+    if (hipMemcpy(&v, cy, 8, hipMemcpyDeviceToHost)) return;
+    printf("%-10s %.1f cycles per sample (one wave)\n", name, (double)v / iters / 8);
+  };
+  for (int r = 0; r < 2; ++r) hipLaunchKernelGGL(k_env<0>, dim3(1), dim3(64), 0, 0, d, in, iters, 0.002, 0.9998, cy);
+  report("env/ref");
+  for (int r = 0; r < 2; ++r) hipLaunchKernelGGL(k_env<1>, dim3(1), dim3(64), 0, 0, d, in, iters, 0.002, 0.9998, cy);
+  report("env/abs");
+  for (int r = 0; r < 2; ++r) hipLaunchKernelGGL(k_comb<0>, dim3(1), dim3(64), 0, 0, d, in, iters, 0.45, 0.55, cy);
+  report("comb/ref");
+  for (int r = 0; r < 2; ++r) hipLaunchKernelGGL(k_comb<1>, dim3(1), dim3(64), 0, 0, d, in, iters, 0.45, 0.55, cy);
+  report("comb/int");
+  return 0;
+}
