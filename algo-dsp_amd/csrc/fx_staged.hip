@@ -44,6 +44,20 @@ constexpr int kCombB = 16; // K_comb samples per load/store batch
 
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 
+// Global-address-space view of a buffer.  Plain HIP pointers are generic:
+// where the compiler cannot prove the space it emits flat loads and stores,
+// which count in BOTH the vector-memory and the LDS/scalar counters, so every
+// LDS wait (lgkmcnt) also waits for the flat accesses in flight, and the
+// waits it inserts at merges degrade to vmcnt(0).  That drained the
+// prefetched delay-line batches of K_comb and made K_eq's last section and
+// detector wait each step for the previous step's row stores.  Every stage
+// buffer below is accessed through these pointers (global_load / store only).
+#define AD_GLOBAL __attribute__((address_space(1)))
+template <class T>
+__device__ __forceinline__ AD_GLOBAL T* glob(T* p) {
+  return (AD_GLOBAL T*)p;
+}
+
 // A pointer the compiler can prove wave-uniform (SGPR pair), so that p[lane]
 // becomes a scalar-base + 32-bit VGPR-offset access with no 64-bit VALU add.
 template <class T>
@@ -113,8 +127,8 @@ __global__ __launch_bounds__(64 * (kMaxSecPerPass + 2)) void k_fx_eq(FxStageArgs
   const int64_t steps = nst + W - 1;
   const int cp = a.cpad;
   const unsigned uc = (unsigned)c;
-  const double* xin = P.in;  // uniform row pointers; a lane indexes [uc]
-  double* tmo = P.out;
+  const AD_GLOBAL double* xin = glob(P.in);  // uniform row pointers; a lane indexes [uc]
+  AD_GLOBAL double* tmo = glob(P.out);
 
   // Wave 0's input comes from xring, filled by the loader wave (wave W):
   // it loads each step's rows kEqPF steps before it writes them to LDS, in
@@ -126,8 +140,8 @@ __global__ __launch_bounds__(64 * (kMaxSecPerPass + 2)) void k_fx_eq(FxStageArgs
     for (int d = 0; d < kEqP; ++d) x[d] = xring[(my & 1)][d][l];
   };
   // time-major rows of step `my`: full steps walk a uniform row pointer
-  auto put_rows = [&](double* base, int64_t my, const double (&y)[kEqP], int nreal) {
-    double* o = uniform_ptr(base + my * kEqP * cp);
+  auto put_rows = [&](AD_GLOBAL double* base, int64_t my, const double (&y)[kEqP], int nreal) {
+    AD_GLOBAL double* o = uniform_ptr(base + my * kEqP * cp);
     if (nreal == kEqP) {
 #pragma unroll
       for (int d = 0; d < kEqP; ++d) {
@@ -148,17 +162,14 @@ __global__ __launch_bounds__(64 * (kMaxSecPerPass + 2)) void k_fx_eq(FxStageArgs
   } else if (w == W) {
     // ---- loader
     double buf[kEqPF][kEqP];
+    // Branch-free: every call issues exactly kEqP loads (rows past the chunk
+    // re-read its last row), so the compiler's vmcnt bookkeeping stays exact
+    // across the unrolled buffers and each put waits only for its own step.
     auto fetch = [&](double (&dst)[kEqP], int64_t step) {
-      if ((step + 1) * kEqP <= len) {
-        const double* r = uniform_ptr(xin + step * kEqP * cp);
 #pragma unroll
-        for (int d = 0; d < kEqP; ++d) {
-          dst[d] = r[uc];
-          r += cp;
-        }
-      } else if (step < nst) {
-#pragma unroll
-        for (int d = 0; d < kEqP; ++d) dst[d] = xin[min(step * kEqP + d, len - 1) * cp + uc];
+      for (int d = 0; d < kEqP; ++d) {
+        const int64_t row = __builtin_amdgcn_readfirstlane(min(step * kEqP + d, len - 1));
+        dst[d] = uniform_ptr(xin + row * cp)[uc];
       }
     };
     auto put = [&](const double (&src)[kEqP], int64_t step) {
@@ -187,12 +198,16 @@ __global__ __launch_bounds__(64 * (kMaxSecPerPass + 2)) void k_fx_eq(FxStageArgs
   } else if (w < ns) {
     // ---- EQ section P.s0 + w (section.go:47-53 with the chain gain as pre-gain)
     const int gs = P.s0 + w;  // the section's index in the chain
-    const double* sec = a.eq.sec + (int64_t)cc * a.eq.sec_ch_stride + gs * kSecStride;
+    const AD_GLOBAL double* sec = glob(a.eq.sec) + (int64_t)cc * a.eq.sec_ch_stride + gs * kSecStride;
     double q[kSecStride];
 #pragma unroll
     for (int k = 0; k < kSecStride; ++k) q[k] = sec[k];
-    double* st = a.eq.state + ((int64_t)cc * a.eq.nsec + gs) * 2;
+    AD_GLOBAL double* st = glob(a.eq.state) + ((int64_t)cc * a.eq.nsec + gs) * 2;
     double d0 = st[0], d1 = st[1];
+    // the coefficient and state loads land here, before the step loop: left
+    // pending, the loop-head merge with the stores in flight made the
+    // compiler wait vmcnt(0) at every step (the last section's row stores)
+    __builtin_amdgcn_s_waitcnt(0);
     const bool to_ring = w < ns - 1 || det;
     const bool last = w == ns - 1;
     unsigned long long tc = 0, tb = 0;
@@ -237,9 +252,10 @@ __global__ __launch_bounds__(64 * (kMaxSecPerPass + 2)) void k_fx_eq(FxStageArgs
   } else if (det) {
     // ---- detector + envelope (core.go:274-286, 331-400)
     const CompParams& p = a.cp;
-    CompChState cs = a.cs[cc];
-    double* rring = a.rms_ring + (int64_t)cc * p.rms_n;
-    double* eo = P.env;
+    CompChState cs = a.cs[cc];  // generic load: drained by the wait below
+    AD_GLOBAL double* rring = glob(a.rms_ring) + (int64_t)cc * p.rms_n;
+    AD_GLOBAL double* eo = glob(P.env);
+    __builtin_amdgcn_s_waitcnt(0);  // state loads land before the step loop (see the section waves)
     lds_barrier();  // the loader's prologue (step 0 in xring)
     unsigned long long tc = 0, tb = 0;
     for (int64_t k = 0; k < steps; ++k) {
@@ -311,7 +327,7 @@ __global__ __launch_bounds__(64 * (kMaxSecPerPass + 2)) void k_fx_eq(FxStageArgs
       a.prof[2 * (P.s0 + ns) + 1] = tb;
     }
     if (active) {  // only the fields this stage owns
-      CompChState* o = a.cs + c;
+      AD_GLOBAL CompChState* o = glob(a.cs) + c;
       o->env = cs.env;
       o->lp = cs.lp;
       o->hp = cs.hp;
@@ -476,12 +492,13 @@ __global__ __launch_bounds__(64) void k_fx_comb(FxStageArgs a) {
   // channels of a handle advance their delay lines together (every call
   // processes every channel over the same samples, Reset clears all), so
   // the ring index is uniform and lane 0's copy drives the addresses.
-  double* line = a.vbuf + (int64_t)comb_off(i) * cp;
-  double* co = a.coT + (int64_t)i * a.tmax * cp;
-  const double* in = a.inT;
+  AD_GLOBAL double* line = glob(a.vbuf) + (int64_t)comb_off(i) * cp;
+  AD_GLOBAL double* co = glob(a.coT) + (int64_t)i * a.tmax * cp;
+  const AD_GLOBAL double* in = glob(a.inT);
   const VerbParams& p = a.vp;
-  int idx = __builtin_amdgcn_readfirstlane(a.vs[cc].comb_idx[i]);
-  double fs = a.vs[cc].filter_store[i];
+  AD_GLOBAL VerbChState* vs = glob(a.vs);
+  int idx = __builtin_amdgcn_readfirstlane(vs[cc].comb_idx[i]);
+  double fs = vs[cc].filter_store[i];
   const int64_t len = a.len;
   // three batches in flight: batch m sits in buffer m % 3 and is loaded two
   // batches before it runs (~100 samples of lead at ~80 cycles/sample).
@@ -494,8 +511,8 @@ __global__ __launch_bounds__(64) void k_fx_comb(FxStageArgs a) {
   auto load = [&](int b) {
     int pos = lpos;
     if (pos + kCombB <= clen && lt + kCombB <= len) {
-      const double* lr = uniform_ptr(line + (int64_t)pos * cp);
-      const double* ir = uniform_ptr(in + lt * cp);
+      const AD_GLOBAL double* lr = uniform_ptr(line + (int64_t)pos * cp);
+      const AD_GLOBAL double* ir = uniform_ptr(in + lt * cp);
 #pragma unroll
       for (int j = 0; j < kCombB; ++j) {
         dl[b][j] = lr[uc];
@@ -521,8 +538,8 @@ __global__ __launch_bounds__(64) void k_fx_comb(FxStageArgs a) {
     double nv[kCombB];
     if (nb == kCombB && idx + kCombB <= clen) {
       comb_batch<true>(p, fs, dl[b], xg[b], nv, nb);
-      double* cr = uniform_ptr(co + t0 * cp);
-      double* lr = uniform_ptr(line + (int64_t)idx * cp);
+      AD_GLOBAL double* cr = uniform_ptr(co + t0 * cp);
+      AD_GLOBAL double* lr = uniform_ptr(line + (int64_t)idx * cp);
 #pragma unroll
       for (int j = 0; j < kCombB; ++j) {
         cr[uc] = dl[b][j];
@@ -561,8 +578,8 @@ __global__ __launch_bounds__(64) void k_fx_comb(FxStageArgs a) {
     run(2, t0 + 2 * kCombB);
   }
   if (active) {
-    a.vs[uc].comb_idx[i] = idx;
-    a.vs[uc].filter_store[i] = fs;
+    vs[uc].comb_idx[i] = idx;
+    vs[uc].filter_store[i] = fs;
   }
 }
 

@@ -28,7 +28,9 @@ sys.path.insert(0, str(ROOT / "algo-dsp_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FX_CLOCK_HZ = 2.4e9     # MI355X engine clock (MI355X_MICROARCH.md)
-FX_DETECTOR_CLK = 109   # envelope follower, clocks per sample (tools/env_latency.hip)
+FX_CHAIN_CLK = 52       # longest per-sample dependency chain of config 5, clocks: the DF-II-T
+                        # section (tools/biquad_latency.hip); the envelope follower is 24.5
+                        # (tools/chain_latency.hip), a Freeverb comb 38
 
 
 def parse():
@@ -690,19 +692,19 @@ def main_fx(args):
                        "parallelism": "replicas" if world > 1 else "single GPU"},
             # The bound is the serial recurrence, not HBM (16 B/sample moves
             # 0.5 % of peak): one lane per channel, 64 channels per wave, and
-            # the longest per-sample dependency chain is the compressor's
-            # envelope follower, 109 clocks per sample measured in isolation
-            # (tools/env_latency.hip; a DF-II-T section: 52, tools/biquad_latency.hip).
-            # Ceiling = clock x 64 channels / 109 clk per 64-channel group,
+            # the longest per-sample dependency chain is a DF-II-T EQ section,
+            # 52 clocks per sample in isolation (tools/biquad_latency.hip; the
+            # envelope follower: 24.5, a comb: 38, tools/chain_latency.hip).
+            # Ceiling = clock x 64 channels / 52 clk per 64-channel group,
             # times the groups (ceil(C / 64) = 4 at 256 channels).
             "roofline": {"bound": "serial-recurrence latency", "achieved": round(value, 3),
-                         "peak": round(FX_CLOCK_HZ * 64 / FX_DETECTOR_CLK * (-(-C // 64)) / 1e6, 1),
+                         "peak": round(FX_CLOCK_HZ * 64 / FX_CHAIN_CLK * (-(-C // 64)) / 1e6, 1),
                          "unit": "Msamples/s",
-                         "frac": round(value / (FX_CLOCK_HZ * 64 / FX_DETECTOR_CLK * (-(-C // 64)) / 1e6), 4),
+                         "frac": round(value / (FX_CLOCK_HZ * 64 / FX_CHAIN_CLK * (-(-C // 64)) / 1e6), 4),
                          "traffic": None,
                          "hbm_GBps": round(value * 16e6 / 1e9, 3),
-                         "note": f"ceiling = {FX_CLOCK_HZ / 1e9} GHz x 64 ch / {FX_DETECTOR_CLK} clk per sample "
-                                 f"(envelope-follower floor) x {-(-C // 64)} channel groups; HBM carries 16 B/sample"},
+                         "note": f"ceiling = {FX_CLOCK_HZ / 1e9} GHz x 64 ch / {FX_CHAIN_CLK} clk per sample "
+                                 f"(DF-II-T section chain) x {-(-C // 64)} channel groups; HBM carries 16 B/sample"},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
