@@ -86,50 +86,164 @@ __device__ __forceinline__ double pack_scale(const unsigned long long* amax, boo
 
 // {max|a[0..n)|, max|b[0..m)|} as bit patterns (non-negative doubles order
 // like their unsigned bit patterns; a NaN sorts above +inf and disables the
-// scale).  out must be zeroed first.
+// scale).  out must be zeroed first.  16-B loads, four in flight per thread,
+// and one atomic per workgroup: same-address atomics serialise (one per wave
+// over 8192 waves took 120-196 us for a 134 MB read).
 __global__ __launch_bounds__(256) void k_absmax2(const double* __restrict__ a, int64_t n, const double* __restrict__ b,
                                                  int64_t m, unsigned long long* out) {
   const double* x = blockIdx.y ? b : a;
   const int64_t len = blockIdx.y ? m : n;
   unsigned long long mx = 0;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < len; i += (int64_t)gridDim.x * 256) {
-    const unsigned long long v = (unsigned long long)__double_as_longlong(fabs(x[i]));
-    mx = v > mx ? v : mx;
+  auto acc = [&](double v) {
+    const unsigned long long u = (unsigned long long)__double_as_longlong(fabs(v));
+    mx = u > mx ? u : mx;
+  };
+  const int head = ((uintptr_t)x & 15) ? 1 : 0;  // doubles are 8-B aligned
+  const int64_t t0 = (int64_t)blockIdx.x * 256 + threadIdx.x, stride = (int64_t)gridDim.x * 256;
+  if (t0 == 0 && len > 0) {
+    if (head) acc(x[0]);
+    if ((len - head) & 1) acc(x[len - 1]);
+  }
+  const double2* x2 = reinterpret_cast<const double2*>(x + head);
+  const int64_t n2 = len > head ? (len - head) / 2 : 0;
+  int64_t i = t0;
+  for (; i + 3 * stride < n2; i += 4 * stride) {
+    const double2 v0 = x2[i], v1 = x2[i + stride], v2 = x2[i + 2 * stride], v3 = x2[i + 3 * stride];
+    acc(v0.x), acc(v0.y), acc(v1.x), acc(v1.y), acc(v2.x), acc(v2.y), acc(v3.x), acc(v3.y);
+  }
+  for (; i < n2; i += stride) {
+    const double2 v = x2[i];
+    acc(v.x), acc(v.y);
   }
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) {
     const unsigned long long t = __shfl_xor(mx, o);
     mx = t > mx ? t : mx;
   }
-  if ((threadIdx.x & 63) == 0) atomicMax(out + blockIdx.y, mx);
+  __shared__ unsigned long long wmax[4];
+  if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long m4 = wmax[0];
+    for (int w = 1; w < 4; ++w) m4 = wmax[w] > m4 ? wmax[w] : m4;
+    atomicMax(out + blockIdx.y, m4);
+  }
 }
 
 // ---------------------------------------------------------------------------
 // One global Stockham pass of radix R (16 <= R <= 4096): F = BLOCK*16/R
 // butterflies per workgroup.
 // ---------------------------------------------------------------------------
-// FW = butterflies per workgroup (Plan::F: 2 workgroups per CU; 8192/R: one
-// workgroup per CU with twice-longer contiguous runs per access).
-template <int R, int FW>
+// Pass shape.  V values per thread (FftPlan<R, V>); FW butterflies per
+// workgroup (FftPlan's F, times AD_FFT_FWX).  Compile-time A/B knobs for
+// tools/ builds only (the product library is built with the defaults).
+#ifndef AD_FFT_V
+#define AD_FFT_V 8
+#endif
+#ifndef AD_FFT_FWX
+#define AD_FFT_FWX 2
+#endif
+#ifndef AD_FFT_PAIR
+#define AD_FFT_PAIR 1  // mirror-paired tiles in the half inverse's first pass
+#endif
+#ifndef AD_FFT_TWC
+#define AD_FFT_TWC 1  // twiddles computed in the kernel (no table loads after the data loads)
+#endif
+template <int R>
 struct PassShape {
-  static constexpr int T = FftPlan<R, 16>::T;
-  static constexpr int BLOCK = FW * T;
+  static constexpr int V = AD_FFT_V;
+  static constexpr int T = FftPlan<R, V>::T;
+  static constexpr int F = FftPlan<R, V>::F * AD_FFT_FWX;
+  static constexpr int BLOCK = F * T;
 };
 // HALF: the first inverse pass of the spectral row's half-length inverse
 // (FftPassArgs::half), instantiated only where it can occur.
-template <int R, int FW, bool FWD, bool REALIN, bool REALOUT, int HALF = 0>
-__global__ __launch_bounds__((PassShape<R, FW>::BLOCK)) void k_fft_pass(FftPassArgs a) {
-  using Plan = FftPlan<R, 16>;
+// PAIR (HALF only, Z = FFT(a + i b) packed, Ns = 1, not the last pass): the
+// workgroup takes the butterfly tile [j0, j0 + F/2) and its Hermitian mirror
+// tile {nb - j}: the four Z values a lane loads (Z[g], Z[g + NF/2] and their
+// mirrors) give one element of each tile, so Z is read once instead of twice.
+template <int R, bool FWD, bool REALIN, bool REALOUT, int HALF = 0, bool PAIR = false>
+__global__ __launch_bounds__((PassShape<R>::BLOCK)) void k_fft_pass(FftPassArgs a) {
+  using Sh = PassShape<R>;
+  using Plan = FftPlan<R, Sh::V>;
   // per-butterfly LDS stride: odd when a 16-lane group stays inside one
   // transform (T >= 16), so the jj-fastest staging accesses spread over the banks
-  constexpr int V = 16, T = Plan::T, F = FW, BLOCK = PassShape<R, FW>::BLOCK, MP = Plan::MP + (T >= 16 ? 1 : 0);
+  constexpr int V = Sh::V, T = Plan::T, F = Sh::F, BLOCK = Sh::BLOCK, MP = Plan::MP + (T >= 16 ? 1 : 0);
   __shared__ __attribute__((aligned(16))) double2 lds_all[F * MP];
+  __shared__ __attribute__((aligned(16))) double2 ltw[AD_FFT_TWC ? TwSplit<R>::N : 1];
   const int bt = blockIdx.y;
   const int64_t nb = a.N / R;  // butterflies
-  const int64_t j0 = (int64_t)blockIdx.x * F;
+  // XCD-contiguous tiles: neighbouring butterfly tiles read neighbouring
+  // runs of the same rows, so they share an L2 and DRAM pages
+  const int64_t j0 = (int64_t)xcd_remap((int)blockIdx.x, (int)gridDim.x) * F;
+#if AD_FFT_TWC
+  const TwLds<R> twr = tw_lds_compute<R>(ltw, (int)threadIdx.x, BLOCK);
+#else
+  const TwGlobal twr{a.twR};
+#endif
 
   // stage in: element r of butterfly j0 + jj is x[j0 + jj + r nb]; jj fastest
   const double bscale = REALIN ? pack_scale(a.amax, false) : 1.0;
+  // The half inverse's input (HALF): X[q] = op(A[q], B[q]) from the forward
+  // spectrum Z = FFT(a + i b), A = (Z[q] + conj Z[-q]) / 2,
+  // B = (Z[q] - conj Z[-q]) / 2i (HALF = 1: the correlation, op fixed; 2: any
+  // op), then z[g] = E + i O with E = (X[g] + X[g + NF/2]) / 2 and
+  // O = (X[g] - X[g + NF/2]) W_NF^-g / 2.  spec2 set: A and B come from two
+  // separate transforms, in and spec2 (the division of Deconvolve must not
+  // take B out of a transform that A dominates).
+  const int64_t NF = a.NF, msk = NF - 1;
+  auto xop = [&](double2 zk, double2 zm, int64_t q) {  // zk = Z[q], zm = Z[-q]
+    const double2 A = make_double2(0.5 * (zk.x + zm.x), 0.5 * (zk.y - zm.y));
+    const double2 B = make_double2(0.5 * (zk.y + zm.y), -0.5 * (zk.x - zm.x));
+    return HALF == 1 ? go_cmul(A, c_conj(B)) : spec_op(a.op, A, B, a.eps, q, a.bad);
+  };
+  auto xq = [&](int64_t q) {
+    if (HALF == 2 && a.spec2) return spec_op(a.op, a.in[q], a.spec2[q], a.eps, q, a.bad);
+    return xop(a.in[q], a.in[(NF - q) & msk], q);
+  };
+  auto wneg = [&](int64_t g) {  // W_NF^-g
+#if AD_FFT_TWC
+    double sn, cs;
+    sincospi(2.0 * (double)g / (double)NF, &sn, &cs);  // g / NF exact (NF a power of two)
+    return make_double2(cs, sn);
+#else
+    const int64_t fm = ((int64_t)1 << a.fS) - 1;
+    return c_conj(c_mul(a.ftw_lo[g & fm], a.ftw_hi[g >> a.fS]));
+#endif
+  };
+  auto zcomb = [&](double2 x1, double2 x2, double2 w) {
+    const double2 e = make_double2(0.5 * (x1.x + x2.x), 0.5 * (x1.y + x2.y));
+    const double2 o = c_mul(make_double2(0.5 * (x1.x - x2.x), 0.5 * (x1.y - x2.y)), w);
+    return make_double2(e.x - o.y, e.y + o.x);
+  };
+  auto half_in = [&](int64_t g) { return zcomb(xq(g), xq(g + NF / 2), wneg(g)); };
+  constexpr int FP = F / 2;  // PAIR: butterflies per tile
+  const int64_t jp0 = PAIR ? j0 / 2 : 0;  // PAIR: tile A = [jp0, jp0 + FP)
+  if constexpr (PAIR) {
+    static_assert(HALF != 0 && !REALIN && !REALOUT, "PAIR: first pass of the half inverse only");
+#pragma unroll
+    for (int i = 0; i < V / 2; ++i) {
+      const int idx = i * BLOCK + (int)threadIdx.x;
+      const int jj = idx % FP, r = idx / FP;
+      const int64_t j = jp0 + jj;
+      double2 vA, vB;
+      if (j == 0) {  // butterfly 0 is its own mirror; tile B's slot 0 takes butterfly nb/2 (also its own)
+        vA = half_in((int64_t)r * nb);
+        vB = half_in(nb / 2 + (int64_t)(R - 1 - r) * nb);
+      } else {
+        // element (j, r) of tile A and (nb - j, R - 1 - r) of tile B:
+        //   g = j + r nb,  g* = NF/2 - g = (nb - j) + (R - 1 - r) nb
+        const int64_t g = j + (int64_t)r * nb, gs = (nb - j) + (int64_t)(R - 1 - r) * nb;
+        const double2 z1 = a.in[g], z2 = a.in[g + NF / 2];        // Z[g], Z[g + NF/2]
+        const double2 z3 = a.in[gs], z4 = a.in[gs + NF / 2];      // Z[-(g + NF/2)], Z[-g]
+        const double2 w = wneg(g);                                // W_NF^-g* = -conj(W_NF^-g)
+        vA = zcomb(xop(z1, z4, g), xop(z2, z3, g + NF / 2), w);
+        vB = zcomb(xop(z3, z2, gs), xop(z4, z1, gs + NF / 2), make_double2(-w.x, w.y));
+      }
+      lds_all[jj * MP + lds_slot(r)] = vA;
+      lds_all[(FP + jj) * MP + lds_slot(R - 1 - r)] = vB;
+    }
+  } else {
 #pragma unroll
   for (int i = 0; i < V; ++i) {
     const int idx = i * BLOCK + (int)threadIdx.x;
@@ -146,31 +260,13 @@ __global__ __launch_bounds__((PassShape<R, FW>::BLOCK)) void k_fft_pass(FftPassA
           v.x = g < a.nr[bt] ? a.xb[bt][g] : 0.0;
         }
       } else if constexpr (HALF != 0) {
-        // X[q] = op(A[q], B[q]) from the forward spectrum Z = FFT(a + i b):
-        // A = (Z[q] + conj Z[-q]) / 2, B = (Z[q] - conj Z[-q]) / 2i
-        const int64_t NF = a.NF, msk = NF - 1;
-        // (spec2 set: A and B come from two separate transforms, in and spec2 --
-        // the division of Deconvolve must not take B out of a transform that
-        // A dominates)
-        // HALF = 1: the correlation from Z = FFT(a + i b) (op fixed); 2: any op
-        auto xq = [&](int64_t q) {
-          if (HALF == 2 && a.spec2) return spec_op(a.op, a.in[q], a.spec2[q], a.eps, q, a.bad);
-          const double2 zk = a.in[q], zm = a.in[(NF - q) & msk];
-          const double2 A = make_double2(0.5 * (zk.x + zm.x), 0.5 * (zk.y - zm.y));
-          const double2 B = make_double2(0.5 * (zk.y + zm.y), -0.5 * (zk.x - zm.x));
-          return HALF == 1 ? go_cmul(A, c_conj(B)) : spec_op(a.op, A, B, a.eps, q, a.bad);
-        };
-        const double2 x1 = xq(g), x2 = xq(g + NF / 2);
-        const int64_t fm = ((int64_t)1 << a.fS) - 1;
-        const double2 w = c_conj(c_mul(a.ftw_lo[g & fm], a.ftw_hi[g >> a.fS]));  // W_NF^-g
-        const double2 e = make_double2(0.5 * (x1.x + x2.x), 0.5 * (x1.y + x2.y));
-        const double2 o = c_mul(make_double2(0.5 * (x1.x - x2.x), 0.5 * (x1.y - x2.y)), w);
-        v = make_double2(e.x - o.y, e.y + o.x);
+        v = half_in(g);
       } else {
         v = a.in[bt * a.in_batch + g];
       }
     }
     lds_all[jj * MP + lds_slot(r)] = v;
+  }
   }
   __syncthreads();
 
@@ -191,7 +287,14 @@ __global__ __launch_bounds__((PassShape<R, FW>::BLOCK)) void k_fft_pass(FftPassA
     const int64_t mask = ((int64_t)1 << a.S) - 1;
     auto tw = [&](int64_t e) {
       e &= a.N - 1;
+#if AD_FFT_TWC
+      (void)mask;
+      double sn, cs;
+      sincospi(-2.0 * (double)e / (double)a.N, &sn, &cs);  // e / N exact (N a power of two)
+      return make_double2(cs, sn);
+#else
       return c_mul(a.tw_lo[e & mask], a.tw_hi[e >> a.S]);
+#endif
     };
     double2 base = tw(jm * step * tid);  // u^tid
     const double2 cT = tw(jm * step * T);  // u^T
@@ -207,7 +310,7 @@ __global__ __launch_bounds__((PassShape<R, FW>::BLOCK)) void k_fft_pass(FftPassA
     }
   }
   __syncthreads();
-  fft_run<R, V, FWD>(v, tid, lds, TwGlobal{a.twR});
+  fft_run<R, V, FWD>(v, tid, lds, twr);
   __syncthreads();
 #pragma unroll
   for (int s = 0; s < V; ++s) lds[lds_slot(last_pass_index<R, V>(tid, s))] = v[s];
@@ -227,7 +330,8 @@ __global__ __launch_bounds__((PassShape<R, FW>::BLOCK)) void k_fft_pass(FftPassA
       jj = idx % F;
       rr = idx / F;
     }
-    const int64_t jo = j0 + jj;
+    int64_t jo = j0 + jj;
+    if constexpr (PAIR) jo = jj < FP ? jp0 + jj : (jp0 + jj == FP ? nb / 2 : nb - jp0 - (jj - FP));
     if (jo >= nb) continue;
     const double2 val = lds_all[jj * MP + lds_slot(rr)];
     const int64_t o = (jo & ~(Ns - 1)) * R + (jo & (Ns - 1)) + (int64_t)rr * Ns;
@@ -303,21 +407,29 @@ double2* upload(const std::vector<double2>& v) {
 
 template <int R, bool FWD, bool RI, bool RO>
 void go_pass(const FftPassArgs& a, int batch, hipStream_t s) {
+  using Sh = PassShape<R>;
+  const dim3 grid((unsigned)((a.N / R + Sh::F - 1) / Sh::F), (unsigned)batch);
   if constexpr (!FWD && !RI) {
     if (a.half) {
-      constexpr int F1 = FftPlan<R, 16>::F;
-      const dim3 grid((unsigned)((a.N / R + F1 - 1) / F1), (unsigned)batch);
+      // mirror-paired tiles: packed spectrum, not the last pass, whole tile pairs
+      const bool pair = AD_FFT_PAIR && !a.spec2 && !RO && (a.N / R) % Sh::F == 0;
+      if constexpr (!RO) {
+        if (pair) {
+          if (a.op == kSpecCorr)
+            hipLaunchKernelGGL((k_fft_pass<R, FWD, RI, RO, 1, true>), grid, dim3(Sh::BLOCK), 0, s, a);
+          else
+            hipLaunchKernelGGL((k_fft_pass<R, FWD, RI, RO, 2, true>), grid, dim3(Sh::BLOCK), 0, s, a);
+          return;
+        }
+      }
       if (a.op == kSpecCorr && !a.spec2)
-        hipLaunchKernelGGL((k_fft_pass<R, F1, FWD, RI, RO, 1>), grid, dim3(PassShape<R, F1>::BLOCK), 0, s, a);
+        hipLaunchKernelGGL((k_fft_pass<R, FWD, RI, RO, 1>), grid, dim3(Sh::BLOCK), 0, s, a);
       else
-        hipLaunchKernelGGL((k_fft_pass<R, F1, FWD, RI, RO, 2>), grid, dim3(PassShape<R, F1>::BLOCK), 0, s, a);
+        hipLaunchKernelGGL((k_fft_pass<R, FWD, RI, RO, 2>), grid, dim3(Sh::BLOCK), 0, s, a);
       return;
     }
   }
-  const int64_t nb = a.N / R;
-  constexpr int F1 = FftPlan<R, 16>::F;
-  const dim3 grid((unsigned)((nb + F1 - 1) / F1), (unsigned)batch);
-  hipLaunchKernelGGL((k_fft_pass<R, F1, FWD, RI, RO>), grid, dim3(PassShape<R, F1>::BLOCK), 0, s, a);
+  hipLaunchKernelGGL((k_fft_pass<R, FWD, RI, RO>), grid, dim3(Sh::BLOCK), 0, s, a);
 }
 
 template <bool FWD, bool RI, bool RO>
@@ -402,7 +514,7 @@ void BigFft::correlate_half(const BigFft& half, const double* a_, int64_t n, con
                             hipStream_t s) const {
   AD_HIP(hipMemsetAsync(amax, 0, 2 * sizeof(unsigned long long), s));
   const int64_t mx = std::max(n, m);
-  const unsigned gx = (unsigned)std::min<int64_t>(1024, (mx + 255) / 256);
+  const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>(256, (mx / 2 + 1023) / 1024));
   hipLaunchKernelGGL(k_absmax2, dim3(gx, 2), dim3(256), 0, s, a_, n, b_, m, amax);
   AD_HIP(hipGetLastError());
   // lags 0..n-1 from the front, -(m-1)..-1 from the back (correlate.go:165-171)

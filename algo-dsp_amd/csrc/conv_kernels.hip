@@ -33,17 +33,6 @@
 
 namespace adsp {
 
-// Workgroups are dealt round-robin over the 8 XCDs (b % 8 share one L2).
-// Remap the hardware index so each XCD owns a contiguous run of logical
-// indices: neighbouring blocks (which share input samples / X rows) then run
-// on the same XCD at about the same time.  Bijective for any grid size; a
-// different placement changes speed only, never results.
-__device__ __forceinline__ int xcd_remap(int b, int G) {
-  const int xcd = b & 7, r = b >> 3;
-  const int q = G >> 3, rem = G & 7;
-  return (xcd < rem) ? xcd * (q + 1) + r : rem * (q + 1) + (xcd - rem) * q + r;
-}
-
 // ---------------------------------------------------------------------------
 // K2: frequency-domain delay-line multiply-accumulate.
 //   Y[c][j][k] = sum_{p<P} X[c][g0+j-p][k] * H[ir(c)][p][k]

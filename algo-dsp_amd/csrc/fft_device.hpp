@@ -165,6 +165,17 @@ struct FftPlan {
   static constexpr int ns(int p) { return p == 0 ? 1 : R0 * (1 << (LOGV * (p - 1))); }
 };
 
+// Workgroups are dealt round-robin over the 8 XCDs (b % 8 share one L2).
+// Remap the hardware index so each XCD owns a contiguous run of logical
+// indices: neighbouring blocks (which share input samples / X rows) then run
+// on the same XCD at about the same time.  Bijective for any grid size; a
+// different placement changes speed only, never results.
+__device__ __forceinline__ int xcd_remap(int b, int G) {
+  const int xcd = b & 7, r = b >> 3;
+  const int q = G >> 3, rem = G & 7;
+  return (xcd < rem) ? xcd * (q + 1) + r : rem * (q + 1) + (xcd - rem) * q + r;
+}
+
 // Swizzled LDS index: the low 4 bits XOR g(i >> 4), g(q) = (q ^ ((q & 4) << 1)) & 15,
 // a bijection on each aligned 16-block (tools/lds_conflicts.py checks the plans).
 __device__ __forceinline__ int lds_slot(int i) {

@@ -30,17 +30,6 @@
 
 namespace adsp {
 
-// Workgroups are dealt round-robin over the 8 XCDs (b % 8 share one L2).
-// Remap the hardware index so each XCD owns a contiguous run of logical
-// indices: neighbouring blocks (which share input samples) then run on the
-// same XCD at about the same time.  Bijective for any grid size; a different
-// placement changes speed only, never results.
-__device__ __forceinline__ int xcd_remap_fft(int b, int G) {
-  const int xcd = b & 7, r = b >> 3;
-  const int q = G >> 3, rem = G & 7;
-  return (xcd < rem) ? xcd * (q + 1) + r : rem * (q + 1) + (xcd - rem) * q + r;
-}
-
 __device__ __forceinline__ double2 fetch_pair(const double* xc, int64_t t, int64_t n, bool aligned) {
   if (t + 1 < n && aligned) return *reinterpret_cast<const double2*>(xc + t);
   return make_double2(t < n ? xc[t] : 0.0, t + 1 < n ? xc[t + 1] : 0.0);
@@ -122,7 +111,7 @@ __global__ __launch_bounds__((FftPlan<M, V>::BLOCK)) void k_window_rfft(RfftArgs
   __shared__ __attribute__((aligned(16))) double2 lds_all[Plan::F * Plan::MP];
   const int f = threadIdx.x / T;
   const int tid = threadIdx.x % T;
-  const int64_t e = (int64_t)xcd_remap_fft(blockIdx.x, gridDim.x) * a.per_wg + f;
+  const int64_t e = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * a.per_wg + f;
   const bool active = f < a.per_wg && e < (int64_t)a.channels * a.jc;
   const int c = active ? (int)(e / a.jc) : 0;
   const int j = active ? (int)(e % a.jc) : 0;
@@ -151,7 +140,7 @@ __global__ __launch_bounds__((FftPlan<M, V>::BLOCK)) void k_irfft_store(IrfftArg
   __shared__ __attribute__((aligned(16))) double2 lds_all[Plan::F * Plan::MP];
   const int f = threadIdx.x / T;
   const int tid = threadIdx.x % T;
-  const int64_t e = (int64_t)xcd_remap_fft(blockIdx.x, gridDim.x) * Plan::F + f;
+  const int64_t e = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * Plan::F + f;
   const bool active = e < (int64_t)a.channels * a.jc;
   const int c = active ? (int)(e / a.jc) : 0;
   const int j = active ? (int)(e % a.jc) : 0;
@@ -287,7 +276,7 @@ __global__ __launch_bounds__((SplitPlan<M>::T)) __attribute__((amdgpu_waves_per_
     j = __builtin_amdgcn_readfirstlane((k / a.channels) * a.ord_R - a.ord_pc + t);
     if (j < 0 || j >= a.jc) return;
   } else {
-    const int e = __builtin_amdgcn_readfirstlane(xcd_remap_fft(blockIdx.x, gridDim.x));  // uniform: SGPRs
+    const int e = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, gridDim.x));  // uniform: SGPRs
     c = __builtin_amdgcn_readfirstlane(e / a.jc);
     j = __builtin_amdgcn_readfirstlane(e - c * a.jc);
   }
@@ -351,7 +340,7 @@ __global__ __launch_bounds__((SplitPlan<M>::T)) __attribute__((amdgpu_waves_per_
     j = __builtin_amdgcn_readfirstlane((k / a.channels) * a.ord_R + t);
     if (j >= a.jc) return;
   } else {
-    const int e = __builtin_amdgcn_readfirstlane(xcd_remap_fft(blockIdx.x, gridDim.x));
+    const int e = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, gridDim.x));
     c = __builtin_amdgcn_readfirstlane(e / a.jc);
     j = __builtin_amdgcn_readfirstlane(e - c * a.jc);
   }
