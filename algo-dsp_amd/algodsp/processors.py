@@ -63,7 +63,7 @@ class _FxChain:
 
     # engine selection (include/algodsp.h ad_fx_chain_set_engine); results are
     # identical in every engine
-    ENGINE_AUTO, ENGINE_FUSED, ENGINE_STAGED_NOSPLIT = 0, 1, 2
+    ENGINE_AUTO, ENGINE_FUSED, ENGINE_STAGED_NOSPLIT, ENGINE_STAGED = 0, 1, 2, 3
 
     def SetEngine(self, engine: int, chunk: int = 0):
         check(lib().ad_fx_chain_set_engine(self._h, int(engine), int(chunk)))

@@ -128,6 +128,12 @@ struct ad_fx_chain {
   hipEvent_t ev[3][kFxSlots] = {};
   DevBuf<double> xT[kFxSlots], vT[kFxSlots], envT[kFxSlots], inT[kFxSlots], coT[kFxSlots];
   DevBuf<double> midT[kFxSlots];  // split K_eq: the first part's output rows
+  // time-parallel engine (fx_tp.hip): K_eq segment states
+  DevBuf<double> tp_zs, tp_carry;
+  DevBuf<double> inC[kFxSlots];  // reverb input, channel-major [cpad][tmax]
+  DevBuf<double> vbufC;          // Freeverb lines channel-major [channels][kVerbLen] (K_verb)
+  DevBuf<double> coC;            // K_verb comb outputs [channels][8][tmax] (scratch, stream st[1] only)
+  bool verb_cm = false;          // vbufC (not vbuf) holds the current delay lines
   int64_t tmax = 0;
   // engine selection (ad_fx_chain_set_engine) and per-wave clock counters of
   // the first chunk of each call (ad_fx_chain_set_profiling)
@@ -180,6 +186,7 @@ void fx_reset_verb(ad_fx_chain* h) {
   if (!h->verb_on) return;
   AD_HIP(hipMemsetAsync(h->vs.p, 0, h->vs.n * sizeof(VerbChState), h->stream));
   AD_HIP(hipMemsetAsync(h->vbuf.p, 0, h->vbuf.n * sizeof(double), h->stream));
+  if (h->vbufC.p) AD_HIP(hipMemsetAsync(h->vbufC.p, 0, h->vbufC.n * sizeof(double), h->stream));
 }
 
 // The staged engine runs the chain as stage kernels over time chunks of T
@@ -382,11 +389,154 @@ void fx_run_staged(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hip
   if (verb) AD_HIP(hipStreamWaitEvent(s, h->ev[EA][k], 0));  // the last chunk's allpasses follow all work
 }
 
+// The time-parallel engine (fx_tp.hip): per chunk of T samples, the caller's
+// stream runs the input transpose and the nsec + 1 K_eq launches; st[0] the
+// detector (one wave per 64 channels, serial) of that chunk; st[1] the gain,
+// the combs and the allpasses.  So chunk i's EQ overlaps chunk i-1's detector
+// and chunk i-2's reverb.  A slot is reused only after st[1] is done with it
+// (the detector precedes st[1]'s work on every chunk).
+constexpr int64_t kFxTpChunk = 16384;
+constexpr int kFxTpSeg = 64;     // K_eq segment (samples), at least
+constexpr int kFxTpMaxSeg = 256;  // K_eq segments per chunk, at most (fx_tp.hip kTpQ)
+
+// K_comb warm-up: samples after which the damping filter's start value is
+// below 2^-60 of the run (da^wu < 2^-60); 0 without damping; a filter that
+// forgets too slowly runs each window as one segment.
+int fx_comb_warmup(const VerbParams& vp) {
+  const double da = std::fabs(vp.damp_a);
+  if (da == 0.0) return 0;
+  if (da >= 0.97) return 1 << 20;
+  return (int)std::ceil(-60.0 * std::log(2.0) / std::log(da));
+}
+
+void fx_run_tp(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hipStream_t s) {
+  const bool eq = h->nsec > 0, comp = h->comp_on, verb = h->verb_on;
+  const int64_t T = std::min(h->chunk > 0 ? h->chunk : kFxTpChunk, n);
+  if (!h->st[0]) {
+    for (auto& x : h->st) AD_HIP(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
+    for (auto& e2 : h->ev)
+      for (auto& e : e2) AD_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    AD_HIP(hipEventCreateWithFlags(&h->ev_in, hipEventDisableTiming));
+  }
+  if (T > h->tmax || !h->xT[0].p || (eq && !h->vT[0].p) || (comp && !h->envT[0].p) ||
+      (comp && verb && (!h->inC[0].p || !h->coC.p)) || (eq && !h->tp_zs.p)) {  // (re)size once no stage is running
+    for (hipStream_t x : h->st) AD_HIP(hipStreamSynchronize(x));
+    AD_HIP(hipStreamSynchronize(s));
+    const size_t r = (size_t)h->cpad * std::max(T, h->tmax);
+    for (int k = 0; k < kFxSlots; ++k) {
+      h->xT[k].alloc(r);
+      if (eq) h->vT[k].alloc(r);
+      if (comp) h->envT[k].alloc(r);
+      if (comp && verb) h->inC[k].alloc(r);
+    }
+    if (comp && verb) h->coC.alloc((size_t)h->channels * kVerbCombs * std::max(T, h->tmax));
+    if (eq) {
+      h->tp_zs.alloc((size_t)kFxTpMaxSeg * h->cpad * 2);
+      h->tp_carry.alloc((size_t)kFxTpMaxSeg * h->cpad * 2);
+    }
+    h->tmax = std::max(T, h->tmax);
+  }
+#ifdef AD_FX_TP_SERIAL  // tools/ builds only: every stage on the caller's stream (isolated kernel times)
+  hipStream_t sd = s, sv = s;
+#else
+  hipStream_t sd = h->st[0], sv = h->st[1];
+#endif
+  enum { EE = 0, ED = 1, EA = 2 };
+  if (verb && !h->verb_cm) {  // the delay lines into K_verb's channel-major layout
+    h->vbufC.reserve((size_t)kVerbLen * h->channels);
+    launch_vbuf_layout(h->vbuf.p, h->vbufC.p, h->cpad, h->channels, true, s);
+    h->verb_cm = true;
+  }
+  AD_HIP(hipEventRecord(h->ev_in, s));
+  AD_HIP(hipStreamWaitEvent(sd, h->ev_in, 0));
+  AD_HIP(hipStreamWaitEvent(sv, h->ev_in, 0));
+  const int wu = verb ? fx_comb_warmup(h->vp) : 0;
+  int64_t i = 0;
+  int k = 0;
+  for (int64_t t0 = 0; t0 < n; t0 += T, ++i) {
+    k = (int)(i % kFxSlots);
+    FxStageArgs a{};
+    a.channels = h->channels;
+    a.cpad = h->cpad;
+    a.len = std::min(T, n - t0);
+    a.buf = d_buf + t0;
+    a.stride = stride;
+    a.xT = h->xT[k].p;
+    a.vT = eq ? h->vT[k].p : h->xT[k].p;  // the EQ output (or the input)
+    a.envT = h->envT[k].p;
+    a.inT = nullptr;
+    a.tmax = h->tmax;
+    a.eq.nsec = h->nsec;
+    a.eq.sec = h->sec_dev.p;
+    a.eq.sec_ch_stride = h->eq_uniform ? 0 : (int64_t)h->nsec * kSecStride;
+    a.eq.state = h->eq_state.p;
+    a.cp = h->cp;
+    a.cs = h->cs.p;
+    a.rms_ring = h->ring.p;
+    a.vp = h->vp;
+    a.vs = h->vs.p;
+    a.vbuf = h->vbuf.p;
+    if (i >= kFxSlots) AD_HIP(hipStreamWaitEvent(s, h->ev[EA][k], 0));  // slot k consumed
+    launch_fx_transpose_in(a, a.xT, s);
+    if (eq) {
+      FxTpEqArgs e{};
+      e.channels = h->channels;
+      e.cpad = h->cpad;
+      e.len = a.len;
+      e.seg = (int)std::max<int64_t>(kFxTpSeg, ((a.len + kFxTpMaxSeg - 1) / kFxTpMaxSeg + 15) / 16 * 16);
+      e.nseg = (int)((a.len + e.seg - 1) / e.seg);
+      e.xT = a.xT;
+      e.vT = a.vT;
+      e.eq = a.eq;
+      e.zs = h->tp_zs.p;
+      e.carry = h->tp_carry.p;
+      for (int kk = 0; kk <= h->nsec; ++kk) {
+        e.k = kk;
+        launch_fxtp_eq(e, s);
+        if (kk < h->nsec) launch_fxtp_carry(e, s);
+      }
+    }
+    AD_HIP(hipEventRecord(h->ev[EE][k], s));
+    if (comp) {
+      AD_HIP(hipStreamWaitEvent(sd, h->ev[EE][k], 0));
+      launch_fxtp_det(a, sd);
+      AD_HIP(hipEventRecord(h->ev[ED][k], sd));
+      AD_HIP(hipStreamWaitEvent(sv, h->ev[ED][k], 0));
+      if (verb) {  // the compressor output channel-major into inC, then Freeverb into the user buffer
+        FxStageArgs b = a;
+        b.buf = h->inC[k].p;
+        b.stride = h->tmax;
+        launch_fx_gain(b, true, sv);
+        launch_fxtp_verb(a, h->inC[k].p, h->tmax, h->vbufC.p, h->coC.p, wu, sv);
+      } else {
+        launch_fx_gain(a, true, sv);
+      }
+    } else {
+      AD_HIP(hipStreamWaitEvent(sv, h->ev[EE][k], 0));
+      launch_fx_transpose_out(a, a.vT, sv);  // (not reached: the engine runs with a compressor)
+    }
+    AD_HIP(hipEventRecord(h->ev[EA][k], sv));
+  }
+  AD_HIP(hipGetLastError());
+  AD_HIP(hipStreamWaitEvent(s, h->ev[EA][k], 0));  // the last chunk's reverb / output follows all work
+}
+
 void fx_run(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hipStream_t s) {
   if (n <= 0) return;
   if (!h->ev_last) AD_HIP(hipEventCreateWithFlags(&h->ev_last, hipEventDisableTiming));
+  const bool tp = fx_staged_ok(h) && h->engine == AD_FX_ENGINE_AUTO && h->comp_on;
+  if (h->verb_on && h->verb_cm && !tp) {  // the delay lines back into vbuf's layout
+    launch_vbuf_layout(h->vbuf.p, h->vbufC.p, h->cpad, h->channels, false, s);
+    h->verb_cm = false;
+  }
   if (fx_staged_ok(h)) {
-    fx_run_staged(h, d_buf, stride, n, s);
+    // time-parallel where the chain is already a tolerance (the compressor's
+    // log2 / exp2): its EQ segments start from chained states, so
+    // an EQ-only chain keeps the staged engine and stays bit-exact
+    if (tp)
+      fx_run_tp(h, d_buf, stride, n, s);
+    else
+      fx_run_staged(h, d_buf, stride, n, s);
     AD_HIP(hipEventRecord(h->ev_last, s));
     return;
   }
@@ -658,7 +808,7 @@ int ad_fx_chain_set_eq_state(ad_fx_chain* h, const double* state, int64_t n) {
 
 int ad_fx_chain_set_engine(ad_fx_chain* h, int engine, int64_t chunk) {
   return fx_guard(h, [&] {
-    if (engine < AD_FX_ENGINE_AUTO || engine > AD_FX_ENGINE_STAGED_NOSPLIT)
+    if (engine < AD_FX_ENGINE_AUTO || engine > AD_FX_ENGINE_STAGED)
       AD_FAIL(AD_ERR_INVALID_ARGUMENT, "unknown effect-chain engine");
     if (chunk != 0 && chunk < 256) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "staged chunk must be 0 (default) or >= 256");
     fx_quiesce(h);

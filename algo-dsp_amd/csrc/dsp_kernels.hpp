@@ -137,6 +137,32 @@ void launch_fx_comb(const FxStageArgs& a, hipStream_t s);
 void launch_fx_allpass(const FxStageArgs& a, hipStream_t s);
 constexpr int kFxOutVT = 1, kFxOutInT = 2;
 
+// Time-parallel engine (fx_tp.hip; host: fx_run_tp).  K_eq launch k of
+// nsec + 1 over a chunk cut into nseg <= 256 segments of `seg` samples:
+// section k - 1 exactly from the segment start states in `carry`, fused with
+// the zero-state run of section k (end states to `zs`); K_carry then chains
+// section k's start states into `carry`.
+struct FxTpEqArgs {
+  int channels, cpad;
+  int64_t len;
+  int seg, nseg;
+  const double* xT;  // chunk input rows [len][cpad]
+  double* vT;        // EQ output rows (in place between launches)
+  EqArgs eq;
+  int k;
+  double* zs;        // [nseg][cpad][2]
+  double* carry;     // [nseg][cpad][2]
+};
+void launch_fxtp_eq(const FxTpEqArgs& a, hipStream_t s);
+void launch_fxtp_carry(const FxTpEqArgs& a, hipStream_t s);  // section a.k's segment start states
+void launch_fxtp_det(const FxStageArgs& a, hipStream_t s);           // vT -> envT (+ detector state)
+// Freeverb, one channel per workgroup: xC [channels][xstride] (channel-major
+// reverb input) -> user buffer, delay lines in vbufC [channels][kVerbLen],
+// comb outputs through coC [channels][8][a.tmax] (scratch)
+void launch_fxtp_verb(const FxStageArgs& a, const double* xC, int64_t xstride, double* vbufC, double* coC, int wu,
+                      hipStream_t s);
+void launch_vbuf_layout(double* vbuf, double* vbufC, int cpad, int channels, bool to_cm, hipStream_t s);
+
 // Fan-in average of an effect-chain graph node (mixParentEdgesInto,
 // chain_process.go:295-318): dst = (0 + src0 + src1 + ...) * (1/nsrc).
 struct FxMixArgs {

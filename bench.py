@@ -47,6 +47,9 @@ def parse():
     p.add_argument("--mixdown", choices=["auto", "on", "off"], default="auto")
     p.add_argument("--host-io", choices=["on", "off"], default="on",
                    help="N = 1: also time the same step host buffer -> host buffer (PCIe included)")
+    p.add_argument("--shard-sub", choices=["on", "off"], default="on",
+                   help="N = 1 conv: also measure config 4's per-GPU shard (8 ch x 2^24 + the stereo mixdown "
+                        "through the ABI at world 1), the like-for-like base of the N > 1 curve")
     p.add_argument("--pipeline", choices=["on", "off"], default="on",
                    help="N > 1: overlap step i's mixdown reduce with step i+1's convolution (two output buffers)")
     p.add_argument("--segments", type=int, default=1,
@@ -191,125 +194,12 @@ def main():
     if args.samples is None:
         args.samples = 1 << 24
     ir = irlib.large_church()                       # [2][131072], Large Church zero padded
-    K = ir.shape[1]
-    n = args.samples
-    out_len = n + K - 1                             # full linear convolution (OverlapSave.Process)
-    from algodsp import shard
-
-    C = args.channels
-    if mixdown and C % 2 and world > 1:
-        raise SystemExit("--channels must be even for the multi-GPU stereo mixdown")
-    ids = list(shard.channel_group(rank, world, C * world))  # this rank's global channel ids
-    x_host = np.stack([signals.white_noise(n, 0x5EED + c) for c in ids])
-    x = torch.from_numpy(x_host).to(dev)
-    # Mixdown through the library's own RCCL communicator (ad_mixdown_reduce),
-    # the path a cgo caller takes: k_mixdown of this rank's group + one
-    # in-place sum-reduce to rank 0, on a side stream.  Two output buffers:
-    # step i's mixdown/reduce overlaps step i+1's convolution into the other
-    # buffer; a buffer is rewritten only after its reduce (event wait on the
-    # device, no host block).  The last step's reduce completes inside the
-    # timed region.
-    comm = None
-    if mixdown:
-        def bootstrap(uid: bytes) -> bytes:
-            if world == 1:
-                return uid
-            obj = [uid]
-            dist.broadcast_object_list(obj, src=0)
-            return obj[0]
-
-        comm = shard.Comm(rank, world, local, bootstrap)
-    nbuf = 2 if (mixdown and args.pipeline == "on") else 1
-    ys = [torch.empty((C, out_len), dtype=torch.float64, device=dev) for _ in range(nbuf)]
-    mixes = [y if C == 2 else torch.empty((2, out_len), dtype=torch.float64, device=dev) for y in ys]
-
-    eng = conv.MultiChannelConvolver(ir, hop=args.hop, channels=C, ir_index=shard.ir_index(ids),
-                                     chunk_blocks=args.chunk, device=local)
-    stream = torch.cuda.current_stream(dev)
-    sptr = stream.cuda_stream
-    side = torch.cuda.Stream(dev)  # mixdown + reduce
-    blocks = -(-out_len // args.hop)
-    cuts = [min(out_len, args.hop * (blocks * i // args.segments)) for i in range(args.segments + 1)]
-    segs = [(b, e) for b, e in zip(cuts[:-1], cuts[1:]) if e > b]
-    red_done = [None] * nbuf
-    it = [0]
-
-    def step():
-        i = it[0] % nbuf
-        it[0] += 1
-        if red_done[i] is not None:  # the reduce that last read this buffer
-            stream.wait_event(red_done[i])
-        yb, mb = ys[i], mixes[i]
-        for b, e in segs:
-            if len(segs) == 1:
-                eng.process_device(x.data_ptr(), n, n, yb.data_ptr(), out_len, out_len, sptr)
-            else:
-                eng.process_device_segment(x.data_ptr(), n, n, yb.data_ptr(), out_len, out_len, b, e, sptr)
-            if mixdown:
-                done = torch.cuda.Event()
-                done.record(stream)
-                side.wait_event(done)
-                # stereo group: the two output rows are the partial mix (no k_mixdown)
-                comm.mixdown_reduce(yb.data_ptr() + 8 * b, 0 if C == 2 else C, out_len, e - b,
-                                    mb.data_ptr() + 8 * b, out_len, ids[0] % 2, 0, side.cuda_stream)
-        if mixdown:
-            ev = torch.cuda.Event()
-            ev.record(side)
-            red_done[i] = ev
-
-    def drain():
-        if mixdown:
-            side.synchronize()
-
-    for _ in range(args.warmup):
-        step()
-    drain()
-    torch.cuda.synchronize(dev)
-    eng.profile_read()  # clear
-
-    mode = args.kernel_timing
-    dom_mask = 7
-    if mode == "dominant":  # one profiled warm-up pass names the dominant kernel
-        eng.profile_enable(True)
-        for _ in range(2):
-            step()
-        drain()
-        torch.cuda.synchronize(dev)
-        pw = eng.profile_read()
-        dom_mask = 1 << list(pw).index(max(pw, key=lambda k: pw[k][0]))
-    eng.profile_enable(mode != "off", kernels=dom_mask if mode == "dominant" else 7)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    drain()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    last = (it[0] - 1) % nbuf
-    prof_live = eng.profile_read() if mode != "off" else {}
-    if mode != "on":  # the kernels not timed live: a separate event-timed pass
-        eng.profile_enable(True)
-        for _ in range(max(2, args.steps // 2)):
-            step()
-        drain()
-        torch.cuda.synchronize(dev)
-        last = (it[0] - 1) % nbuf
-        prof = eng.profile_read()
-        for k, v in prof_live.items():  # live (timed-region) numbers win
-            if v[1] > 0:
-                prof[k] = v
-    else:
-        prof = prof_live
-    eng.profile_enable(False)
-
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    r = run_conv(args, world, rank, local, dev, ir, args.channels, shard_cfg, mixdown, args.steps, args.warmup,
+                 args.kernel_timing)
+    C, n, K, out_len = args.channels, args.samples, ir.shape[1], r["out_len"]
+    elapsed, prof, prof_live, mode = r["elapsed"], r["prof"], r["prof_live"], args.kernel_timing
+    ids, x_host, eng, ys, mixes, last = r["ids"], r["x_host"], r["eng"], r["ys"], r["mixes"], r["last"]
+    comm = r["comm"]
 
     total_samples = world * C * n * args.steps
     value = total_samples / elapsed / 1e6
@@ -369,17 +259,46 @@ def main():
             # D2H on three streams) -- PCIe included, not the metric
             yh = eng.process_host(x_host)  # warm-up (pinned buffers, device scratch, output pages)
             reps = 3
+            split = [0.0, 0.0, 0.0]
             th = time.perf_counter()
             for _ in range(reps):
                 eng.process_host(x_host, out=yh)  # ProcessTo into the caller's buffer
+                split = [a + b for a, b in zip(split, eng.host_io_profile())]
             dth = (time.perf_counter() - th) / reps
+            split = [v / reps for v in split]
             hd = ys[last].cpu().numpy() if not mixdown else None
+            pcie_bytes = C * (n + out_len) * 8
+            # the same call through the staged path (host memcpy into pinned chunks)
+            eng.set_host_io(eng.HOST_IO_STAGE)
+            eng.process_host(x_host, out=yh)
+            ts = time.perf_counter()
+            for _ in range(2):
+                eng.process_host(x_host, out=yh)
+            dts = (time.perf_counter() - ts) / 2
+            eng.set_host_io(eng.HOST_IO_AUTO)
             host_io = {"value": round(C * n / dth / 1e6, 3), "unit": "Msamples/s", "ms_per_call": round(dth * 1e3, 3),
                        "bytes_per_sample_pcie": 8 + 8 * out_len / n,
+                       "split_ms": {"hipHostRegister": round(split[0], 3), "transfers_and_compute": round(split[1], 3),
+                                    "hipHostUnregister": round(split[2], 3)},
+                       "pcie_GBps_in_transfer_phase": round(pcie_bytes / (split[1] * 1e-3) / 1e9, 2) if split[1] else None,
+                       "staged_path": {"value": round(C * n / dts / 1e6, 3), "ms_per_call": round(dts * 1e3, 3)},
                        "equals_device_result": bool(hd is not None and np.array_equal(yh, hd)),
                        "note": "host buffer in -> host buffer out per call (ad_conv_ols_process_multi), "
-                               "PCIe + host copies included; wall time"}
+                               "PCIe + host copies included; wall time.  Default path: the caller's pages are "
+                               "registered for the call (split_ms); staged_path: memcpy through pinned chunks"}
             del yh, hd
+        shard_sub = None
+        if world == 1 and args.workload == "conv" and args.shard_sub == "on" and not shard_cfg:
+            ys.clear(), mixes.clear()
+            r8 = run_conv(args, 1, 0, local, dev, ir, 8, True, True, min(args.steps, 5), 2, "off")
+            shard_sub = {"value": round(8 * n * min(args.steps, 5) / r8["elapsed"] / 1e6, 3), "unit": "Msamples/s",
+                         "ms_per_step": round(r8["elapsed"] / min(args.steps, 5) * 1e3, 4),
+                         "workload": f"config 4 shard at N = 1: 8 ch x {n} samples (IR[c mod 2]) + k_mixdown + "
+                                     "RCCL reduce through ad_mixdown_reduce (world 1), the per-GPU work of every "
+                                     "rank at N > 1",
+                         "kernels_avg_us": {k: round(v[0] / max(v[1], 1) * 1e3, 1) for k, v in r8["prof"].items()}}
+            r8["comm"].close()
+            del r8
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(ir, args.cpu_sample)
@@ -440,6 +359,7 @@ def main():
                         for k, v in kernels.items()},
             "parity": parity,
             "host_io": host_io,
+            "shard_per_gpu": shard_sub,
             "cpu_baseline": cpu,
         }
         if cpu:
@@ -451,6 +371,139 @@ def main():
         dist.barrier()
         dist.destroy_process_group()
     return 0
+
+
+def run_conv(args, world, rank, local, dev, ir, C, shard_cfg, mixdown, steps, warmup, mode):
+    """One conv measurement: C channels x args.samples per GPU per step (IR[c mod 2]),
+    optionally with the RCCL stereo mixdown; `steps` timed steps after `warmup`,
+    bracketed by barrier + synchronize, max over ranks.  Returns the timing, the
+    per-kernel event profile and the buffers for the parity check."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from algodsp import conv, shard, signals
+
+    K = ir.shape[1]
+    n = args.samples
+    comm = None
+    out_len = n + K - 1                             # full linear convolution (OverlapSave.Process)
+    from algodsp import shard
+
+    if mixdown and C % 2 and world > 1:
+        raise SystemExit("--channels must be even for the multi-GPU stereo mixdown")
+    ids = list(shard.channel_group(rank, world, C * world))  # this rank's global channel ids
+    x_host = np.stack([signals.white_noise(n, 0x5EED + c) for c in ids])
+    x = torch.from_numpy(x_host).to(dev)
+    # Mixdown through the library's own RCCL communicator (ad_mixdown_reduce),
+    # the path a cgo caller takes: k_mixdown of this rank's group + one
+    # in-place sum-reduce to rank 0, on a side stream.  Two output buffers:
+    # step i's mixdown/reduce overlaps step i+1's convolution into the other
+    # buffer; a buffer is rewritten only after its reduce (event wait on the
+    # device, no host block).  The last step's reduce completes inside the
+    # timed region.
+    if mixdown:
+        def bootstrap(uid: bytes) -> bytes:
+            if world == 1:
+                return uid
+            obj = [uid]
+            dist.broadcast_object_list(obj, src=0)
+            return obj[0]
+
+        comm = shard.Comm(rank, world, local, bootstrap)
+    nbuf = 2 if (mixdown and args.pipeline == "on") else 1
+    ys = [torch.empty((C, out_len), dtype=torch.float64, device=dev) for _ in range(nbuf)]
+    mixes = [y if C == 2 else torch.empty((2, out_len), dtype=torch.float64, device=dev) for y in ys]
+
+    eng = conv.MultiChannelConvolver(ir, hop=args.hop, channels=C, ir_index=shard.ir_index(ids),
+                                     chunk_blocks=args.chunk, device=local)
+    stream = torch.cuda.current_stream(dev)
+    sptr = stream.cuda_stream
+    side = torch.cuda.Stream(dev)  # mixdown + reduce
+    blocks = -(-out_len // args.hop)
+    cuts = [min(out_len, args.hop * (blocks * i // args.segments)) for i in range(args.segments + 1)]
+    segs = [(b, e) for b, e in zip(cuts[:-1], cuts[1:]) if e > b]
+    red_done = [None] * nbuf
+    it = [0]
+
+    def step():
+        i = it[0] % nbuf
+        it[0] += 1
+        if red_done[i] is not None:  # the reduce that last read this buffer
+            stream.wait_event(red_done[i])
+        yb, mb = ys[i], mixes[i]
+        for b, e in segs:
+            if len(segs) == 1:
+                eng.process_device(x.data_ptr(), n, n, yb.data_ptr(), out_len, out_len, sptr)
+            else:
+                eng.process_device_segment(x.data_ptr(), n, n, yb.data_ptr(), out_len, out_len, b, e, sptr)
+            if mixdown:
+                done = torch.cuda.Event()
+                done.record(stream)
+                side.wait_event(done)
+                # stereo group: the two output rows are the partial mix (no k_mixdown)
+                comm.mixdown_reduce(yb.data_ptr() + 8 * b, 0 if C == 2 else C, out_len, e - b,
+                                    mb.data_ptr() + 8 * b, out_len, ids[0] % 2, 0, side.cuda_stream)
+        if mixdown:
+            ev = torch.cuda.Event()
+            ev.record(side)
+            red_done[i] = ev
+
+    def drain():
+        if mixdown:
+            side.synchronize()
+
+    for _ in range(warmup):
+        step()
+    drain()
+    torch.cuda.synchronize(dev)
+    eng.profile_read()  # clear
+
+    dom_mask = 7
+    if mode == "dominant":  # one profiled warm-up pass names the dominant kernel
+        eng.profile_enable(True)
+        for _ in range(2):
+            step()
+        drain()
+        torch.cuda.synchronize(dev)
+        pw = eng.profile_read()
+        dom_mask = 1 << list(pw).index(max(pw, key=lambda k: pw[k][0]))
+    eng.profile_enable(mode != "off", kernels=dom_mask if mode == "dominant" else 7)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    drain()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    last = (it[0] - 1) % nbuf
+    prof_live = eng.profile_read() if mode != "off" else {}
+    if mode != "on":  # the kernels not timed live: a separate event-timed pass
+        eng.profile_enable(True)
+        for _ in range(max(2, steps // 2)):
+            step()
+        drain()
+        torch.cuda.synchronize(dev)
+        last = (it[0] - 1) % nbuf
+        prof = eng.profile_read()
+        for k, v in prof_live.items():  # live (timed-region) numbers win
+            if v[1] > 0:
+                prof[k] = v
+    else:
+        prof = prof_live
+    eng.profile_enable(False)
+
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    return {"elapsed": elapsed, "prof": prof, "prof_live": prof_live, "ids": ids, "x_host": x_host, "eng": eng,
+            "ys": ys, "mixes": mixes, "last": last, "comm": comm, "out_len": out_len}
 
 
 def main_stream(args):

@@ -356,11 +356,14 @@ int ad_fx_chain_set_eq_state(ad_fx_chain* h, const double* state, int64_t n);
  *                   Freeverb -- with the EQ split over two CUs when a
  *                   compressor and >= 3 sections are on; else FUSED;
  *   FUSED           the fused per-sample kernels (dsp_kernels.hip k_chain*);
- *   STAGED_NOSPLIT  staged, one EQ pipeline per channel group.
+ *   STAGED_NOSPLIT  staged, one EQ pipeline per channel group;
+ *   STAGED          staged with the split EQ stage (AUTO's engine before the
+ *                   time-parallel one).
  * chunk: samples per staged chunk (0: 16384; otherwise >= 256).           */
 #define AD_FX_ENGINE_AUTO 0
 #define AD_FX_ENGINE_FUSED 1
 #define AD_FX_ENGINE_STAGED_NOSPLIT 2
+#define AD_FX_ENGINE_STAGED 3
 int ad_fx_chain_set_engine(ad_fx_chain* h, int engine, int64_t chunk);
 /* Per-wave clock counters (s_memtime ticks) of the first chunk of each call,
  * for profiling the serial stages: {compute, barrier wait} pairs per wave. */
