@@ -6,6 +6,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <map>
+#include <memory>
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
@@ -130,9 +132,13 @@ struct ad_fx_chain {
   DevBuf<double> midT[kFxSlots];  // split K_eq: the first part's output rows
   // time-parallel engine (fx_tp.hip): K_eq segment states
   DevBuf<double> tp_zs, tp_carry;
+  // K_carry's segment maps per (seg, nseg): M = A^seg and M^Q per section and
+  // coefficient set, double-double [nsec][sets][2][4][2] (fx_tp_mats)
+  std::vector<double> sec_host;
+  std::map<std::pair<int, int>, std::unique_ptr<DevBuf<double>>> tp_mats;
   DevBuf<double> inC[kFxSlots];  // reverb input, channel-major [cpad][tmax]
   DevBuf<double> vbufC;          // Freeverb lines channel-major [channels][kVerbLen] (K_verb)
-  DevBuf<double> coC;            // K_verb comb outputs [channels][8][tmax] (scratch, stream st[1] only)
+  DevBuf<double> coC;            // K_verb comb outputs [channels][8][kFxVerbSB] (scratch, stream st[1] only)
   bool verb_cm = false;          // vbufC (not vbuf) holds the current delay lines
   int64_t tmax = 0;
   // engine selection (ad_fx_chain_set_engine) and per-wave clock counters of
@@ -395,9 +401,58 @@ void fx_run_staged(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hip
 // the combs and the allpasses.  So chunk i's EQ overlaps chunk i-1's detector
 // and chunk i-2's reverb.  A slot is reused only after st[1] is done with it
 // (the detector precedes st[1]'s work on every chunk).
-constexpr int64_t kFxTpChunk = 16384;
+#ifndef AD_FX_TP_CHUNK  // tools/ A/B builds only
+#define AD_FX_TP_CHUNK 65536  // 16384: 7.13, 32768: 8.21, 65536: 8.93, 131072: 8.69 Gsamples/s at config 5
+#endif
+constexpr int64_t kFxTpChunk = AD_FX_TP_CHUNK;
 constexpr int kFxTpSeg = 64;     // K_eq segment (samples), at least
 constexpr int kFxTpMaxSeg = 256;  // K_eq segments per chunk, at most (fx_tp.hip kTpQ)
+
+// K_carry's maps for a chunk cut into nseg segments of seg samples: per
+// section and coefficient set, M = A^seg and M^Q (Q = segments per K_carry
+// wave), A = [[-a1, 1], [-a2, 0]] the section's zero-input step, computed in
+// 64-bit-mantissa long double and stored as double-double pairs.  Built once
+// per (seg, nseg) and coefficient table (a chunk length and the last chunk's).
+const double* fx_tp_mats(ad_fx_chain* h, int seg, int nseg) {
+  auto& slot = h->tp_mats[std::make_pair(seg, nseg)];
+  if (slot) return slot->p;
+  const int sets = h->eq_uniform ? 1 : h->channels, nsec = h->nsec;
+  const int Q = (nseg + kFxTpCarryWaves - 1) / kFxTpCarryWaves;
+  typedef long double ld;
+  auto mul = [](const ld* x, const ld* y, ld* r) {
+    const ld t[4] = {x[0] * y[0] + x[1] * y[2], x[0] * y[1] + x[1] * y[3], x[2] * y[0] + x[3] * y[2],
+                     x[2] * y[1] + x[3] * y[3]};
+    for (int i = 0; i < 4; ++i) r[i] = t[i];
+  };
+  auto pw = [&](const ld* b0, int e, ld* m) {
+    ld b[4] = {b0[0], b0[1], b0[2], b0[3]};
+    m[0] = 1, m[1] = 0, m[2] = 0, m[3] = 1;
+    for (; e > 0; e >>= 1) {
+      if (e & 1) mul(m, b, m);
+      mul(b, b, b);
+    }
+  };
+  std::vector<double> t((size_t)nsec * sets * 16);
+  for (int k = 0; k < nsec; ++k)
+    for (int c = 0; c < sets; ++c) {
+      const double* q = h->sec_host.data() + ((size_t)c * nsec + k) * kSecStride;
+      const ld A[4] = {-(ld)q[4], 1, -(ld)q[5], 0};
+      ld M[4], MQ[4];
+      pw(A, seg, M);
+      pw(M, Q, MQ);
+      double* o = t.data() + ((size_t)k * sets + c) * 16;
+      for (int i = 0; i < 4; ++i) {
+        o[2 * i] = (double)M[i];
+        o[2 * i + 1] = (double)(M[i] - (ld)o[2 * i]);
+        o[8 + 2 * i] = (double)MQ[i];
+        o[8 + 2 * i + 1] = (double)(MQ[i] - (ld)o[8 + 2 * i]);
+      }
+    }
+  slot.reset(new DevBuf<double>());
+  slot->alloc(t.size());
+  AD_HIP(hipMemcpy(slot->p, t.data(), t.size() * sizeof(double), hipMemcpyHostToDevice));
+  return slot->p;
+}
 
 // K_comb warm-up: samples after which the damping filter's start value is
 // below 2^-60 of the run (da^wu < 2^-60); 0 without damping; a filter that
@@ -429,7 +484,7 @@ void fx_run_tp(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hipStre
       if (comp) h->envT[k].alloc(r);
       if (comp && verb) h->inC[k].alloc(r);
     }
-    if (comp && verb) h->coC.alloc((size_t)h->channels * kVerbCombs * std::max(T, h->tmax));
+    if (comp && verb) h->coC.alloc((size_t)h->channels * kVerbCombs * kFxVerbSB);
     if (eq) {
       h->tp_zs.alloc((size_t)kFxTpMaxSeg * h->cpad * 2);
       h->tp_carry.alloc((size_t)kFxTpMaxSeg * h->cpad * 2);
@@ -490,6 +545,8 @@ void fx_run_tp(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hipStre
       e.eq = a.eq;
       e.zs = h->tp_zs.p;
       e.carry = h->tp_carry.p;
+      e.mats = fx_tp_mats(h, e.seg, e.nseg);
+      e.mat_sets = h->eq_uniform ? 1 : h->channels;
       for (int kk = 0; kk <= h->nsec; ++kk) {
         e.k = kk;
         launch_fxtp_eq(e, s);
@@ -642,6 +699,8 @@ int ad_fx_chain_set_eq(ad_fx_chain* h, const double* sections, int nsec, int per
     h->eq_uniform = !per_channel;
     h->sec_dev.alloc((size_t)(per_channel ? h->channels : 1) * nsec * kSecStride);
     if (nsec > 0) AD_HIP(hipMemcpy(h->sec_dev.p, sections, h->sec_dev.n * sizeof(double), hipMemcpyHostToDevice));
+    h->sec_host.assign(sections, sections + h->sec_dev.n);
+    h->tp_mats.clear();
     // Section state survives a coefficient update with the same section
     // count, like filterRuntime.Configure (runtime_filter_pitch_reverb.go:150-165).
     if (!keep_state || !h->eq_state.p) {

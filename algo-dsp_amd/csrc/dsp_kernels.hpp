@@ -152,13 +152,17 @@ struct FxTpEqArgs {
   int k;
   double* zs;        // [nseg][cpad][2]
   double* carry;     // [nseg][cpad][2]
+  const double* mats;  // [nsec][mat_sets][M, M^Q][4 entries][hi, lo] (host fx_tp_mats)
+  int mat_sets;        // 1 (one coefficient table) or channels
 };
+constexpr int kFxTpCarryWaves = 8;  // K_carry waves per 64 channels
+constexpr int kFxVerbSB = 4096;     // K_verb sub-block (samples)
 void launch_fxtp_eq(const FxTpEqArgs& a, hipStream_t s);
 void launch_fxtp_carry(const FxTpEqArgs& a, hipStream_t s);  // section a.k's segment start states
 void launch_fxtp_det(const FxStageArgs& a, hipStream_t s);           // vT -> envT (+ detector state)
 // Freeverb, one channel per workgroup: xC [channels][xstride] (channel-major
 // reverb input) -> user buffer, delay lines in vbufC [channels][kVerbLen],
-// comb outputs through coC [channels][8][a.tmax] (scratch)
+// comb outputs through coC [channels][8][kFxVerbSB] (scratch)
 void launch_fxtp_verb(const FxStageArgs& a, const double* xC, int64_t xstride, double* vbufC, double* coC, int wu,
                       hipStream_t s);
 void launch_vbuf_layout(double* vbuf, double* vbufC, int cpad, int channels, bool to_cm, hipStream_t s);

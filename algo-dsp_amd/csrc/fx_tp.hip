@@ -168,22 +168,6 @@ __device__ __forceinline__ dd dd_mul(dd x, dd y) {
 struct dd2x2 {
   dd m[4];
 };
-__device__ __forceinline__ dd2x2 dd_mm(const dd2x2& x, const dd2x2& y) {
-  dd2x2 r;
-  r.m[0] = dd_add(dd_mul(x.m[0], y.m[0]), dd_mul(x.m[1], y.m[2]));
-  r.m[1] = dd_add(dd_mul(x.m[0], y.m[1]), dd_mul(x.m[1], y.m[3]));
-  r.m[2] = dd_add(dd_mul(x.m[2], y.m[0]), dd_mul(x.m[3], y.m[2]));
-  r.m[3] = dd_add(dd_mul(x.m[2], y.m[1]), dd_mul(x.m[3], y.m[3]));
-  return r;
-}
-__device__ __forceinline__ dd2x2 dd_pow(dd2x2 b, int e) {
-  dd2x2 m{{dd{1, 0}, dd{0, 0}, dd{0, 0}, dd{1, 0}}};
-  for (; e > 0; e >>= 1) {
-    if (e & 1) m = dd_mm(m, b);
-    b = dd_mm(b, b);
-  }
-  return m;
-}
 // s' = M s + z
 __device__ __forceinline__ void dd_step(const dd2x2& M, dd& s0, dd& s1, dd z0, dd z1) {
   const dd t0 = dd_add(dd_add(dd_mul(M.m[0], s0), dd_mul(M.m[1], s1)), z0);
@@ -199,7 +183,7 @@ __device__ __forceinline__ void dd_step(const dd2x2& M, dd& s0, dd& s1, dd z0, d
 // consecutive segments: it chains its zs from zero (e_u), the start of its
 // range is M^Q-chained over e_0 .. e_{u-1} (LDS), then it walks its range
 // again writing the starts rounded to double.
-constexpr int kCyW = 8;  // K_carry waves: 16 KiB of LDS, so it fits beside a K_verb workgroup
+constexpr int kCyW = kFxTpCarryWaves;  // 16 KiB of LDS, so it fits beside a K_verb workgroup
 __global__ __launch_bounds__(64 * kCyW) void k_fxtp_carry(FxTpEqArgs a) {
   const int w = wave_of_thread();
   const int l = threadIdx.x & 63;
@@ -208,11 +192,15 @@ __global__ __launch_bounds__(64 * kCyW) void k_fxtp_carry(FxTpEqArgs a) {
   const int cp = a.cpad;
   const int k = a.k, nsec = a.eq.nsec;
   __shared__ dd agg[kCyW][2][64];
-  const double* q = a.eq.sec + (int64_t)cc * a.eq.sec_ch_stride + k * kSecStride;
-  const dd2x2 A{{dd{-q[4], 0}, dd{1, 0}, dd{-q[5], 0}, dd{0, 0}}};  // zero-input step [[-a1, 1], [-a2, 0]]
-  const dd2x2 M = dd_pow(A, a.seg);
+  // M = A^seg and M^Q, A the zero-input step [[-a1, 1], [-a2, 0]] (host, fx_tp_mats)
+  const double* mt = a.mats + ((int64_t)k * a.mat_sets + (a.mat_sets > 1 ? cc : 0)) * 16;
+  dd2x2 M, MQ;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    M.m[i] = dd{mt[2 * i], mt[2 * i + 1]};
+    MQ.m[i] = dd{mt[8 + 2 * i], mt[8 + 2 * i + 1]};
+  }
   const int Q = (a.nseg + kCyW - 1) / kCyW;
-  const dd2x2 MQ = dd_pow(M, Q);
   const int v0 = w * Q, nv = max(0, min(a.nseg - v0, Q));
   const double2* zs = reinterpret_cast<const double2*>(a.zs) + (int64_t)v0 * cp + c;
   // zs streamed twice (8 loads ahead): chain from zero, then walk from the true start
@@ -244,16 +232,20 @@ __global__ __launch_bounds__(64 * kCyW) void k_fxtp_carry(FxTpEqArgs a) {
 
 // ---------------------------------------------------------------------------
 // K_det: side-chain prefilters, detector and envelope (core.go:274-286,
-// 331-400), serial over the chunk, 16 channels per workgroup (lanes 0..15 of
-// wave 0): a 64-channel group would need ~40 GB/s of row traffic into one
-// CU for the detector's pace; 16 channels need a quarter of that, on four
-// times the CUs.  Wave 1 loads the rows (4 rows x 16 channels per load
-// instruction) kDetNB batches ahead into an LDS ring, one barrier per batch.
+// 331-400), serial over the chunk, kDetCh channels per workgroup (lanes of
+// wave 0; the other lanes repeat them): a 64-channel group would need
+// ~40 GB/s of row traffic into one CU at the detector's pace.  Wave 1 keeps
+// kDetNB batches of row loads in flight in registers (every load covers
+// 64 / kDetCh rows of kDetCh channels; <= 63 outstanding) and puts each
+// batch into a small LDS ring one step before the detector reads it; one
+// barrier per batch.  The lookahead (kDetNB batches) is what hides the
+// memory latency: 10 batches of 16 measured 481 us per chunk, 14 370 us.
 // ---------------------------------------------------------------------------
-constexpr int kDetCh = 16;     // channels per workgroup
+constexpr int kDetCh = 8;      // channels per workgroup
 constexpr int kDetB = 16;      // rows per batch
-constexpr int kDetNB = 10;     // batches in flight in the loader (4 loads each: <= 63 outstanding)
-constexpr int kDetSlots = 12;  // ring slots (> kDetNB): 24 KiB, room beside K_verb's 131 KiB
+constexpr int kDetLd = kDetB * kDetCh / 64;  // loads per batch (2)
+constexpr int kDetNB = 28;     // batches in flight in the loader (56 loads outstanding)
+constexpr int kDetSlots = 4;   // LDS ring slots (a batch lives there for one step)
 __device__ __forceinline__ void lds_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 __global__ __launch_bounds__(128) void k_fxtp_det(FxStageArgs a) {
@@ -267,9 +259,9 @@ __global__ __launch_bounds__(128) void k_fxtp_det(FxStageArgs a) {
   const int64_t nb = (len + kDetB - 1) / kDetB;
   const int64_t nbp = (nb + kDetNB - 1) / kDetNB * kDetNB;
   if (w == 0) {
-    // lanes 16..63 repeat lanes 0..15 (same channel, same values, same
-    // stores): no branch around the stores, so the ring reads of a batch
-    // are issued together ahead of the envelope chain
+    // lanes >= kDetCh repeat lanes 0..kDetCh-1 (same channel, same values,
+    // same stores): no branch around the stores, so the ring reads of a
+    // batch are issued together ahead of the envelope chain
     const int c = c0 + (l & (kDetCh - 1));
     const bool active = l < kDetCh && c < a.channels;
     const int cc = c < a.channels ? c : a.channels - 1;
@@ -288,14 +280,25 @@ __global__ __launch_bounds__(128) void k_fxtp_det(FxStageArgs a) {
       const int64_t r0 = k * kDetB;
       const int n = (int)max((int64_t)0, min((int64_t)kDetB, len - r0));
       if (bare && n == kDetB) {
-        AD_TPG double* o = eo + r0 * cp + uc;
-        double xv[kDetB];
+        double xv[kDetB], ev[kDetB];
 #pragma unroll
         for (int d = 0; d < kDetB; ++d) xv[d] = ring[slot][d][li];
 #pragma unroll
         for (int d = 0; d < kDetB; ++d) {
           cs.env = env_step(p, cs.env, fabs(xv[d]));
-          o[(int64_t)d * cp] = cs.env;
+          ev[d] = cs.env;
+        }
+        // kDetLd stores per batch, not kDetB: lane l stores row
+        // l / kDetCh + RS i of its channel (every lane holds its channel's
+        // whole batch), picked out of ev[] by selects
+        constexpr int RS = 64 / kDetCh;
+        const int rq = l / kDetCh;
+#pragma unroll
+        for (int i = 0; i < kDetLd; ++i) {
+          double v = ev[RS * i];
+#pragma unroll
+          for (int q = 1; q < RS; ++q) v = rq == q ? ev[RS * i + q] : v;
+          eo[(r0 + rq + RS * i) * cp + uc] = v;
         }
       } else {
         for (int d = 0; d < n; ++d) {
@@ -337,24 +340,26 @@ __global__ __launch_bounds__(128) void k_fxtp_det(FxStageArgs a) {
       o->rms_filled = cs.rms_filled;
     }
   } else {
-    // loader: lane l covers row (l >> 4) + 4 i of a batch, channel l & 15;
-    // its register ring holds kDetNB batches, entry = batch mod kDetNB
+    // loader: lane l covers row (l / kDetCh) + (64 / kDetCh) i of a batch,
+    // channel l % kDetCh; its register ring holds kDetNB batches, entry =
+    // batch mod kDetNB
     const AD_TPG double* vin = gptr((const double*)a.vT);
     const unsigned col = (unsigned)(c0 + (l & (kDetCh - 1)));
-    const int rl = l >> 4;
-    double buf[kDetNB][kDetB / 4];
-    auto load = [&](double (&r)[kDetB / 4], int64_t b) {
+    const int rl = l / kDetCh;
+    constexpr int RS = 64 / kDetCh;  // rows per load
+    double buf[kDetNB][kDetLd];
+    auto load = [&](double (&r)[kDetLd], int64_t b) {
 #pragma unroll
-      for (int i = 0; i < kDetB / 4; ++i) r[i] = vin[min(b * kDetB + rl + 4 * i, len - 1) * cp + col];
+      for (int i = 0; i < kDetLd; ++i) r[i] = vin[min(b * kDetB + rl + RS * i, len - 1) * cp + col];
     };
     // branch-free: every step loads (rows past the chunk re-read its last
     // row) and stores one batch, so the compiler's vmcnt waits stay counted
     // (a conditional put or load made it drain every load at every step);
-    // a batch past the last lands in a slot whose batch was consumed 15 steps ago
-    auto put = [&](const double (&r)[kDetB / 4], int64_t b) {
+    // a batch past the last lands in a slot whose batch was already consumed
+    auto put = [&](const double (&r)[kDetLd], int64_t b) {
       const int slot = (int)(b % kDetSlots);
 #pragma unroll
-      for (int i = 0; i < kDetB / 4; ++i) ring[slot][rl + 4 * i][l & (kDetCh - 1)] = r[i];
+      for (int i = 0; i < kDetLd; ++i) ring[slot][rl + RS * i][l & (kDetCh - 1)] = r[i];
     };
 #pragma unroll
     for (int e = 0; e < kDetNB; ++e) load(buf[e], e);
@@ -395,7 +400,7 @@ __global__ __launch_bounds__(128) void k_fxtp_det(FxStageArgs a) {
 //               window's samples are independent), one lane each, the next
 //               window's comb outputs loaded during the current one
 // ---------------------------------------------------------------------------
-constexpr int kVbSB = 4096;
+constexpr int kVbSB = kFxVerbSB;
 constexpr int kVbSeg = 32;  // comb segments per piece, at most
 constexpr int kVbThreads = 64 * (kVerbCombs + 4);
 constexpr int kVbXr = (kVbSB + kVbThreads - 1) / kVbThreads;  // input values per thread per sub-block
@@ -421,7 +426,10 @@ __global__ __launch_bounds__(kVbThreads) void k_fxtp_verb(FxStageArgs a, const d
   double* vl = vbufC + (int64_t)c * kVerbLen;
   for (int e = tid; e < kVerbLen; e += kVbThreads) lines[e] = vl[e];
   const double* xc = xC + (int64_t)c * xstride;
-  double* coc = coC + (int64_t)c * kVerbCombs * a.tmax;  // [comb][tmax] of this channel
+  // [comb][kVbSB] of this channel, reused by every sub-block: 67 MB at 256
+  // channels, rewritten while still in the Infinity Cache (a chunk-long
+  // buffer left ~1 GB of dirty lines per 64K-sample chunk to reach HBM)
+  double* coc = coC + (int64_t)c * kVerbCombs * kVbSB;
   double xr[kVbXr];
 #pragma unroll
   for (int q = 0; q < kVbXr; ++q) {
@@ -456,7 +464,7 @@ __global__ __launch_bounds__(kVbThreads) void k_fxtp_verb(FxStageArgs a, const d
 #endif
       const int D = kCombLen[w];
       double* L = lines + comb_off(w);
-      double* cw = coc + (int64_t)w * a.tmax + t0;
+      double* cw = coc + (int64_t)w * kVbSB;
       for (int r = 0; r < sb;) {
         const int pos0 = idx;
         const int m = min(sb - r, D - pos0);
@@ -516,7 +524,7 @@ __global__ __launch_bounds__(kVbThreads) void k_fxtp_verb(FxStageArgs a, const d
     double cv[kVerbCombs];
     auto loadc = [&](int r) {
 #pragma unroll
-      for (int i = 0; i < kVerbCombs; ++i) cv[i] = coc[(int64_t)i * a.tmax + t0 + min(r + j, sb - 1)];
+      for (int i = 0; i < kVerbCombs; ++i) cv[i] = coc[(int64_t)i * kVbSB + min(r + j, sb - 1)];
     };
     if (apw) loadc(0);
     for (int r = 0; r < sb; r += 225) {

@@ -5,7 +5,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-TAG=${TAG:-r02}
+TAG=${TAG:-r03}
 OUT=gpurun_out/pmc_$TAG
 mkdir -p $OUT
 BARGS=${BENCH_ARGS:---steps 3 --warmup 1 --no-cpu-baseline --kernel-timing off}

@@ -4,7 +4,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-TAG=${TAG:-r02}
+TAG=${TAG:-r03}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 BARGS=${BENCH_ARGS:---steps 5 --warmup 2 --no-cpu-baseline --host-io off}
