@@ -28,9 +28,10 @@ sys.path.insert(0, str(ROOT / "algo-dsp_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FX_CLOCK_HZ = 2.4e9     # MI355X engine clock (MI355X_MICROARCH.md)
-FX_CHAIN_CLK = 52       # longest per-sample dependency chain of config 5, clocks: the DF-II-T
-                        # section (tools/biquad_latency.hip); the envelope follower is 24.5
-                        # (tools/chain_latency.hip), a Freeverb comb 38
+FX_CHAIN_CLK = 24.5     # config 5's serial chain per sample, clocks: the compressor's envelope
+                        # follower (tools/chain_latency.hip).  The EQ sections and the Freeverb
+                        # combs run time-parallel in the default engine,
+                        # so the envelope is the one recurrence left serial per channel
 
 
 def parse():
@@ -743,21 +744,21 @@ def main_fx(args):
                                     f"{n} samples per GPU per step, fused per sample"),
                        "channels_per_gpu": C, "samples_per_channel": n,
                        "parallelism": "replicas" if world > 1 else "single GPU"},
-            # The bound is the serial recurrence, not HBM (16 B/sample moves
-            # 0.5 % of peak): one lane per channel, 64 channels per wave, and
-            # the longest per-sample dependency chain is a DF-II-T EQ section,
-            # 52 clocks per sample in isolation (tools/biquad_latency.hip; the
-            # envelope follower: 24.5, a comb: 38, tools/chain_latency.hip).
-            # Ceiling = clock x 64 channels / 52 clk per 64-channel group,
-            # times the groups (ceil(C / 64) = 4 at 256 channels).
-            "roofline": {"bound": "serial-recurrence latency", "achieved": round(value, 3),
-                         "peak": round(FX_CLOCK_HZ * 64 / FX_CHAIN_CLK * (-(-C // 64)) / 1e6, 1),
+            # The bound is the one serial recurrence left, not HBM (16 B/sample
+            # of input and output moves 0.5 % of peak): the time-parallel engine
+            # cuts the EQ sections and the Freeverb combs into time segments,
+            # but the envelope follower (attack or release by the sign of
+            # src - env) is serial per channel, 24.5 clocks per sample
+            # (tools/chain_latency.hip).  Ceiling = clock x channels / 24.5.
+            "roofline": {"bound": "serial-recurrence latency (compressor envelope)", "achieved": round(value, 3),
+                         "peak": round(FX_CLOCK_HZ * C / FX_CHAIN_CLK / 1e6, 1),
                          "unit": "Msamples/s",
-                         "frac": round(value / (FX_CLOCK_HZ * 64 / FX_CHAIN_CLK * (-(-C // 64)) / 1e6), 4),
+                         "frac": round(value / (FX_CLOCK_HZ * C / FX_CHAIN_CLK / 1e6), 4),
                          "traffic": None,
                          "hbm_GBps": round(value * 16e6 / 1e9, 3),
-                         "note": f"ceiling = {FX_CLOCK_HZ / 1e9} GHz x 64 ch / {FX_CHAIN_CLK} clk per sample "
-                                 f"(DF-II-T section chain) x {-(-C // 64)} channel groups; HBM carries 16 B/sample"},
+                         "note": f"ceiling = {FX_CLOCK_HZ / 1e9} GHz x {C} channels / {FX_CHAIN_CLK} clk per sample "
+                                 f"(the envelope follower's dependency chain, each channel's own); HBM carries "
+                                 f"16 B/sample of input and output"},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
