@@ -18,6 +18,7 @@
 
 #include "ad_common.hpp"
 #include "bigfft.hpp"
+#include "host_pipeline.hpp"
 
 using namespace adsp;
 
@@ -139,6 +140,9 @@ int ad_correlate_fft(const double* a, int64_t n, const double* b, int64_t m, dou
     hipStream_t s = nullptr;
     const int64_t N = next_pow2(n + m - 1);  // correlate.go:119
     SpectralRun run(dc, N);
+    // the caller's arrays page-locked for the call: DMA, not pageable staging
+    // (a fresh output array otherwise faults its pages in during the copy)
+    const HostPin pa(a, (size_t)n * 8), pb(b, (size_t)m * 8), po(out, (size_t)(n + m - 1) * 8);
     if (run.fused()) {
       // a and b to the device unpadded, the fused transforms (see the device
       // form below), the n + m - 1 lags back in one copy
@@ -241,6 +245,7 @@ int ad_deconvolve(const double* signal, int64_t n, const double* kernel, int64_t
     std::lock_guard<std::mutex> g(dc.mu);
     hipStream_t s = nullptr;
     SpectralRun run(dc, N);
+    const HostPin ps(signal, (size_t)n * 8), pk(kernel, (size_t)m * 8), po(out, (size_t)olen * 8);
     if (run.fused()) {
       // one forward transform of signal + i kernel, the division fused into
       // the inverse's first pass, the inverse at half length, olen outputs
@@ -304,6 +309,7 @@ int ad_inverse_filter(const double* kernel, int64_t m, int64_t length, double ep
     hipStream_t s = nullptr;
     SpectralRun run(dc, N);
     const int64_t mk = m < N ? m : N;  // kernel truncated to the transform (:367)
+    const HostPin pk(kernel, (size_t)mk * 8), po(out, (size_t)length * 8);
     if (run.fused()) {
       dc.xr.reserve((size_t)mk);
       dc.res.reserve((size_t)length);

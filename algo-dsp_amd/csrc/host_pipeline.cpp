@@ -5,6 +5,7 @@
 #include "host_pipeline.hpp"
 
 #include <chrono>
+#include <exception>
 
 #include <algorithm>
 #include <cstdlib>
@@ -121,6 +122,23 @@ void copy_out(double* const* out, const double* pin, int C, int64_t col0, int64_
 
 void parallel_for(int64_t n, const std::function<void(int64_t)>& fn, int workers) {
   Pool::get().run(n, fn, workers);
+}
+
+HostPin::HostPin(const void* ptr, size_t bytes, size_t min_bytes) {
+  if (!ptr || bytes < min_bytes) return;
+  if (hipHostRegister(const_cast<void*>(ptr), bytes, hipHostRegisterDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    return;
+  }
+  p = const_cast<void*>(ptr);
+  ok = true;
+}
+HostPin::~HostPin() {
+  if (!ok) return;
+  // unwinding from an error: copies into or out of these pages may still be
+  // queued, and the caller may free them as soon as the error returns
+  if (std::uncaught_exceptions() > 0) (void)hipDeviceSynchronize();
+  (void)hipHostUnregister(p);
 }
 
 HostPipeline::HostPipeline(int) {

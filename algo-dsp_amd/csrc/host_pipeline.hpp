@@ -28,6 +28,20 @@ namespace adsp {
 // Runs fn(i) for i in [0, n) on up to `workers` pool threads plus the caller.
 void parallel_for(int64_t n, const std::function<void(int64_t)>& fn, int workers = 8);
 
+// Page-locks a caller's host range for the scope of one call
+// (hipHostRegister), so the DMA engines move it directly instead of staging
+// pageable memory.  Ranges below `min_bytes` are left alone; `ok` is false
+// when the runtime refuses (the copies then stay pageable).  The scope must
+// end after every copy touching the range has completed.
+struct HostPin {
+  void* p = nullptr;
+  bool ok = false;
+  HostPin(const void* ptr, size_t bytes, size_t min_bytes = size_t(4) << 20);
+  ~HostPin();
+  HostPin(const HostPin&) = delete;
+  HostPin& operator=(const HostPin&) = delete;
+};
+
 class HostPipeline {
  public:
   explicit HostPipeline(int device);
