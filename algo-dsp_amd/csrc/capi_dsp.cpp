@@ -396,58 +396,93 @@ void fx_run_staged(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hip
 }
 
 // The time-parallel engine (fx_tp.hip): per chunk of T samples, the caller's
-// stream runs the input transpose and the nsec + 1 K_eq launches; st[0] the
-// detector (one wave per 64 channels, serial) of that chunk; st[1] the gain,
-// the combs and the allpasses.  So chunk i's EQ overlaps chunk i-1's detector
-// and chunk i-2's reverb.  A slot is reused only after st[1] is done with it
-// (the detector precedes st[1]'s work on every chunk).
+// stream runs the input transpose and the three EQ launches (K_eqz, K_carry,
+// K_eqx); st[0] the detector (serial per channel) and the gain of that chunk;
+// st[1] the reverb.  So chunk i's EQ overlaps chunk i-1's detector and chunk
+// i-2's reverb.  A slot is reused only after st[1] is done with it (the
+// detector and the gain precede st[1]'s work on every chunk).
 #ifndef AD_FX_TP_CHUNK  // tools/ A/B builds only
 #define AD_FX_TP_CHUNK 65536  // 16384: 7.13, 32768: 8.21, 65536: 8.93, 131072: 8.69 Gsamples/s at config 5
 #endif
 constexpr int64_t kFxTpChunk = AD_FX_TP_CHUNK;
 constexpr int kFxTpSeg = 64;     // K_eq segment (samples), at least
-constexpr int kFxTpMaxSeg = 256;  // K_eq segments per chunk, at most (fx_tp.hip kTpQ)
 
-// K_carry's maps for a chunk cut into nseg segments of seg samples: per
-// section and coefficient set, M = A^seg and M^Q (Q = segments per K_carry
-// wave), A = [[-a1, 1], [-a2, 0]] the section's zero-input step, computed in
+// K_carry's maps for a chunk cut into nseg segments of seg samples, per
+// coefficient set (layout: fx_tp_mat_stride in dsp_kernels.hpp): the cascade's
+// zero-input step A (2 nsec x 2 nsec, block lower triangular: section k's
+// input is section k-1's output), its segment map B = A^seg as 2 x 2 blocks,
+// and per section the scan maps B(k,k)^(2^i).  Computed in
 // 64-bit-mantissa long double and stored as double-double pairs.  Built once
 // per (seg, nseg) and coefficient table (a chunk length and the last chunk's).
 const double* fx_tp_mats(ad_fx_chain* h, int seg, int nseg) {
   auto& slot = h->tp_mats[std::make_pair(seg, nseg)];
   if (slot) return slot->p;
-  const int sets = h->eq_uniform ? 1 : h->channels, nsec = h->nsec;
-  const int Q = (nseg + kFxTpCarryWaves - 1) / kFxTpCarryWaves;
+  const int sets = h->eq_uniform ? 1 : h->channels, nsec = h->nsec, D = 2 * nsec;
   typedef long double ld;
-  auto mul = [](const ld* x, const ld* y, ld* r) {
-    const ld t[4] = {x[0] * y[0] + x[1] * y[2], x[0] * y[1] + x[1] * y[3], x[2] * y[0] + x[3] * y[2],
-                     x[2] * y[1] + x[3] * y[3]};
-    for (int i = 0; i < 4; ++i) r[i] = t[i];
+  typedef std::vector<ld> mat;  // D x D row-major
+  auto mul = [D](const mat& x, const mat& y) {
+    mat r((size_t)D * D, 0);
+    for (int i = 0; i < D; ++i)
+      for (int k = 0; k < D; ++k) {
+        const ld v = x[(size_t)i * D + k];
+        if (v != 0)
+          for (int j = 0; j < D; ++j) r[(size_t)i * D + j] += v * y[(size_t)k * D + j];
+      }
+    return r;
   };
-  auto pw = [&](const ld* b0, int e, ld* m) {
-    ld b[4] = {b0[0], b0[1], b0[2], b0[3]};
-    m[0] = 1, m[1] = 0, m[2] = 0, m[3] = 1;
+  auto pw = [&](mat b, int e) {
+    mat m((size_t)D * D, 0);
+    for (int i = 0; i < D; ++i) m[(size_t)i * D + i] = 1;
     for (; e > 0; e >>= 1) {
-      if (e & 1) mul(m, b, m);
-      mul(b, b, b);
+      if (e & 1) m = mul(m, b);
+      b = mul(b, b);
     }
+    return m;
   };
-  std::vector<double> t((size_t)nsec * sets * 16);
-  for (int k = 0; k < nsec; ++k)
-    for (int c = 0; c < sets; ++c) {
-      const double* q = h->sec_host.data() + ((size_t)c * nsec + k) * kSecStride;
-      const ld A[4] = {-(ld)q[4], 1, -(ld)q[5], 0};
-      ld M[4], MQ[4];
-      pw(A, seg, M);
-      pw(M, Q, MQ);
-      double* o = t.data() + ((size_t)k * sets + c) * 16;
-      for (int i = 0; i < 4; ++i) {
-        o[2 * i] = (double)M[i];
-        o[2 * i + 1] = (double)(M[i] - (ld)o[2 * i]);
-        o[8 + 2 * i] = (double)MQ[i];
-        o[8 + 2 * i + 1] = (double)(MQ[i] - (ld)o[8 + 2 * i]);
+  auto m2 = [](const ld* x, const ld* y, ld* r) {
+    const ld u[4] = {x[0] * y[0] + x[1] * y[2], x[0] * y[1] + x[1] * y[3], x[2] * y[0] + x[3] * y[2],
+                     x[2] * y[1] + x[3] * y[3]};
+    for (int i = 0; i < 4; ++i) r[i] = u[i];
+  };
+  auto put = [](double* o, ld v) {
+    o[0] = (double)v;
+    o[1] = (double)(v - (ld)o[0]);
+  };
+  const int stride = fx_tp_mat_stride(nsec);
+  std::vector<double> t((size_t)sets * stride, 0.0);
+  for (int c = 0; c < sets; ++c) {
+    const double* q = h->sec_host.data() + (size_t)c * nsec * kSecStride;
+    // A's column i: one zero-input step of the cascade (section.go:47-53)
+    // from the unit state e_i; state order (d0, d1) per section
+    mat A((size_t)D * D, 0);
+    for (int i = 0; i < D; ++i) {
+      std::vector<ld> st(D, 0);
+      st[i] = 1;
+      ld x = 0;
+      for (int k = 0; k < nsec; ++k) {
+        const double* g = q + k * kSecStride;
+        const ld v = x * g[0];
+        const ld y = g[1] * v + st[2 * k];
+        A[(size_t)(2 * k) * D + i] = g[2] * v - g[4] * y + st[2 * k + 1];
+        A[(size_t)(2 * k + 1) * D + i] = g[3] * v - g[5] * y;
+        x = y;
       }
     }
+    const mat B = pw(A, seg);
+    double* o = t.data() + (size_t)c * stride;
+    for (int k = 0; k < nsec; ++k)
+      for (int j = 0; j <= k; ++j)
+        for (int e = 0; e < 4; ++e)
+          put(o + ((size_t)k * nsec + j) * 8 + 2 * e, B[(size_t)(2 * k + e / 2) * D + 2 * j + e % 2]);
+    for (int k = 0; k < nsec; ++k) {  // B(k,k) and its repeated squares
+      ld P[4];
+      for (int e = 0; e < 4; ++e) P[e] = B[(size_t)(2 * k + e / 2) * D + 2 * k + e % 2];
+      for (int i = 0; i < kFxTpScan; ++i) {
+        for (int e = 0; e < 4; ++e) put(o + ((size_t)nsec * nsec + k * kFxTpScan + i) * 8 + 2 * e, P[e]);
+        m2(P, P, P);
+      }
+    }
+  }
   slot.reset(new DevBuf<double>());
   slot->alloc(t.size());
   AD_HIP(hipMemcpy(slot->p, t.data(), t.size() * sizeof(double), hipMemcpyHostToDevice));
@@ -474,7 +509,8 @@ void fx_run_tp(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hipStre
     AD_HIP(hipEventCreateWithFlags(&h->ev_in, hipEventDisableTiming));
   }
   if (T > h->tmax || !h->xT[0].p || (eq && !h->vT[0].p) || (comp && !h->envT[0].p) ||
-      (comp && verb && (!h->inC[0].p || !h->coC.p)) || (eq && !h->tp_zs.p)) {  // (re)size once no stage is running
+      (comp && verb && (!h->inC[0].p || !h->coC.p)) ||
+      (eq && h->tp_zs.n < (size_t)kFxTpMaxSeg * h->nsec * h->cpad * 2)) {  // (re)size once no stage is running
     for (hipStream_t x : h->st) AD_HIP(hipStreamSynchronize(x));
     AD_HIP(hipStreamSynchronize(s));
     const size_t r = (size_t)h->cpad * std::max(T, h->tmax);
@@ -486,8 +522,8 @@ void fx_run_tp(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hipStre
     }
     if (comp && verb) h->coC.alloc((size_t)h->channels * kVerbCombs * kFxVerbSB);
     if (eq) {
-      h->tp_zs.alloc((size_t)kFxTpMaxSeg * h->cpad * 2);
-      h->tp_carry.alloc((size_t)kFxTpMaxSeg * h->cpad * 2);
+      h->tp_zs.alloc((size_t)kFxTpMaxSeg * h->nsec * h->cpad * 2);
+      h->tp_carry.alloc((size_t)kFxTpMaxSeg * h->nsec * h->cpad * 4);
     }
     h->tmax = std::max(T, h->tmax);
   }
@@ -544,30 +580,33 @@ void fx_run_tp(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hipStre
       e.vT = a.vT;
       e.eq = a.eq;
       e.zs = h->tp_zs.p;
-      e.carry = h->tp_carry.p;
+      e.sdd = h->tp_carry.p;
       e.mats = fx_tp_mats(h, e.seg, e.nseg);
       e.mat_sets = h->eq_uniform ? 1 : h->channels;
-      for (int kk = 0; kk <= h->nsec; ++kk) {
-        e.k = kk;
-        launch_fxtp_eq(e, s);
-        if (kk < h->nsec) launch_fxtp_carry(e, s);
-      }
+      launch_fxtp_eq(e, false, s);
+      launch_fxtp_carry(e, s);
+      launch_fxtp_eq(e, true, s);
     }
     AD_HIP(hipEventRecord(h->ev[EE][k], s));
     if (comp) {
       AD_HIP(hipStreamWaitEvent(sd, h->ev[EE][k], 0));
       launch_fxtp_det(a, sd);
-      AD_HIP(hipEventRecord(h->ev[ED][k], sd));
-      AD_HIP(hipStreamWaitEvent(sv, h->ev[ED][k], 0));
-      if (verb) {  // the compressor output channel-major into inC, then Freeverb into the user buffer
+      if (verb) {
+        // the compressor output channel-major into inC on the detector's
+        // stream (the reverb's stream is the longer one), then Freeverb into
+        // the user buffer; inC[k] is free once chunk i - kFxSlots's reverb ran
+        if (i >= kFxSlots) AD_HIP(hipStreamWaitEvent(sd, h->ev[EA][k], 0));
         FxStageArgs b = a;
         b.buf = h->inC[k].p;
         b.stride = h->tmax;
-        launch_fx_gain(b, true, sv);
-        launch_fxtp_verb(a, h->inC[k].p, h->tmax, h->vbufC.p, h->coC.p, wu, sv);
-      } else {
-        launch_fx_gain(a, true, sv);
+        launch_fx_gain(b, true, sd);
       }
+      AD_HIP(hipEventRecord(h->ev[ED][k], sd));
+      AD_HIP(hipStreamWaitEvent(sv, h->ev[ED][k], 0));
+      if (verb)
+        launch_fxtp_verb(a, h->inC[k].p, h->tmax, h->vbufC.p, h->coC.p, wu, sv);
+      else
+        launch_fx_gain(a, true, sv);
     } else {
       AD_HIP(hipStreamWaitEvent(sv, h->ev[EE][k], 0));
       launch_fx_transpose_out(a, a.vT, sv);  // (not reached: the engine runs with a compressor)

@@ -137,28 +137,33 @@ void launch_fx_comb(const FxStageArgs& a, hipStream_t s);
 void launch_fx_allpass(const FxStageArgs& a, hipStream_t s);
 constexpr int kFxOutVT = 1, kFxOutInT = 2;
 
-// Time-parallel engine (fx_tp.hip; host: fx_run_tp).  K_eq launch k of
-// nsec + 1 over a chunk cut into nseg <= 256 segments of `seg` samples:
-// section k - 1 exactly from the segment start states in `carry`, fused with
-// the zero-state run of section k (end states to `zs`); K_carry then chains
-// section k's start states into `carry`.
+// Time-parallel engine (fx_tp.hip; host: fx_run_tp).  The EQ cascade of a
+// chunk cut into nseg <= 256 segments of `seg` samples runs in three launches:
+// K_eqz the cascade's zero-state runs (end states to `zs`), K_carry the
+// segment start states of every section (double-double, to `sdd`), K_eqx the
+// exact cascade from those starts (rows to vT, chunk-end states to eq.state).
 struct FxTpEqArgs {
   int channels, cpad;
   int64_t len;
   int seg, nseg;
   const double* xT;  // chunk input rows [len][cpad]
-  double* vT;        // EQ output rows (in place between launches)
+  double* vT;        // EQ output rows [len][cpad]
   EqArgs eq;
-  int k;
-  double* zs;        // [nseg][cpad][2]
-  double* carry;     // [nseg][cpad][2]
-  const double* mats;  // [nsec][mat_sets][M, M^Q][4 entries][hi, lo] (host fx_tp_mats)
+  double* zs;          // [nseg][nsec][cpad][d0, d1]
+  double* sdd;         // [nseg][nsec][cpad][d0.hi, d0.lo, d1.hi, d1.lo]
+  const double* mats;  // [mat_sets][fx_tp_mat_stride(nsec)] (host fx_tp_mats)
   int mat_sets;        // 1 (one coefficient table) or channels
 };
-constexpr int kFxTpCarryWaves = 8;  // K_carry waves per 64 channels
+constexpr int kFxTpMaxSeg = 256;  // segments per chunk, at most (K_carry: one thread each)
+constexpr int kFxTpScan = 8;      // K_carry scan steps (log2 kFxTpMaxSeg)
+// per coefficient set: the segment map's 2 x 2 blocks B(k, j) (section k's end
+// state from section j's start, j <= k; [nsec][nsec]), then per section the
+// scan maps B(k, k)^(2^i), i < kFxTpScan; every block 4
+// double-double entries (row-major), i.e. 8 doubles
+__host__ __device__ constexpr int fx_tp_mat_stride(int nsec) { return nsec * (nsec + kFxTpScan) * 8; }
 constexpr int kFxVerbSB = 4096;     // K_verb sub-block (samples)
-void launch_fxtp_eq(const FxTpEqArgs& a, hipStream_t s);
-void launch_fxtp_carry(const FxTpEqArgs& a, hipStream_t s);  // section a.k's segment start states
+void launch_fxtp_eq(const FxTpEqArgs& a, bool exact, hipStream_t s);  // K_eqz (exact = false) or K_eqx
+void launch_fxtp_carry(const FxTpEqArgs& a, hipStream_t s);
 void launch_fxtp_det(const FxStageArgs& a, hipStream_t s);           // vT -> envT (+ detector state)
 // Freeverb, one channel per workgroup: xC [channels][xstride] (channel-major
 // reverb input) -> user buffer, delay lines in vbufC [channels][kVerbLen],

@@ -11,17 +11,18 @@
 // waves: a one-lane-per-channel engine is bound by its recurrences' issue
 // and latency on a handful of CUs.  Here time is a parallel axis too:
 //
-//   K_eq   a DF-II-T section is linear in its state s = (d0, d1): over a
-//          segment of L samples, s_end = A^L s_start + s_zs, where s_zs is
-//          the zero-state run of the segment and A = [[-a1, 1], [-a2, 0]].
-//          Launch k runs, for every (segment, channel), the exact section k-1
-//          from its true start state (the reference operations, so only the
-//          start state carries rounding) fused with the zero-state run of
-//          section k; the last workgroup to finish then chains the segment
-//          start states of section k (S steps of a 2 x 2 map per channel).
-//          nsec + 1 launches over the whole chip per chunk.
+//   K_eq   the biquad cascade is linear in its state S (2 values per
+//          section): over a segment of L samples S_end = B S_start + Z, with
+//          Z the cascade's zero-state run of the segment and B = A^L (A the
+//          cascade's zero-input step, block lower triangular).  K_eqz runs
+//          every (segment, channel) from zero (Z); K_carry chains the segment
+//          start states in double-double (an LDS scan over the segments per
+//          section, the earlier sections' starts folded in through B's
+//          off-diagonal blocks); K_eqx reruns the cascade from those starts
+//          with the reference operations (only the start states carry
+//          rounding).  Three launches and two passes over the chunk.
 //   K_det  the envelope follower is not linear (attack or release by the
-//          sign of src - env): one wave per 64 channels, serial.
+//          sign of src - env): serial per channel, 8 channels per workgroup.
 //   K_verb a comb reads its line D >= 1116 samples back, so between two
 //          wraps of its ring index every line value read is known before
 //          the first sample; only the one-pole damping filter
@@ -63,73 +64,81 @@ __device__ __forceinline__ double sec_step(const double (&q)[kSecStride], double
   return y;
 }
 
-constexpr int kTpSegB = 16;  // K_eq: rows per load batch
+constexpr int kTpSegB = 16;  // K_eqz / K_eqx: rows per load batch
 
+// K_eqz (EXACT = false): the whole cascade from zero states over each
+// (segment, channel), end states of every section to zs.  K_eqx (EXACT):
+// the cascade from the segment start states K_carry chained (rounded from
+// double-double), the reference operations per sample, rows to vT; the last
+// segment leaves the chunk-end states in eq.state.  One wave per segment,
+// one lane per channel.
+template <bool EXACT>
 __global__ __launch_bounds__(256) void k_fxtp_eq(FxTpEqArgs a) {
 #pragma clang fp contract(off)
   const int w = wave_of_thread();
   const int l = threadIdx.x & 63;
-  const int g = blockIdx.y;
-  const int c = g * 64 + l;
+  const int c = blockIdx.y * 64 + l;
   const bool active = c < a.channels;
   const int cc = active ? c : a.channels - 1;
   const unsigned uc = (unsigned)c;
   const int cp = a.cpad;
   const int sg = blockIdx.x * 4 + w;  // segment
-  const int k = a.k, nsec = a.eq.nsec;
-  const bool p3 = k >= 1, p1 = k < nsec;
-  if (sg < a.nseg) {
-    const int64_t n0 = (int64_t)sg * a.seg, n1 = min(a.len, n0 + a.seg);
-    const double* secs = a.eq.sec + (int64_t)cc * a.eq.sec_ch_stride;
-    double q3[kSecStride], q1[kSecStride];
+  const int nsec = a.eq.nsec;
+  if (sg >= a.nseg) return;
+  const int64_t n0 = (int64_t)sg * a.seg, n1 = min(a.len, n0 + a.seg);
+  const double* secs = a.eq.sec + (int64_t)cc * a.eq.sec_ch_stride;
+  double q[kMaxSecPerPass][kSecStride], d0[kMaxSecPerPass], d1[kMaxSecPerPass];
 #pragma unroll
-    for (int j = 0; j < kSecStride; ++j) {
-      q3[j] = p3 ? secs[(k - 1) * kSecStride + j] : 0.0;
-      q1[j] = p1 ? secs[k * kSecStride + j] : 0.0;
+  for (int k = 0; k < kMaxSecPerPass; ++k) {
+#pragma unroll
+    for (int j = 0; j < kSecStride; ++j) q[k][j] = k < nsec ? secs[k * kSecStride + j] : 0.0;
+    d0[k] = d1[k] = 0.0;
+    if (EXACT && k < nsec) {
+      const double4 s = reinterpret_cast<const double4*>(a.sdd)[((int64_t)sg * nsec + k) * cp + c];
+      d0[k] = s.x + s.y;
+      d1[k] = s.z + s.w;
     }
-    double d0 = 0.0, d1 = 0.0, z0 = 0.0, z1 = 0.0;
-    if (p3) {
-      const double2 s = reinterpret_cast<const double2*>(a.carry)[(int64_t)sg * cp + c];
-      d0 = s.x;
-      d1 = s.y;
-    }
-    // section k-1's input: the chunk input for section 0, else the rows the
-    // previous launch wrote (in place: a lane rewrites only rows it has read)
-    const AD_TPG double* src = gptr(k >= 2 ? (const double*)a.vT : a.xT);
-    AD_TPG double* dst = gptr(a.vT);
-    double xb[2][kTpSegB];
-    auto load = [&](double (&b)[kTpSegB], int64_t r0) {
+  }
+  const AD_TPG double* src = gptr(a.xT);
+  AD_TPG double* dst = gptr(a.vT);
+  double xb[2][kTpSegB];
+  auto load = [&](double (&b)[kTpSegB], int64_t r0) {
 #pragma unroll
-      for (int j = 0; j < kTpSegB; ++j) b[j] = src[min(r0 + j, a.len - 1) * cp + uc];
-    };
-    auto run = [&](double (&b)[kTpSegB], int64_t r0) {
-      const int nb = (int)min((int64_t)kTpSegB, n1 - r0);
+    for (int j = 0; j < kTpSegB; ++j) b[j] = src[min(r0 + j, a.len - 1) * cp + uc];
+  };
+  auto run = [&](double (&b)[kTpSegB], int64_t r0) {
+    const int nb = (int)min((int64_t)kTpSegB, n1 - r0);
 #pragma unroll
-      for (int j = 0; j < kTpSegB; ++j) {
-        if (j < nb) {
-          double x = b[j];
-          if (p3) {
-            x = sec_step(q3, d0, d1, x);
-            dst[(r0 + j) * cp + uc] = x;
-          }
-          if (p1) (void)sec_step(q1, z0, z1, x);
-        }
+    for (int j = 0; j < kTpSegB; ++j) {
+      if (j < nb) {
+        double x = b[j];
+#pragma unroll
+        for (int k = 0; k < kMaxSecPerPass; ++k)
+          if (k < nsec) x = sec_step(q[k], d0[k], d1[k], x);
+        if (EXACT) dst[(r0 + j) * cp + uc] = x;
       }
-    };
-    if (n0 < n1) load(xb[0], n0);
-    for (int64_t r = n0; r < n1; r += 2 * kTpSegB) {
-      if (r + kTpSegB < n1) load(xb[1], r + kTpSegB);
-      run(xb[0], r);
-      if (r + kTpSegB >= n1) break;
-      if (r + 2 * kTpSegB < n1) load(xb[0], r + 2 * kTpSegB);
-      run(xb[1], r + kTpSegB);
     }
-    if (p3 && sg == a.nseg - 1 && active) {  // the chunk-end state of section k-1
-      double* st = a.eq.state + ((int64_t)c * nsec + (k - 1)) * 2;
-      st[0] = d0;
-      st[1] = d1;
+  };
+  load(xb[0], n0);
+  for (int64_t r = n0; r < n1; r += 2 * kTpSegB) {
+    if (r + kTpSegB < n1) load(xb[1], r + kTpSegB);
+    run(xb[0], r);
+    if (r + kTpSegB >= n1) break;
+    if (r + 2 * kTpSegB < n1) load(xb[0], r + 2 * kTpSegB);
+    run(xb[1], r + kTpSegB);
+  }
+#pragma unroll
+  for (int k = 0; k < kMaxSecPerPass; ++k) {
+    if (k >= nsec) break;
+    if (EXACT) {
+      if (sg == a.nseg - 1 && active) {  // the chunk-end state of section k
+        double* st = a.eq.state + ((int64_t)c * nsec + k) * 2;
+        st[0] = d0[k];
+        st[1] = d1[k];
+      }
+    } else {
+      reinterpret_cast<double2*>(a.zs)[((int64_t)sg * nsec + k) * cp + c] = make_double2(d0[k], d1[k]);
     }
-    if (p1) reinterpret_cast<double2*>(a.zs)[(int64_t)sg * cp + c] = make_double2(z0, z1);
   }
 }
 
@@ -168,89 +177,120 @@ __device__ __forceinline__ dd dd_mul(dd x, dd y) {
 struct dd2x2 {
   dd m[4];
 };
-// s' = M s + z
-__device__ __forceinline__ void dd_step(const dd2x2& M, dd& s0, dd& s1, dd z0, dd z1) {
-  const dd t0 = dd_add(dd_add(dd_mul(M.m[0], s0), dd_mul(M.m[1], s1)), z0);
-  const dd t1 = dd_add(dd_add(dd_mul(M.m[2], s0), dd_mul(M.m[3], s1)), z1);
-  s0 = t0;
-  s1 = t1;
+__device__ __forceinline__ dd2x2 dd_block(const double* p) {
+  dd2x2 b;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) b.m[i] = dd{p[2 * i], p[2 * i + 1]};
+  return b;
 }
+// (t0, t1) += B (s0, s1)
+__device__ __forceinline__ void dd_madd(const dd2x2& B, dd s0, dd s1, dd& t0, dd& t1) {
+  t0 = dd_add(t0, dd_add(dd_mul(B.m[0], s0), dd_mul(B.m[1], s1)));
+  t1 = dd_add(t1, dd_add(dd_mul(B.m[2], s0), dd_mul(B.m[3], s1)));
+}
+struct dd2v {
+  dd a, b;
+};
 
-// K_carry (after the launch that ran section k's zero-state segments): one
-// workgroup of kCyW waves per 64 channels chains section k's segment start
-// states in double-double, carry[0] = the chunk-start state,
-// carry[v + 1] = M carry[v] + zs[v], M = A^seg.  Wave u takes Q = nseg/kCyW
-// consecutive segments: it chains its zs from zero (e_u), the start of its
-// range is M^Q-chained over e_0 .. e_{u-1} (LDS), then it walks its range
-// again writing the starts rounded to double.
-constexpr int kCyW = kFxTpCarryWaves;  // 16 KiB of LDS, so it fits beside a K_verb workgroup
-__global__ __launch_bounds__(64 * kCyW) void k_fxtp_carry(FxTpEqArgs a) {
-  const int w = wave_of_thread();
-  const int l = threadIdx.x & 63;
-  const int c = blockIdx.x * 64 + l;
-  const int cc = c < a.channels ? c : a.channels - 1;
-  const int cp = a.cpad;
-  const int k = a.k, nsec = a.eq.nsec;
-  __shared__ dd agg[kCyW][2][64];
-  // M = A^seg and M^Q, A the zero-input step [[-a1, 1], [-a2, 0]] (host, fx_tp_mats)
-  const double* mt = a.mats + ((int64_t)k * a.mat_sets + (a.mat_sets > 1 ? cc : 0)) * 16;
-  dd2x2 M, MQ;
+// K_carry: one workgroup per channel, one thread per segment v, the
+// sections in turn.  Over a segment the cascade state S = (s_0 .. s_{nsec-1})
+// maps as S' = B S + Z (B block lower triangular, Z the zero-state end states
+// from K_eqz), so section k's start states obey
+//   s_k(v+1) = B(k,k) s_k(v) + u_k(v),  u_k(v) = Z_k(v) + sum_{j<k} B(k,j) s_j(v).
+// Thread v keeps the cross terms of the later sections in registers (acc[k]),
+// adding B(k,j) s_j(v) as soon as s_j(v) is known.  The chain itself is an
+// inclusive scan over the segments in LDS (Hillis-Steele, maps B(k,k)^(2^i)),
+// with the chunk-start state folded into segment 0.
+__global__ __launch_bounds__(kFxTpMaxSeg) void k_fxtp_carry(FxTpEqArgs a) {
+  const int v = threadIdx.x;  // segment
+  const int c = blockIdx.x;   // channel
+  const int cp = a.cpad, nsec = a.eq.nsec;
+  const bool live = v < a.nseg;
+  __shared__ dd2v scan[2][kFxTpMaxSeg];
+  const double* ms = a.mats + (int64_t)(a.mat_sets > 1 ? c : 0) * fx_tp_mat_stride(nsec);
+  const double2* zs = reinterpret_cast<const double2*>(a.zs);
+  double4* sdd = reinterpret_cast<double4*>(a.sdd);
+  dd acc0[kMaxSecPerPass], acc1[kMaxSecPerPass];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    M.m[i] = dd{mt[2 * i], mt[2 * i + 1]};
-    MQ.m[i] = dd{mt[8 + 2 * i], mt[8 + 2 * i + 1]};
-  }
-  const int Q = (a.nseg + kCyW - 1) / kCyW;
-  const int v0 = w * Q, nv = max(0, min(a.nseg - v0, Q));
-  const double2* zs = reinterpret_cast<const double2*>(a.zs) + (int64_t)v0 * cp + c;
-  // zs streamed twice (8 loads ahead): chain from zero, then walk from the true start
-  auto walk = [&](dd& s0, dd& s1, bool store) {
-    double2* cy = reinterpret_cast<double2*>(a.carry) + (int64_t)v0 * cp + c;
-    for (int j0 = 0; j0 < nv; j0 += 8) {
-      double2 zr[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) zr[j] = zs[(int64_t)min(j0 + j, nv - 1) * cp];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        if (j0 + j < nv) {
-          if (store) cy[(int64_t)(j0 + j) * cp] = make_double2(s0.hi + s0.lo, s1.hi + s1.lo);
-          dd_step(M, s0, s1, dd{zr[j].x, 0}, dd{zr[j].y, 0});
-        }
-      }
+  for (int k = 0; k < kMaxSecPerPass; ++k) {
+    acc0[k] = acc1[k] = dd{0, 0};
+    if (k < nsec && live) {
+      const double2 z = zs[((int64_t)v * nsec + k) * cp + c];
+      acc0[k] = dd{z.x, 0};
+      acc1[k] = dd{z.y, 0};
     }
-  };
-  dd e0{0, 0}, e1{0, 0};
-  walk(e0, e1, false);
-  agg[w][0][l] = e0;
-  agg[w][1][l] = e1;
-  __syncthreads();
-  const double* st = a.eq.state + ((int64_t)cc * nsec + k) * 2;
-  dd s0{st[0], 0}, s1{st[1], 0};
-  for (int u = 0; u < w; ++u) dd_step(MQ, s0, s1, agg[u][0][l], agg[u][1][l]);
-  walk(s0, s1, true);
+  }
+#pragma unroll
+  for (int k = 0; k < kMaxSecPerPass; ++k) {
+    if (k >= nsec) break;
+    const double* st = a.eq.state + ((int64_t)c * nsec + k) * 2;
+    const dd S0{st[0], 0}, S1{st[1], 0};
+    dd e0 = acc0[k], e1 = acc1[k];
+    if (v == 0) dd_madd(dd_block(ms + ((int64_t)k * nsec + k) * 8), S0, S1, e0, e1);
+    // inclusive scan: E_v = sum_{v' <= v} B(k,k)^(v - v') e_v'  (segment v's end state)
+    int cur = 0;
+    scan[cur][v] = dd2v{e0, e1};
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kFxTpScan; ++i) {
+      const int d = 1 << i;
+      if (v >= d) {
+        const dd2v p = scan[cur][v - d];
+        dd_madd(dd_block(ms + ((int64_t)nsec * nsec + k * kFxTpScan + i) * 8), p.a, p.b, e0, e1);
+      }
+      scan[cur ^ 1][v] = dd2v{e0, e1};
+      cur ^= 1;
+      __syncthreads();
+    }
+    // segment v's start: segment v - 1's end, the chunk-start state for v = 0
+    dd s0 = S0, s1 = S1;
+    if (v > 0) {
+      const dd2v p = scan[cur][v - 1];
+      s0 = p.a;
+      s1 = p.b;
+    }
+    if (live) sdd[((int64_t)v * nsec + k) * cp + c] = make_double4(s0.hi, s0.lo, s1.hi, s1.lo);
+    // the later sections' cross terms
+#pragma unroll
+    for (int k2 = k + 1; k2 < kMaxSecPerPass; ++k2)
+      if (k2 < nsec) dd_madd(dd_block(ms + ((int64_t)k2 * nsec + k) * 8), s0, s1, acc0[k2], acc1[k2]);
+    __syncthreads();  // scan[] is rewritten by the next section
+  }
 }
 
 // ---------------------------------------------------------------------------
 // K_det: side-chain prefilters, detector and envelope (core.go:274-286,
 // 331-400), serial over the chunk, kDetCh channels per workgroup (lanes of
 // wave 0; the other lanes repeat them): a 64-channel group would need
-// ~40 GB/s of row traffic into one CU at the detector's pace.  Wave 1 keeps
-// kDetNB batches of row loads in flight in registers (every load covers
-// 64 / kDetCh rows of kDetCh channels; <= 63 outstanding) and puts each
-// batch into a small LDS ring one step before the detector reads it; one
-// barrier per batch.  The lookahead (kDetNB batches) is what hides the
+// ~40 GB/s of row traffic into one CU at the detector's pace.  Three waves:
+//   wave 1 (loader) keeps kDetNB batches of row loads in flight in registers
+//          (every load covers 64 / kDetCh rows of kDetCh channels; <= 63
+//          outstanding) and puts each batch into a small LDS ring two steps
+//          before the detector consumes it;
+//   wave 0 (detector) reads batch k + 1 out of the ring before it runs the
+//          envelope chain over batch k (the LDS latency hides under the
+//          chain) and puts the 16 envelopes into a second ring;
+//   wave 2 (storer) writes the envelopes of batch k - 1 to memory with two
+//          full-width stores (no selects or address arithmetic on the
+//          detector's issue slots, and no stores in the loader's vmcnt).
+// One barrier per batch.  The lookahead (kDetNB batches) is what hides the
 // memory latency: 10 batches of 16 measured 481 us per chunk, 14 370 us.
 // ---------------------------------------------------------------------------
 constexpr int kDetCh = 8;      // channels per workgroup
-constexpr int kDetB = 16;      // rows per batch
+#ifndef AD_DET_B  // tools/ A/B builds may override
+#define AD_DET_B 32
+#define AD_DET_NB 14
+#endif
+constexpr int kDetB = AD_DET_B;  // rows per batch
 constexpr int kDetLd = kDetB * kDetCh / 64;  // loads per batch (2)
-constexpr int kDetNB = 28;     // batches in flight in the loader (56 loads outstanding)
-constexpr int kDetSlots = 4;   // LDS ring slots (a batch lives there for one step)
+constexpr int kDetNB = AD_DET_NB;  // batches in flight in the loader (56 loads outstanding)
+constexpr int kDetSlots = 4;   // input ring slots (put two steps ahead, read one step ahead)
 __device__ __forceinline__ void lds_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-__global__ __launch_bounds__(128) void k_fxtp_det(FxStageArgs a) {
+__global__ __launch_bounds__(192) void k_fxtp_det(FxStageArgs a) {
 #pragma clang fp contract(off)
   __shared__ double ring[kDetSlots][kDetB][kDetCh];
+  __shared__ double evr[2][kDetB][kDetCh];  // envelopes of a bare full batch, for the storer
   const int w = wave_of_thread();
   const int l = threadIdx.x & 63;
   const int c0 = blockIdx.x * kDetCh;
@@ -258,47 +298,44 @@ __global__ __launch_bounds__(128) void k_fxtp_det(FxStageArgs a) {
   const int64_t len = a.len;
   const int64_t nb = (len + kDetB - 1) / kDetB;
   const int64_t nbp = (nb + kDetNB - 1) / kDetNB * kDetNB;
+  const CompParams& p = a.cp;
+  const bool bare = !p.lp_on && !p.hp_on && !p.detector_rms;
+  constexpr int RS = 64 / kDetCh;  // rows per load / store
   if (w == 0) {
-    // lanes >= kDetCh repeat lanes 0..kDetCh-1 (same channel, same values,
-    // same stores): no branch around the stores, so the ring reads of a
-    // batch are issued together ahead of the envelope chain
+    // lanes >= kDetCh repeat lanes 0..kDetCh-1 (same channel, same values)
     const int c = c0 + (l & (kDetCh - 1));
     const bool active = l < kDetCh && c < a.channels;
     const int cc = c < a.channels ? c : a.channels - 1;
     const unsigned uc = (unsigned)c;
     const int li = l & (kDetCh - 1);
-    const CompParams& p = a.cp;
     CompChState cs = a.cs[cc];
     AD_TPG double* rring = gptr(a.rms_ring) + (int64_t)cc * p.rms_n;
     AD_TPG double* eo = gptr(a.envT);
-    const bool bare = !p.lp_on && !p.hp_on && !p.detector_rms;
+#ifdef AD_DET_PRIO  // tools/ A/B builds only
+    __builtin_amdgcn_s_setprio(AD_DET_PRIO);
+#endif
     __builtin_amdgcn_s_waitcnt(0);  // the state loads land before the step loop
-    lds_bar();                      // the loader's prologue
-    // nbp steps (nb rounded up to the loader's unroll): the barrier counts match
-    for (int64_t k = 0; k < nbp; ++k) {
-      const int slot = (int)(k % kDetSlots);
+    lds_bar();                      // the loader's prologue (batches 0 and 1)
+    // one step: batch k from cur (read one step earlier), batch k + 1 into nxt
+    auto step = [&](int64_t k, double (&cur)[kDetB], double (&nxt)[kDetB]) {
+      const int slot = (int)(k % kDetSlots), sn = (int)((k + 1) % kDetSlots);
       const int64_t r0 = k * kDetB;
       const int n = (int)max((int64_t)0, min((int64_t)kDetB, len - r0));
       if (bare && n == kDetB) {
-        double xv[kDetB], ev[kDetB];
 #pragma unroll
-        for (int d = 0; d < kDetB; ++d) xv[d] = ring[slot][d][li];
+        for (int d = 0; d < kDetB; ++d) nxt[d] = ring[sn][d][li];
+        double ev[kDetB];
 #pragma unroll
         for (int d = 0; d < kDetB; ++d) {
-          cs.env = env_step(p, cs.env, fabs(xv[d]));
+          cs.env = env_step(p, cs.env, fabs(cur[d]));
           ev[d] = cs.env;
         }
-        // kDetLd stores per batch, not kDetB: lane l stores row
-        // l / kDetCh + RS i of its channel (every lane holds its channel's
-        // whole batch), picked out of ev[] by selects
-        constexpr int RS = 64 / kDetCh;
-        const int rq = l / kDetCh;
+        // one masked region per batch: lanes >= kDetCh would write the same
+        // addresses again (8-way conflicts on every write)
+        if (l < kDetCh) {
+          double(*e)[kDetCh] = evr[k & 1];
 #pragma unroll
-        for (int i = 0; i < kDetLd; ++i) {
-          double v = ev[RS * i];
-#pragma unroll
-          for (int q = 1; q < RS; ++q) v = rq == q ? ev[RS * i + q] : v;
-          eo[(r0 + rq + RS * i) * cp + uc] = v;
+          for (int d = 0; d < kDetB; ++d) e[d][li] = ev[d];
         }
       } else {
         for (int d = 0; d < n; ++d) {
@@ -327,8 +364,19 @@ __global__ __launch_bounds__(128) void k_fxtp_det(FxStageArgs a) {
           cs.env = env_step(p, cs.env, src);
           if (l < kDetCh) eo[(r0 + d) * cp + uc] = cs.env;
         }
+#pragma unroll
+        for (int d = 0; d < kDetB; ++d) nxt[d] = ring[sn][d][li];
       }
       lds_bar();
+    };
+    double xa[kDetB], xb[kDetB];
+#pragma unroll
+    for (int d = 0; d < kDetB; ++d) xa[d] = ring[0][d][li];
+    // nbp steps (nb rounded up to the loader's unroll, an even count): the
+    // barrier counts match
+    for (int64_t k = 0; k < nbp; k += 2) {
+      step(k, xa, xb);
+      step(k + 1, xb, xa);
     }
     if (active) {  // only the fields this stage owns
       AD_TPG CompChState* o = gptr(a.cs) + c;
@@ -339,14 +387,12 @@ __global__ __launch_bounds__(128) void k_fxtp_det(FxStageArgs a) {
       o->rms_index = cs.rms_index;
       o->rms_filled = cs.rms_filled;
     }
-  } else {
-    // loader: lane l covers row (l / kDetCh) + (64 / kDetCh) i of a batch,
-    // channel l % kDetCh; its register ring holds kDetNB batches, entry =
-    // batch mod kDetNB
+  } else if (w == 1) {
+    // loader: lane l covers row (l / kDetCh) + RS i of a batch, channel
+    // l % kDetCh; its register ring holds kDetNB batches, entry = batch mod kDetNB
     const AD_TPG double* vin = gptr((const double*)a.vT);
     const unsigned col = (unsigned)(c0 + (l & (kDetCh - 1)));
     const int rl = l / kDetCh;
-    constexpr int RS = 64 / kDetCh;  // rows per load
     double buf[kDetNB][kDetLd];
     auto load = [&](double (&r)[kDetLd], int64_t b) {
 #pragma unroll
@@ -365,17 +411,40 @@ __global__ __launch_bounds__(128) void k_fxtp_det(FxStageArgs a) {
     for (int e = 0; e < kDetNB; ++e) load(buf[e], e);
     put(buf[0], 0);
     load(buf[0], kDetNB);
+    put(buf[1], 1);
+    load(buf[1], kDetNB + 1);
     lds_bar();
-    // step k (det consumes batch k): batch k + 1 goes into its slot, batch
-    // k + 1 + kDetNB is requested into the freed entry
+    // step k (the detector consumes batch k and reads k + 1): batch k + 2
+    // goes into its slot, batch k + 2 + kDetNB is requested into the freed entry
     for (int64_t k = 0; k < nbp; k += kDetNB) {
 #pragma unroll
       for (int u = 0; u < kDetNB; ++u) {
-        put(buf[(u + 1) % kDetNB], k + u + 1);
-        load(buf[(u + 1) % kDetNB], k + u + 1 + kDetNB);
+        put(buf[(u + 2) % kDetNB], k + u + 2);
+        load(buf[(u + 2) % kDetNB], k + u + 2 + kDetNB);
         lds_bar();
       }
     }
+  } else {
+    // storer: after step k's barrier, the envelopes of batch k (a bare full
+    // batch) go out, lane l rows (l / kDetCh) + RS i of channel l % kDetCh
+    AD_TPG double* eo = gptr(a.envT);
+    const unsigned col = (unsigned)(c0 + (l & (kDetCh - 1)));
+    const int rl = l / kDetCh;
+    auto flush = [&](int64_t k) {
+      const int64_t r0 = k * kDetB;
+      if (!bare || r0 + kDetB > len) return;
+      double v[kDetLd];
+#pragma unroll
+      for (int i = 0; i < kDetLd; ++i) v[i] = evr[k & 1][rl + RS * i][l & (kDetCh - 1)];
+#pragma unroll
+      for (int i = 0; i < kDetLd; ++i) eo[(r0 + rl + RS * i) * cp + col] = v[i];
+    };
+    lds_bar();
+    for (int64_t k = 0; k < nbp; ++k) {
+      if (k > 0) flush(k - 1);
+      lds_bar();
+    }
+    flush(nbp - 1);
   }
 }
 
@@ -585,20 +654,24 @@ __global__ __launch_bounds__(256) void k_vbuf_layout(double* vbuf, double* vbufC
 
 }  // namespace
 
-void launch_fxtp_eq(const FxTpEqArgs& a, hipStream_t s) {
+void launch_fxtp_eq(const FxTpEqArgs& a, bool exact, hipStream_t s) {
   if (a.len <= 0) return;
   const dim3 grid((unsigned)((a.nseg + 3) / 4), (unsigned)((a.channels + 63) / 64));
-  hipLaunchKernelGGL(k_fxtp_eq, grid, dim3(256), 0, s, a);
+  if (exact)
+    hipLaunchKernelGGL(k_fxtp_eq<true>, grid, dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL(k_fxtp_eq<false>, grid, dim3(256), 0, s, a);
 }
 
 void launch_fxtp_carry(const FxTpEqArgs& a, hipStream_t s) {
   if (a.len <= 0) return;
-  hipLaunchKernelGGL(k_fxtp_carry, dim3((unsigned)((a.channels + 63) / 64)), dim3(64 * kCyW), 0, s, a);
+  // the host keeps nseg <= kFxTpMaxSeg (one thread per segment)
+  hipLaunchKernelGGL(k_fxtp_carry, dim3((unsigned)a.channels), dim3(kFxTpMaxSeg), 0, s, a);
 }
 
 void launch_fxtp_det(const FxStageArgs& a, hipStream_t s) {
   if (a.len <= 0) return;
-  hipLaunchKernelGGL(k_fxtp_det, dim3((unsigned)((a.channels + kDetCh - 1) / kDetCh)), dim3(128), 0, s, a);
+  hipLaunchKernelGGL(k_fxtp_det, dim3((unsigned)((a.channels + kDetCh - 1) / kDetCh)), dim3(192), 0, s, a);
 }
 
 void launch_fxtp_verb(const FxStageArgs& a, const double* xC, int64_t xstride, double* vbufC, double* coC, int wu,

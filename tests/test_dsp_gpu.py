@@ -356,6 +356,50 @@ def test_staged_engine_matches_fused(gpu, case):
             assert np.allclose(m[3], m[2], rtol=1e-11, atol=0), (c, m)
 
 
+@pytest.mark.parametrize("chunk", [0, 4096])
+def test_time_parallel_per_channel_eq(gpu, chunk):
+    """The time-parallel engine with a coefficient table per channel
+    (ad_fx_chain_set_eq per_channel = 1: one set of segment maps per channel
+    in K_carry) against the fused kernels: <= 1e-12 relative RMS, over a full
+    65536-sample chunk (256 segments, every scan step) and a partial one
+    (chunk 0 = the engine's default), or 4096-sample chunks; then a
+    coefficient update with the same section count keeps the state (the maps
+    are rebuilt)."""
+    import ctypes as Cc
+
+    from algodsp._lib import lib
+    from algodsp.processors import section_table
+
+    fs = 48000.0
+    C, n = 70, 70000
+    comp = {"auto_makeup": 0, "makeup_db": 0.0}
+    verb = (0.3, 0.8, 0.8, 0.3, 0.02)
+    x = np.stack([0.5 * signals.white_noise(n, 4100 + c) for c in range(C)])
+
+    def table(scale):
+        tabs = []
+        for c in range(C):
+            eq = design.config5_eq(fs * (1.0 + scale * 0.01 * (c % 7)))
+            tabs.append(np.concatenate([section_table(co, g) for co, g in eq]))
+        return np.ascontiguousarray(np.stack(tabs))
+
+    outs = {}
+    for eng in ("tp", "0"):
+        fx = P.EffectChain(C, (), comp, verb, fs)
+        t = table(1.0)
+        assert lib().ad_fx_chain_set_eq(fx._h, t.ctypes.data_as(Cc.POINTER(Cc.c_double)), t.shape[1], 1) == 0
+        fx.SetEngine(P.EffectChain.ENGINE_AUTO if eng == "tp" else P.EffectChain.ENGINE_FUSED, chunk)
+        y = x.copy()
+        a, b = y[:, :66000].copy(), y[:, 66000:].copy()
+        fx.Process(a)
+        t = table(2.0)
+        assert lib().ad_fx_chain_set_eq(fx._h, t.ctypes.data_as(Cc.POINTER(Cc.c_double)), t.shape[1], 1) == 0
+        fx.Process(b)
+        outs[eng] = np.concatenate([a, b], axis=1)
+    a, b = outs["tp"], outs["0"]
+    assert rms(a, b) <= 1e-12 * max(1.0, float(np.sqrt(np.mean(b ** 2)))), rms(a, b)
+
+
 # ------------------------------------------------------------------ FIR
 @pytest.mark.parametrize("taps", [1, 5, 31, 32, 64, 257])
 def test_fir_vs_oracle(gpu, taps):

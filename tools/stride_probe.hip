@@ -81,16 +81,31 @@ int main() {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  for (long Ns : {1L, 256L, 65536L}) {
-    run<256, 16, 256>(in, out, N, Ns, e0, e1);   // today's radix-256 pass
-    run<256, 16, 512>(in, out, N, Ns, e0, e1);
-    run<256, 32, 512>(in, out, N, Ns, e0, e1);
-    run<128, 32, 256>(in, out, N, Ns, e0, e1);
-    run<128, 64, 512>(in, out, N, Ns, e0, e1);
-    run<64, 64, 256>(in, out, N, Ns, e0, e1);
-    run<64, 128, 512>(in, out, N, Ns, e0, e1);
-    run<512, 8, 256>(in, out, N, Ns, e0, e1);
-    run<4096, 1, 256>(in, out, N, Ns, e0, e1);
+  // Ns must stay <= N / R (the last pass of a plan has Ns = N / R)
+  const bool two_pass = std::getenv("PROBE_TWO_PASS") != nullptr;
+  if (!two_pass) {
+    for (long Ns : {1L, 256L, 65536L}) {
+      run<256, 16, 256>(in, out, N, Ns, e0, e1);  // today's radix-256 pass
+      run<256, 16, 512>(in, out, N, Ns, e0, e1);
+      run<256, 32, 512>(in, out, N, Ns, e0, e1);
+      run<128, 32, 256>(in, out, N, Ns, e0, e1);
+      run<128, 64, 512>(in, out, N, Ns, e0, e1);
+      run<64, 64, 256>(in, out, N, Ns, e0, e1);
+      run<64, 128, 512>(in, out, N, Ns, e0, e1);
+      run<512, 8, 256>(in, out, N, Ns, e0, e1);
+    }
+  } else {
+    // a two-pass 4096 x 4096 plan: both passes read runs of F values
+    for (long Ns : {1L, 4096L}) {
+      run<4096, 1, 256>(in, out, N, Ns, e0, e1);
+      run<4096, 2, 512>(in, out, N, Ns, e0, e1);
+      run<4096, 4, 1024>(in, out, N, Ns, e0, e1);
+      run<4096, 8, 1024>(in, out, N, Ns, e0, e1);
+    }
+    for (long Ns : {1L, 8192L}) {
+      run<2048, 4, 512>(in, out, N, Ns, e0, e1);
+      run<2048, 8, 1024>(in, out, N, Ns, e0, e1);
+    }
   }
   return 0;
 }
