@@ -356,15 +356,16 @@ def test_staged_engine_matches_fused(gpu, case):
             assert np.allclose(m[3], m[2], rtol=1e-11, atol=0), (c, m)
 
 
-@pytest.mark.parametrize("chunk", [0, 4096])
-def test_time_parallel_per_channel_eq(gpu, chunk):
+@pytest.mark.parametrize("chunk,nsec", [(0, 5), (4096, 5), (0, 8), (4096, 8), (0, 1)])
+def test_time_parallel_per_channel_eq(gpu, chunk, nsec):
     """The time-parallel engine with a coefficient table per channel
     (ad_fx_chain_set_eq per_channel = 1: one set of segment maps per channel
     in K_carry) against the fused kernels: <= 1e-12 relative RMS, over a full
     65536-sample chunk (256 segments, every scan step) and a partial one
-    (chunk 0 = the engine's default), or 4096-sample chunks; then a
-    coefficient update with the same section count keeps the state (the maps
-    are rebuilt)."""
+    (chunk 0 = the engine's default), or 4096-sample chunks; 1, 5 (config 5)
+    and 8 (the most a pass takes) sections, a 20 Hz highpass among them and a
+    chain gain != 1; then a coefficient update with the same section count
+    keeps the state (the maps are rebuilt)."""
     import ctypes as Cc
 
     from algodsp._lib import lib
@@ -379,8 +380,13 @@ def test_time_parallel_per_channel_eq(gpu, chunk):
     def table(scale):
         tabs = []
         for c in range(C):
-            eq = design.config5_eq(fs * (1.0 + scale * 0.01 * (c % 7)))
-            tabs.append(np.concatenate([section_table(co, g) for co, g in eq]))
+            f = fs * (1.0 + scale * 0.01 * (c % 7))
+            secs = [co[0] for co, _ in design.config5_eq(f)]
+            secs += [design.peak(300.0, 4.0, 2.0, f), design.highpass(20.0, 0.707, f),
+                     design.low_shelf(60.0, 6.0, 0.707, f)]
+            if nsec == 1:
+                secs = [design.highpass(40.0, 0.707, f)]
+            tabs.append(section_table(np.array(secs[:nsec]), 0.8))
         return np.ascontiguousarray(np.stack(tabs))
 
     outs = {}
