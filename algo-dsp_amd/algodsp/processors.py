@@ -63,7 +63,7 @@ class _FxChain:
 
     # engine selection (include/algodsp.h ad_fx_chain_set_engine); results are
     # identical in every engine
-    ENGINE_AUTO, ENGINE_FUSED, ENGINE_STAGED_NOSPLIT, ENGINE_STAGED = 0, 1, 2, 3
+    ENGINE_AUTO, ENGINE_FUSED, ENGINE_STAGED_NOSPLIT, ENGINE_STAGED, ENGINE_TIME_PARALLEL = 0, 1, 2, 3, 4
 
     def SetEngine(self, engine: int, chunk: int = 0):
         check(lib().ad_fx_chain_set_engine(self._h, int(engine), int(chunk)))

@@ -609,7 +609,7 @@ void fx_run_tp(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hipStre
         launch_fx_gain(a, true, sv);
     } else {
       AD_HIP(hipStreamWaitEvent(sv, h->ev[EE][k], 0));
-      launch_fx_transpose_out(a, a.vT, sv);  // (not reached: the engine runs with a compressor)
+      launch_fx_transpose_out(a, a.vT, sv);  // an EQ-only chain (AD_FX_ENGINE_TIME_PARALLEL)
     }
     AD_HIP(hipEventRecord(h->ev[EA][k], sv));
   }
@@ -620,15 +620,17 @@ void fx_run_tp(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hipStre
 void fx_run(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hipStream_t s) {
   if (n <= 0) return;
   if (!h->ev_last) AD_HIP(hipEventCreateWithFlags(&h->ev_last, hipEventDisableTiming));
-  const bool tp = fx_staged_ok(h) && h->engine == AD_FX_ENGINE_AUTO && h->comp_on;
+  // time-parallel: by default where the chain is already a tolerance (the
+  // compressor's log2 / exp2); on request for an EQ-only chain
+  // (its reverb input would need the compressor's channel-major output)
+  const bool tp_ok = fx_staged_ok(h) && (h->comp_on || (h->nsec > 0 && !h->verb_on));
+  const bool tp = tp_ok && ((h->engine == AD_FX_ENGINE_AUTO && h->comp_on) || h->engine == AD_FX_ENGINE_TIME_PARALLEL);
   if (h->verb_on && h->verb_cm && !tp) {  // the delay lines back into vbuf's layout
     launch_vbuf_layout(h->vbuf.p, h->vbufC.p, h->cpad, h->channels, false, s);
     h->verb_cm = false;
   }
   if (fx_staged_ok(h)) {
-    // time-parallel where the chain is already a tolerance (the compressor's
-    // log2 / exp2): its EQ segments start from chained states, so
-    // an EQ-only chain keeps the staged engine and stays bit-exact
+    // an EQ-only chain keeps the staged engine (bit-exact) unless asked
     if (tp)
       fx_run_tp(h, d_buf, stride, n, s);
     else
@@ -906,7 +908,7 @@ int ad_fx_chain_set_eq_state(ad_fx_chain* h, const double* state, int64_t n) {
 
 int ad_fx_chain_set_engine(ad_fx_chain* h, int engine, int64_t chunk) {
   return fx_guard(h, [&] {
-    if (engine < AD_FX_ENGINE_AUTO || engine > AD_FX_ENGINE_STAGED)
+    if (engine < AD_FX_ENGINE_AUTO || engine > AD_FX_ENGINE_TIME_PARALLEL)
       AD_FAIL(AD_ERR_INVALID_ARGUMENT, "unknown effect-chain engine");
     if (chunk != 0 && chunk < 256) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "staged chunk must be 0 (default) or >= 256");
     fx_quiesce(h);

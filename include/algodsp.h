@@ -349,21 +349,31 @@ int ad_fx_chain_eq_state(ad_fx_chain* h, double* state, int64_t cap);
  * states[i] for every section).  With ad_fx_chain_eq_state this is the
  * reference's checkpoint / resume surface for the EQ.                       */
 int ad_fx_chain_set_eq_state(ad_fx_chain* h, const double* state, int64_t n);
-/* Which engine runs the chain (results are identical in every engine):
- *   AUTO            the staged engine (stage kernels over time chunks on three
- *                   streams, fx_staged.hip) where it applies -- feed-forward
- *                   dynamics, <= 8 EQ sections, <= 8192 channels with
- *                   Freeverb -- with the EQ split over two CUs when a
- *                   compressor and >= 3 sections are on; else FUSED;
+/* Which engine runs the chain:
+ *   AUTO            with a compressor, the time-parallel engine (below);
+ *                   otherwise the staged engine (stage kernels over time
+ *                   chunks on three streams, fx_staged.hip) where it applies
+ *                   -- feed-forward dynamics, <= 8 EQ sections, <= 8192
+ *                   channels with Freeverb -- with the EQ split over two CUs
+ *                   when >= 3 sections are on; else FUSED;
  *   FUSED           the fused per-sample kernels (dsp_kernels.hip k_chain*);
  *   STAGED_NOSPLIT  staged, one EQ pipeline per channel group;
- *   STAGED          staged with the split EQ stage (AUTO's engine before the
- *                   time-parallel one).
- * chunk: samples per staged chunk (0: 16384; otherwise >= 256).           */
+ *   STAGED          staged with the split EQ stage;
+ *   TIME_PARALLEL   the time-parallel engine (fx_tp.hip) also for an EQ-only
+ *                   chain (EQ, or EQ + compressor, + Freeverb only with a
+ *                   compressor; otherwise as AUTO).
+ * FUSED, STAGED_NOSPLIT and STAGED perform the reference's operations in its
+ * order: their outputs are identical.  The time-parallel engine starts the
+ * EQ's time segments from chained states (double-double): its outputs are
+ * within ~1e-12 relative RMS of those (the serial recurrence's own rounding
+ * noise for low-frequency sections), not bit-identical.
+ * chunk: samples per staged / time-parallel chunk (0: the engine's default;
+ * otherwise >= 256).                                                         */
 #define AD_FX_ENGINE_AUTO 0
 #define AD_FX_ENGINE_FUSED 1
 #define AD_FX_ENGINE_STAGED_NOSPLIT 2
 #define AD_FX_ENGINE_STAGED 3
+#define AD_FX_ENGINE_TIME_PARALLEL 4
 int ad_fx_chain_set_engine(ad_fx_chain* h, int engine, int64_t chunk);
 /* Per-wave clock counters (s_memtime ticks) of the first chunk of each call,
  * for profiling the serial stages: {compute, barrier wait} pairs per wave. */

@@ -406,6 +406,44 @@ def test_time_parallel_per_channel_eq(gpu, chunk, nsec):
     assert rms(a, b) <= 1e-12 * max(1.0, float(np.sqrt(np.mean(b ** 2)))), rms(a, b)
 
 
+@pytest.mark.parametrize("what", ["eq", "eq+comp", "verb"])
+def test_time_parallel_engine_on_request(gpu, what):
+    """AD_FX_ENGINE_TIME_PARALLEL runs an EQ-only chain (and EQ + compressor)
+    on the time-parallel engine: outputs within 1e-12 relative RMS of the
+    fused kernels and EQ end states within the serial recurrence's noise,
+    over a full 65536-sample chunk and a partial one; a Freeverb chain
+    without a compressor stays on the staged engine (identical outputs)."""
+    fs = 48000.0
+    eq = design.config5_eq(fs) if what != "verb" else ()
+    comp = {"auto_makeup": 0, "makeup_db": 0.0} if what == "eq+comp" else None
+    verb = (0.3, 0.8, 0.8, 0.3, 0.02) if what == "verb" else None
+    C, n = 70, 70000
+    x = np.stack([0.5 * signals.white_noise(n, 5100 + c) for c in range(C)])
+    outs, states = {}, {}
+    for eng in (P.EffectChain.ENGINE_TIME_PARALLEL, P.EffectChain.ENGINE_FUSED):
+        fx = P.EffectChain(C, eq, comp, verb, fs)
+        fx.SetEngine(eng)
+        y = x.copy()
+        a, b = y[:, :66000].copy(), y[:, 66000:].copy()
+        fx.Process(a)
+        fx.Process(b)
+        outs[eng] = np.concatenate([a, b], axis=1)
+        if eq:
+            from algodsp._lib import lib
+            import ctypes as Cc
+
+            st = np.zeros(C * len(eq) * 2)
+            assert lib().ad_fx_chain_eq_state(fx._h, st.ctypes.data_as(Cc.POINTER(Cc.c_double)), st.size) == 0
+            states[eng] = st
+    a, b = outs[P.EffectChain.ENGINE_TIME_PARALLEL], outs[P.EffectChain.ENGINE_FUSED]
+    if what == "verb":
+        assert np.array_equal(a, b)
+    else:
+        assert rms(a, b) <= 1e-12 * max(1.0, float(np.sqrt(np.mean(b ** 2)))), rms(a, b)
+        sa, sb = states[P.EffectChain.ENGINE_TIME_PARALLEL], states[P.EffectChain.ENGINE_FUSED]
+        assert np.max(np.abs(sa - sb)) <= 1e-11 * max(1.0, float(np.max(np.abs(sb)))), np.max(np.abs(sa - sb))
+
+
 # ------------------------------------------------------------------ FIR
 @pytest.mark.parametrize("taps", [1, 5, 31, 32, 64, 257])
 def test_fir_vs_oracle(gpu, taps):
