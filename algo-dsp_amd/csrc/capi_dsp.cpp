@@ -509,7 +509,7 @@ void fx_run_tp(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hipStre
     AD_HIP(hipEventCreateWithFlags(&h->ev_in, hipEventDisableTiming));
   }
   if (T > h->tmax || !h->xT[0].p || (eq && !h->vT[0].p) || (comp && !h->envT[0].p) ||
-      (comp && verb && (!h->inC[0].p || !h->coC.p)) ||
+      (comp && verb && !h->inC[0].p) || (verb && !h->coC.p) ||
       (eq && h->tp_zs.n < (size_t)kFxTpMaxSeg * h->nsec * h->cpad * 2)) {  // (re)size once no stage is running
     for (hipStream_t x : h->st) AD_HIP(hipStreamSynchronize(x));
     AD_HIP(hipStreamSynchronize(s));
@@ -520,7 +520,7 @@ void fx_run_tp(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hipStre
       if (comp) h->envT[k].alloc(r);
       if (comp && verb) h->inC[k].alloc(r);
     }
-    if (comp && verb) h->coC.alloc((size_t)h->channels * kVerbCombs * kFxVerbSB);
+    if (verb) h->coC.alloc((size_t)h->channels * kVerbCombs * kFxVerbSB);
     if (eq) {
       h->tp_zs.alloc((size_t)kFxTpMaxSeg * h->nsec * h->cpad * 2);
       h->tp_carry.alloc((size_t)kFxTpMaxSeg * h->nsec * h->cpad * 4);
@@ -568,7 +568,7 @@ void fx_run_tp(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hipStre
     a.vs = h->vs.p;
     a.vbuf = h->vbuf.p;
     if (i >= kFxSlots) AD_HIP(hipStreamWaitEvent(s, h->ev[EA][k], 0));  // slot k consumed
-    launch_fx_transpose_in(a, a.xT, s);
+    if (eq || comp) launch_fx_transpose_in(a, a.xT, s);  // the rows the EQ / the detector read
     if (eq) {
       FxTpEqArgs e{};
       e.channels = h->channels;
@@ -607,9 +607,10 @@ void fx_run_tp(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hipStre
         launch_fxtp_verb(a, h->inC[k].p, h->tmax, h->vbufC.p, h->coC.p, wu, sv);
       else
         launch_fx_gain(a, true, sv);
-    } else {
+    } else {  // no compressor (AD_FX_ENGINE_TIME_PARALLEL): the EQ output back, then Freeverb in place
       AD_HIP(hipStreamWaitEvent(sv, h->ev[EE][k], 0));
-      launch_fx_transpose_out(a, a.vT, sv);  // an EQ-only chain (AD_FX_ENGINE_TIME_PARALLEL)
+      if (eq) launch_fx_transpose_out(a, a.vT, sv);
+      if (verb) launch_fxtp_verb(a, a.buf, a.stride, h->vbufC.p, h->coC.p, wu, sv);
     }
     AD_HIP(hipEventRecord(h->ev[EA][k], sv));
   }
@@ -621,9 +622,8 @@ void fx_run(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hipStream_
   if (n <= 0) return;
   if (!h->ev_last) AD_HIP(hipEventCreateWithFlags(&h->ev_last, hipEventDisableTiming));
   // time-parallel: by default where the chain is already a tolerance (the
-  // compressor's log2 / exp2); on request for an EQ-only chain
-  // (its reverb input would need the compressor's channel-major output)
-  const bool tp_ok = fx_staged_ok(h) && (h->comp_on || (h->nsec > 0 && !h->verb_on));
+  // compressor's log2 / exp2); on request for any other chain
+  const bool tp_ok = fx_staged_ok(h) && (h->comp_on || h->nsec > 0 || h->verb_on);
   const bool tp = tp_ok && ((h->engine == AD_FX_ENGINE_AUTO && h->comp_on) || h->engine == AD_FX_ENGINE_TIME_PARALLEL);
   if (h->verb_on && h->verb_cm && !tp) {  // the delay lines back into vbuf's layout
     launch_vbuf_layout(h->vbuf.p, h->vbufC.p, h->cpad, h->channels, false, s);
