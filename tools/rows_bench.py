@@ -226,17 +226,21 @@ def main():
                             "not by HBM; 16 B/sample is the in+out stream"))
             fx.close()
         # the time-parallel engine on request (AD_FX_ENGINE_TIME_PARALLEL): the
-        # EQ-only chain within 1e-12 of the serial recurrence instead of bit-exact
+        # EQ-only and Freeverb-only chains within 1e-12 of the serial recurrences
+        # instead of bit-exact
         if chn == 256:
-            fx = processors.EffectChain(chn, sample_rate=fs, eq=eq)
-            fx.SetEngine(processors.EffectChain.ENGINE_TIME_PARALLEL)
-            ms = dev_time(lambda s: fx.process_device(xb.data_ptr(), n, n, s), reps=3, warm=1)
-            cs = cpu_time(cpu_eq, budget_s=1.0)
-            rows.append(row("a12-a14 (time-parallel)", procs[0][1], f"{chn} ch x {n} samples (time-parallel engine, "
-                            "<= 1e-12 relative of the serial recurrence)", chn * n, "samples", ms, cs, nc,
-                            f"{procs[0][4]}, 1 x {nc} samples", "hbm", 16.0 * chn * n,
-                            "two passes over the chunk plus a per-channel scan; 16 B/sample is the in+out stream"))
-            fx.close()
+            for pi, note in ((0, "two passes over the chunk plus a per-channel scan"),
+                             (2, "one channel per CU, its delay lines in LDS")):
+                name, ref, kw, cfn, cdesc = procs[pi]
+                fx = processors.EffectChain(chn, sample_rate=fs, **kw)
+                fx.SetEngine(processors.EffectChain.ENGINE_TIME_PARALLEL)
+                ms = dev_time(lambda s: fx.process_device(xb.data_ptr(), n, n, s), reps=3, warm=1)
+                cs = cpu_time(cfn, budget_s=1.0)
+                rows.append(row(f"{name} (time-parallel)", ref, f"{chn} ch x {n} samples (time-parallel engine, "
+                                "<= 1e-12 relative of the serial recurrence)", chn * n, "samples", ms, cs, nc,
+                                f"{cdesc}, 1 x {nc} samples", "hbm", 16.0 * chn * n,
+                                f"{note}; 16 B/sample is the in+out stream"))
+                fx.close()
         del xb
 
     # ---- config 5: the fused effect chain ------------------------------------
