@@ -125,6 +125,9 @@ void parallel_for(int64_t n, const std::function<void(int64_t)>& fn, int workers
 }
 
 HostPin::HostPin(const void* ptr, size_t bytes, size_t min_bytes) {
+#ifdef AD_HOSTPIN_OFF  // tools/ A/B builds only
+  return;
+#endif
   if (!ptr || bytes < min_bytes) return;
   if (hipHostRegister(const_cast<void*>(ptr), bytes, hipHostRegisterDefault) != hipSuccess) {
     (void)hipGetLastError();

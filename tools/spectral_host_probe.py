@@ -7,9 +7,21 @@ import time
 
 import numpy as np
 
+if "--torch-first" in sys.argv:  # torch's HIP runtime loaded before the library (rows_bench, bench.py)
+    import torch  # noqa: F401
+
+    if "--init" in sys.argv:
+        torch.cuda.set_device(0)
+
 ROOT = pathlib.Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "algo-dsp_amd"))
 from algodsp import conv, signals  # noqa: E402
+
+if "--torch" in sys.argv:  # the rows_bench process state: torch's HIP runtime initialised first
+    import torch
+
+    torch.cuda.set_device(0)
+    torch.zeros(1, device="cuda")
 
 n = 1 << 22
 hi = signals.white_noise(4096, 43)
