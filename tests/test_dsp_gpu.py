@@ -447,6 +447,30 @@ def test_time_parallel_engine_on_request(gpu, what):
         assert np.max(np.abs(sa - sb)) <= 1e-11 * max(1.0, float(np.max(np.abs(sb)))), np.max(np.abs(sa - sb))
 
 
+@pytest.mark.parametrize("C,n", [(1, 5000), (3, 257), (65, 64), (2, 1)])
+def test_time_parallel_small_shapes(gpu, C, n):
+    """The time-parallel engine at edge shapes -- one channel, a ragged
+    channel group, one segment (len <= 64), a one-sample call -- against the
+    fused kernels (config-5 chain, then two more calls continuing the state)."""
+    fs = 48000.0
+    eq = design.config5_eq(fs)
+    comp = {"auto_makeup": 0, "makeup_db": 0.0}
+    verb = (0.3, 0.8, 0.8, 0.3, 0.02)
+    x = np.stack([0.5 * signals.white_noise(3 * n, 6100 + c) for c in range(C)])
+    outs = {}
+    for eng in (P.EffectChain.ENGINE_AUTO, P.EffectChain.ENGINE_FUSED):
+        fx = P.EffectChain(C, eq, comp, verb, fs)
+        fx.SetEngine(eng)
+        parts = []
+        for k in range(3):
+            b = x[:, k * n:(k + 1) * n].copy()
+            fx.Process(b)
+            parts.append(b)
+        outs[eng] = np.concatenate(parts, axis=1)
+    a, b = outs[P.EffectChain.ENGINE_AUTO], outs[P.EffectChain.ENGINE_FUSED]
+    assert rms(a, b) <= 1e-12 * max(1.0, float(np.sqrt(np.mean(b ** 2)))), rms(a, b)
+
+
 # ------------------------------------------------------------------ FIR
 @pytest.mark.parametrize("taps", [1, 5, 31, 32, 64, 257])
 def test_fir_vs_oracle(gpu, taps):

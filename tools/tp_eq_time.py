@@ -12,8 +12,14 @@ from algodsp import design, processors as P  # noqa: E402
 fs = 48000.0
 C, n = 256, 1 << 20
 x = torch.randn(C, n, dtype=torch.float64, device="cuda") * 0.3
-for name, kw in (("eq", dict(eq=design.config5_eq(fs))), ("freeverb", dict(freeverb=(0.22, 1.0, 0.72, 0.45, 0.015)))):
-    for eng in (P.EffectChain.ENGINE_AUTO, P.EffectChain.ENGINE_TIME_PARALLEL):
+comp = {"auto_makeup": 0, "makeup_db": 0.0}
+names = {P.EffectChain.ENGINE_AUTO: "auto", P.EffectChain.ENGINE_STAGED: "staged",
+         P.EffectChain.ENGINE_TIME_PARALLEL: "time-parallel"}
+for name, kw in (("eq", dict(eq=design.config5_eq(fs))), ("freeverb", dict(freeverb=(0.22, 1.0, 0.72, 0.45, 0.015))),
+                 ("compressor", dict(compressor=comp))):
+    engines = ((P.EffectChain.ENGINE_STAGED, P.EffectChain.ENGINE_TIME_PARALLEL) if name == "compressor"
+               else (P.EffectChain.ENGINE_AUTO, P.EffectChain.ENGINE_TIME_PARALLEL))
+    for eng in engines:
         fx = P.EffectChain(C, sample_rate=fs, **kw)
         fx.SetEngine(eng)
         s = torch.cuda.current_stream()
@@ -24,5 +30,5 @@ for name, kw in (("eq", dict(eq=design.config5_eq(fs))), ("freeverb", dict(freev
             fx.process_device(x.data_ptr(), n, n, s.cuda_stream)
         s.synchronize()
         dt = (time.perf_counter() - t) / 3
-        print(name, "time-parallel" if eng else "auto", f"{C * n / dt / 1e9:.2f} Gsamples/s", f"{dt * 1e3:.2f} ms")
+        print(name, names[eng], f"{C * n / dt / 1e9:.2f} Gsamples/s", f"{dt * 1e3:.2f} ms")
         fx.close()
