@@ -402,7 +402,7 @@ void fx_run_staged(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hip
 // i-2's reverb.  A slot is reused only after st[1] is done with it (the
 // detector and the gain precede st[1]'s work on every chunk).
 #ifndef AD_FX_TP_CHUNK  // tools/ A/B builds only
-#define AD_FX_TP_CHUNK 65536  // 16384: 7.13, 32768: 8.21, 65536: 8.93, 131072: 8.69 Gsamples/s at config 5
+#define AD_FX_TP_CHUNK 65536  // config 5 (tools/fx_chunk_sweep.py): 32768 10.89, 65536 11.09, 131072 11.06, 262144 10.67 Gsamples/s
 #endif
 constexpr int64_t kFxTpChunk = AD_FX_TP_CHUNK;
 constexpr int kFxTpSeg = 64;     // K_eq segment (samples), at least
