@@ -628,6 +628,17 @@ def main_corr(args):
         dtc = time.perf_counter() - tc
         cpu = {"value": 2 * m / dtc / 1e6, "unit": "Msamples/s", "cores": 1, "kind": "port",
                "sample": f"oracle CorrelateFFT of two 2^20-sample signals (N = 2^21 radix-2); {dtc:.2f} s"}
+    # HBM bytes per call from the committed PMC passes of this same workload
+    # (tools/gpu_corr_prof.sh -> tools/pmc_call_traffic.py), max-abs included
+    traffic = None
+    tfile = ROOT / "profiles" / "corr_pmc_traffic.json"
+    if tfile.exists():
+        try:
+            tab = json.loads(tfile.read_text())
+            if tab.get("_config") == {"workload": "corr", "n": n}:
+                traffic = tab["hbm_bytes_per_call"]
+        except Exception:
+            traffic = None
     line = {
         "metric": "Msamples/sec, CorrelateFFT of two 2^23-sample signals (input samples per second)",
         "value": round(2 * n / (ms * 1e-3) / 1e6, 3), "unit": "Msamples/s", "n_gpus": 1, "steps": args.steps,
@@ -637,8 +648,10 @@ def main_corr(args):
                                f"inverse: {Ph} passes at N/2), device buffers",
                    "fft_size": N},
         "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
-                     "note": "whole call: algorithmic bytes of all passes (pointwise op and lag order fused) / event time"},
+                     "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "note": "whole call: algorithmic bytes of all passes (pointwise op and lag order fused) / event "
+                             "time; traffic = HBM bytes per call from PMC (FETCH_SIZE x2 + WRITE_SIZE, the max-abs "
+                             "pre-pass included)"},
         "cpu_baseline": cpu,
         "wall_ms_per_step": round(dt / args.steps * 1e3, 4),
     }
