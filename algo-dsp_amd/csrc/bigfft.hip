@@ -1,5 +1,12 @@
 // Device kernels of the large power-of-two FFT and the pointwise spectral
 // operations of CorrelateFFT / Deconvolve / InverseFilter (see bigfft.hpp).
+// Pass outputs are stored non-temporally (1; a whole pass's output, 268-537 MB
+// at 2^24 points, overflows the Infinity Cache before the next pass reads it):
+// CorrelateFFT 0.670 -> 0.641-0.652 ms.  2 (tools/ A/B): non-temporal pass
+// inputs too (no better).
+#ifndef AD_FFT_NT
+#define AD_FFT_NT 1
+#endif
 #include "bigfft.hpp"
 
 #include <algorithm>
@@ -262,7 +269,13 @@ __global__ __launch_bounds__((PassShape<R>::BLOCK)) void k_fft_pass(FftPassArgs 
       } else if constexpr (HALF != 0) {
         v = half_in(g);
       } else {
+#if AD_FFT_NT >= 2
+        typedef double d2v __attribute__((ext_vector_type(2)));
+        const d2v t = __builtin_nontemporal_load(reinterpret_cast<const d2v*>(a.in + bt * a.in_batch + g));
+        v = make_double2(t.x, t.y);
+#else
         v = a.in[bt * a.in_batch + g];
+#endif
       }
     }
     lds_all[jj * MP + lds_slot(r)] = v;
@@ -353,7 +366,12 @@ __global__ __launch_bounds__((PassShape<R>::BLOCK)) void k_fft_pass(FftPassArgs 
         emit(o, val.x);
       }
     } else {
+#if AD_FFT_NT  // non-temporal pass outputs (AD_FFT_NT above)
+      typedef double d2v __attribute__((ext_vector_type(2)));
+      __builtin_nontemporal_store(d2v{val.x, val.y}, reinterpret_cast<d2v*>(a.out + bt * a.out_batch + o));
+#else
       a.out[bt * a.out_batch + o] = val;
+#endif
     }
   }
 }
