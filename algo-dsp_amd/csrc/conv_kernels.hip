@@ -214,7 +214,12 @@ struct ZEpilogue {
     const double2 z = make_double2(fma(-tw.x, sy, fma(-tw.y, sdx, sx * S)), fma(-tw.y, sy, fma(tw.x, sdx, S * sdy)));
     double2* zp = (zb + j * jstride) + zo;
     if constexpr (FIRST) {
+#ifdef AD_K2_NT  // tools/ A/B builds only
+      typedef double d2v __attribute__((ext_vector_type(2)));
+      __builtin_nontemporal_store(d2v{z.x, z.y}, reinterpret_cast<d2v*>(zp));
+#else
       *zp = z;
+#endif
     } else {
       const double2 o = *zp;
       *zp = make_double2(o.x + z.x, o.y + z.y);
