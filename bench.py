@@ -91,7 +91,7 @@ def launch_ranks(n: int) -> int:
 
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(ROOT / "bench.py")] + sys.argv[1:]
-    return subprocess.call(cmd)
+    return subprocess.call(cmd, stdout=sys.stdout)  # the JSON channel, not the fd-1 banner sink
 
 
 def host_cores() -> int:
@@ -781,4 +781,10 @@ def main_fx(args):
 
 
 if __name__ == "__main__":
+    # stdout carries exactly one JSON line: native libraries that print to
+    # fd 1 (RCCL's version banner at comm init) are sent to stderr, and
+    # Python's stdout keeps a private duplicate of the original fd 1.
+    sys.stdout.flush()
+    sys.stdout = os.fdopen(os.dup(1), "w", buffering=1)
+    os.dup2(2, 1)
     sys.exit(main() or 0)
