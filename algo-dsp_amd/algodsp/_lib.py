@@ -214,6 +214,7 @@ def _declare(L: C.CDLL) -> None:
         "ad_fx_chain_eq_state": (C.c_int, [vp, c_double_p, i64]),
         "ad_fx_chain_set_eq_state": (C.c_int, [vp, c_double_p, i64]),
         "ad_fx_chain_set_engine": (C.c_int, [vp, C.c_int, i64]),
+        "ad_fx_chain_last_engine": (C.c_int, [vp, C.POINTER(C.c_int), C.POINTER(C.c_double)]),
         "ad_fx_chain_set_profiling": (C.c_int, [vp, C.c_int]),
         "ad_fx_chain_read_profile": (C.c_int, [vp, C.POINTER(C.c_ulonglong), C.c_int, C.POINTER(C.c_int)]),
         "ad_fx_chain_destroy": (None, [vp]),

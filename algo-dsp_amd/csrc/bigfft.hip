@@ -77,18 +77,38 @@ __device__ __forceinline__ double2 spec_op(int op, double2 x, double2 h, double 
 }
 #pragma clang fp contract(fast)  // the HIP default again for the transforms below
 
-// The packing scale of a CorrelateFFT (FftPassArgs::amax): 2^e with
-// e = exponent(max|a|) - exponent(max|b|) (inv: 2^-e); 1 when either maximum
-// is zero or not finite.  A power of two, so scaling by it is exact.
-__device__ __forceinline__ double pack_scale(const unsigned long long* amax, bool inv) {
-  if (!amax) return 1.0;
+// The packing scales of a CorrelateFFT (FftPassArgs::amax): both signals are
+// normalised before they share one transform, a' = a 2^-ea, b' = b 2^-eb with
+// ea, eb = the exponents of max|a|, max|b| (clamped to [-1000, 1000] so every
+// factor is a normal power of two), and the output is scaled back by
+// 2^(ea + eb), applied as two factors when the sum leaves [-1000, 1000] (the
+// result itself is then near the double range's ends, as the reference's is).
+// All 1 when either maximum is zero or not finite.  Powers of two, so in the
+// normal range the scaling is exact and the result is that of the unscaled
+// transform; without it an |a| / |b| of 2^1000 made 2^e or 2^-e overflow.
+struct PackScale {
+  double a = 1.0, b = 1.0, o1 = 1.0, o2 = 1.0;
+};
+__device__ __forceinline__ PackScale pack_scale(const unsigned long long* amax) {
+  PackScale p;
+  if (!amax) return p;
   const double ma = __longlong_as_double((long long)amax[0]), mb = __longlong_as_double((long long)amax[1]);
-  if (!(ma > 0.0) || !(mb > 0.0) || !__builtin_isfinite(ma) || !__builtin_isfinite(mb)) return 1.0;
+  if (!(ma > 0.0) || !(mb > 0.0) || !__builtin_isfinite(ma) || !__builtin_isfinite(mb)) return p;
   int ea = 0, eb = 0;
   (void)frexp(ma, &ea);
   (void)frexp(mb, &eb);
-  const int e = ea - eb;
-  return ldexp(1.0, inv ? -e : e);
+  ea = max(-1000, min(1000, ea));
+  eb = max(-1000, min(1000, eb));
+  const int e = ea + eb, e1 = e / 2;
+  p.a = ldexp(1.0, -ea);
+  p.b = ldexp(1.0, -eb);
+  if (e >= -1000 && e <= 1000) {
+    p.o1 = ldexp(1.0, e);
+  } else {
+    p.o1 = ldexp(1.0, e1);
+    p.o2 = ldexp(1.0, e - e1);
+  }
+  return p;
 }
 
 // {max|a[0..n)|, max|b[0..m)|} as bit patterns (non-negative doubles order
@@ -190,7 +210,7 @@ __global__ __launch_bounds__((PassShape<R>::BLOCK)) void k_fft_pass(FftPassArgs 
 #endif
 
   // stage in: element r of butterfly j0 + jj is x[j0 + jj + r nb]; jj fastest
-  const double bscale = REALIN ? pack_scale(a.amax, false) : 1.0;
+  const PackScale ps = REALIN ? pack_scale(a.amax) : PackScale{};
   // The half inverse's input (HALF): X[q] = op(A[q], B[q]) from the forward
   // spectrum Z = FFT(a + i b), A = (Z[q] + conj Z[-q]) / 2,
   // B = (Z[q] - conj Z[-q]) / 2i (HALF = 1: the correlation, op fixed; 2: any
@@ -261,8 +281,8 @@ __global__ __launch_bounds__((PassShape<R>::BLOCK)) void k_fft_pass(FftPassArgs 
       const int64_t g = j + (int64_t)r * nb;
       if constexpr (REALIN) {
         if (a.pack2) {
-          v.x = g < a.nr[0] ? a.xb[0][g] : 0.0;
-          v.y = g < a.nr[1] ? a.xb[1][g] * bscale : 0.0;
+          v.x = g < a.nr[0] ? a.xb[0][g] * ps.a : 0.0;
+          v.y = g < a.nr[1] ? a.xb[1][g] * ps.b : 0.0;
         } else {
           v.x = g < a.nr[bt] ? a.xb[bt][g] : 0.0;
         }
@@ -331,7 +351,8 @@ __global__ __launch_bounds__((PassShape<R>::BLOCK)) void k_fft_pass(FftPassArgs 
 
   // stage out: output rr of butterfly j goes to (j/Ns) Ns R + (j mod Ns) + rr Ns
   const int64_t Ns = a.Ns;
-  const double oscale = REALOUT ? a.scale * pack_scale(a.amax, true) : a.scale;  // powers of two: exact
+  const PackScale ops = REALOUT ? pack_scale(a.amax) : PackScale{};
+  const double oscale = a.scale * ops.o1, oscale2 = ops.o2;  // powers of two: exact
 #pragma unroll
   for (int i = 0; i < V; ++i) {
     const int idx = i * BLOCK + (int)threadIdx.x;
@@ -352,9 +373,9 @@ __global__ __launch_bounds__((PassShape<R>::BLOCK)) void k_fft_pass(FftPassArgs 
       auto emit = [&](int64_t q, double x) {
         if (a.remap) {
           if (q < a.n_front)
-            a.out_real[a.front_off + q] = x * oscale;
+            a.out_real[a.front_off + q] = x * oscale * oscale2;
           else if (q >= a.back_from)
-            a.out_real[q - a.back_from] = x * oscale;
+            a.out_real[q - a.back_from] = x * oscale * oscale2;
         } else {
           a.out_real[bt * a.out_batch + q] = x * a.scale;
         }

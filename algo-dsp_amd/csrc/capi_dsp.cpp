@@ -135,7 +135,7 @@ struct ad_fx_chain {
   // K_carry's segment maps per (seg, nseg): M = A^seg and M^Q per section and
   // coefficient set, double-double [nsec][sets][2][4][2] (fx_tp_mats)
   std::vector<double> sec_host;
-  std::map<std::pair<int, int>, std::unique_ptr<DevBuf<double>>> tp_mats;
+  std::map<int, std::unique_ptr<DevBuf<double>>> tp_mats;  // by segment length
   DevBuf<double> inC[kFxSlots];  // reverb input, channel-major [cpad][tmax]
   DevBuf<double> vbufC;          // Freeverb lines channel-major [channels][kVerbLen] (K_verb)
   DevBuf<double> coC;            // K_verb comb outputs [channels][8][kFxVerbSB] (scratch, stream st[1] only)
@@ -145,6 +145,11 @@ struct ad_fx_chain {
   // the first chunk of each call (ad_fx_chain_set_profiling)
   int engine = AD_FX_ENGINE_AUTO;
   int64_t chunk = 0;  // staged chunk length (0: kFxChunk)
+  int last_engine = -1;  // the engine that ran the last call (ad_fx_chain_last_engine)
+  // the EQ's round-off noise estimate (fx_eq_noise) and whether it is small
+  // enough for the time-parallel engine to stay within the chain's 1e-12 bar
+  double eq_noise = 0.0;
+  bool tp_cond_ok = true;
   bool prof_on = false;
   DevBuf<unsigned long long> prof;
 
@@ -236,6 +241,21 @@ unsigned long long* fx_prof_begin(ad_fx_chain* h, size_t words, hipStream_t s) {
   return h->prof.p;
 }
 
+// Raise the chunk row stride tmax shared by both engines.  A buffer of either
+// engine that a raised stride would overrun is released here, so the engine
+// that next uses it reallocates it at cpad * tmax (alternating
+// engines with growing calls wrote past the other engine's buffers).
+void fx_grow_tmax(ad_fx_chain* h, int64_t t) {
+  if (t <= h->tmax) return;
+  const size_t r = (size_t)h->cpad * t;
+  for (int k = 0; k < kFxSlots; ++k) {
+    for (DevBuf<double>* b : {&h->xT[k], &h->vT[k], &h->envT[k], &h->inT[k], &h->midT[k], &h->inC[k]})
+      if (b->p && b->n < r) b->release();
+    if (h->coT[k].p && h->coT[k].n < r * kVerbCombs) h->coT[k].release();
+  }
+  h->tmax = t;
+}
+
 void fx_run_staged(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hipStream_t s) {
   const bool eq = h->nsec > 0, comp = h->comp_on, verb = h->verb_on;
   const int64_t T = std::min(h->chunk > 0 ? h->chunk : kFxChunk, n);
@@ -247,22 +267,33 @@ void fx_run_staged(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hip
   }
   const bool need_x = eq || comp, need_v = comp || (eq && !verb);
   const int s1 = fx_eq_split(h);
-  if (T > h->tmax || (need_x && !h->xT[0].p) || (need_v && !h->vT[0].p) || (comp && !h->envT[0].p) ||
-      (verb && !h->inT[0].p) || (s1 && !h->midT[0].p)) {  // (re)size the chunk buffers once no stage is running
-    for (hipStream_t x : h->st) AD_HIP(hipStreamSynchronize(x));
-    AD_HIP(hipStreamSynchronize(s));
+  {
+    // Every buffer a kernel indexes at row stride tmax must hold cpad * tmax
+    // rows: tmax is shared with the time-parallel engine, which may have
+    // raised it without sizing this engine's buffers (each buffer's own
+    // capacity is checked, not tmax).
     const size_t r = (size_t)h->cpad * std::max(T, h->tmax);
-    for (int k = 0; k < kFxSlots; ++k) {
-      if (need_x) h->xT[k].alloc(r);
-      if (need_v) h->vT[k].alloc(r);
-      if (comp) h->envT[k].alloc(r);
-      if (verb) {
-        h->inT[k].alloc(r);
-        h->coT[k].alloc(r * kVerbCombs);
+    auto shortb = [](const DevBuf<double>& b, size_t want) { return !b.p || b.n < want; };
+    bool grow = false;
+    for (int k = 0; k < kFxSlots; ++k)
+      grow = grow || (need_x && shortb(h->xT[k], r)) || (need_v && shortb(h->vT[k], r)) ||
+             (comp && shortb(h->envT[k], r)) || (verb && (shortb(h->inT[k], r) || shortb(h->coT[k], r * kVerbCombs))) ||
+             (s1 && shortb(h->midT[k], r));
+    if (grow || T > h->tmax) {  // (re)size the chunk buffers once no stage is running
+      for (hipStream_t x : h->st) AD_HIP(hipStreamSynchronize(x));
+      AD_HIP(hipStreamSynchronize(s));
+      fx_grow_tmax(h, std::max(T, h->tmax));
+      for (int k = 0; k < kFxSlots; ++k) {
+        if (need_x) h->xT[k].reserve(r);
+        if (need_v) h->vT[k].reserve(r);
+        if (comp) h->envT[k].reserve(r);
+        if (verb) {
+          h->inT[k].reserve(r);
+          h->coT[k].reserve(r * kVerbCombs);
+        }
+        if (s1) h->midT[k].reserve(r);
       }
-      if (s1) h->midT[k].alloc(r);
     }
-    h->tmax = std::max(T, h->tmax);
   }
   // stage streams: the caller's stream runs input transpose + EQ/detector +
   // gain; st[0] the combs, st[1] the allpasses (three queues in all)
@@ -395,6 +426,35 @@ void fx_run_staged(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hip
   if (verb) AD_HIP(hipStreamWaitEvent(s, h->ev[EA][k], 0));  // the last chunk's allpasses follow all work
 }
 
+// The EQ's round-off noise relative to its signal, as the time-parallel
+// engine's distance from the serial recurrence: eps sqrt(sum_k NG_k) over the
+// sections of the worst coefficient set, NG = (1 + a2) / ((1 - a2)((1 + a2)^2 -
+// a1^2)) the noise gain of a section's all-pole part (infinite for poles on or
+// outside the unit circle).  Both the serial recurrence and the chained
+// segment starts carry that noise, so the two differ by about this much:
+// tools/tp_cond.py simulates the engine's arithmetic against the oracle, e.g.
+// a 40 Hz highpass at 48 kHz (config 5) 3.5e-13 estimated vs 3.5e-13
+// simulated, 40 Hz at 96 kHz 9.9e-13 vs 1.4e-12, 10 Hz at 192 kHz 2.2e-11 vs
+// 3.7e-11 (the simulated distance runs up to 1.7x the estimate).  Past
+// kFxTpNoiseMax the chain keeps the bit-exact staged engine.
+constexpr double kFxTpNoiseMax = 4.5e-13;
+double fx_eq_noise(const std::vector<double>& tab, int sets, int nsec) {
+  typedef long double ld;
+  double worst = 0.0;
+  for (int c = 0; c < sets; ++c) {
+    ld sum = 0;
+    for (int k = 0; k < nsec; ++k) {
+      const double* g = tab.data() + ((size_t)c * nsec + k) * kSecStride;
+      const ld a1 = g[4], a2 = g[5];
+      const ld d = (1 - a2) * ((1 + a2) * (1 + a2) - a1 * a1);
+      if (!(d > 0) || !std::isfinite((double)d)) return INFINITY;  // not stable: no estimate
+      sum += (1 + a2) / d;
+    }
+    worst = std::max(worst, (double)(std::sqrt(sum) * std::ldexp(1.0L, -52)));
+  }
+  return worst;
+}
+
 // The time-parallel engine (fx_tp.hip): per chunk of T samples, the caller's
 // stream runs the input transpose and the three EQ launches (K_eqz, K_carry,
 // K_eqx); st[0] the detector (serial per channel) and the gain of that chunk;
@@ -406,6 +466,7 @@ void fx_run_staged(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hip
 #endif
 constexpr int64_t kFxTpChunk = AD_FX_TP_CHUNK;
 constexpr int kFxTpSeg = 64;     // K_eq segment (samples), at least
+constexpr size_t kFxTpMatsCached = 8;  // segment lengths whose maps stay cached
 
 // K_carry's maps for a chunk cut into nseg segments of seg samples, per
 // coefficient set (layout: fx_tp_mat_stride in dsp_kernels.hpp): the cascade's
@@ -413,10 +474,19 @@ constexpr int kFxTpSeg = 64;     // K_eq segment (samples), at least
 // input is section k-1's output), its segment map B = A^seg as 2 x 2 blocks,
 // and per section the scan maps B(k,k)^(2^i).  Computed in
 // 64-bit-mantissa long double and stored as double-double pairs.  Built once
-// per (seg, nseg) and coefficient table (a chunk length and the last chunk's).
-const double* fx_tp_mats(ad_fx_chain* h, int seg, int nseg) {
-  auto& slot = h->tp_mats[std::make_pair(seg, nseg)];
-  if (slot) return slot->p;
+// per segment length and coefficient table (the maps do not depend on the
+// segment count).
+const double* fx_tp_mats(ad_fx_chain* h, int seg, hipStream_t s) {
+  {
+    auto it = h->tp_mats.find(seg);
+    if (it != h->tp_mats.end()) return it->second->p;
+  }
+  if (h->tp_mats.size() >= kFxTpMatsCached) {  // a caller cycling through chunk lengths: drop the cache
+    for (hipStream_t x : h->st) AD_HIP(hipStreamSynchronize(x));
+    AD_HIP(hipStreamSynchronize(s));
+    h->tp_mats.clear();
+  }
+  auto& slot = h->tp_mats[seg];
   const int sets = h->eq_uniform ? 1 : h->channels, nsec = h->nsec, D = 2 * nsec;
   typedef long double ld;
   typedef std::vector<ld> mat;  // D x D row-major
@@ -508,24 +578,32 @@ void fx_run_tp(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hipStre
       for (auto& e : e2) AD_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     AD_HIP(hipEventCreateWithFlags(&h->ev_in, hipEventDisableTiming));
   }
-  if (T > h->tmax || !h->xT[0].p || (eq && !h->vT[0].p) || (comp && !h->envT[0].p) ||
-      (comp && verb && !h->inC[0].p) || (verb && !h->coC.p) ||
-      (eq && h->tp_zs.n < (size_t)kFxTpMaxSeg * h->nsec * h->cpad * 2)) {  // (re)size once no stage is running
-    for (hipStream_t x : h->st) AD_HIP(hipStreamSynchronize(x));
-    AD_HIP(hipStreamSynchronize(s));
+  {
+    // each buffer's own capacity against cpad * tmax (tmax is shared with the
+    // staged engine, which may have raised it; see fx_run_staged)
     const size_t r = (size_t)h->cpad * std::max(T, h->tmax);
-    for (int k = 0; k < kFxSlots; ++k) {
-      h->xT[k].alloc(r);
-      if (eq) h->vT[k].alloc(r);
-      if (comp) h->envT[k].alloc(r);
-      if (comp && verb) h->inC[k].alloc(r);
+    auto shortb = [](const DevBuf<double>& b, size_t want) { return !b.p || b.n < want; };
+    bool grow = (verb && shortb(h->coC, (size_t)h->channels * kVerbCombs * kFxVerbSB)) ||
+                (eq && shortb(h->tp_zs, (size_t)kFxTpMaxSeg * h->nsec * h->cpad * 2));
+    for (int k = 0; k < kFxSlots; ++k)
+      grow = grow || shortb(h->xT[k], r) || (eq && shortb(h->vT[k], r)) || (comp && shortb(h->envT[k], r)) ||
+             (comp && verb && shortb(h->inC[k], r));
+    if (grow || T > h->tmax) {  // (re)size once no stage is running
+      for (hipStream_t x : h->st) AD_HIP(hipStreamSynchronize(x));
+      AD_HIP(hipStreamSynchronize(s));
+      fx_grow_tmax(h, std::max(T, h->tmax));
+      for (int k = 0; k < kFxSlots; ++k) {
+        h->xT[k].reserve(r);
+        if (eq) h->vT[k].reserve(r);
+        if (comp) h->envT[k].reserve(r);
+        if (comp && verb) h->inC[k].reserve(r);
+      }
+      if (verb) h->coC.reserve((size_t)h->channels * kVerbCombs * kFxVerbSB);
+      if (eq) {
+        h->tp_zs.reserve((size_t)kFxTpMaxSeg * h->nsec * h->cpad * 2);
+        h->tp_carry.reserve((size_t)kFxTpMaxSeg * h->nsec * h->cpad * 4);
+      }
     }
-    if (verb) h->coC.alloc((size_t)h->channels * kVerbCombs * kFxVerbSB);
-    if (eq) {
-      h->tp_zs.alloc((size_t)kFxTpMaxSeg * h->nsec * h->cpad * 2);
-      h->tp_carry.alloc((size_t)kFxTpMaxSeg * h->nsec * h->cpad * 4);
-    }
-    h->tmax = std::max(T, h->tmax);
   }
 #ifdef AD_FX_TP_SERIAL  // tools/ builds only: every stage on the caller's stream (isolated kernel times)
   hipStream_t sd = s, sv = s;
@@ -581,7 +659,7 @@ void fx_run_tp(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hipStre
       e.eq = a.eq;
       e.zs = h->tp_zs.p;
       e.sdd = h->tp_carry.p;
-      e.mats = fx_tp_mats(h, e.seg, e.nseg);
+      e.mats = fx_tp_mats(h, e.seg, s);
       e.mat_sets = h->eq_uniform ? 1 : h->channels;
       launch_fxtp_eq(e, false, s);
       launch_fxtp_carry(e, s);
@@ -622,8 +700,11 @@ void fx_run(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hipStream_
   if (n <= 0) return;
   if (!h->ev_last) AD_HIP(hipEventCreateWithFlags(&h->ev_last, hipEventDisableTiming));
   // time-parallel: by default where the chain is already a tolerance (the
-  // compressor's log2 / exp2); on request for any other chain
-  const bool tp_ok = fx_staged_ok(h) && (h->comp_on || h->nsec > 0 || h->verb_on);
+  // compressor's log2 / exp2); on request for any other chain.
+  // Never for an EQ whose round-off noise gain would put its distance from
+  // the serial recurrence past the chain's bar (fx_eq_noise): such chains run
+  // on the staged engine, which is bit-exact.
+  const bool tp_ok = fx_staged_ok(h) && (h->comp_on || h->nsec > 0 || h->verb_on) && h->tp_cond_ok;
   const bool tp = tp_ok && ((h->engine == AD_FX_ENGINE_AUTO && h->comp_on) || h->engine == AD_FX_ENGINE_TIME_PARALLEL);
   if (h->verb_on && h->verb_cm && !tp) {  // the delay lines back into vbuf's layout
     launch_vbuf_layout(h->vbuf.p, h->vbufC.p, h->cpad, h->channels, false, s);
@@ -631,10 +712,13 @@ void fx_run(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hipStream_
   }
   if (fx_staged_ok(h)) {
     // an EQ-only chain keeps the staged engine (bit-exact) unless asked
-    if (tp)
+    if (tp) {
       fx_run_tp(h, d_buf, stride, n, s);
-    else
+      h->last_engine = AD_FX_ENGINE_TIME_PARALLEL;
+    } else {
       fx_run_staged(h, d_buf, stride, n, s);
+      h->last_engine = fx_eq_split(h) ? AD_FX_ENGINE_STAGED : AD_FX_ENGINE_STAGED_NOSPLIT;
+    }
     AD_HIP(hipEventRecord(h->ev_last, s));
     return;
   }
@@ -669,6 +753,7 @@ void fx_run(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hipStream_
   } while (s0 < h->nsec);
   AD_HIP(hipGetLastError());
   AD_HIP(hipEventRecord(h->ev_last, s));
+  h->last_engine = AD_FX_ENGINE_FUSED;
 }
 
 }  // namespace
@@ -742,6 +827,8 @@ int ad_fx_chain_set_eq(ad_fx_chain* h, const double* sections, int nsec, int per
     if (nsec > 0) AD_HIP(hipMemcpy(h->sec_dev.p, sections, h->sec_dev.n * sizeof(double), hipMemcpyHostToDevice));
     h->sec_host.assign(sections, sections + h->sec_dev.n);
     h->tp_mats.clear();
+    h->eq_noise = nsec > 0 ? fx_eq_noise(h->sec_host, per_channel ? h->channels : 1, nsec) : 0.0;
+    h->tp_cond_ok = h->eq_noise <= kFxTpNoiseMax;
     // Section state survives a coefficient update with the same section
     // count, like filterRuntime.Configure (runtime_filter_pitch_reverb.go:150-165).
     if (!keep_state || !h->eq_state.p) {
@@ -914,6 +1001,13 @@ int ad_fx_chain_set_engine(ad_fx_chain* h, int engine, int64_t chunk) {
     fx_quiesce(h);
     h->engine = engine;
     h->chunk = chunk;
+  });
+}
+
+int ad_fx_chain_last_engine(ad_fx_chain* h, int* engine, double* eq_noise) {
+  return fx_guard(h, [&] {
+    if (engine) *engine = h->last_engine;
+    if (eq_noise) *eq_noise = h->eq_noise;
   });
 }
 

@@ -124,24 +124,71 @@ void parallel_for(int64_t n, const std::function<void(int64_t)>& fn, int workers
   Pool::get().run(n, fn, workers);
 }
 
+namespace {
+// Process-wide registry of the caller ranges page-locked by calls in flight.
+// hipHostRegister is process-wide, so two threads that pass the same (or an
+// overlapping) array must not register it twice or unregister it under each
+// other's copies: a range is registered once, every call holding it takes a
+// reference, and it is unregistered when the last reference goes.  A call
+// whose range only partly overlaps a registered one does not register its own
+// (its copies stay pageable) but still holds the overlapping entries, so their
+// pages stay locked while its copies run.
+struct PinEntry {
+  uintptr_t lo, hi;
+  int refs;
+};
+std::mutex g_pin_mu;
+std::vector<PinEntry> g_pins;
+
+bool pin_acquire(const void* ptr, size_t bytes, std::vector<uintptr_t>& held) {
+  const uintptr_t lo = (uintptr_t)ptr, hi = lo + bytes;
+  std::lock_guard<std::mutex> lk(g_pin_mu);
+  bool covered = false, overlap = false;
+  for (PinEntry& e : g_pins)
+    if (e.lo < hi && lo < e.hi) {
+      overlap = true;
+      covered = covered || (e.lo <= lo && hi <= e.hi);
+      ++e.refs;
+      held.push_back(e.lo);
+    }
+  if (overlap) return covered;
+  if (hipHostRegister(const_cast<void*>(ptr), bytes, hipHostRegisterDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  g_pins.push_back(PinEntry{lo, hi, 1});
+  held.push_back(lo);
+  return true;
+}
+
+void pin_release(std::vector<uintptr_t>& held) {
+  std::lock_guard<std::mutex> lk(g_pin_mu);
+  for (uintptr_t k : held)
+    for (size_t i = 0; i < g_pins.size(); ++i)
+      if (g_pins[i].lo == k) {
+        if (--g_pins[i].refs == 0) {
+          (void)hipHostUnregister((void*)k);
+          g_pins.erase(g_pins.begin() + (ptrdiff_t)i);
+        }
+        break;
+      }
+  held.clear();
+}
+}  // namespace
+
 HostPin::HostPin(const void* ptr, size_t bytes, size_t min_bytes) {
 #ifdef AD_HOSTPIN_OFF  // tools/ A/B builds only
   return;
 #endif
   if (!ptr || bytes < min_bytes) return;
-  if (hipHostRegister(const_cast<void*>(ptr), bytes, hipHostRegisterDefault) != hipSuccess) {
-    (void)hipGetLastError();
-    return;
-  }
-  p = const_cast<void*>(ptr);
-  ok = true;
+  ok = pin_acquire(ptr, bytes, held);
 }
 HostPin::~HostPin() {
-  if (!ok) return;
+  if (held.empty()) return;
   // unwinding from an error: copies into or out of these pages may still be
   // queued, and the caller may free them as soon as the error returns
   if (std::uncaught_exceptions() > 0) (void)hipDeviceSynchronize();
-  (void)hipHostUnregister(p);
+  pin_release(held);
 }
 
 HostPipeline::HostPipeline(int) {
@@ -186,22 +233,16 @@ void HostPipeline::ensure_pinned(int64_t doubles) {
 namespace {
 // Page-locks [p, p + bytes) for the scope of one call (hipHostRegister);
 // `ok` is false when the runtime refuses, and the caller then stages.
+// Shares the process-wide registry with HostPin (another thread may hold
+// the same arrays).
 struct Registration {
-  std::vector<void*> ptrs;
+  std::vector<uintptr_t> held;
   bool ok = true;
   void add(const void* p, size_t bytes) {
     if (!ok) return;
-    if (hipHostRegister(const_cast<void*>(p), bytes, hipHostRegisterDefault) != hipSuccess) {
-      (void)hipGetLastError();
-      ok = false;
-      return;
-    }
-    ptrs.push_back(const_cast<void*>(p));
+    ok = pin_acquire(p, bytes, held);
   }
-  void release() {
-    for (void* p : ptrs) (void)hipHostUnregister(p);
-    ptrs.clear();
-  }
+  void release() { pin_release(held); }
   ~Registration() { release(); }
 };
 

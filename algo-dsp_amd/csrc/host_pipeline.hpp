@@ -31,11 +31,13 @@ void parallel_for(int64_t n, const std::function<void(int64_t)>& fn, int workers
 // Page-locks a caller's host range for the scope of one call
 // (hipHostRegister), so the DMA engines move it directly instead of staging
 // pageable memory.  Ranges below `min_bytes` are left alone; `ok` is false
-// when the runtime refuses (the copies then stay pageable).  The scope must
-// end after every copy touching the range has completed.
+// when the runtime refuses or another call holds an overlapping range (the
+// copies then stay pageable).  Registrations are reference-counted process-
+// wide, so threads passing the same array share one.  The scope must end
+// after every copy touching the range has completed.
 struct HostPin {
-  void* p = nullptr;
-  bool ok = false;
+  std::vector<uintptr_t> held;  // registry entries this scope keeps locked
+  bool ok = false;              // the whole range is page-locked
   HostPin(const void* ptr, size_t bytes, size_t min_bytes = size_t(4) << 20);
   ~HostPin();
   HostPin(const HostPin&) = delete;

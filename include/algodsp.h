@@ -359,14 +359,18 @@ int ad_fx_chain_set_eq_state(ad_fx_chain* h, const double* state, int64_t n);
  *   FUSED           the fused per-sample kernels (dsp_kernels.hip k_chain*);
  *   STAGED_NOSPLIT  staged, one EQ pipeline per channel group;
  *   STAGED          staged with the split EQ stage;
- *   TIME_PARALLEL   the time-parallel engine (fx_tp.hip) also for an EQ-only
- *                   chain (EQ, or EQ + compressor, + Freeverb only with a
- *                   compressor; otherwise as AUTO).
+ *   TIME_PARALLEL   the time-parallel engine (fx_tp.hip) also for chains
+ *                   without a compressor: EQ only, Freeverb only, EQ +
+ *                   Freeverb (where the staged engine applies; otherwise as
+ *                   AUTO).
  * FUSED, STAGED_NOSPLIT and STAGED perform the reference's operations in its
  * order: their outputs are identical.  The time-parallel engine starts the
  * EQ's time segments from chained states (double-double): its outputs are
- * within ~1e-12 relative RMS of those (the serial recurrence's own rounding
- * noise for low-frequency sections), not bit-identical.
+ * within 1e-12 relative RMS of those (the serial recurrence's own rounding
+ * noise for low-frequency sections), not bit-identical.  That noise grows
+ * with the sections' round-off noise gain (poles near z = 1: a low highpass
+ * at a high sample rate), so AUTO and TIME_PARALLEL keep the staged engine
+ * for an EQ whose noise estimate exceeds 4.5e-13 (ad_fx_chain_last_engine).
  * chunk: samples per staged / time-parallel chunk (0: the engine's default;
  * otherwise >= 256).                                                         */
 #define AD_FX_ENGINE_AUTO 0
@@ -375,6 +379,12 @@ int ad_fx_chain_set_eq_state(ad_fx_chain* h, const double* state, int64_t n);
 #define AD_FX_ENGINE_STAGED 3
 #define AD_FX_ENGINE_TIME_PARALLEL 4
 int ad_fx_chain_set_engine(ad_fx_chain* h, int engine, int64_t chunk);
+/* The engine that ran the last process call (AD_FX_ENGINE_FUSED, _STAGED,
+ * _STAGED_NOSPLIT or _TIME_PARALLEL; -1 before the first call) and the EQ's
+ * round-off noise estimate eps sqrt(sum NG) that gates the time-parallel
+ * engine (0 without an EQ, inf for an unstable section).  Either pointer may
+ * be NULL.  No reference counterpart (engine introspection). */
+int ad_fx_chain_last_engine(ad_fx_chain* h, int* engine, double* eq_noise);
 /* Per-wave clock counters (s_memtime ticks) of the first chunk of each call,
  * for profiling the serial stages: {compute, barrier wait} pairs per wave. */
 int ad_fx_chain_set_profiling(ad_fx_chain* h, int enable);

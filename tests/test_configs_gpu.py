@@ -119,11 +119,12 @@ def test_config4_shard(gpu):
 
 def test_config5_chain(gpu):
     """configs[4] at the shape bench.py --workload fx times: 256 channels,
-    device buffers, the staged engine (default), 2^18 samples = 16 of its
-    16384-sample chunks, in two calls (the second ends mid-chunk); channels 0,
-    63, 64 (the first of the second 64-channel group) and 255 against the
-    oracle chain (chain_process.go:11-33: biquad chains -> Compressor ->
-    Freeverb)."""
+    device buffers, the engine AUTO picks for a chain with a compressor -- the
+    time-parallel engine (fx_tp.hip; the EQ's noise estimate, 3.6e-13 at
+    48 kHz, is under its 4.5e-13 gate) -- 2^18 samples = 4 of its 65536-sample
+    chunks, in two calls (the second starts mid-chunk); channels 0, 63, 64
+    (the first of the second 64-channel group) and 255 against the oracle
+    chain (chain_process.go:11-33: biquad chains -> Compressor -> Freeverb)."""
     import torch
 
     fs = 48000.0
@@ -139,6 +140,9 @@ def test_config5_chain(gpu):
     fx.process_device(dx.data_ptr(), n, cut, s.cuda_stream)
     fx.process_device(dx.data_ptr() + 8 * cut, n, n - cut, s.cuda_stream)
     s.synchronize()
+    engine, noise = fx.LastEngine()
+    assert engine == P.EffectChain.ENGINE_TIME_PARALLEL, engine
+    assert 3e-13 < noise < 4.5e-13, noise
     y = dx.cpu().numpy()
     for c in (0, 63, 64, 255):
         v = x[c].copy()

@@ -363,9 +363,11 @@ def test_time_parallel_per_channel_eq(gpu, chunk, nsec):
     in K_carry) against the fused kernels: <= 1e-12 relative RMS, over a full
     65536-sample chunk (256 segments, every scan step) and a partial one
     (chunk 0 = the engine's default), or 4096-sample chunks; 1, 5 (config 5)
-    and 8 (the most a pass takes) sections, a 20 Hz highpass among them and a
-    chain gain != 1; then a coefficient update with the same section count
-    keeps the state (the maps are rebuilt)."""
+    and 8 (the most a pass takes) sections with a chain gain != 1, every
+    table's noise estimate under the engine's gate (<= 4.4e-13 at the highest
+    channel rate; a 20 Hz highpass among them would send the chain to the
+    staged engine, test_time_parallel_noise_guard); then a coefficient update
+    with the same section count keeps the state (the maps are rebuilt)."""
     import ctypes as Cc
 
     from algodsp._lib import lib
@@ -382,8 +384,8 @@ def test_time_parallel_per_channel_eq(gpu, chunk, nsec):
         for c in range(C):
             f = fs * (1.0 + scale * 0.01 * (c % 7))
             secs = [co[0] for co, _ in design.config5_eq(f)]
-            secs += [design.peak(300.0, 4.0, 2.0, f), design.highpass(20.0, 0.707, f),
-                     design.low_shelf(60.0, 6.0, 0.707, f)]
+            secs += [design.peak(300.0, 4.0, 2.0, f), design.highpass(120.0, 0.707, f),
+                     design.low_shelf(250.0, 6.0, 0.707, f)]
             if nsec == 1:
                 secs = [design.highpass(40.0, 0.707, f)]
             tabs.append(section_table(np.array(secs[:nsec]), 0.8))
@@ -402,8 +404,47 @@ def test_time_parallel_per_channel_eq(gpu, chunk, nsec):
         assert lib().ad_fx_chain_set_eq(fx._h, t.ctypes.data_as(Cc.POINTER(Cc.c_double)), t.shape[1], 1) == 0
         fx.Process(b)
         outs[eng] = np.concatenate([a, b], axis=1)
+        assert fx.LastEngine()[0] == (P.EffectChain.ENGINE_TIME_PARALLEL if eng == "tp" else
+                                      P.EffectChain.ENGINE_FUSED)
     a, b = outs["tp"], outs["0"]
     assert rms(a, b) <= 1e-12 * max(1.0, float(np.sqrt(np.mean(b ** 2)))), rms(a, b)
+
+
+@pytest.mark.parametrize("fs", [96000.0, 192000.0])
+@pytest.mark.parametrize("what", ["config5", "eq-only"])
+def test_time_parallel_noise_guard(gpu, fs, what):
+    """the time-parallel engine's distance from the serial
+    recurrence grows with the EQ's round-off noise gain (tools/tp_cond.py: a
+    10 Hz highpass at 192 kHz puts it near 4e-11).  A 10 Hz highpass at 96 and
+    192 kHz ahead of config 5's other sections (designed at that rate): the
+    noise estimate is past the gate, so AUTO (with the compressor) and an
+    explicit TIME_PARALLEL request (EQ only) run the staged engine, and the
+    output is within 1e-12 RMS of the oracle chain (EQ only: bit-exact)."""
+    eq = [([design.highpass(10.0, 0.707, fs)], 1.0)] + design.config5_eq(fs)[1:]
+    comp = {"auto_makeup": 0, "makeup_db": 0.0} if what == "config5" else None
+    verb = (0.22, 1.0, 0.72, 0.45, 0.015) if what == "config5" else None
+    C, n = 8, 70000
+    x = np.stack([0.5 * signals.white_noise(n, 8100 + c) for c in range(C)])
+    fx = P.EffectChain(C, eq, comp, verb, fs)
+    fx.SetEngine(P.EffectChain.ENGINE_AUTO if what == "config5" else P.EffectChain.ENGINE_TIME_PARALLEL)
+    y = x.copy()
+    fx.Process(y[:, :40000])
+    fx.Process(y[:, 40000:])
+    engine, noise = fx.LastEngine()
+    assert noise > 4.5e-13, noise
+    assert engine in (P.EffectChain.ENGINE_STAGED, P.EffectChain.ENGINE_STAGED_NOSPLIT), engine
+    for c in (0, 7):
+        v = x[c].copy()
+        for co, g in eq:
+            v, _ = O.biquad_chain_block(np.ravel(co), np.zeros(2 * len(co)), g, v)
+        if what == "config5":
+            v = O.Compressor(fs, **comp).process_in_place(v)
+            o = O.Freeverb()
+            o.set(*verb)
+            v = o.process_in_place(v)
+            assert rms(y[c], v) <= RMS_TOL, (c, rms(y[c], v))
+        else:
+            assert np.array_equal(y[c], v), (c, float(np.max(np.abs(y[c] - v))))
 
 
 @pytest.mark.parametrize("what", ["eq", "eq+comp", "verb", "eq+verb"])
@@ -445,6 +486,40 @@ def test_time_parallel_engine_on_request(gpu, what):
     if eq:
         sa, sb = states[P.EffectChain.ENGINE_TIME_PARALLEL], states[P.EffectChain.ENGINE_FUSED]
         assert np.max(np.abs(sa - sb)) <= 1e-11 * max(1.0, float(np.max(np.abs(sb)))), np.max(np.abs(sa - sb))
+
+
+def test_engine_switch_growing_calls(gpu):
+    """the staged and time-parallel engines share the chunk
+    row stride tmax; alternating them with growing call lengths (each call
+    larger than the other engine's buffers) must resize every buffer a kernel
+    indexes at that stride.  Config-5 chain, engines switched between calls,
+    against the fused kernels run over the same calls (the staged calls are
+    bit-identical to fused, the time-parallel ones within 1e-12 relative)."""
+    fs = 48000.0
+    eq = design.config5_eq(fs)
+    comp = {"auto_makeup": 0, "makeup_db": 0.0}
+    verb = (0.3, 0.8, 0.8, 0.3, 0.02)
+    C = 70
+    E = P.EffectChain
+    calls = [(E.ENGINE_TIME_PARALLEL, 1000), (E.ENGINE_STAGED, 16384), (E.ENGINE_TIME_PARALLEL, 20000),
+             (E.ENGINE_STAGED, 30000), (E.ENGINE_STAGED_NOSPLIT, 40000), (E.ENGINE_TIME_PARALLEL, 70000),
+             (E.ENGINE_STAGED, 1000)]
+    n = sum(k for _, k in calls)
+    x = np.stack([0.5 * signals.white_noise(n, 7100 + c) for c in range(C)])
+    outs = {}
+    for mode in ("switch", "fused"):
+        fx = P.EffectChain(C, eq, comp, verb, fs)
+        parts, t = [], 0
+        for eng, k in calls:
+            fx.SetEngine(eng if mode == "switch" else E.ENGINE_FUSED)
+            b = x[:, t:t + k].copy()
+            fx.Process(b)
+            parts.append(b)
+            t += k
+        outs[mode] = np.concatenate(parts, axis=1)
+    a, b = outs["switch"], outs["fused"]
+    assert np.all(np.isfinite(a))
+    assert rms(a, b) <= 1e-12 * max(1.0, float(np.sqrt(np.mean(b ** 2)))), rms(a, b)
 
 
 @pytest.mark.parametrize("C,n", [(1, 5000), (3, 257), (65, 64), (2, 1)])

@@ -68,7 +68,8 @@ def test_correlate_fft_device_matches_host(gpu, n, m):
     close(got, O.correlate_fft(a, b))
 
 
-@pytest.mark.parametrize("sa,sb", [(3.0e4, 3.0e-3), (1.0e-4, 2.0e3), (1.0, 1.0e-9)])
+@pytest.mark.parametrize("sa,sb", [(3.0e4, 3.0e-3), (1.0e-4, 2.0e3), (1.0, 1.0e-9), (2.0**600, 2.0**-600),
+                                   (2.0**-600, 2.0**560)])
 @pytest.mark.parametrize("n,m", [(40000, 25000), (1 << 17, 4096)])
 def test_correlate_fft_unequal_scales(gpu, n, m, sa, sb):
     """Signals whose magnitudes differ by 1e6 .. 1e9 (an int16-scale recording
@@ -76,7 +77,10 @@ def test_correlate_fft_unequal_scales(gpu, n, m, sa, sb):
     a + i b, so without its power-of-two rescaling of b, B's spectrum would
     carry rounding of order eps |A| and the correlation's error would grow by
     |a| / |b|.  The reference transforms a and b separately (correlate.go:122-147);
-    the result must stay within the same relative bar as equal-scale inputs."""
+    the result must stay within the same relative bar as equal-scale inputs.
+    Ratios beyond 2^1000 take the scale's clamped two-factor path:
+    a single 2^e would overflow there (parity unpinned: no reference fixture
+    covers it, the oracle transforms a and b separately)."""
     a, b = sa * signals.white_noise(n, 3 + n), sb * signals.white_noise(m, 4 + m)
     close(conv.CorrelateFFT(a, b), O.correlate_fft(a, b))
 
