@@ -179,6 +179,7 @@ def _declare(L: C.CDLL) -> None:
                                            C.c_int, C.POINTER(vp)]),
         "ad_conv_multi_process_device": (C.c_int, [vp, vp, i64, i64, vp, i64, i64, vp]),
         "ad_conv_multi_process_device_segment": (C.c_int, [vp, vp, i64, i64, vp, i64, i64, i64, i64, vp]),
+        "ad_conv_multi_process_device_mix": (C.c_int, [vp, vp, i64, i64, vp, i64, i64, C.c_int, i64, i64, vp]),
         "ad_conv_mixdown_device": (C.c_int, [vp, C.c_int, i64, i64, vp, i64, C.c_int, vp]),
         "ad_comm_get_unique_id": (C.c_int, [C.POINTER(C.c_uint8)]),
         "ad_comm_create": (C.c_int, [C.POINTER(C.c_uint8), C.c_int, C.c_int, C.c_int, C.POINTER(vp)]),

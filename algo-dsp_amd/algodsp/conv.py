@@ -389,6 +389,17 @@ class MultiChannelConvolver(_Handle):
                                                          C.c_void_p(d_out), out_stride, out_len, out_begin,
                                                          out_end, C.c_void_p(stream)))
 
+    def process_device_mix(self, d_in: int, in_stride: int, in_len: int, d_mix: int, mix_stride: int,
+                           out_len: int, first_parity: int = 0, out_begin: int = 0, out_end: int = 0,
+                           stream: int = 0) -> None:
+        """Every channel's full linear convolution with the stereo mixdown fused
+        (ad_conv_multi_process_device_mix): d_mix [2][mix_stride] gets L (even
+        global channels) and R (odd) over [out_begin, out_end); the per-channel
+        outputs are not stored."""
+        check(lib().ad_conv_multi_process_device_mix(self._h, C.c_void_p(d_in), in_stride, in_len,
+                                                     C.c_void_p(d_mix), mix_stride, out_len, int(first_parity),
+                                                     out_begin, out_end, C.c_void_p(stream)))
+
 
 def _row_ptrs(a: np.ndarray):
     """(c_double_p * rows) of a C-contiguous 2-D float64 array."""

@@ -92,6 +92,7 @@ struct ad_conv {
   std::vector<double> w_in, w_out;     // float32 calls: widened block
   int64_t hop = 0;
   int64_t seg_next = -1;  // next out_begin of a segmented offline call (-1: none open)
+  DevBuf<double> mix_scratch;  // ad_conv_multi_process_device_mix at hop < 2048: per-channel outputs
 
   // streaming blocks that are not a whole number of hops: samples of the
   // unfinished block carried in pin_in (stream_convolve)
@@ -1017,6 +1018,44 @@ int ad_conv_multi_process_device_segment(ad_conv* h, const double* d_in, int64_t
     if (out_begin == 0) h->eng->begin_offline(s);
     h->eng->run(d_in, in_stride, in_len, d_out, out_stride, out_len, /*use_hist=*/false, s, out_begin / L,
                 (out_end + L - 1) / L);
+    mark_last(h, s);
+    h->seg_next = out_end < out_len ? out_end : -1;
+  });
+}
+
+int ad_conv_multi_process_device_mix(ad_conv* h, const double* d_in, int64_t in_stride, int64_t in_len,
+                                     double* d_mix, int64_t mix_stride, int64_t out_len, int first_parity,
+                                     int64_t out_begin, int64_t out_end, void* stream) {
+  return guard([&] {
+    if (!h || h->kind != Kind::Multi) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "not a multi-channel convolver");
+    if (in_len <= 0) AD_FAIL(AD_ERR_EMPTY_INPUT, "conv: empty input");
+    if (out_len > in_len + h->K - 1 || out_len <= 0)
+      AD_FAIL(AD_ERR_LENGTH_MISMATCH, "conv: buffer length mismatch");
+    if (!d_mix) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "mixdown: null mix buffer");
+    if (mix_stride < out_len) AD_FAIL(AD_ERR_LENGTH_MISMATCH, "mixdown: mix stride shorter than the output");
+    const int64_t L = h->eng->hop();
+    if (out_end <= 0) out_end = out_len;
+    out_end = std::min(out_end, out_len);
+    if (out_begin < 0 || out_begin >= out_end || out_begin % L != 0 || (out_end % L != 0 && out_end != out_len))
+      AD_FAIL(AD_ERR_INVALID_ARGUMENT, "conv segment: bounds must be hop multiples within the output");
+    if (out_begin != 0 && out_begin != h->seg_next)
+      AD_FAIL(AD_ERR_INVALID_ARGUMENT, "conv segment: segments must follow each other in order");
+    DeviceScope ds(h->device);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    order_after_last(h, s);
+    if (out_begin == 0) h->eng->begin_offline(s);
+    const int64_t jb = out_begin / L, je = (out_end + L - 1) / L;
+    if (h->eng->can_mix()) {
+      const MixOut mix{d_mix, mix_stride, first_parity & 1};
+      h->eng->run(d_in, in_stride, in_len, nullptr, 0, out_len, /*use_hist=*/false, s, jb, je, false, &mix);
+    } else {  // hop < 2048: per-channel outputs into scratch, then k_mixdown (same sums)
+      const int C = h->eng->channels();
+      h->mix_scratch.reserve((size_t)C * out_len);
+      h->eng->run(d_in, in_stride, in_len, h->mix_scratch.p, out_len, out_len, false, s, jb, je);
+      launch_mixdown(h->mix_scratch.p + out_begin, C, out_len, out_end - out_begin, d_mix + out_begin, mix_stride,
+                     first_parity & 1, s);
+      AD_HIP(hipGetLastError());
+    }
     mark_last(h, s);
     h->seg_next = out_end < out_len ? out_end : -1;
   });

@@ -171,10 +171,15 @@ struct IrfftArgs {
   // decreasing t, newest first.  Grid: channels * ord_ny * ord_R.
   int ord_R, ord_ny;
   StreamGate sg;        // split kernel, one item: run only if K1 ran; publish completion
+  int mix_parity;       // launch_irfft_mix: global index parity of local channel 0 (out: [2][out_stride] mix)
 };
 
 bool launch_window_rfft(int M, const RfftArgs& a, hipStream_t s);
 bool launch_irfft_store(int M, const IrfftArgs& a, hipStream_t s);
+// K3 with the stereo mixdown fused (M >= 2048; false otherwise): a.out is
+// the [2][out_stride] mix (L: even global channels, R: odd), the per-channel
+// outputs are not written.
+bool launch_irfft_mix(int M, const IrfftArgs& a, hipStream_t s);
 bool launch_fdl_mac(int PC, int NH, const MacArgs& a, int channels, hipStream_t s);
 // K2's run geometry for a launch (run length R: R_req, or auto when <= 0;
 // runs ny), shared with the K1/K3 launches that order their items by it.

@@ -252,10 +252,10 @@ __device__ double2 mid_bin_z(const IrfftArgs& a, int c, int j, MidLoads first) {
   return make_double2(fma(-te.x, sy, sx * S), -te.y * sy);
 }
 
-template <int M>
+template <int M, int VV = 8>
 struct SplitPlan {
   static constexpr int M2 = M / 2;
-  static constexpr int V = 8;
+  static constexpr int V = VV;
   using Sub = FftPlan<M2, V>;
   static constexpr int T = Sub::T;  // threads per workgroup
   static constexpr int LDS = Sub::MP + TwSplit<M2>::N + TwSplit<M>::N;  // double2 elements
@@ -402,6 +402,83 @@ __global__ __launch_bounds__((SplitPlan<M>::T)) __attribute__((amdgpu_waves_per_
   gate_done(a.sg);
 }
 
+// K3 with the stereo mixdown fused (Upols::run with a MixOut,
+// ad_conv_multi_process_device_mix).  One workgroup per (output block j,
+// side s): it runs the split inverse transform above for every channel of the
+// group on side s (local channel c with (mix_parity + c) & 1 == s, i.e. global
+// index parity s), in increasing c, and sums the channels' output blocks in
+// registers; only the mix block is stored.  The per-channel outputs never
+// reach memory (k_mixdown re-read the 8 channel rows and wrote
+// the 2 mix rows, 1.35 GB per shard step, and K3 wrote 8 rows where 2 are
+// needed).  Registers: the accumulator's 32 VGPRs do not fit beside both
+// halves A and B at the kernel's 128-VGPR cap (two workgroups per CU; 88
+// VGPRs of spills when A and B were both live), so A is added into the
+// accumulator as soon as its transform is done and B's loads are issued after
+// that, and each channel enters the mix as (acc + A) - W^-m B instead of
+// acc + (A - W^-m B): the same terms, rounded in another order (the mix agrees
+// with k_mixdown over the per-channel outputs to rounding, and is exactly
+// the per-channel output for a side with one channel).  The other workgroup
+// on the CU hides B's load wait.
+template <int M, bool NT, int VV>
+__global__ __launch_bounds__((SplitPlan<M, VV>::T)) __attribute__((amdgpu_waves_per_eu(32 / VV))) void k_irfft_mix_split(IrfftArgs a) {
+  using SP = SplitPlan<M, VV>;
+  constexpr int M2 = SP::M2, V = SP::V, T = SP::T, L = M;
+  __shared__ __attribute__((aligned(16))) double2 lds[SP::LDS];
+  const int tid = threadIdx.x;
+  const int e = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, gridDim.x));
+  const int j = __builtin_amdgcn_readfirstlane(e >> 1);
+  const int side = __builtin_amdgcn_readfirstlane(e & 1);
+  const int c0 = (side ^ a.mix_parity) & 1;  // first local channel of this side
+  const TwLds<M2> twS = tw_lds_compute<M2>(lds + FftPlan<M2, V>::MP, tid, T);
+  const TwLds<M> twC = tw_lds_compute<M>(lds + FftPlan<M2, V>::MP + TwSplit<M2>::N, tid, T);
+  double2 acc[V];
+#pragma unroll
+  for (int s = 0; s < V; ++s) acc[s] = make_double2(0.0, 0.0);
+  for (int c = c0; c < a.channels; c += 2) {
+    // an opaque copy of tid per channel: the index arithmetic below is redone
+    // each iteration instead of being hoisted out of the loop into ~24 live
+    // VGPRs (that hoisting spilled at the 128-VGPR cap)
+    int t = tid;
+    asm volatile("" : "+v"(t));
+    const double2* Zb = a.Y + (int64_t)c * a.y_ch_stride + (int64_t)j * a.MS;
+    double2 av[V], bv[V];
+    const bool mid = a.mid.on && tid < 64;
+    MidLoads ml{};
+    if (mid) ml = mid_bin_issue<M>(a, c, j);
+#pragma unroll
+    for (int s = 0; s < V; ++s) av[s] = ld2<NT>(Zb + zrow_pos(2 * pass0_index<M2, V>(t, s), M));
+    if (mid) {
+      const double2 z = mid_bin_z<M>(a, c, j, ml);
+      if (tid == 0) av[FftPlan<M2, V>::R0 / 2] = z;
+    }
+    __syncthreads();  // twiddle tables (first channel) / the previous channel's last LDS reads
+    fft_run<M2, V, false>(av, t, lds, twS);
+#pragma unroll
+    for (int s = 0; s < V; ++s) acc[s] = c_add(acc[s], av[s]);
+    __builtin_amdgcn_sched_barrier(0);  // B's loads stay behind A's transform (registers)
+#pragma unroll
+    for (int s = 0; s < V; ++s) bv[s] = ld2<NT>(Zb + zrow_pos(2 * pass0_index<M2, V>(t, s) + 1, M));
+    __syncthreads();
+    fft_run<M2, V, false>(bv, t, lds, twS);
+#pragma unroll
+    for (int s = 0; s < V; ++s) acc[s] = c_sub(acc[s], c_mul(c_conj(twC(last_pass_index<M2, V>(t, s))), bv[s]));
+  }
+  const int64_t ob = a.o0 + (int64_t)j * L;  // output of time index M/2 + m is at ob + 2m
+  double* yb = a.out + (int64_t)side * a.out_stride + ob;
+  if (a.aligned && ob + 2 * M2 <= a.out_len) {
+#pragma unroll
+    for (int s = 0; s < V; ++s) st2<NT>(reinterpret_cast<double2*>(yb + 2 * last_pass_index<M2, V>(tid, s)), acc[s]);
+  } else {
+    const int64_t left = a.out_len - ob;
+#pragma unroll
+    for (int s = 0; s < V; ++s) {
+      const int o = 2 * last_pass_index<M2, V>(tid, s);
+      if (o < left) yb[o] = acc[s].x;
+      if (o + 1 < left) yb[o + 1] = acc[s].y;
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Launchers
 // ---------------------------------------------------------------------------
@@ -448,7 +525,29 @@ void irfft_split_go(const IrfftArgs& a, hipStream_t s) {
     timed_launch(k_irfft_store_split<M, false>, g, b, s, a);
 }
 
+#ifndef AD_K3MIX_V
+#define AD_K3MIX_V 8
+#endif
+template <int M>
+void irfft_mix_go(const IrfftArgs& a, hipStream_t s) {
+  const dim3 g((unsigned)(2 * a.jc)), b(SplitPlan<M, AD_K3MIX_V>::T);
+  if (k3_nt((int64_t)a.channels * a.jc))
+    timed_launch(k_irfft_mix_split<M, true, AD_K3MIX_V>, g, b, s, a);
+  else
+    timed_launch(k_irfft_mix_split<M, false, AD_K3MIX_V>, g, b, s, a);
+}
+
 }  // namespace
+
+bool launch_irfft_mix(int M, const IrfftArgs& a, hipStream_t s) {
+  if (a.jc <= 0) return true;
+  switch (M) {
+    case 2048: irfft_mix_go<2048>(a, s); return true;
+    case 4096: irfft_mix_go<4096>(a, s); return true;
+    case 8192: irfft_mix_go<8192>(a, s); return true;
+    default: return false;
+  }
+}
 
 bool launch_window_rfft(int M, const RfftArgs& a, hipStream_t s) {
   if (a.channels <= 0 || a.jc <= 0) return true;

@@ -183,12 +183,17 @@ void Upols::begin_offline(hipStream_t) {
 }
 
 void Upols::run(const double* d_in, int64_t in_stride, int64_t n, double* d_out, int64_t out_stride, int64_t out_len,
-                bool use_hist, hipStream_t s, int64_t jb, int64_t je, bool accumulate) {
+                bool use_hist, hipStream_t s, int64_t jb, int64_t je, bool accumulate, const MixOut* mix) {
   if (out_len <= 0) return;
+  if (mix && (!can_mix() || accumulate || gate_on_)) AD_FAIL(AD_ERR_INTERNAL, "UPOLS: fused mixdown needs hop >= 2048");
   if (je < 0) je = (out_len + L_ - 1) / L_;
   const int64_t J = je - jb;
   if (J <= 0) return;
   const int in_aligned = ((reinterpret_cast<uintptr_t>(d_in) & 15) == 0) && (in_stride % 2 == 0);
+  if (mix) {
+    d_out = mix->p;
+    out_stride = mix->stride;
+  }
   const int out_aligned = ((reinterpret_cast<uintptr_t>(d_out) & 15) == 0) && (out_stride % 2 == 0);
   // call blocks holding input samples: [0, nb_in); K1 transforms only those,
   // K2 reads every later block as zeros
@@ -236,7 +241,7 @@ void Upols::run(const double* d_in, int64_t in_stride, int64_t n, double* d_out,
     const int64_t rows_per_step = (int64_t)C_ * runNy;
     const int64_t steps_cached = (int64_t(256) << 20) / ((int64_t)MS_ * 16 * std::max<int64_t>(1, rows_per_step));
     const bool ordered = M_ >= 2048 && !(NH_ == 1 && jc <= 2) && runNy > 1 &&
-                         steps_cached * 4 >= runR;
+                         steps_cached * 4 >= runR && !mix;
     if (ordered) {
       a.ord_R = runR;
       a.ord_ny = runNy;
@@ -307,8 +312,14 @@ void Upols::run(const double* d_in, int64_t in_stride, int64_t n, double* d_out,
     }
     b.sg = sg;
     prof_begin(s, &e0, 2);
-    launch_irfft_store(M_, b, s);
-    prof_end(s, e0, 2, blocks * ((double)(M_ + 1) * 16 + (double)L_ * 8));
+    if (mix) {  // every channel's Z rows in, the two mix rows out
+      b.mix_parity = mix->first_parity & 1;
+      launch_irfft_mix(M_, b, s);
+      prof_end(s, e0, 2, blocks * (double)(M_ + 1) * 16 + 2.0 * jc * L_ * 8);
+    } else {
+      launch_irfft_store(M_, b, s);
+      prof_end(s, e0, 2, blocks * ((double)(M_ + 1) * 16 + (double)L_ * 8));
+    }
     AD_HIP(hipGetLastError());
     g_next_ += jc;
   }

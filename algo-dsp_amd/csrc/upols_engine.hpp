@@ -15,6 +15,15 @@
 
 namespace adsp {
 
+// Stereo mixdown fused into the engine's inverse transform (Upols::run):
+// mix [2][stride] receives L = the sum of the channels whose global index
+// (first_parity + c) is even, R = the odd ones, instead of per-channel outputs.
+struct MixOut {
+  double* p;
+  int64_t stride;
+  int first_parity;
+};
+
 class Upols {
  public:
   // kernels: host [n_ir][K].  L: hop (power of two, 16..4096).  C: channels.
@@ -54,8 +63,12 @@ class Upols {
   // Offline segments of one signal run in increasing order (the delay line
   // carries from one segment to the next).
   // accumulate: K3 adds into d_out instead of storing (partitioned stages).
+  // mix (hop >= 2048 only): d_out / out_stride are ignored and K3 writes the
+  // group's stereo mix (MixOut) with the per-channel outputs never stored.
   void run(const double* d_in, int64_t in_stride, int64_t n, double* d_out, int64_t out_stride, int64_t out_len,
-           bool use_hist, hipStream_t s, int64_t jb = 0, int64_t je = -1, bool accumulate = false);
+           bool use_hist, hipStream_t s, int64_t jb = 0, int64_t je = -1, bool accumulate = false,
+           const MixOut* mix = nullptr);
+  bool can_mix() const { return M_ >= 2048; }
   // Kept for API symmetry: the ring already holds the last block's spectrum
   // (checks that a streaming call covers at least one hop).
   void save_history(const double* d_in, int64_t in_stride, int64_t n, hipStream_t s);

@@ -53,6 +53,10 @@ def parse():
                         "through the ABI at world 1), the like-for-like base of the N > 1 curve")
     p.add_argument("--pipeline", choices=["on", "off"], default="on",
                    help="N > 1: overlap step i's mixdown reduce with step i+1's convolution (two output buffers)")
+    p.add_argument("--mix-fused", choices=["on", "off"], default="on",
+                   help="shard with mixdown: the stereo mix fused into the inverse transform "
+                        "(ad_conv_multi_process_device_mix, no per-channel outputs) or per-channel outputs + "
+                        "k_mixdown inside ad_mixdown_reduce")
     p.add_argument("--segments", type=int, default=1,
                    help="output segments per step (ad_conv_multi_process_device_segment); each segment's "
                         "mixdown reduce starts as soon as it is computed")
@@ -222,37 +226,7 @@ def main():
         # against exact float64 dot products -- the signal start, a K2 run
         # boundary (auto run length: multiples of 16 blocks), the middle and
         # the tail of the output.
-        L = args.hop
-        wins = sorted({t for t in (K - 32, 192 * L - 32, 16 * L - 7, out_len // 2, out_len - 64)
-                       if 0 <= t <= out_len - 64})
-        errs = []
-        if mixdown:
-            got = mixes[last].cpu().numpy()
-            for s_ in range(2):
-                for t0w in wins:
-                    ref = np.zeros(64)
-                    a0 = t0w - K + 1
-                    lo, hi = max(0, a0), min(n, t0w + 64)
-                    for c in range(C * world):
-                        if c % 2 == s_ and hi > lo:
-                            # the input span this window reads, regenerated (counter-based noise)
-                            seg = np.zeros(64 + K - 1)
-                            seg[lo - a0:hi - a0] = signals.white_noise(hi - lo, 0x5EED + c, start=lo)
-                            ref += np.convolve(seg, ir[c % 2], mode="valid")
-                    errs.append(got[s_, t0w:t0w + 64] - ref)
-        else:
-            got = ys[last].cpu().numpy()
-            for ci, c in enumerate(ids):
-                for t0w in wins:
-                    errs.append(got[ci, t0w:t0w + 64] - exact_window(x_host[ci], ir[c % 2], t0w, 64))
-        err = np.concatenate(errs)
-        parity = {"rms": float(np.sqrt(np.mean(err ** 2))), "max_abs": float(np.max(np.abs(err))),
-                  "outputs_checked": int(err.size),
-                  "against": "exact float64 dot products (numpy) over windows at " + ", ".join(map(str, wins)) +
-                             (" of the whole-job stereo mix" if mixdown else " of every channel"),
-                  "tolerance_rms": 1e-7}
-        if parity["rms"] > 1e-7:
-            print(f"bench.py: PARITY FAILURE {parity}", file=sys.stderr)
+        parity = output_parity(args, r, ir, C * world, mixdown)
         host_io = None
         if world == 1 and args.host_io == "on":
             # the same step from HOST buffers to HOST buffers through the C ABI
@@ -292,12 +266,16 @@ def main():
         if world == 1 and args.workload == "conv" and args.shard_sub == "on" and not shard_cfg:
             ys.clear(), mixes.clear()
             r8 = run_conv(args, 1, 0, local, dev, ir, 8, True, True, min(args.steps, 5), 2, "off")
+            fused = args.mix_fused == "on"
             shard_sub = {"value": round(8 * n * min(args.steps, 5) / r8["elapsed"] / 1e6, 3), "unit": "Msamples/s",
                          "ms_per_step": round(r8["elapsed"] / min(args.steps, 5) * 1e3, 4),
-                         "workload": f"config 4 shard at N = 1: 8 ch x {n} samples (IR[c mod 2]) + k_mixdown + "
+                         "workload": f"config 4 shard at N = 1: 8 ch x {n} samples (IR[c mod 2]), device-resident, " +
+                                     ("stereo mixdown fused into the inverse transform "
+                                      "(ad_conv_multi_process_device_mix) + " if fused else "k_mixdown + ") +
                                      "RCCL reduce through ad_mixdown_reduce (world 1), the per-GPU work of every "
                                      "rank at N > 1",
-                         "kernels_avg_us": {k: round(v[0] / max(v[1], 1) * 1e3, 1) for k, v in r8["prof"].items()}}
+                         "kernels_avg_us": {k: round(v[0] / max(v[1], 1) * 1e3, 1) for k, v in r8["prof"].items()},
+                         "parity": output_parity(args, r8, ir, 8, True)}
             r8["comm"].close()
             del r8
         cpu = None
@@ -314,10 +292,13 @@ def main():
                 traffic = tab[key]["hbm_bytes_per_launch"] if key and same else None
             except Exception:
                 traffic = None
-        workload = ("OverlapSave partitioned conv, stereo, 131072-tap IR, full linear convolution "
+        workload = ("OverlapSave partitioned conv, stereo, 131072-tap IR, full linear convolution, "
+                    "input and output device-resident (PCIe excluded; host_io is the host-buffer rate) "
                     if not shard_cfg else
                     f"{C * world}-channel x 131072-tap IR convolution reverb (IR[c mod 2]), channels "
-                    f"sharded {C}-per-GPU" + (", RCCL stereo mixdown (ad_mixdown_reduce) " if mixdown else " "))
+                    f"sharded {C}-per-GPU, device-resident (PCIe excluded)" +
+                    ((", stereo mixdown fused into the inverse transform" if args.mix_fused == "on" else
+                      ", k_mixdown") + " + RCCL reduce (ad_mixdown_reduce) " if mixdown else " "))
         line = {
             "metric": "Msamples/sec, overlap-save conv 131072-tap IR @48kHz; achieved HBM GB/s",
             "value": round(value, 3),
@@ -374,6 +355,50 @@ def main():
     return 0
 
 
+def output_parity(args, r, ir, C_total, mixdown):
+    """Parity of a measured step's output itself: 64-sample windows of the last
+    step's result (the whole-job stereo mix when the mixdown runs, else every
+    channel) against exact float64 dot products -- the signal start, K2 run
+    boundaries of the stereo (R = 176-192) and the shard (R = 688) geometries,
+    the middle and the tail of the output."""
+    import numpy as np
+
+    from algodsp import signals
+
+    K, n, out_len, L = ir.shape[1], args.samples, r["out_len"], args.hop
+    wins = sorted({t for t in (K - 32, 192 * L - 32, 16 * L - 7, 688 * L - 32, out_len // 2, out_len - 64)
+                   if 0 <= t <= out_len - 64})
+    errs = []
+    if mixdown:
+        got = r["mixes"][r["last"]].cpu().numpy()
+        for s_ in range(2):
+            for t0w in wins:
+                ref = np.zeros(64)
+                a0 = t0w - K + 1
+                lo, hi = max(0, a0), min(n, t0w + 64)
+                for c in range(C_total):
+                    if c % 2 == s_ and hi > lo:
+                        # the input span this window reads, regenerated (counter-based noise)
+                        seg = np.zeros(64 + K - 1)
+                        seg[lo - a0:hi - a0] = signals.white_noise(hi - lo, 0x5EED + c, start=lo)
+                        ref += np.convolve(seg, ir[c % 2], mode="valid")
+                errs.append(got[s_, t0w:t0w + 64] - ref)
+    else:
+        got = r["ys"][r["last"]].cpu().numpy()
+        for ci, c in enumerate(r["ids"]):
+            for t0w in wins:
+                errs.append(got[ci, t0w:t0w + 64] - exact_window(r["x_host"][ci], ir[c % 2], t0w, 64))
+    err = np.concatenate(errs)
+    parity = {"rms": float(np.sqrt(np.mean(err ** 2))), "max_abs": float(np.max(np.abs(err))),
+              "outputs_checked": int(err.size),
+              "against": "exact float64 dot products (numpy) over windows at " + ", ".join(map(str, wins)) +
+                         (f" of the whole-job stereo mix ({C_total} channels)" if mixdown else " of every channel"),
+              "tolerance_rms": 1e-7}
+    if parity["rms"] > 1e-7:
+        print(f"bench.py: PARITY FAILURE {parity}", file=sys.stderr)
+    return parity
+
+
 def run_conv(args, world, rank, local, dev, ir, C, shard_cfg, mixdown, steps, warmup, mode):
     """One conv measurement: C channels x args.samples per GPU per step (IR[c mod 2]),
     optionally with the RCCL stereo mixdown; `steps` timed steps after `warmup`,
@@ -413,8 +438,10 @@ def run_conv(args, world, rank, local, dev, ir, C, shard_cfg, mixdown, steps, wa
 
         comm = shard.Comm(rank, world, local, bootstrap)
     nbuf = 2 if (mixdown and args.pipeline == "on") else 1
-    ys = [torch.empty((C, out_len), dtype=torch.float64, device=dev) for _ in range(nbuf)]
-    mixes = [y if C == 2 else torch.empty((2, out_len), dtype=torch.float64, device=dev) for y in ys]
+    # fused: the engine writes the stereo mix directly (no per-channel rows)
+    fused = mixdown and C != 2 and args.mix_fused == "on"
+    ys = [torch.empty((2 if fused else C, out_len), dtype=torch.float64, device=dev) for _ in range(nbuf)]
+    mixes = [y if (C == 2 or fused) else torch.empty((2, out_len), dtype=torch.float64, device=dev) for y in ys]
 
     eng = conv.MultiChannelConvolver(ir, hop=args.hop, channels=C, ir_index=shard.ir_index(ids),
                                      chunk_blocks=args.chunk, device=local)
@@ -434,7 +461,9 @@ def run_conv(args, world, rank, local, dev, ir, C, shard_cfg, mixdown, steps, wa
             stream.wait_event(red_done[i])
         yb, mb = ys[i], mixes[i]
         for b, e in segs:
-            if len(segs) == 1:
+            if fused:
+                eng.process_device_mix(x.data_ptr(), n, n, mb.data_ptr(), out_len, out_len, ids[0] % 2, b, e, sptr)
+            elif len(segs) == 1:
                 eng.process_device(x.data_ptr(), n, n, yb.data_ptr(), out_len, out_len, sptr)
             else:
                 eng.process_device_segment(x.data_ptr(), n, n, yb.data_ptr(), out_len, out_len, b, e, sptr)
@@ -442,8 +471,8 @@ def run_conv(args, world, rank, local, dev, ir, C, shard_cfg, mixdown, steps, wa
                 done = torch.cuda.Event()
                 done.record(stream)
                 side.wait_event(done)
-                # stereo group: the two output rows are the partial mix (no k_mixdown)
-                comm.mixdown_reduce(yb.data_ptr() + 8 * b, 0 if C == 2 else C, out_len, e - b,
+                # stereo group or fused mix: mb already holds the partial mix (no k_mixdown)
+                comm.mixdown_reduce(yb.data_ptr() + 8 * b, 0 if (C == 2 or fused) else C, out_len, e - b,
                                     mb.data_ptr() + 8 * b, out_len, ids[0] % 2, 0, side.cuda_stream)
         if mixdown:
             ev = torch.cuda.Event()

@@ -194,6 +194,24 @@ int ad_conv_multi_process_device(ad_conv* h, const double* d_in, int64_t in_stri
 int ad_conv_multi_process_device_segment(ad_conv* h, const double* d_in, int64_t in_stride, int64_t in_len,
                                          double* d_out, int64_t out_stride, int64_t out_len, int64_t out_begin,
                                          int64_t out_end, void* stream);
+/* The full linear convolution of every channel with the stereo mixdown of
+ * the group fused into the inverse transform (config 4's per-GPU work, SURVEY
+ * 8(e)): d_mix [2][mix_stride] receives, for out_begin <= t < out_end,
+ *   d_mix[t]              (L) = sum of the channels with an even global index,
+ *   d_mix[mix_stride + t] (R) = sum of those with an odd global index,
+ * where local channel c has global index first_parity + c (mod 2), summed in
+ * increasing c.  The per-channel outputs are not written to memory (hop >=
+ * 2048; smaller hops convolve into an internal buffer and mix it).  Equal to
+ * ad_conv_multi_process_device + ad_conv_mixdown_device to rounding (each
+ * channel's block enters the sum as (acc + A) - W B of its split inverse
+ * transform's halves; a side with one channel is bit-identical).  out_begin /
+ * out_end follow ad_conv_multi_process_device_segment (out_end <= 0: out_len;
+ * 0, 0 = the whole output in one call).  A caller mixing into the RCCL reduce
+ * then passes channels = 0 to ad_mixdown_reduce.  Reference: the batch
+ * OverlapSave.Process (overlap_save.go:126-254) per channel, then the mix.  */
+int ad_conv_multi_process_device_mix(ad_conv* h, const double* d_in, int64_t in_stride, int64_t in_len,
+                                     double* d_mix, int64_t mix_stride, int64_t out_len, int first_parity,
+                                     int64_t out_begin, int64_t out_end, void* stream);
 /* OverlapSave.Process / ProcessTo (overlap_save.go:126-272) of every channel
  * of a multi-channel handle on HOST buffers: in[c] holds n samples, out[c]
  * receives n + kernel_len - 1.  The signal crosses PCIe in chunks through

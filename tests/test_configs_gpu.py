@@ -7,7 +7,7 @@ oracle (oracle/, the C restatement of the Go reference):
   config 1  conv.Direct, 256-tap kernel, 1 s mono 48 kHz white noise     bit-exact
   config 2  StreamingOverlapSave, 16384-tap IR, 4096-sample blocks       <= 1e-7 RMS
   config 3  OverlapSave, stereo x 2^24, 131072-tap Large Church (bench)  <= 1e-7 RMS
-  config 4  8-channel shard of the 64-channel job + stereo mixdown        <= 4e-7 RMS
+  config 4  8-channel shard of the 64-channel job, mixdown fused (2^24)  <= 4e-7 RMS
   config 5  effectchain EQ -> Compressor -> Freeverb, 256 channels        <= 1e-12 RMS
 
 Tolerances are north_star's (<= 1e-12 RMS direct/per-sample, <= 1e-7 RMS FFT
@@ -89,32 +89,43 @@ def test_config3_bench_instance(gpu):
 
 
 def test_config4_shard(gpu):
-    """configs[3]'s per-GPU shard as bench.py --workload shard runs it (8 of the
-    64 channels, channel c with IR[c mod 2], 131072 taps, hop 8192, auto chunk
-    and run length; 2^22 samples per channel here), then the stereo mixdown
-    (L = even channels, R = odd).  The mix against the oracle's per-channel
-    OverlapSave outputs summed by parity."""
+    """configs[3]'s per-GPU shard exactly as bench.py --workload shard runs it
+    (8 of the 64 channels, channel c with IR[c mod 2], 131072 taps, hop 8192,
+    auto chunk and run length, 2^24 samples per channel -- the measured
+    geometry, K2 runs of R = 688), with the stereo mixdown fused into K3
+    (ad_conv_multi_process_device_mix: L = even channels, R = odd).  The mix
+    against the oracle's per-channel OverlapSave outputs summed by parity
+    (8 oracle channels on host threads), plus exact dot-product windows at the
+    signal start, K2 run boundaries and the tail."""
+    from concurrent.futures import ThreadPoolExecutor
+
     import torch
 
     ir = irlib.large_church()
     K = ir.shape[1]
-    C_, n = 8, 1 << 22
+    C_, n = 8, 1 << 24
     out_len = n + K - 1
     x = np.stack([signals.white_noise(n, 0x5EED + c) for c in range(C_)])
     eng = conv.MultiChannelConvolver(ir, hop=8192, channels=C_, ir_index=[c % 2 for c in range(C_)])
     dx = torch.from_numpy(x).cuda()
-    dy = torch.empty((C_, out_len), dtype=torch.float64, device="cuda")
     mix = torch.empty((2, out_len), dtype=torch.float64, device="cuda")
-    eng.process_device(dx.data_ptr(), n, n, dy.data_ptr(), out_len, out_len)
-    conv.mixdown_device(dy.data_ptr(), C_, out_len, out_len, mix.data_ptr())
+    eng.process_device_mix(dx.data_ptr(), n, n, mix.data_ptr(), out_len, out_len, 0)
     torch.cuda.synchronize()
+    del dx
     m = mix.cpu().numpy()
-    want = np.zeros((2, out_len))
-    for c in range(C_):
-        want[c % 2] += O.OverlapSave(ir[c % 2], 0).process(x[c])
+    del mix
+    with ThreadPoolExecutor(8) as ex:  # ctypes releases the GIL
+        per = list(ex.map(lambda c: O.OverlapSave(ir[c % 2], 0).process(x[c]), range(C_)))
     for s in range(2):
-        assert rms(m[s], want[s]) < FFT_RMS_TOL * 4
-        assert np.max(np.abs(m[s] - want[s])) < 4e-9
+        want = per[s] + per[s + 2] + per[s + 4] + per[s + 6]
+        assert rms(m[s], want) < FFT_RMS_TOL * 4
+        assert np.max(np.abs(m[s] - want)) < 4e-9
+    del per
+    L = 8192
+    for s in range(2):
+        for t0 in [0, K - 64, 688 * L - 32, 1376 * L - 7, n - 40, out_len - 64]:
+            ref = sum(_exact_window(x[c], ir[c % 2], t0, 64) for c in range(s, C_, 2))
+            assert np.max(np.abs(m[s][t0:t0 + 64] - ref)) < 4e-9, (s, t0)
 
 
 def test_config5_chain(gpu):
