@@ -427,9 +427,10 @@ def test_time_parallel_noise_guard(gpu, fs, what):
     x = np.stack([0.5 * signals.white_noise(n, 8100 + c) for c in range(C)])
     fx = P.EffectChain(C, eq, comp, verb, fs)
     fx.SetEngine(P.EffectChain.ENGINE_AUTO if what == "config5" else P.EffectChain.ENGINE_TIME_PARALLEL)
-    y = x.copy()
-    fx.Process(y[:, :40000])
-    fx.Process(y[:, 40000:])
+    a, b = x[:, :40000].copy(), x[:, 40000:].copy()
+    fx.Process(a)
+    fx.Process(b)
+    y = np.concatenate([a, b], axis=1)
     engine, noise = fx.LastEngine()
     assert noise > 4.5e-13, noise
     assert engine in (P.EffectChain.ENGINE_STAGED, P.EffectChain.ENGINE_STAGED_NOSPLIT), engine
