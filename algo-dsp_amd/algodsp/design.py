@@ -33,6 +33,68 @@ def _norm(b0, b1, b2, a0, a1, a2):  # normalizeBiquad design.go:214-223
     return (b0 / a0, b1 / a0, b2 / a0, a1 / a0, a2 / a0)
 
 
+def bilinear_transform(s_coeffs, fs):  # BilinearTransform design.go:17-35
+    """c0 s^2 + c1 s + c2 -> (1, d1/d0, d2/d0); (1, 0, 0) for fs <= 0 or a
+    degenerate d0."""
+    if fs <= 0:
+        return (1.0, 0.0, 0.0)
+    k = 2 * fs
+    c0, c1, c2 = s_coeffs
+    d0 = c0 * k * k + c1 * k + c2
+    d1 = -2 * c0 * k * k + 2 * c2
+    d2 = c0 * k * k - c1 * k + c2
+    if d0 == 0 or math.isnan(d0) or math.isinf(d0):
+        return (1.0, 0.0, 0.0)
+    return (1.0, d1 / d0, d2 / d0)
+
+
+def bandpass(freq, q, fs):  # Bandpass design.go:47-69 (constant skirt gain)
+    w0 = _w0(freq, fs)
+    if w0 is None:
+        return _ZERO
+    q = _q(q)
+    cw, sw = math.cos(w0), math.sin(w0)
+    alpha = sw / (2 * q)
+    return _norm(sw / 2, 0.0, -sw / 2, 1 + alpha, -2 * cw, 1 - alpha)
+
+
+def notch(freq, q, fs):  # Notch design.go:71-92
+    w0 = _w0(freq, fs)
+    if w0 is None:
+        return _ZERO
+    q = _q(q)
+    cw, sw = math.cos(w0), math.sin(w0)
+    alpha = sw / (2 * q)
+    return _norm(1.0, -2 * cw, 1.0, 1 + alpha, -2 * cw, 1 - alpha)
+
+
+def allpass(freq, q, fs):  # Allpass design.go:94-115
+    w0 = _w0(freq, fs)
+    if w0 is None:
+        return _ZERO
+    q = _q(q)
+    cw, sw = math.cos(w0), math.sin(w0)
+    alpha = sw / (2 * q)
+    return _norm(1 - alpha, -2 * cw, 1 + alpha, 1 + alpha, -2 * cw, 1 - alpha)
+
+
+def response(sec, freq, fs):  # Coefficients.Response biquad/response.go:10-19
+    """H(e^{jw}) of one section (b0, b1, b2, a1, a2)."""
+    import cmath
+
+    b0, b1, b2, a1, a2 = sec
+    w = 2 * math.pi * freq / fs
+    ejw, ej2w = cmath.exp(complex(0, -w)), cmath.exp(complex(0, -2 * w))
+    return (b0 + b1 * ejw + b2 * ej2w) / (1 + a1 * ejw + a2 * ej2w)
+
+
+def chain_response(secs, freq, fs, gain=1.0):  # Chain.Response biquad/response.go:52-59
+    h = complex(gain, 0)
+    for sec in secs:
+        h *= response(sec, freq, fs)
+    return h
+
+
 def lowpass(freq, q, fs):  # pass.LowpassRBJ butterworth.go:56-88
     if fs <= 0 or freq <= 0 or freq >= fs / 2:
         return _ZERO
