@@ -93,6 +93,13 @@ struct ad_conv {
   int64_t hop = 0;
   int64_t seg_next = -1;  // next out_begin of a segmented offline call (-1: none open)
   DevBuf<double> mix_scratch;  // ad_conv_multi_process_device_mix at hop < 2048: per-channel outputs
+  // multi-channel streaming with a block size that is not a whole number of
+  // hops (ms_partial): [C][carry_w] device rows holding the unfinished block's
+  // samples + the call's block (two, swapped per call), and the touched
+  // blocks' outputs [C][ms_out_w]
+  DevBuf<double> carry[2], ms_out;
+  int carry_cur = 0;
+  int64_t carry_w = 0, ms_out_w = 0;
 
   // streaming blocks that are not a whole number of hops: samples of the
   // unfinished block carried in pin_in (stream_convolve)
@@ -1090,10 +1097,21 @@ int ad_conv_multi_stream_create(const double* kernels, int n_ir, int64_t K, int6
     if (block_size <= 0)
       AD_FAIL(AD_ERR_INVALID_ARGUMENT, "conv: blockSize must be positive, got " + std::to_string(block_size));
     if (channels <= 0) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "channels must be positive");
-    const int64_t hop = largest_pow2_divisor(block_size, 8192);
-    if (hop < 64)
-      AD_FAIL(AD_ERR_INVALID_BLOCK_SIZE, "multi-channel streaming needs a block size with a power-of-two divisor "
-                                         ">= 64, got " + std::to_string(block_size));
+    // The hop: the largest power-of-two divisor of the block when it is >= 256
+    // (or the block itself, a power of two >= 64): every call is whole blocks.
+    // Any other block size (480, 960, 1000, 4800, < 64 ...) carries the
+    // unfinished block between calls as the single-channel handle does
+    // (setup_stream_engine): hop = nextPow2(B), at least K/64 (<= 64
+    // partitions per K2 row wave) and 64, at most 8192; a call transforms the
+    // <= ceil((hop - 1 + B) / hop) blocks it touches, so it costs FFT blocks
+    // and never a hop below 256 on a long IR (B = 4800 used to run at hop 64:
+    // 2048 partitions at K = 131072).
+    int64_t hop = largest_pow2_divisor(block_size, 8192);
+    bool partial = false;
+    if (hop < 256 && hop != block_size) {
+      hop = std::min<int64_t>(8192, std::max<int64_t>(64, std::max(next_pow2(block_size), next_pow2((K + 63) / 64))));
+      partial = (block_size % hop) != 0;
+    }
     const int dev = pick_device(device);
     DeviceScope ds(dev);
     std::unique_ptr<ad_conv> h(new_handle(Kind::MultiStream, dev));
@@ -1102,13 +1120,63 @@ int ad_conv_multi_stream_create(const double* kernels, int n_ir, int64_t K, int6
     h->block_size = block_size;
     h->fft_size = next_pow2(block_size + K - 1);  // FFTSize() of the reference streaming convolver
     h->channels = channels;
-    const int jc = (int)std::max<int64_t>(1, std::min<int64_t>(block_size / hop, 4096));
+    h->partial = partial;
+    h->part_fill = 0;
+    const int64_t blocks = partial ? (hop - 1 + block_size + hop - 1) / hop : block_size / hop;
+    const int jc = (int)std::max<int64_t>(1, std::min<int64_t>(blocks, 4096));
     h->eng.reset(new Upols(dev, kernels, n_ir, K, (int)hop, channels, ir_index, jc, h->stream));
     h->eng->reset_stream(h->stream);
+    if (partial) {
+      h->carry_w = (hop + block_size + 1) / 2 * 2;  // even: 16-byte aligned rows
+      h->ms_out_w = blocks * hop;
+      for (auto& b : h->carry) {
+        b.alloc((size_t)channels * h->carry_w);
+        AD_HIP(hipMemsetAsync(b.p, 0, b.n * sizeof(double), h->stream));
+      }
+      h->ms_out.alloc((size_t)channels * h->ms_out_w);
+    }
     AD_HIP(hipStreamSynchronize(h->stream));
     return h.release();
   });
 }
+
+namespace {
+// One block of every channel of a multi-channel streaming handle (device
+// buffers).  Partial form: the call's block is appended after the carried
+// samples of the unfinished block (part_fill of them) in carry[cur], the
+// engine transforms every block they touch (zeros past the last sample; an
+// output sample depends only on inputs up to it, so the zeros never reach an
+// emitted one), the call's outputs are the slice [part_fill, part_fill + B)
+// of those blocks, and the samples of a still unfinished block move to the
+// front of the other carry buffer; the engine steps back over that block so
+// the next call transforms it again with more samples.
+void multi_stream_run(ad_conv* h, const double* d_in, int64_t in_stride, double* d_out, int64_t out_stride,
+                      hipStream_t s) {
+  const int64_t B = h->block_size;
+  if (!h->partial) {
+    h->eng->run(d_in, in_stride, B, d_out, out_stride, B, /*use_hist=*/true, s);
+    return;
+  }
+  const int C = h->channels;
+  const int64_t L = h->hop, f0 = h->part_fill, tot = f0 + B, blocks = (tot + L - 1) / L, full = (tot / L) * L;
+  DevBuf<double>& cur = h->carry[h->carry_cur];
+  const size_t cw = (size_t)h->carry_w * sizeof(double);
+  AD_HIP(hipMemcpy2DAsync(cur.p + f0, cw, d_in, (size_t)in_stride * sizeof(double), (size_t)B * sizeof(double), C,
+                          hipMemcpyDeviceToDevice, s));
+  h->eng->run(cur.p, h->carry_w, tot, h->ms_out.p, h->ms_out_w, blocks * L, /*use_hist=*/true, s);
+  if (full < tot) h->eng->rewind(1);  // the last block is not complete yet
+  AD_HIP(hipMemcpy2DAsync(d_out, (size_t)out_stride * sizeof(double), h->ms_out.p + f0,
+                          (size_t)h->ms_out_w * sizeof(double), (size_t)B * sizeof(double), C,
+                          hipMemcpyDeviceToDevice, s));
+  if (tot > full) {
+    DevBuf<double>& nxt = h->carry[h->carry_cur ^ 1];
+    AD_HIP(hipMemcpy2DAsync(nxt.p, cw, cur.p + full, cw, (size_t)(tot - full) * sizeof(double), C,
+                            hipMemcpyDeviceToDevice, s));
+    h->carry_cur ^= 1;
+  }
+  h->part_fill = tot - full;
+}
+}  // namespace
 
 int ad_conv_multi_stream_process_block_device(ad_conv* h, const double* d_in, int64_t in_stride, double* d_out,
                                               int64_t out_stride, void* stream) {
@@ -1123,7 +1191,7 @@ int ad_conv_multi_stream_process_block_device(ad_conv* h, const double* d_in, in
     DeviceScope ds(h->device);
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     order_after_last(h, s);
-    h->eng->run(d_in, in_stride, B, d_out, out_stride, B, /*use_hist=*/true, s);
+    multi_stream_run(h, d_in, in_stride, d_out, out_stride, s);
     mark_last(h, s);
   });
 }
@@ -1163,7 +1231,7 @@ int ad_conv_multi_stream_process_block(ad_conv* h, const double* const* in, doub
     parallel_for(channels, [&](int64_t c) { std::memcpy(h->pin_in + c * n, in[c], (size_t)n * sizeof(double)); },
                  workers);
     AD_HIP(hipMemcpyAsync(h->din.p, h->pin_in, cnt * sizeof(double), hipMemcpyHostToDevice, s));
-    h->eng->run(h->din.p, n, n, h->dout.p, n, n, /*use_hist=*/true, s);
+    multi_stream_run(h, h->din.p, n, h->dout.p, n, s);
     AD_HIP(hipMemcpyAsync(h->pin_out, h->dout.p, cnt * sizeof(double), hipMemcpyDeviceToHost, s));
     mark_last(h, s);
     AD_HIP(hipStreamSynchronize(s));

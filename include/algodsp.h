@@ -226,8 +226,13 @@ int ad_conv_ols_process_multi(ad_conv* h, const double* const* in, double* const
  * block call runs every channel with ONE launch per engine kernel, the
  * frequency-domain delay line and input history stay on the device between
  * calls (config 4 real-time form: 64 reverb channels, block by block).
- * block_size needs a power-of-two divisor >= 64 (the hop).  Zero latency:
- * out = the newest block_size samples of each channel's linear convolution.
+ * Any block_size > 0: with a power-of-two divisor >= 256 (or a power of two
+ * >= 64) that divisor is the hop and a call is whole engine blocks; any other
+ * size (480, 960, 1000, 4800 ...) runs at hop = nextPow2(block_size) (at least
+ * kernel_len/64, within 64..8192) and carries the unfinished block between
+ * calls, so a call costs at most ceil((hop - 1 + block_size) / hop) FFT
+ * blocks per channel.  Zero latency: out = the newest block_size samples of
+ * each channel's linear convolution.
  * Reset / getters: ad_conv_reset, ad_conv_block_size, ad_conv_fft_size.   */
 int ad_conv_multi_stream_create(const double* kernels, int n_ir, int64_t kernel_len, int64_t block_size,
                                 int channels, const int32_t* ir_index, int device, ad_conv** out);

@@ -602,6 +602,53 @@ def test_multi_stream_vs_oracle(gpu, K, B):
         s.ProcessBlock(x[:4, :B])
 
 
+@pytest.mark.parametrize("C_,K,B", [(64, 131072, 480), (64, 131072, 960), (8, 131072, 1000), (64, 131072, 4800),
+                                    (5, 16384, 100), (3, 3000, 33), (4, 20000, 12000)])
+def test_multi_stream_any_block_size(gpu, C_, K, B):
+    """ad_conv_multi_stream_* takes any block size, as the
+    reference's NewStreamingOverlapSave does (streaming_overlap_save.go:45-58):
+    blocks that are not a whole number of hops carry the unfinished block
+    between calls at hop = nextPow2(B) (>= K/64), so none runs below hop 256
+    on a long IR.  64 channels x the 131072-tap Large Church IR[c mod 2] at
+    B = 480 / 960 / 4800 (config 4's real-time form at 48 kHz block sizes),
+    odd sizes and B > hop; host and device calls interleaved, then Reset;
+    every channel against the oracle's StreamingOverlapSave."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    import torch
+
+    irs = irlib.large_church()[:, :K]
+    ir_index = [c % 2 for c in range(C_)]
+    nb = 5
+    x = np.stack([signals.white_noise(B * nb, 170 + c) for c in range(C_)])
+    s = conv.MultiChannelStreamingConvolver(irs, B, C_, ir_index=ir_index)
+    assert s.BlockSize() == B and s.FFTSize() == O.Streaming(irs[0], B).fft_size()
+    dx = torch.from_numpy(x).cuda()
+    dy = torch.zeros_like(dx)
+
+    def want_of(c):
+        o = O.Streaming(irs[ir_index[c]], B)
+        return np.concatenate([o.process_block(x[c, i * B:(i + 1) * B]) for i in range(nb)])
+
+    chans = list(range(C_)) if C_ <= 8 else [0, 1, 2, 31, 62, 63]
+    with ThreadPoolExecutor(8) as ex:
+        want = dict(zip(chans, ex.map(want_of, chans)))
+    for rep in range(2):
+        got = np.empty_like(x)
+        for i in range(nb):
+            if i % 2:
+                st = torch.cuda.current_stream()
+                s.process_block_device(dx.data_ptr() + 8 * i * B, B * nb, dy.data_ptr() + 8 * i * B, B * nb,
+                                       st.cuda_stream)
+                st.synchronize()
+                got[:, i * B:(i + 1) * B] = dy.cpu().numpy()[:, i * B:(i + 1) * B]
+            else:
+                got[:, i * B:(i + 1) * B] = s.ProcessBlock(np.ascontiguousarray(x[:, i * B:(i + 1) * B]))
+        for c in chans:
+            assert rms(got[c], want[c]) < FFT_RMS_TOL and np.max(np.abs(got[c] - want[c])) < 1e-9, (rep, c)
+        s.Reset()
+
+
 @pytest.mark.parametrize("K,B", [(131072, 4096), (16384, 8192), (3000, 1024), (40000, 2048)])
 def test_stream_blocks_bit_identical_to_offline(gpu, K, B):
     """A streaming call (one output block per channel: K2's single-row form,

@@ -349,6 +349,19 @@ def main():
                     "streaming_overlap_save.go:152-164", f"64 ch x {B4}-sample blocks, 131072-tap Large Church "
                     "IR[c mod 2], device buffers, one handle", C4 * B4, "samples", ms, None, 0, "", None, 0,
                     "one launch per engine kernel per block for all 64 channels (hop 4096, P = 32)"))
+    for Bx in (480, 960, 4800):  # block sizes that are not a whole number of hops (partial-block carry)
+        msx = conv.MultiChannelStreamingConvolver(ir, Bx, C4, ir_index=[c % 2 for c in range(C4)])
+        dxx = torch.from_numpy(np.stack([signals.white_noise(Bx, 0x5EED + c) for c in range(C4)])).cuda()
+        dyx = torch.empty_like(dxx)
+        ms = dev_time(lambda sp: msx.process_block_device(dxx.data_ptr(), Bx, dyx.data_ptr(), Bx, sp),
+                      8 if q else 128)
+        hop = max(1 << (Bx - 1).bit_length(), 2048)
+        rows.append(row(f"a5 x64 B={Bx}", "StreamingOverlapSave.ProcessBlockTo x 64 channels "
+                        "streaming_overlap_save.go:45-58,152-164", f"64 ch x {Bx}-sample blocks, 131072-tap Large "
+                        "Church IR[c mod 2], device buffers, one handle", C4 * Bx, "samples", ms, None, 0, "", None,
+                        0, f"hop {hop} with the unfinished block carried between calls (<= "
+                        f"{(hop - 1 + Bx + hop - 1) // hop} FFT blocks per channel per call)"))
+        del msx, dxx, dyx
     pcm = conv.PartitionedConvolutionMulti(kpc, 7, 13, C4)
     dxp = torch.from_numpy(np.stack([signals.white_noise(lam * 64, c) for c in range(C4)])).cuda()
     dyp = torch.empty_like(dxp)
