@@ -121,6 +121,11 @@ struct ad_conv {
   uint64_t seq = 0;            // last block sequence number issued
   uint64_t chain_pending = 0;  // sequence number of the pre-enqueued chain (0: none)
   uint64_t gate_timeout = 0;   // K1's wait, ticks of the device's real-time counter
+  // pre-enqueueing pays only for back-to-back calls: the call
+  // interval (EMA, ms) and the pre-enqueued chains that timed out in a row
+  double gate_gap_ms = 0;
+  int gate_misses = 0;
+  std::chrono::steady_clock::time_point gate_last{};
 
   // time-domain streaming path (blocks of fewer than 64 samples)
   bool direct_stream = false;
@@ -303,16 +308,43 @@ void gate_cancel(ad_conv* h) {
   h->chain_pending = 0;
 }
 
+// Whether the next block's chain is pre-enqueued: only while calls come
+// back to back.  A caller paced in real time (hop 2048 at 48 kHz calls every
+// 42.7 ms) would otherwise leave a K1 workgroup polling mapped memory for the
+// whole 20-ms timeout and then pay the cancel-and-relaunch fallback on every
+// block: with an interval (EMA) above a quarter of the timeout, or after 3
+// chains in a row timed out, the blocks run through ordinary launches (still
+// completing through the done word) until calls come fast again.
+bool gate_pre_enqueue(ad_conv* h) {
+  const auto now = Clock::now();
+  if (h->gate_last.time_since_epoch().count() != 0) {
+    const double gap = std::chrono::duration<double, std::milli>(now - h->gate_last).count();
+    h->gate_gap_ms = h->gate_gap_ms == 0 ? gap : 0.75 * h->gate_gap_ms + 0.25 * gap;
+  }
+  h->gate_last = now;
+  const double timeout_ms = 20.0;
+  return h->gate_misses < 3 && h->gate_gap_ms < timeout_ms / 4;
+}
+
 // One block of n = hop samples (already in pin_in) through the chains.
 void gate_block(ad_conv* h, int64_t n) {
   const uint64_t sq = ++h->seq;
+  const bool pre = gate_pre_enqueue(h);
   if (h->chain_pending == sq) {
     __atomic_store_n(&h->ctl->go, sq, __ATOMIC_RELEASE);  // the waiting K1 takes the block
-    gate_enqueue(h, sq + 1, true, n);                      // the next block's chain, behind this one
-    h->chain_pending = sq + 1;
+    if (pre) {
+      gate_enqueue(h, sq + 1, true, n);  // the next block's chain, behind this one
+      h->chain_pending = sq + 1;
+    } else {
+      h->chain_pending = 0;
+    }
     // done, or this chain's K1 gave up before go (the caller came late)
     gate_spin(h, [&] { return ctl_load(&h->ctl->done) == sq || ctl_load(&h->ctl->k1_state) == (sq | kGateSkipped); });
-    if (ctl_load(&h->ctl->done) == sq) return;
+    if (ctl_load(&h->ctl->done) == sq) {
+      h->gate_misses = 0;
+      return;
+    }
+    ++h->gate_misses;
     gate_cancel(h);       // the chain behind it
     h->eng->rewind(1);    // this block's skipped chain
     gate_enqueue(h, sq, false, n);
@@ -320,9 +352,12 @@ void gate_block(ad_conv* h, int64_t n) {
     return;
   }
   gate_enqueue(h, sq, false, n);  // ordinary launches, completion through done
-  gate_enqueue(h, sq + 1, true, n);
-  h->chain_pending = sq + 1;
+  if (pre) {
+    gate_enqueue(h, sq + 1, true, n);
+    h->chain_pending = sq + 1;
+  }
   gate_spin(h, [&] { return ctl_load(&h->ctl->done) == sq; });
+  if (!pre && h->gate_misses >= 3 && h->gate_gap_ms < 2.0) h->gate_misses = 0;  // fast again: retry
 }
 
 void stream_reset(ad_conv* h) {
