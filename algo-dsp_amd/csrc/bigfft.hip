@@ -176,6 +176,78 @@ __global__ __launch_bounds__(256) void k_absmax2(const double* __restrict__ a, i
 #ifndef AD_FFT_TWC
 #define AD_FFT_TWC 1  // twiddles computed in the kernel (no table loads after the data loads)
 #endif
+#ifndef AD_CORR_FUSED
+#define AD_CORR_FUSED 1  // CorrelateFFT: forward last pass + half inverse first pass in one kernel
+#endif
+// Pieces shared by k_fft_pass and the fused CorrelateFFT kernel below, so
+// both round identically.
+// Pre-twiddle of a pass (Ns > 1): v[slot s] *= W_{Ns R}^{(j mod Ns) r_s}.
+// With u = W_N^{(j mod Ns) N/(Ns R)}, slot s holds r = tid + T k_s, where
+// k_s = b + r0 V/R0 (pass0_index) runs over 0..V-1: w_s = u^tid (u^T)^k_s.
+// Two twiddle evaluations per thread and a power recurrence in registers, not
+// one per value; <= V roundings, far inside the 1e-10 parity bars.
+template <int R, int V, bool FWD>
+__device__ __forceinline__ void pass_pretwiddle(double2* v, int64_t j, int64_t Ns, int64_t N, int tid,
+                                                const double2* tw_lo, const double2* tw_hi, int S) {
+  using Plan = FftPlan<R, V>;
+  constexpr int T = Plan::T;
+  const int64_t jm = j & (Ns - 1);
+  const int64_t step = N / (Ns * R);
+  const int64_t mask = ((int64_t)1 << S) - 1;
+  auto tw = [&](int64_t e) {
+    e &= N - 1;
+#if AD_FFT_TWC
+    (void)mask;
+    double sn, cs;
+    sincospi(-2.0 * (double)e / (double)N, &sn, &cs);  // e / N exact (N a power of two)
+    return make_double2(cs, sn);
+#else
+    return c_mul(tw_lo[e & mask], tw_hi[e >> S]);
+#endif
+  };
+  double2 base = tw(jm * step * tid);  // u^tid
+  const double2 cT = tw(jm * step * T);  // u^T
+  if (!FWD) base = c_conj(base);
+  const double2 c = FWD ? cT : c_conj(cT);
+  constexpr int R0 = Plan::R0;
+#pragma unroll
+  for (int k = 0; k < V; ++k) {  // base = u^tid (u^T)^k
+#pragma unroll
+    for (int s = 0; s < V; ++s)
+      if ((s / R0) + (s % R0) * (V / R0) == k) v[s] = c_mul(v[s], base);
+    if (k + 1 < V) base = c_mul(base, c);
+  }
+}
+// The half inverse's input pieces (FftPassArgs::half): the correlation
+// product X[q] = A conj(B) from the packed spectrum, A = (Z[q] + conj Z[-q]) / 2,
+// B = (Z[q] - conj Z[-q]) / 2i; W_NF^-g; z = E + i O from X[g], X[g + NF/2].
+__device__ __forceinline__ double2 corr_ab(double2 zk, double2 zm, double2* B) {
+  *B = make_double2(0.5 * (zk.y + zm.y), -0.5 * (zk.x - zm.x));
+  return make_double2(0.5 * (zk.x + zm.x), 0.5 * (zk.y - zm.y));
+}
+__device__ __forceinline__ double2 corr_xop(double2 zk, double2 zm) {
+  double2 B;
+  const double2 A = corr_ab(zk, zm, &B);
+  return go_cmul(A, c_conj(B));
+}
+__device__ __forceinline__ double2 half_wneg(int64_t g, int64_t NF, const double2* ftw_lo, const double2* ftw_hi,
+                                             int fS) {  // W_NF^-g
+#if AD_FFT_TWC
+  (void)ftw_lo, (void)ftw_hi, (void)fS;
+  double sn, cs;
+  sincospi(2.0 * (double)g / (double)NF, &sn, &cs);  // g / NF exact (NF a power of two)
+  return make_double2(cs, sn);
+#else
+  const int64_t fm = ((int64_t)1 << fS) - 1;
+  return c_conj(c_mul(ftw_lo[g & fm], ftw_hi[g >> fS]));
+#endif
+}
+__device__ __forceinline__ double2 half_zcomb(double2 x1, double2 x2, double2 w) {
+  const double2 e = make_double2(0.5 * (x1.x + x2.x), 0.5 * (x1.y + x2.y));
+  const double2 o = c_mul(make_double2(0.5 * (x1.x - x2.x), 0.5 * (x1.y - x2.y)), w);
+  return make_double2(e.x - o.y, e.y + o.x);
+}
+
 template <int R>
 struct PassShape {
   static constexpr int V = AD_FFT_V;
@@ -220,29 +292,20 @@ __global__ __launch_bounds__((PassShape<R>::BLOCK)) void k_fft_pass(FftPassArgs 
   // take B out of a transform that A dominates).
   const int64_t NF = a.NF, msk = NF - 1;
   auto xop = [&](double2 zk, double2 zm, int64_t q) {  // zk = Z[q], zm = Z[-q]
-    const double2 A = make_double2(0.5 * (zk.x + zm.x), 0.5 * (zk.y - zm.y));
-    const double2 B = make_double2(0.5 * (zk.y + zm.y), -0.5 * (zk.x - zm.x));
-    return HALF == 1 ? go_cmul(A, c_conj(B)) : spec_op(a.op, A, B, a.eps, q, a.bad);
+    if constexpr (HALF == 1) {
+      return corr_xop(zk, zm);
+    } else {
+      double2 B;
+      const double2 A = corr_ab(zk, zm, &B);
+      return spec_op(a.op, A, B, a.eps, q, a.bad);
+    }
   };
   auto xq = [&](int64_t q) {
     if (HALF == 2 && a.spec2) return spec_op(a.op, a.in[q], a.spec2[q], a.eps, q, a.bad);
     return xop(a.in[q], a.in[(NF - q) & msk], q);
   };
-  auto wneg = [&](int64_t g) {  // W_NF^-g
-#if AD_FFT_TWC
-    double sn, cs;
-    sincospi(2.0 * (double)g / (double)NF, &sn, &cs);  // g / NF exact (NF a power of two)
-    return make_double2(cs, sn);
-#else
-    const int64_t fm = ((int64_t)1 << a.fS) - 1;
-    return c_conj(c_mul(a.ftw_lo[g & fm], a.ftw_hi[g >> a.fS]));
-#endif
-  };
-  auto zcomb = [&](double2 x1, double2 x2, double2 w) {
-    const double2 e = make_double2(0.5 * (x1.x + x2.x), 0.5 * (x1.y + x2.y));
-    const double2 o = c_mul(make_double2(0.5 * (x1.x - x2.x), 0.5 * (x1.y - x2.y)), w);
-    return make_double2(e.x - o.y, e.y + o.x);
-  };
+  auto wneg = [&](int64_t g) { return half_wneg(g, NF, a.ftw_lo, a.ftw_hi, a.fS); };
+  auto zcomb = [&](double2 x1, double2 x2, double2 w) { return half_zcomb(x1, x2, w); };
   auto half_in = [&](int64_t g) { return zcomb(xq(g), xq(g + NF / 2), wneg(g)); };
   constexpr int FP = F / 2;  // PAIR: butterflies per tile
   const int64_t jp0 = PAIR ? j0 / 2 : 0;  // PAIR: tile A = [jp0, jp0 + FP)
@@ -309,39 +372,8 @@ __global__ __launch_bounds__((PassShape<R>::BLOCK)) void k_fft_pass(FftPassArgs 
   double2 v[V];
 #pragma unroll
   for (int s = 0; s < V; ++s) v[s] = lds[lds_slot(pass0_index<R, V>(tid, s))];
-  if (a.Ns > 1) {  // pre-twiddle W_{Ns R}^{(j mod Ns) r} = W_N^{(j mod Ns) r N/(Ns R)}
-    // With u = W_N^{(j mod Ns) N/(Ns R)}, slot s holds r = tid + T k_s, where
-    // k_s = b + r0 V/R0 (pass0_index) runs over 0..V-1: w_s = u^tid (u^T)^k_s.
-    // Two table lookups per thread and a power recurrence in registers, not
-    // one lookup pair per value (the lookups are L2 round trips after the
-    // staging loads); <= V roundings, far inside the 1e-10 parity bars.
-    const int64_t jm = j & (a.Ns - 1);
-    const int64_t step = a.N / (a.Ns * R);
-    const int64_t mask = ((int64_t)1 << a.S) - 1;
-    auto tw = [&](int64_t e) {
-      e &= a.N - 1;
-#if AD_FFT_TWC
-      (void)mask;
-      double sn, cs;
-      sincospi(-2.0 * (double)e / (double)a.N, &sn, &cs);  // e / N exact (N a power of two)
-      return make_double2(cs, sn);
-#else
-      return c_mul(a.tw_lo[e & mask], a.tw_hi[e >> a.S]);
-#endif
-    };
-    double2 base = tw(jm * step * tid);  // u^tid
-    const double2 cT = tw(jm * step * T);  // u^T
-    if (!FWD) base = c_conj(base);
-    const double2 c = FWD ? cT : c_conj(cT);
-    constexpr int R0 = Plan::R0;
-#pragma unroll
-    for (int k = 0; k < V; ++k) {  // base = u^tid (u^T)^k
-#pragma unroll
-      for (int s = 0; s < V; ++s)
-        if ((s / R0) + (s % R0) * (V / R0) == k) v[s] = c_mul(v[s], base);
-      if (k + 1 < V) base = c_mul(base, c);
-    }
-  }
+  if (a.Ns > 1)  // pre-twiddle W_{Ns R}^{(j mod Ns) r} = W_N^{(j mod Ns) r N/(Ns R)}
+    pass_pretwiddle<R, V, FWD>(v, j, a.Ns, a.N, tid, a.tw_lo, a.tw_hi, a.S);
   __syncthreads();
   fft_run<R, V, FWD>(v, tid, lds, twr);
   __syncthreads();
@@ -394,6 +426,149 @@ __global__ __launch_bounds__((PassShape<R>::BLOCK)) void k_fft_pass(FftPassArgs 
       a.out[bt * a.out_batch + o] = val;
 #endif
     }
+  }
+}
+
+// CorrelateFFT: the forward transform's last pass fused with the half
+// inverse's first pass (the 2 x 268 MB round trip of the packed
+// spectrum Z through HBM at N = 2^24).  Both passes have radix R; the forward
+// pass has nbF = N/R butterflies (Ns = nbF: butterfly j writes
+// Z[j + nbF k]), the half inverse's first pass nbH = NH/R = nbF/2 (Ns = 1:
+// butterfly j' reads z[j' + nbH r] and writes its R outputs contiguously).
+// z[g] needs X[g] and X[g + NH], X[q] needs Z[q] and Z[-q]: with
+// g = j' + nbH r, Z[g] and Z[g + NH] are outputs r/2 and r/2 + R/2 of forward
+// butterfly j' (r even) or j' + nbH (r odd), and Z[-g], Z[-(g + NH)] those of
+// butterflies nbF - j' / nbH - j'.  The inverse butterfly pair {j', nbH - j'}
+// (the mirror tiles of k_fft_pass's PAIR form) needs exactly the four forward
+// butterflies {j', j' + nbH, nbF - j', nbH - j'} (for j' = 0: {0, nbH, nbH/2,
+// 3 nbH/2}, the pair {0, nbH/2}).  A workgroup takes FP = 4 inverse pairs: it
+// loads the 16 forward butterflies' inputs (runs of 4 values), runs the
+// forward pass with k_fft_pass's arithmetic, keeps Z in LDS, forms z with the
+// PAIR form's arithmetic, runs the 8 inverse butterflies (waves 0-3; waves 4-7
+// take the barriers only) and stores their outputs contiguously.  Z never
+// reaches memory, and the values are bit-identical to the two passes run
+// separately (the same operations on the same doubles).
+struct CorrFusedArgs {
+  const double2* in;  // the forward transform's next-to-last pass output [N]
+  double2* out;       // the half inverse's first-pass output [NH]
+  int64_t N;          // forward size (NH = N/2)
+  const double2* tw_lo;  // forward plan's pre-twiddle tables (AD_FFT_TWC = 0 builds)
+  const double2* tw_hi;
+  int S;
+  const double2* htw_lo;  // W_NF tables for W_NF^-g (AD_FFT_TWC = 0 builds)
+  const double2* htw_hi;
+  int hS;
+};
+template <int R>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k_corr_fwd_last_inv_first(CorrFusedArgs a) {
+  constexpr int V = 8;
+  using Plan = FftPlan<R, V>;
+  constexpr int T = Plan::T;          // threads per butterfly
+  constexpr int NBF = 512 / T;        // forward butterflies per workgroup
+  constexpr int FP = NBF / 4;         // inverse butterfly pairs per workgroup
+  constexpr int MP = Plan::MP + (T >= 16 ? 1 : 0);
+  static_assert(FP >= 1 && 2 * FP <= NBF, "fused CorrelateFFT pass shape");
+  __shared__ __attribute__((aligned(16))) double2 lds_all[NBF * MP];
+  __shared__ __attribute__((aligned(16))) double2 ltw[AD_FFT_TWC ? TwSplit<R>::N : 1];
+  const int64_t N = a.N, NH = N / 2, nbF = N / R, nbH = nbF / 2;
+  const int64_t jp0 = (int64_t)xcd_remap((int)blockIdx.x, (int)gridDim.x) * FP;
+  const TwLds<R> twr = tw_lds_compute<R>(ltw, (int)threadIdx.x, 512);
+  // forward butterfly of slot b = set * FP + jj (set: j', j' + nbH, nbF - j', nbH - j')
+  auto fbut = [&](int b) -> int64_t {
+    const int set = b / FP;
+    const int64_t j = jp0 + (b % FP);
+    if (set == 0) return j;
+    if (set == 1) return j + nbH;
+    if (set == 2) return j == 0 ? nbH / 2 : nbF - j;
+    return j == 0 ? 3 * (nbH / 2) : nbH - j;
+  };
+  // 1. stage the forward butterflies' inputs: element r of slot b is in[fbut(b) + r nbF]
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    const int idx = i * 512 + (int)threadIdx.x;
+    const int b = idx % NBF, r = idx / NBF;
+    lds_all[b * MP + lds_slot(r)] = a.in[fbut(b) + (int64_t)r * nbF];
+  }
+  __syncthreads();
+  // 2. the forward last pass (k_fft_pass<R, true, ...> with Ns = nbF)
+  const int fs = (int)threadIdx.x / T, tid = (int)threadIdx.x % T;
+  double2* lds = lds_all + fs * MP;
+  double2 v[V];
+#pragma unroll
+  for (int s = 0; s < V; ++s) v[s] = lds[lds_slot(pass0_index<R, V>(tid, s))];
+  pass_pretwiddle<R, V, true>(v, fbut(fs), nbF, N, tid, a.tw_lo, a.tw_hi, a.S);
+  __syncthreads();
+  fft_run<R, V, true>(v, tid, lds, twr);
+  __syncthreads();
+#pragma unroll
+  for (int s = 0; s < V; ++s) lds[lds_slot(last_pass_index<R, V>(tid, s))] = v[s];  // Z[fbut(fs) + nbF k]
+  __syncthreads();
+  // 3. z for the inverse pairs (k_fft_pass's PAIR form): element (jj, r) of
+  //    tile A and (jj, R-1-r) of tile B; Z of slot b, output k:
+  auto zs = [&](int b, int k) { return lds_all[b * MP + lds_slot(k)]; };
+  auto zq = [&](int64_t q) {  // Z[q] for the j' = 0 pair (any of its four butterflies)
+    const int64_t fb = q & (nbF - 1);
+    const int k = (int)(q / nbF);
+    const int set = fb == 0 ? 0 : fb == nbH ? 1 : fb == nbH / 2 ? 2 : 3;
+    return zs(set * FP, k);
+  };
+  auto half_in0 = [&](int64_t g) {  // half_in of k_fft_pass for the j' = 0 pair
+    const double2 x1 = corr_xop(zq(g), zq((N - g) & (N - 1)));
+    const double2 x2 = corr_xop(zq(g + NH), zq((N - g - NH) & (N - 1)));
+    return half_zcomb(x1, x2, half_wneg(g, N, a.htw_lo, a.htw_hi, a.hS));
+  };
+  constexpr int NPAIR = FP * R / 512;  // (jj, r) pairs per thread
+  double2 vA[NPAIR], vB[NPAIR];
+#pragma unroll
+  for (int i = 0; i < NPAIR; ++i) {
+    const int idx = i * 512 + (int)threadIdx.x;
+    const int jj = idx % FP, r = idx / FP;
+    const int64_t j = jp0 + jj;
+    if (j == 0) {
+      vA[i] = half_in0((int64_t)r * nbH);
+      vB[i] = half_in0(nbH / 2 + (int64_t)(R - 1 - r) * nbH);
+    } else {
+      const int odd = r & 1, k1 = r >> 1, k3 = (R - 1 - r) >> 1;
+      const double2 z1 = zs(odd * FP + jj, k1), z2 = zs(odd * FP + jj, k1 + R / 2);          // Z[g], Z[g + NH]
+      const double2 z3 = zs((3 - odd) * FP + jj, k3), z4 = zs((3 - odd) * FP + jj, k3 + R / 2);  // Z[-(g + NH)], Z[-g]
+      const int64_t g = j + (int64_t)r * nbH;
+      const double2 w = half_wneg(g, N, a.htw_lo, a.htw_hi, a.hS);  // W_NF^-g* = -conj(W_NF^-g)
+      vA[i] = half_zcomb(corr_xop(z1, z4), corr_xop(z2, z3), w);
+      vB[i] = half_zcomb(corr_xop(z3, z2), corr_xop(z4, z1), make_double2(-w.x, w.y));
+    }
+  }
+  __syncthreads();  // every Z read is done: the inverse staging reuses slots 0 .. 2 FP - 1
+#pragma unroll
+  for (int i = 0; i < NPAIR; ++i) {
+    const int idx = i * 512 + (int)threadIdx.x;
+    const int jj = idx % FP, r = idx / FP;
+    lds_all[jj * MP + lds_slot(r)] = vA[i];
+    lds_all[(FP + jj) * MP + lds_slot(R - 1 - r)] = vB[i];
+  }
+  __syncthreads();
+  // 4. the inverse first pass (Ns = 1: no pre-twiddle) on slots 0 .. 2 FP - 1
+  const bool act = fs < 2 * FP;  // wave-uniform (T divides the wave or a wave holds whole butterflies)
+  if (act) {
+#pragma unroll
+    for (int s = 0; s < V; ++s) v[s] = lds[lds_slot(pass0_index<R, V>(tid, s))];
+  }
+  __syncthreads();
+  fft_run_active<R, V, false>(v, tid, lds, twr, act);
+  __syncthreads();
+  if (act) {
+#pragma unroll
+    for (int s = 0; s < V; ++s) lds[lds_slot(last_pass_index<R, V>(tid, s))] = v[s];
+  }
+  __syncthreads();
+  // 5. outputs: inverse butterfly jo's R values at jo R .. jo R + R - 1
+#pragma unroll
+  for (int i = 0; i < 2 * FP * R / 512; ++i) {
+    const int idx = i * 512 + (int)threadIdx.x;
+    const int rr = idx % R, jj = idx / R;
+    const int64_t jo = jj < FP ? jp0 + jj : (jp0 + jj == FP ? nbH / 2 : nbH - jp0 - (jj - FP));
+    const double2 val = lds_all[jj * MP + lds_slot(rr)];
+    typedef double d2v __attribute__((ext_vector_type(2)));
+    __builtin_nontemporal_store(d2v{val.x, val.y}, reinterpret_cast<d2v*>(a.out + jo * R + rr));
   }
 }
 
@@ -574,7 +749,30 @@ void BigFft::spectral_half(const BigFft& half, int op, double eps, unsigned long
   a.nr[0] = n;
   a.xb[1] = b_;
   a.nr[1] = m;
-  if (pack) {
+  // The correlation's forward last pass and half inverse's first pass fused
+  // (k_corr_fwd_last_inv_first): both radix 256, three passes each side.
+  const int P = (int)radix_.size(), PH = (int)half.radix_.size();
+  const bool fused = AD_CORR_FUSED && pack && op == kSpecCorr && P >= 2 && PH >= 2 && radix_.back() == 256 &&
+                     half.radix_.front() == 256 && N_ / 256 >= 16;
+  if (fused) {
+    a.pack2 = 1;
+    a.amax = amax;
+    const double2* mid = run_passes(true, a, nullptr, a_, 0, nullptr, nullptr, N_, 1, scratch, s, 0, P - 1);
+    CorrFusedArgs f{};
+    f.in = mid;
+    f.out = scratch;  // the half plan's first scratch half (the forward pass p - 2's output, consumed)
+    f.N = N_;
+    f.tw_lo = tw_lo_;
+    f.tw_hi = tw_hi_;
+    f.S = S_;
+    f.htw_lo = tw_lo_;
+    f.htw_hi = tw_hi_;
+    f.hS = S_;
+    if (mid == scratch) AD_FAIL(AD_ERR_INTERNAL, "BigFft: fused pass would overwrite its input");
+    const unsigned groups = (unsigned)(N_ / 256 / 2 / 2 / (512 / FftPlan<256, 8>::T / 4));
+    hipLaunchKernelGGL(k_corr_fwd_last_inv_first<256>, dim3(groups), dim3(512), 0, s, f);
+    AD_HIP(hipGetLastError());
+  } else if (pack) {
     a.pack2 = 1;  // Z = FFT(a + i b)
     a.amax = amax;
     run_passes(true, a, nullptr, a_, 0, spec, nullptr, N_, 1, scratch, s);
@@ -601,12 +799,15 @@ void BigFft::spectral_half(const BigFft& half, int op, double eps, unsigned long
   i.n_front = n_front;
   i.front_off = front_off;
   i.back_from = back_from;
-  half.run_passes(false, i, spec, nullptr, half.N_, nullptr, out, 0, 1, scratch, s);
+  if (fused)  // passes 1 .. of the half inverse, from the fused pass's output
+    half.run_passes(false, i, scratch, nullptr, half.N_, nullptr, out, 0, 1, scratch, s, 1);
+  else
+    half.run_passes(false, i, spec, nullptr, half.N_, nullptr, out, 0, 1, scratch, s);
 }
 
-void BigFft::run_passes(bool forward, FftPassArgs a, const double2* in, const double* xr, int64_t in_batch,
-                        double2* out, double* out_real, int64_t out_batch, int batch, double2* scratch,
-                        hipStream_t s) const {
+const double2* BigFft::run_passes(bool forward, FftPassArgs a, const double2* in, const double* xr, int64_t in_batch,
+                                  double2* out, double* out_real, int64_t out_batch, int batch, double2* scratch,
+                                  hipStream_t s, int p_begin, int p_end) const {
   const int64_t n_real = a.nr[0];
   const int pack2 = a.pack2, halfz = a.half;  // first / last pass only
   if (radix_.empty()) {  // N <= 8 (no fused edges: callers check fused_ok())
@@ -619,15 +820,19 @@ void BigFft::run_passes(bool forward, FftPassArgs a, const double2* in, const do
     a.out_batch = out_batch;
     hipLaunchKernelGGL(k_dft_small, dim3(1, (unsigned)batch), dim3(64), 0, s, a, forward ? 1 : 0);
     AD_HIP(hipGetLastError());
-    return;
+    return out;
   }
   // pass p writes the final destination when p is last, else one of two
-  // scratch halves (pass p-1's output is pass p's input)
+  // scratch halves (pass p-1's output is pass p's input).  [p_begin, p_end):
+  // a part of the plan (p_begin > 0: `in` is pass p_begin - 1's output; the
+  // result of a part ending early stays in its scratch half, returned).
   const int P = (int)radix_.size();
+  const int pe = p_end < 0 ? P : p_end;
   double2* half[2] = {scratch, scratch + N_ * batch};
   int64_t Ns = 1;
+  for (int p = 0; p < p_begin; ++p) Ns *= radix_[(size_t)p];
   const double2* cur = in;
-  for (int p = 0; p < P; ++p) {
+  for (int p = p_begin; p < pe; ++p) {
     const int R = radix_[(size_t)p];
     const bool first = p == 0, last = p == P - 1;
     a.in = first ? in : cur;
@@ -653,6 +858,7 @@ void BigFft::run_passes(bool forward, FftPassArgs a, const double2* in, const do
     cur = dst;
     Ns *= R;
   }
+  return cur;
 }
 
 // ---------------------------------------------------------------------------

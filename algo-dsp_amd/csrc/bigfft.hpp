@@ -112,8 +112,9 @@ class BigFft {
   std::vector<double2*> twR_;  // per pass
   double2* tw_lo_ = nullptr;
   double2* tw_hi_ = nullptr;
-  void run_passes(bool forward, FftPassArgs a, const double2* in, const double* xr, int64_t in_batch, double2* out,
-                  double* out_real, int64_t out_batch, int batch, double2* scratch, hipStream_t s) const;
+  const double2* run_passes(bool forward, FftPassArgs a, const double2* in, const double* xr, int64_t in_batch,
+                            double2* out, double* out_real, int64_t out_batch, int batch, double2* scratch,
+                            hipStream_t s, int p_begin = 0, int p_end = -1) const;
 };
 
 // Pointwise spectral operations (contraction off: Go complex128 arithmetic).

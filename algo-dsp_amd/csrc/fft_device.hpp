@@ -365,4 +365,30 @@ __device__ __forceinline__ void fft_run(double2* v, int tid, double2* lds, const
   last_pass_compute<M, V, FWD, TW>(v, tid, twM);
 }
 
+// fft_run for a workgroup where only some waves hold a transform: `active`
+// (wave-uniform) guards the arithmetic and the LDS traffic, while every wave
+// still takes each barrier of the passes (s_barrier counts all waves).
+template <int M, int V, bool FWD, int P = 1, class TW>
+__device__ __forceinline__ void run_middle_passes_active(double2* v, int tid, double2* lds, const TW& twM, bool active) {
+  using Plan = FftPlan<M, V>;
+  if constexpr (P < Plan::NPASS) {
+    __syncthreads();
+    if (active) pass_load<M, V, P>(v, tid, lds);
+    if constexpr (P + 1 < Plan::NPASS) {
+      __syncthreads();
+      if (active) pass_compute_store<M, V, P, FWD, TW>(v, tid, lds, twM);
+      run_middle_passes_active<M, V, FWD, P + 1, TW>(v, tid, lds, twM, active);
+    }
+  }
+}
+template <int M, int V, bool FWD, class TW>
+__device__ __forceinline__ void fft_run_active(double2* v, int tid, double2* lds, const TW& twM, bool active) {
+  using Plan = FftPlan<M, V>;
+  if constexpr (Plan::NPASS > 1) {
+    if (active) pass_compute_store<M, V, 0, FWD, TW>(v, tid, lds, twM);
+    run_middle_passes_active<M, V, FWD, 1, TW>(v, tid, lds, twM, active);
+  }
+  if (active) last_pass_compute<M, V, FWD, TW>(v, tid, twM);
+}
+
 }  // namespace adsp
