@@ -134,6 +134,15 @@ __global__ __launch_bounds__(256) void k_absmax2(const double* __restrict__ a, i
   const double2* x2 = reinterpret_cast<const double2*>(x + head);
   const int64_t n2 = len > head ? (len - head) / 2 : 0;
   int64_t i = t0;
+#if AD_ABSMAX_U8  // tools/ A/B builds: eight 16-B loads in flight per thread
+  for (; i + 7 * stride < n2; i += 8 * stride) {
+    double2 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = x2[i + u * stride];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc(v[u].x), acc(v[u].y);
+  }
+#endif
   for (; i + 3 * stride < n2; i += 4 * stride) {
     const double2 v0 = x2[i], v1 = x2[i + stride], v2 = x2[i + 2 * stride], v3 = x2[i + 3 * stride];
     acc(v0.x), acc(v0.y), acc(v1.x), acc(v1.y), acc(v2.x), acc(v2.y), acc(v3.x), acc(v3.y);

@@ -402,6 +402,9 @@ __global__ __launch_bounds__((SplitPlan<M>::T)) __attribute__((amdgpu_waves_per_
   gate_done(a.sg);
 }
 
+#ifndef AD_K3MIX_AB
+#define AD_K3MIX_AB 0
+#endif  // tools/ A/B builds only
 // K3 with the stereo mixdown fused (Upols::run with a MixOut,
 // ad_conv_multi_process_device_mix).  One workgroup per (output block j,
 // side s): it runs the split inverse transform above for every channel of the
@@ -451,13 +454,19 @@ __global__ __launch_bounds__((SplitPlan<M, VV>::T)) __attribute__((amdgpu_waves_
       const double2 z = mid_bin_z<M>(a, c, j, ml);
       if (tid == 0) av[FftPlan<M2, V>::R0 / 2] = z;
     }
+#if AD_K3MIX_AB  // tools/ A/B builds: B's loads ahead of A's transform (spills)
+#pragma unroll
+    for (int s = 0; s < V; ++s) bv[s] = ld2<NT>(Zb + zrow_pos(2 * pass0_index<M2, V>(t, s) + 1, M));
+#endif
     __syncthreads();  // twiddle tables (first channel) / the previous channel's last LDS reads
     fft_run<M2, V, false>(av, t, lds, twS);
 #pragma unroll
     for (int s = 0; s < V; ++s) acc[s] = c_add(acc[s], av[s]);
+#if !AD_K3MIX_AB
     __builtin_amdgcn_sched_barrier(0);  // B's loads stay behind A's transform (registers)
 #pragma unroll
     for (int s = 0; s < V; ++s) bv[s] = ld2<NT>(Zb + zrow_pos(2 * pass0_index<M2, V>(t, s) + 1, M));
+#endif
     __syncthreads();
     fft_run<M2, V, false>(bv, t, lds, twS);
 #pragma unroll
