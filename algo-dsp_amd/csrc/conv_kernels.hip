@@ -785,6 +785,53 @@ __global__ __launch_bounds__(256) void k_pc_emit(const double* in, int64_t in_st
   }
 }
 
+// The emit + FIFO append of a pre-enqueued low-latency call (NupolsDev,
+// one channel, n <= 256: one workgroup).  Thread 0 waits for the host's go
+// word like the streaming chains' K1 (StreamGate: system-scope acquire loads
+// of mapped memory, s_sleep between polls, give up at the timeout or at
+// kGateAbort) and reports its decision in k1_state; when it runs, the
+// workgroup does k_pc_emit's work and then publishes seq in `done` after its
+// stores are visible system-wide.
+__global__ __launch_bounds__(256) void k_pc_emit_gated(const double* in, double* out, const double* __restrict__ acc,
+                                                       int64_t off, int64_t first, int64_t n, int mix, double wet,
+                                                       double dry, double* append_to, StreamGate g) {
+#pragma clang fp contract(off)
+  __shared__ int ok;
+  if (threadIdx.x == 0) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    int run = 0;
+    for (;;) {
+      const uint64_t v = __hip_atomic_load(g.go, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (v == g.seq) {
+        run = 1;
+        break;
+      }
+      if (v == kGateAbort || __builtin_amdgcn_s_memrealtime() - t0 > g.timeout) break;
+      __builtin_amdgcn_s_sleep(2);
+    }
+    __hip_atomic_store(g.k1_state, run ? g.seq : (g.seq | kGateSkipped), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    ok = run;
+  }
+  __syncthreads();
+  if (!ok) return;
+  const int64_t i = threadIdx.x;
+  if (i < n) {
+    const double x = in[i];
+    append_to[i] = x;
+    const double r = i >= first ? acc[off + i] : 0.0;
+    if (mix) {
+      const double a = dry * x;
+      const double b = wet * r;
+      out[i] = a + b;
+    } else {
+      out[i] = r;
+    }
+  }
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(g.done, g.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // ---------------------------------------------------------------------------
 // Launchers
 // ---------------------------------------------------------------------------
@@ -939,6 +986,12 @@ void launch_pc_emit(const double* in, int64_t in_stride, double* out, int64_t ou
   hipLaunchKernelGGL(k_pc_emit, dim3((unsigned)((n + 255) / 256), (unsigned)channels), dim3(256), 0, s, in, in_stride,
                      out, out_stride, acc, acc_stride, off, first, n, mix, wet, dry, append_to, append_stride,
                      emit ? 1 : 0, row2);
+}
+
+void launch_pc_emit_gated(const double* in, double* out, const double* acc, int64_t off, int64_t first, int64_t n,
+                          int mix, double wet, double dry, double* append_to, const StreamGate& g, hipStream_t s) {
+  hipLaunchKernelGGL(k_pc_emit_gated, dim3(1), dim3(256), 0, s, in, out, acc, off, first, n, mix, wet, dry, append_to,
+                     g);
 }
 
 // ---------------------------------------------------------------------------

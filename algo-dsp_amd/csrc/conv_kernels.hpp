@@ -207,6 +207,11 @@ struct PcSmallArgs {
   const double2* tw;     // W_2048^m, m < 2048
 };
 bool launch_pc_small(int N, const PcSmallArgs& a, int channels, hipStream_t s);
+// k_pc_emit for one channel and n <= 256 samples, pre-enqueued: waits for the
+// host's go word (g.go == g.seq; g.k1_state reports run / skipped), then
+// emits + appends and publishes g.seq in g.done (see NupolsDev::process_host).
+void launch_pc_emit_gated(const double* in, double* out, const double* acc, int64_t off, int64_t first, int64_t n,
+                          int mix, double wet, double dry, double* append_to, const StreamGate& g, hipStream_t s);
 // Several fused stages in ONE launch (their accumulator ranges must be
 // disjoint): stage k takes grid columns [first[k], first[k+1]).
 constexpr int kPcMaxFused = 8;

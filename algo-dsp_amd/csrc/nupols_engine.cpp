@@ -98,6 +98,7 @@ NupolsDev::NupolsDev(int device, const double* h, int64_t K, int64_t lambda, int
 }
 
 void NupolsDev::reset(hipStream_t s) {
+  gate_cancel(s);
   for (auto& st : st_) {
     if (st.eng) st.eng->reset_stream(s);
     st.done = 0;
@@ -242,6 +243,7 @@ void NupolsDev::emit(const double* d_in, int64_t in_stride, double* d_out, int64
 void NupolsDev::process(const double* d_in, int64_t in_stride, double* d_out, int64_t out_stride, int64_t n,
                         bool mix, double wet, double dry, hipStream_t s) {
   if (n <= 0) return;
+  gate_cancel(s);
   append(d_in, in_stride, n, false, s);           // 1. the block joins the input FIFO
   run_stages(emitted_ + n, s);                    // 2. every complete block of every stage (K3 adds at +T)
   emit(d_in, in_stride, d_out, out_stride, n, mix, wet, dry, s);  // 3. y[t - lambda]
@@ -267,6 +269,90 @@ void NupolsDev::ensure_mapped(int64_t n) {
   map_cap_ = n;
 }
 
+namespace {
+uint64_t ctl_load(const uint64_t* w) { return __atomic_load_n(w, __ATOMIC_ACQUIRE); }
+// Spins until pred() holds; after 2 s the stream is synchronised so that a
+// device fault surfaces, then it gives up.
+template <class Pred>
+void ctl_spin(hipStream_t s, Pred&& pred) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t i = 0;; ++i) {
+    if (pred()) return;
+    if ((i & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
+      AD_HIP(hipStreamSynchronize(s));
+      if (pred()) return;
+      AD_FAIL(AD_ERR_INTERNAL, "low-latency call: the pre-enqueued emit never reported");
+    }
+    __builtin_ia32_pause();
+  }
+}
+}  // namespace
+
+// Pre-enqueues the next host call's emit (k_pc_emit_gated), assuming it
+// brings n samples again with the same mix: its slot, FIFO position and
+// accumulator offset are fixed now and the bookkeeping advances as if it had
+// run; gate_cancel undoes that when the next call differs.  Only when the
+// accumulator is already complete for that call's range (the emit-first
+// condition), for one channel, n <= 256, and while calls come back to back
+// (interval EMA under 5 ms, fewer than 3 timed-out emits in a row): a paced
+// caller gets ordinary launches, not a workgroup polling through its period.
+void NupolsDev::gate_arm(int64_t n, bool mix, double wet, double dry, hipStream_t s) {
+  if (C_ != 1 || n > 256 || gp_.on || gmiss_ >= 3 || gap_ms_ >= 5.0) return;
+  if (emitted_ + n - lambda_ > complete_upto()) return;
+  if (!gctl_) {
+    AD_HIP(hipHostMalloc(reinterpret_cast<void**>(&gctl_), sizeof(GateCtl), hipHostMallocMapped | hipHostMallocCoherent));
+    std::memset(gctl_, 0, sizeof(GateCtl));
+    AD_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&gctl_dev_), gctl_, 0));
+    int dev = 0, khz = 0;
+    AD_HIP(hipGetDevice(&dev));
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0) khz = 100000;
+    gtimeout_ = (uint64_t)khz * 20;  // 20 ms
+  }
+  const int slot = in_slot_;
+  in_slot_ ^= 1;
+  if (in_used_[slot]) AD_HIP(hipEventSynchronize(ev_in_[slot]));
+  ensure_xin(received_ + n, s);
+  const int64_t first = std::max<int64_t>(0, std::min<int64_t>(n, lambda_ - emitted_));
+  StreamGate g{};
+  g.go = &gctl_dev_->go;
+  g.k1_state = &gctl_dev_->state;
+  g.done = &gctl_dev_->done;
+  g.seq = ++gseq_;
+  g.timeout = gtimeout_;
+  launch_pc_emit_gated(in_d_[slot], out_d_, acc_[acur_].p, emitted_ - lambda_ - acc_base_, first, n, mix ? 1 : 0, wet,
+                       dry, xin_[xcur_].p + (received_ - xin_base_), g, s);
+  AD_HIP(hipGetLastError());
+  AD_HIP(hipEventRecord(ev_in_[slot], s));
+  in_used_[slot] = true;
+  emitted_ += n;
+  received_ += n;
+  gp_.on = true;
+  gp_.seq = g.seq;
+  gp_.n = n;
+  gp_.slot = slot;
+  gp_.mix = mix;
+  gp_.wet = wet;
+  gp_.dry = dry;
+}
+
+// Drops a pre-enqueued emit (its workgroup exits at once) and rolls the
+// bookkeeping back; the stream is idle afterwards.
+void NupolsDev::gate_cancel(hipStream_t s) {
+  if (!gp_.on) return;
+  __atomic_store_n(&gctl_->go, kGateAbort, __ATOMIC_RELEASE);
+  ctl_spin(s, [&] {
+    const uint64_t v = ctl_load(&gctl_->state);
+    return v == (gp_.seq | kGateSkipped) || v == gp_.seq;
+  });
+  AD_HIP(hipStreamSynchronize(s));
+  if (ctl_load(&gctl_->state) != gp_.seq) {  // skipped: it neither emitted nor appended
+    emitted_ -= gp_.n;
+    received_ -= gp_.n;
+  }
+  __atomic_store_n(&gctl_->go, 0, __ATOMIC_RELEASE);
+  gp_.on = false;
+}
+
 void NupolsDev::process_host(const double* in, double* out, int64_t n, bool mix, double wet, double dry,
                              hipStream_t s) {
   if (n <= 0) return;
@@ -274,6 +360,40 @@ void NupolsDev::process_host(const double* in, double* out, int64_t n, bool mix,
     AD_HIP(hipEventCreateWithFlags(&ev_emit_, hipEventDisableTiming));
     for (auto& e : ev_in_) AD_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   }
+  {
+    const auto now = std::chrono::steady_clock::now();
+    if (glast_.time_since_epoch().count() != 0) {
+      const double gap = std::chrono::duration<double, std::milli>(now - glast_).count();
+      gap_ms_ = gap_ms_ == 0 ? gap : 0.75 * gap_ms_ + 0.25 * gap;
+    }
+    glast_ = now;
+  }
+  if (gp_.on && gp_.n == n && gp_.mix == mix && gp_.wet == wet && gp_.dry == dry) {
+    // the pre-enqueued emit takes this block: publish it, then enqueue this
+    // call's stage work and the next call's emit while the GPU emits
+    std::memcpy(in_h_[gp_.slot], in, (size_t)n * sizeof(double));
+    const uint64_t sq = gp_.seq;
+    __atomic_store_n(&gctl_->go, sq, __ATOMIC_RELEASE);
+    ctl_spin(s, [&] {
+      const uint64_t v = ctl_load(&gctl_->state);
+      return v == sq || v == (sq | kGateSkipped);
+    });
+    gp_.on = false;
+    if (ctl_load(&gctl_->state) == sq) {
+      gmiss_ = 0;
+      run_stages(emitted_, s);
+      gate_arm(n, mix, wet, dry, s);
+      ctl_spin(s, [&] { return ctl_load(&gctl_->done) == sq; });
+      std::memcpy(out, out_h_, (size_t)n * sizeof(double));
+      return;
+    }
+    ++gmiss_;  // it gave up before this call came: roll back and run the ordinary path
+    AD_HIP(hipStreamSynchronize(s));
+    emitted_ -= n;
+    received_ -= n;
+    __atomic_store_n(&gctl_->go, 0, __ATOMIC_RELEASE);
+  }
+  gate_cancel(s);
   ensure_mapped(n);
   const int slot = in_slot_;
   in_slot_ ^= 1;
@@ -305,11 +425,17 @@ void NupolsDev::process_host(const double* in, double* out, int64_t n, bool mix,
     AD_HIP(hipEventRecord(ev_emit_, s));
   }
   in_used_[slot] = true;
+  gate_arm(n, mix, wet, dry, s);
   AD_HIP(hipEventSynchronize(ev_emit_));
   std::memcpy(out, out_h_, (size_t)n * C_ * sizeof(double));
 }
 
 NupolsDev::~NupolsDev() {
+  if (gp_.on && gctl_) __atomic_store_n(&gctl_->go, kGateAbort, __ATOMIC_RELEASE);  // release the waiting emit
+  if (gctl_) {
+    (void)hipDeviceSynchronize();
+    (void)hipHostFree(gctl_);
+  }
   if (ev_emit_) {
     (void)hipDeviceSynchronize();
     (void)hipEventDestroy(ev_emit_);

@@ -12,6 +12,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <climits>
 #include <cstdint>
 #include <memory>
@@ -63,6 +64,31 @@ class NupolsDev {
   bool in_used_[2] = {false, false};
   hipEvent_t ev_emit_ = nullptr;
   hipEvent_t ev_in_[2] = {nullptr, nullptr};
+  // Pre-enqueued emit of the next host call (one channel, n <= 256, calls
+  // back to back): k_pc_emit_gated waits in the stream for the go word, so
+  // the launch leaves the next call's critical path.  ctl: coherent mapped
+  // host memory {go, k1_state, done}, a line each.
+  struct GateCtl {
+    uint64_t go, pad0[15];
+    uint64_t state, pad1[15];
+    uint64_t done, pad2[15];
+  };
+  GateCtl* gctl_ = nullptr;
+  GateCtl* gctl_dev_ = nullptr;
+  uint64_t gseq_ = 0, gtimeout_ = 0;
+  struct Pending {
+    bool on = false;
+    uint64_t seq = 0;
+    int64_t n = 0;
+    int slot = 0;
+    bool mix = false;
+    double wet = 0, dry = 0;
+  } gp_;
+  double gap_ms_ = 0;
+  int gmiss_ = 0;
+  std::chrono::steady_clock::time_point glast_{};
+  void gate_arm(int64_t n, bool mix, double wet, double dry, hipStream_t s);
+  void gate_cancel(hipStream_t s);
 
   struct Stage {
     int64_t p = 0, T = 0, taps = 0;
