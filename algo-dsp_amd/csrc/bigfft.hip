@@ -763,13 +763,16 @@ void BigFft::spectral_half(const BigFft& half, int op, double eps, unsigned long
   const int P = (int)radix_.size(), PH = (int)half.radix_.size();
   const bool fused = AD_CORR_FUSED && pack && op == kSpecCorr && P >= 2 && PH >= 2 && radix_.back() == 256 &&
                      half.radix_.front() == 256 && N_ / 256 >= 16;
+  const double2* fused_out = nullptr;
   if (fused) {
     a.pack2 = 1;
     a.amax = amax;
     const double2* mid = run_passes(true, a, nullptr, a_, 0, nullptr, nullptr, N_, 1, scratch, s, 0, P - 1);
     CorrFusedArgs f{};
     f.in = mid;
-    f.out = scratch;  // the half plan's first scratch half (the forward pass p - 2's output, consumed)
+    // the half plan's first scratch half (a consumed forward pass output) unless
+    // the forward part's result sits there (two-pass plans): then past it
+    f.out = mid == scratch ? scratch + N_ : scratch;
     f.N = N_;
     f.tw_lo = tw_lo_;
     f.tw_hi = tw_hi_;
@@ -777,9 +780,10 @@ void BigFft::spectral_half(const BigFft& half, int op, double eps, unsigned long
     f.htw_lo = tw_lo_;
     f.htw_hi = tw_hi_;
     f.hS = S_;
-    if (mid == scratch) AD_FAIL(AD_ERR_INTERNAL, "BigFft: fused pass would overwrite its input");
+
     const unsigned groups = (unsigned)(N_ / 256 / 2 / 2 / (512 / FftPlan<256, 8>::T / 4));
     hipLaunchKernelGGL(k_corr_fwd_last_inv_first<256>, dim3(groups), dim3(512), 0, s, f);
+    fused_out = f.out;
     AD_HIP(hipGetLastError());
   } else if (pack) {
     a.pack2 = 1;  // Z = FFT(a + i b)
@@ -809,7 +813,7 @@ void BigFft::spectral_half(const BigFft& half, int op, double eps, unsigned long
   i.front_off = front_off;
   i.back_from = back_from;
   if (fused)  // passes 1 .. of the half inverse, from the fused pass's output
-    half.run_passes(false, i, scratch, nullptr, half.N_, nullptr, out, 0, 1, scratch, s, 1);
+    half.run_passes(false, i, fused_out, nullptr, half.N_, nullptr, out, 0, 1, scratch, s, 1);
   else
     half.run_passes(false, i, spec, nullptr, half.N_, nullptr, out, 0, 1, scratch, s);
 }
