@@ -539,7 +539,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
     } else {
       const int odd = r & 1, k1 = r >> 1, k3 = (R - 1 - r) >> 1;
       const double2 z1 = zs(odd * FP + jj, k1), z2 = zs(odd * FP + jj, k1 + R / 2);          // Z[g], Z[g + NH]
-      const double2 z3 = zs((3 - odd) * FP + jj, k3), z4 = zs((3 - odd) * FP + jj, k3 + R / 2);  // Z[-(g + NH)], Z[-g]
+      // gs = (nbH - j) + (R-1-r) nbH: forward butterfly nbF - j (r even, set 2) or nbH - j (r odd, set 3)
+      const double2 z3 = zs((2 + odd) * FP + jj, k3), z4 = zs((2 + odd) * FP + jj, k3 + R / 2);  // Z[-(g + NH)], Z[-g]
       const int64_t g = j + (int64_t)r * nbH;
       const double2 w = half_wneg(g, N, a.htw_lo, a.htw_hi, a.hS);  // W_NF^-g* = -conj(W_NF^-g)
       vA[i] = half_zcomb(corr_xop(z1, z4), corr_xop(z2, z3), w);
