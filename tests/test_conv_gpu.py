@@ -290,6 +290,35 @@ def test_partitioned_matches_oracle(gpu, K, lo, hi):
         g.ProcessBlock(x[:10], np.empty(9))
 
 
+@pytest.mark.parametrize("lo,n", [(7, 128), (7, 64), (8, 256), (6, 200)])
+def test_partitioned_pre_enqueued_calls(gpu, lo, n):
+    """Runs of equal host calls (n <= 256) go through the pre-enqueued emit
+    (k_pc_emit_gated: the next call's emit waits in the stream for a go
+    word); a call of another length, a ConvolutionReverb wet/dry change and
+    Reset cancel it and roll the bookkeeping back.  Every output against the
+    oracle (partitioned.go:348-396, convolution.go:60-85)."""
+    h = irlib.large_church()[0, :30000].copy()
+    g = conv.NewPartitionedConvolution(h, lo, 13)
+    o = O.Partitioned(h, lo, 13)
+    x = signals.white_noise(200_000, 77 + lo)
+    plan = [n] * 40 + [n - 1] + [n] * 30 + ["reset"] + [n] * 25 + [3 * n] + [n] * 10
+    pos, got, want = 0, [], []
+    for m in plan:
+        if m == "reset":
+            g.Reset()
+            o = O.Partitioned(h, lo, 13)
+            continue
+        blk = x[pos:pos + m]
+        out = np.empty(m)
+        g.ProcessBlock(blk, out)
+        got.append(out)
+        want.append(o.process_block(blk))
+        pos += m
+    got, want = np.concatenate(got), np.concatenate(want)
+    assert rms(got, want) < FFT_RMS_TOL
+    assert np.max(np.abs(got - want)) < 1e-9
+
+
 def test_partitioned_dirac(gpu):
     c = KATS["partitioned_dirac"]
     x = signals.white_noise(c["signal_len"], 3)
