@@ -535,7 +535,7 @@ void irfft_split_go(const IrfftArgs& a, hipStream_t s) {
 }
 
 #ifndef AD_K3MIX_V
-#define AD_K3MIX_V 8
+#define AD_K3MIX_V 16  // same-box A/B (tools/shard_ab.sh): shard 62.9 (V = 8) -> 64.9-65.0 Gsamples/s, K3 599 -> 531 us
 #endif
 template <int M>
 void irfft_mix_go(const IrfftArgs& a, hipStream_t s) {
