@@ -188,6 +188,9 @@ __global__ __launch_bounds__(256) void k_absmax2(const double* __restrict__ a, i
 #ifndef AD_CORR_FUSED
 #define AD_CORR_FUSED 1  // CorrelateFFT: forward last pass + half inverse first pass in one kernel
 #endif
+#ifndef AD_CORR_FUSED_NT
+#define AD_CORR_FUSED_NT 512  // tools/ A/B: 1024 = 8 inverse pairs (128-B input runs), one workgroup per CU
+#endif
 // Pieces shared by k_fft_pass and the fused CorrelateFFT kernel below, so
 // both round identically.
 // Pre-twiddle of a pass (Ns > 1): v[slot s] *= W_{Ns R}^{(j mod Ns) r_s}.
@@ -468,12 +471,12 @@ struct CorrFusedArgs {
   const double2* htw_hi;
   int hS;
 };
-template <int R>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k_corr_fwd_last_inv_first(CorrFusedArgs a) {
+template <int R, int NT>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 512 ? 4 : 4))) void k_corr_fwd_last_inv_first(CorrFusedArgs a) {
   constexpr int V = 8;
   using Plan = FftPlan<R, V>;
   constexpr int T = Plan::T;          // threads per butterfly
-  constexpr int NBF = 512 / T;        // forward butterflies per workgroup
+  constexpr int NBF = NT / T;         // forward butterflies per workgroup
   constexpr int FP = NBF / 4;         // inverse butterfly pairs per workgroup
   constexpr int MP = Plan::MP + (T >= 16 ? 1 : 0);
   static_assert(FP >= 1 && 2 * FP <= NBF, "fused CorrelateFFT pass shape");
@@ -481,7 +484,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
   __shared__ __attribute__((aligned(16))) double2 ltw[AD_FFT_TWC ? TwSplit<R>::N : 1];
   const int64_t N = a.N, NH = N / 2, nbF = N / R, nbH = nbF / 2;
   const int64_t jp0 = (int64_t)xcd_remap((int)blockIdx.x, (int)gridDim.x) * FP;
-  const TwLds<R> twr = tw_lds_compute<R>(ltw, (int)threadIdx.x, 512);
+  const TwLds<R> twr = tw_lds_compute<R>(ltw, (int)threadIdx.x, NT);
   // forward butterfly of slot b = set * FP + jj (set: j', j' + nbH, nbF - j', nbH - j')
   auto fbut = [&](int b) -> int64_t {
     const int set = b / FP;
@@ -494,7 +497,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
   // 1. stage the forward butterflies' inputs: element r of slot b is in[fbut(b) + r nbF]
 #pragma unroll
   for (int i = 0; i < V; ++i) {
-    const int idx = i * 512 + (int)threadIdx.x;
+    const int idx = i * NT + (int)threadIdx.x;
     const int b = idx % NBF, r = idx / NBF;
     lds_all[b * MP + lds_slot(r)] = a.in[fbut(b) + (int64_t)r * nbF];
   }
@@ -526,11 +529,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
     const double2 x2 = corr_xop(zq(g + NH), zq((N - g - NH) & (N - 1)));
     return half_zcomb(x1, x2, half_wneg(g, N, a.htw_lo, a.htw_hi, a.hS));
   };
-  constexpr int NPAIR = FP * R / 512;  // (jj, r) pairs per thread
+  constexpr int NPAIR = FP * R / NT;  // (jj, r) pairs per thread
   double2 vA[NPAIR], vB[NPAIR];
 #pragma unroll
   for (int i = 0; i < NPAIR; ++i) {
-    const int idx = i * 512 + (int)threadIdx.x;
+    const int idx = i * NT + (int)threadIdx.x;
     const int jj = idx % FP, r = idx / FP;
     const int64_t j = jp0 + jj;
     if (j == 0) {
@@ -550,7 +553,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
   __syncthreads();  // every Z read is done: the inverse staging reuses slots 0 .. 2 FP - 1
 #pragma unroll
   for (int i = 0; i < NPAIR; ++i) {
-    const int idx = i * 512 + (int)threadIdx.x;
+    const int idx = i * NT + (int)threadIdx.x;
     const int jj = idx % FP, r = idx / FP;
     lds_all[jj * MP + lds_slot(r)] = vA[i];
     lds_all[(FP + jj) * MP + lds_slot(R - 1 - r)] = vB[i];
@@ -572,8 +575,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
   __syncthreads();
   // 5. outputs: inverse butterfly jo's R values at jo R .. jo R + R - 1
 #pragma unroll
-  for (int i = 0; i < 2 * FP * R / 512; ++i) {
-    const int idx = i * 512 + (int)threadIdx.x;
+  for (int i = 0; i < 2 * FP * R / NT; ++i) {
+    const int idx = i * NT + (int)threadIdx.x;
     const int rr = idx % R, jj = idx / R;
     const int64_t jo = jj < FP ? jp0 + jj : (jp0 + jj == FP ? nbH / 2 : nbH - jp0 - (jj - FP));
     const double2 val = lds_all[jj * MP + lds_slot(rr)];
@@ -782,8 +785,9 @@ void BigFft::spectral_half(const BigFft& half, int op, double eps, unsigned long
     f.htw_hi = tw_hi_;
     f.hS = S_;
 
-    const unsigned groups = (unsigned)(N_ / 256 / 2 / 2 / (512 / FftPlan<256, 8>::T / 4));
-    hipLaunchKernelGGL(k_corr_fwd_last_inv_first<256>, dim3(groups), dim3(512), 0, s, f);
+    constexpr int NT = AD_CORR_FUSED_NT;  // threads per workgroup (4 inverse pairs per 512)
+    const unsigned groups = (unsigned)(N_ / 256 / 2 / 2 / (NT / FftPlan<256, 8>::T / 4));
+    hipLaunchKernelGGL((k_corr_fwd_last_inv_first<256, NT>), dim3(groups), dim3(NT), 0, s, f);
     fused_out = f.out;
     AD_HIP(hipGetLastError());
   } else if (pack) {

@@ -1,0 +1,10 @@
+#!/bin/bash
+# Round-4 batch 4: the whole GPU suite, then CorrelateFFT A/B of the fused
+# kernel's workgroup size (512: 4 inverse pairs, 64-B input runs; 1024: 8 pairs,
+# 128-B runs, one workgroup per CU) against the unfused passes.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r04_pytest_gpu.log 2>&1 || { tail -40 gpurun_out/r04_pytest_gpu.log; exit 1; }
+tail -2 gpurun_out/r04_pytest_gpu.log
+CORR_VARIANTS="ab/corr_unfused.so - ab/corr_nt1024.so ab/corr_unfused.so - ab/corr_nt1024.so" timeout -k 10 400 bash tools/corr_ab.sh > gpurun_out/r04_corr_ab2.txt 2>&1; cat gpurun_out/r04_corr_ab2.txt
