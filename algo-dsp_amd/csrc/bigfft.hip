@@ -188,6 +188,9 @@ __global__ __launch_bounds__(256) void k_absmax2(const double* __restrict__ a, i
 #ifndef AD_CORR_FUSED
 #define AD_CORR_FUSED 1  // CorrelateFFT: forward last pass + half inverse first pass in one kernel
 #endif
+#ifndef AD_CORR_INV_V4
+#define AD_CORR_INV_V4 0  // tools/ A/B: the fused kernel's inverse butterflies at 4 values per thread (all threads busy)
+#endif
 #ifndef AD_CORR_FUSED_NT
 #define AD_CORR_FUSED_NT 512  // tools/ A/B: 1024 = 8 inverse pairs (128-B input runs), one workgroup per CU
 #endif
@@ -559,18 +562,29 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 512 ? 
     lds_all[(FP + jj) * MP + lds_slot(R - 1 - r)] = vB[i];
   }
   __syncthreads();
-  // 4. the inverse first pass (Ns = 1: no pre-twiddle) on slots 0 .. 2 FP - 1
-  const bool act = fs < 2 * FP;  // wave-uniform (T divides the wave or a wave holds whole butterflies)
+  // 4. the inverse first pass (Ns = 1: no pre-twiddle) on slots 0 .. 2 FP - 1:
+  //    2 FP butterflies over all NT threads at VI values per thread
+#if AD_CORR_INV_V4
+  constexpr int VI = 4;
+#else
+  constexpr int VI = V;
+#endif
+  using PlanI = FftPlan<R, VI>;
+  constexpr int TI = PlanI::T;
+  const int fi = (int)threadIdx.x / TI, ti = (int)threadIdx.x % TI;
+  double2* ldsi = lds_all + fi * MP;
+  const bool act = fi < 2 * FP;  // wave-uniform (TI is a multiple of the wave or divides it)
+  double2 u[VI];
   if (act) {
 #pragma unroll
-    for (int s = 0; s < V; ++s) v[s] = lds[lds_slot(pass0_index<R, V>(tid, s))];
+    for (int s = 0; s < VI; ++s) u[s] = ldsi[lds_slot(pass0_index<R, VI>(ti, s))];
   }
   __syncthreads();
-  fft_run_active<R, V, false>(v, tid, lds, twr, act);
+  fft_run_active<R, VI, false>(u, ti, ldsi, twr, act);
   __syncthreads();
   if (act) {
 #pragma unroll
-    for (int s = 0; s < V; ++s) lds[lds_slot(last_pass_index<R, V>(tid, s))] = v[s];
+    for (int s = 0; s < VI; ++s) ldsi[lds_slot(last_pass_index<R, VI>(ti, s))] = u[s];
   }
   __syncthreads();
   // 5. outputs: inverse butterfly jo's R values at jo R .. jo R + R - 1

@@ -150,7 +150,7 @@ __host__ __device__ constexpr int ilog2c(int v) { return v <= 1 ? 0 : 1 + ilog2c
 template <int M, int V = 16>
 struct FftPlan {
   static_assert(M >= 16 && M <= 8192 && (M & (M - 1)) == 0, "FFT size must be a power of two in [16, 8192]");
-  static_assert(V == 8 || V == 16, "8 or 16 values per thread");
+  static_assert(V == 4 || V == 8 || V == 16, "4, 8 or 16 values per thread");
   static constexpr int LOGV = ilog2c(V);
   static constexpr int LOG = ilog2c(M);
   static constexpr int NPASS = (LOG + LOGV - 1) / LOGV;
