@@ -465,6 +465,10 @@ double fx_eq_noise(const std::vector<double>& tab, int sets, int nsec) {
 #define AD_FX_TP_CHUNK 65536  // config 5 (tools/fx_chunk_sweep.py): 32768 10.89, 65536 11.09, 131072 11.06, 262144 10.67 Gsamples/s
 #endif
 constexpr int64_t kFxTpChunk = AD_FX_TP_CHUNK;
+#ifndef AD_FX_TP_SERIAL_TAIL  // tools/ A/B builds
+#define AD_FX_TP_SERIAL_TAIL 0
+#endif
+constexpr bool kFxTpSerialTail = AD_FX_TP_SERIAL_TAIL;  // gain + Freeverb on the caller's stream (fx_run_tp)
 constexpr int kFxTpSeg = 64;     // K_eq segment (samples), at least
 constexpr size_t kFxTpMatsCached = 8;  // segment lengths whose maps stay cached
 
@@ -620,6 +624,19 @@ void fx_run_tp(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hipStre
   AD_HIP(hipStreamWaitEvent(sd, h->ev_in, 0));
   AD_HIP(hipStreamWaitEvent(sv, h->ev_in, 0));
   const int wu = verb ? fx_comb_warmup(h->vp) : 0;
+  // kFxTpSerialTail: the gain + Freeverb of a chunk on the caller's stream
+  // (see the loop); slot reuse then follows from that stream's order: chunk i's
+  // transpose and EQ come after chunk i - 1's (and so i - kFxSlots's) tail,
+  // whose wait on the detector orders every reader of the slot before them
+  FxStageArgs prev{};
+  auto tail = [&](const FxStageArgs& p, int kp) {
+    AD_HIP(hipStreamWaitEvent(s, h->ev[ED][kp], 0));
+    FxStageArgs b = p;
+    b.buf = h->inC[kp].p;
+    b.stride = h->tmax;
+    launch_fx_gain(b, true, s);
+    launch_fxtp_verb(p, h->inC[kp].p, h->tmax, h->vbufC.p, h->coC.p, wu, s);
+  };
   int64_t i = 0;
   int k = 0;
   for (int64_t t0 = 0; t0 < n; t0 += T, ++i) {
@@ -645,7 +662,8 @@ void fx_run_tp(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hipStre
     a.vp = h->vp;
     a.vs = h->vs.p;
     a.vbuf = h->vbuf.p;
-    if (i >= kFxSlots) AD_HIP(hipStreamWaitEvent(s, h->ev[EA][k], 0));  // slot k consumed
+    if (i >= kFxSlots && !(kFxTpSerialTail && comp && verb))
+      AD_HIP(hipStreamWaitEvent(s, h->ev[EA][k], 0));  // slot k consumed
     if (eq || comp) launch_fx_transpose_in(a, a.xT, s);  // the rows the EQ / the detector read
     if (eq) {
       FxTpEqArgs e{};
@@ -666,6 +684,17 @@ void fx_run_tp(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hipStre
       launch_fxtp_eq(e, true, s);
     }
     AD_HIP(hipEventRecord(h->ev[EE][k], s));
+    if (kFxTpSerialTail && comp && verb) {
+      // chunk i's detector on sd; chunk i - 1's gain and Freeverb on the
+      // caller's stream behind chunk i's EQ, so the chip-wide kernels never
+      // share CUs with K_verb (only the 32 detector CUs run beside both)
+      AD_HIP(hipStreamWaitEvent(sd, h->ev[EE][k], 0));
+      launch_fxtp_det(a, sd);
+      AD_HIP(hipEventRecord(h->ev[ED][k], sd));
+      if (i > 0) tail(prev, (int)((i - 1) % kFxSlots));
+      prev = a;
+      continue;
+    }
     if (comp) {
       AD_HIP(hipStreamWaitEvent(sd, h->ev[EE][k], 0));
       launch_fxtp_det(a, sd);
@@ -691,6 +720,11 @@ void fx_run_tp(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hipStre
       if (verb) launch_fxtp_verb(a, a.buf, a.stride, h->vbufC.p, h->coC.p, wu, sv);
     }
     AD_HIP(hipEventRecord(h->ev[EA][k], sv));
+  }
+  if (kFxTpSerialTail && comp && verb) {
+    tail(prev, k);  // the last chunk's gain and Freeverb, on s after its detector
+    AD_HIP(hipGetLastError());
+    return;
   }
   AD_HIP(hipGetLastError());
   AD_HIP(hipStreamWaitEvent(s, h->ev[EA][k], 0));  // the last chunk's reverb / output follows all work
