@@ -113,9 +113,13 @@ __device__ __forceinline__ PackScale pack_scale(const unsigned long long* amax) 
 
 // {max|a[0..n)|, max|b[0..m)|} as bit patterns (non-negative doubles order
 // like their unsigned bit patterns; a NaN sorts above +inf and disables the
-// scale).  out must be zeroed first.  16-B loads, four in flight per thread,
-// and one atomic per workgroup: same-address atomics serialise (one per wave
-// over 8192 waves took 120-196 us for a 134 MB read).
+// scale) into out[0..1].  16-B loads, four in flight per thread, one partial
+// per workgroup (same-address atomics serialise: one per wave over 8192 waves
+// took 120-196 us for a 134 MB read); the last workgroup to finish (a counter
+// at out[2], release/acquire at agent scope) reduces the partials at out[8..)
+// and puts the counter back to zero for the next call, so no memset precedes
+// the kernel (kAbsmaxWords words of device scratch, zeroed once).
+constexpr int kAbsmaxPart = 8;  // out[kAbsmaxPart + y * gridDim.x + x]: partial of block (x, y)
 __global__ __launch_bounds__(256) void k_absmax2(const double* __restrict__ a, int64_t n, const double* __restrict__ b,
                                                  int64_t m, unsigned long long* out) {
   const double* x = blockIdx.y ? b : a;
@@ -157,13 +161,38 @@ __global__ __launch_bounds__(256) void k_absmax2(const double* __restrict__ a, i
     mx = t > mx ? t : mx;
   }
   __shared__ unsigned long long wmax[4];
+  __shared__ int last;
   if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = mx;
   __syncthreads();
+  const unsigned nblk = gridDim.x * gridDim.y;
   if (threadIdx.x == 0) {
     unsigned long long m4 = wmax[0];
     for (int w = 1; w < 4; ++w) m4 = wmax[w] > m4 ? wmax[w] : m4;
-    atomicMax(out + blockIdx.y, m4);
+    __hip_atomic_store(out + kAbsmaxPart + blockIdx.y * gridDim.x + blockIdx.x, m4, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long done =
+        __hip_atomic_fetch_add(out + 2, 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    last = done + 1 == nblk;
   }
+  __syncthreads();
+  if (!last) return;
+  // the last workgroup: max over the partials of each signal (wave y = signal y)
+  if (threadIdx.x < 128) {
+    const int y = threadIdx.x >> 6, l = threadIdx.x & 63;
+    unsigned long long r = 0;
+    for (unsigned k = l; k < gridDim.x; k += 64) {
+      const unsigned long long v =
+          __hip_atomic_load(out + kAbsmaxPart + y * gridDim.x + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      r = v > r ? v : r;
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      const unsigned long long t = __shfl_xor(r, o);
+      r = t > r ? t : r;
+    }
+    if (l == 0) __hip_atomic_store(out + y, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(out + 2, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ---------------------------------------------------------------------------
@@ -753,7 +782,6 @@ void BigFft::run(bool forward, const double2* in, const double* xr, int64_t n_re
 void BigFft::correlate_half(const BigFft& half, const double* a_, int64_t n, const double* b_, int64_t m,
                             double2* spec, double* out, double2* scratch, unsigned long long* amax,
                             hipStream_t s) const {
-  AD_HIP(hipMemsetAsync(amax, 0, 2 * sizeof(unsigned long long), s));
   const int64_t mx = std::max(n, m);
   const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>(256, (mx / 2 + 1023) / 1024));
   hipLaunchKernelGGL(k_absmax2, dim3(gx, 2), dim3(256), 0, s, a_, n, b_, m, amax);

@@ -88,7 +88,7 @@ class BigFft {
   // caller's arrays) into spec [N]; then the inverse of the Hermitian
   // A conj(B) on the half plan (N/2 points), written in lag order to out
   // (n + m - 1 values, correlate.go:165-171).  Both plans need passes (N >= 32).
-  // amax: 2 words of device scratch for the packing scale (FftPassArgs::amax):
+  // amax: kAbsmaxWords words of device scratch, zeroed once (FftPassArgs::amax):
   // without it, b's spectrum taken out of FFT(a + i b) would carry rounding
   // error of order eps |A|, which for |a| >> |b| is far above eps |B|.
   void correlate_half(const BigFft& half, const double* a, int64_t n, const double* b, int64_t m, double2* spec,
@@ -123,6 +123,9 @@ class BigFft {
 // reg:     a[k] = a[k] * conj(b[k]) / (|b[k]|^2 + eps)       (deconvolve.go:208-213, 298-303)
 // invfilt: a[k] = conj(a[k]) / (|a[k]|^2 + eps)              (deconvolve.go:384-389)
 enum SpecOp { kSpecCorr = 0, kSpecNaive = 1, kSpecReg = 2, kSpecInvFilt = 3 };
+// Words of device scratch correlate_half's `amax` needs (zeroed once at
+// allocation: the max-abs kernel leaves its counter at zero after each call).
+constexpr int kAbsmaxWords = 8 + 2 * 256;
 void launch_spec_op(int op, double2* a, const double2* b, int64_t n, double eps, unsigned long long* bad,
                     hipStream_t s);
 

@@ -86,7 +86,10 @@ struct SpectralRun {
     if (!h) h.reset(new BigFft(N / 2));
     dc.spec.reserve((size_t)N);
     dc.scratch.reserve((size_t)(2 * N));
-    dc.amax.reserve(2);
+    if (dc.amax.n < (size_t)kAbsmaxWords) {  // zeroed once: the kernel resets its counter itself
+      dc.amax.reserve(kAbsmaxWords);
+      AD_HIP(hipMemsetAsync(dc.amax.p, 0, dc.amax.n * sizeof(unsigned long long), s));
+    }
     fft->correlate_half(*h, a, n, b, m, dc.spec.p, out, dc.scratch.p, dc.amax.p, s);
   }
   // Deconvolve / InverseFilter through the same structure (x: n, h: m real
