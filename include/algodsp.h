@@ -204,7 +204,7 @@ int ad_conv_multi_process_device_segment(ad_conv* h, const double* d_in, int64_t
  * 2048; smaller hops convolve into an internal buffer and mix it).  Equal to
  * ad_conv_multi_process_device + ad_conv_mixdown_device to rounding (each
  * channel's block enters the sum as (acc + A) - W B of its split inverse
- * transform's halves; a side with one channel is bit-identical).  out_begin /
+ * transform's halves, computed at another radix split).  out_begin /
  * out_end follow ad_conv_multi_process_device_segment (out_end <= 0: out_len;
  * 0, 0 = the whole output in one call).  A caller mixing into the RCCL reduce
  * then passes channels = 0 to ad_mixdown_reduce.  Reference: the batch

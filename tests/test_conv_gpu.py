@@ -469,8 +469,8 @@ def test_multi_mix_fused(gpu, hop, C, parity, nseg):
     """ad_conv_multi_process_device_mix (the stereo mixdown fused into K3,
     VERDICT r3): the mix of C channels (IR[c mod 2], first global parity
     `parity`) against per-channel outputs + k_mixdown (to rounding: each block
-    enters the sum as (acc + A) - W B; bit-identical for a side with one
-    channel) and against the oracle's per-channel OverlapSave sums (<= 1e-7
+    enters the sum as (acc + A) - W B, and the fused kernel's transforms run
+    at 16 values per thread where K3's run at 8) and against the oracle's per-channel OverlapSave sums (<= 1e-7
     RMS per channel summed); segments, a short out_len, odd channel counts
     (a side with no channel is all zeros), hop 1024 (the scratch + k_mixdown
     path) and the per-channel outputs untouched."""
@@ -504,8 +504,6 @@ def test_multi_mix_fused(gpu, hop, C, parity, nseg):
             assert not m[side].any()
             continue
         scale = max(1.0, float(np.max(np.abs(r[side]))))
-        if len(chans) == 1 and hop >= 2048:
-            assert np.array_equal(m[side], r[side])
         assert np.max(np.abs(m[side] - r[side])) <= 1e-13 * scale, float(np.max(np.abs(m[side] - r[side])))
         want = np.zeros(out_len)
         for c in chans:
