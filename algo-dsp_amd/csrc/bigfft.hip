@@ -218,7 +218,7 @@ __global__ __launch_bounds__(256) void k_absmax2(const double* __restrict__ a, i
 #define AD_CORR_FUSED 1  // CorrelateFFT: forward last pass + half inverse first pass in one kernel
 #endif
 #ifndef AD_CORR_INV_V4
-#define AD_CORR_INV_V4 0  // tools/ A/B: the fused kernel's inverse butterflies at 4 values per thread (all threads busy)
+#define AD_CORR_INV_V4 1  // the fused kernel's inverse butterflies at 4 values per thread: all threads busy, 80 VGPRs (0.586 -> 0.571-0.575 ms same box)
 #endif
 #ifndef AD_CORR_FUSED_NT
 #define AD_CORR_FUSED_NT 512  // tools/ A/B: 1024 = 8 inverse pairs (128-B input runs), one workgroup per CU
