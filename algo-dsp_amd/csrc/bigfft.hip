@@ -89,10 +89,9 @@ __device__ __forceinline__ double2 spec_op(int op, double2 x, double2 h, double 
 struct PackScale {
   double a = 1.0, b = 1.0, o1 = 1.0, o2 = 1.0;
 };
-__device__ __forceinline__ PackScale pack_scale(const unsigned long long* amax) {
+__device__ __forceinline__ PackScale pack_scale_bits(unsigned long long ba, unsigned long long bb) {
   PackScale p;
-  if (!amax) return p;
-  const double ma = __longlong_as_double((long long)amax[0]), mb = __longlong_as_double((long long)amax[1]);
+  const double ma = __longlong_as_double((long long)ba), mb = __longlong_as_double((long long)bb);
   if (!(ma > 0.0) || !(mb > 0.0) || !__builtin_isfinite(ma) || !__builtin_isfinite(mb)) return p;
   int ea = 0, eb = 0;
   (void)frexp(ma, &ea);
@@ -110,6 +109,10 @@ __device__ __forceinline__ PackScale pack_scale(const unsigned long long* amax) 
   }
   return p;
 }
+__device__ __forceinline__ PackScale pack_scale(const unsigned long long* amax) {
+  if (!amax) return PackScale{};
+  return pack_scale_bits(amax[0], amax[1]);
+}
 
 // {max|a[0..n)|, max|b[0..m)|} as bit patterns (non-negative doubles order
 // like their unsigned bit patterns; a NaN sorts above +inf and disables the
@@ -119,6 +122,10 @@ __device__ __forceinline__ PackScale pack_scale(const unsigned long long* amax) 
 // at out[2], release/acquire at agent scope) reduces the partials at out[8..)
 // and puts the counter back to zero for the next call, so no memset precedes
 // the kernel (kAbsmaxWords words of device scratch, zeroed once).
+#ifndef AD_ABSMAX_G
+#define AD_ABSMAX_G 256  // workgroups per signal (<= kAbsmaxMaxGroups)
+#endif
+static_assert(AD_ABSMAX_G <= kAbsmaxMaxGroups, "max-abs partials");
 constexpr int kAbsmaxPart = 8;  // out[kAbsmaxPart + y * gridDim.x + x]: partial of block (x, y)
 __global__ __launch_bounds__(256) void k_absmax2(const double* __restrict__ a, int64_t n, const double* __restrict__ b,
                                                  int64_t m, unsigned long long* out) {
@@ -220,6 +227,24 @@ __global__ __launch_bounds__(256) void k_absmax2(const double* __restrict__ a, i
 #ifndef AD_CORR_INV_V4
 #define AD_CORR_INV_V4 1  // the fused kernel's inverse butterflies at 4 values per thread: all threads busy, 80 VGPRs (0.586 -> 0.571-0.575 ms same box)
 #endif
+#ifndef AD_FFT_PF
+#define AD_FFT_PF 1  // plain radix-256 passes as a persistent kernel with the next tile's loads in flight
+#endif
+#ifndef AD_CORR_SPLIT
+#define AD_CORR_SPLIT 0  // CorrelateFFT at N = 2^24: the max-abs inside the first pass (k_corr_split0; measured slower, see DESIGN)
+#endif
+#ifndef AD_PACKIN_EXP
+#define AD_PACKIN_EXP 0  // tools/ timing probes only (wrong results): 1 = mirror loads contiguous, 2 = stores contiguous
+#endif
+#ifndef AD_FFT_RO_VEC
+#define AD_FFT_RO_VEC 1  // real-pair outputs in the lag order as 16-B stores
+#endif
+#ifndef AD_FFT_PF_V
+#define AD_FFT_PF_V 8  // its values per thread (4: 1024-thread workgroups)
+#endif
+#ifndef AD_FFT_PF_G
+#define AD_FFT_PF_G 512  // its workgroups (2 per CU)
+#endif
 #ifndef AD_CORR_FUSED_NT
 #define AD_CORR_FUSED_NT 512  // tools/ A/B: 1024 = 8 inverse pairs (128-B input runs), one workgroup per CU
 #endif
@@ -230,9 +255,11 @@ __global__ __launch_bounds__(256) void k_absmax2(const double* __restrict__ a, i
 // k_s = b + r0 V/R0 (pass0_index) runs over 0..V-1: w_s = u^tid (u^T)^k_s.
 // Two twiddle evaluations per thread and a power recurrence in registers, not
 // one per value; <= V roundings, far inside the 1e-10 parity bars.
+// Split in two so a caller can evaluate the factors early (k_fft_pass_pf does
+// it before its next tile's loads occupy registers); same operations either way.
 template <int R, int V, bool FWD>
-__device__ __forceinline__ void pass_pretwiddle(double2* v, int64_t j, int64_t Ns, int64_t N, int tid,
-                                                const double2* tw_lo, const double2* tw_hi, int S) {
+__device__ __forceinline__ void pretwiddle_uc(int64_t j, int64_t Ns, int64_t N, int tid, const double2* tw_lo,
+                                              const double2* tw_hi, int S, double2* base_out, double2* c_out) {
   using Plan = FftPlan<R, V>;
   constexpr int T = Plan::T;
   const int64_t jm = j & (Ns - 1);
@@ -251,9 +278,12 @@ __device__ __forceinline__ void pass_pretwiddle(double2* v, int64_t j, int64_t N
   };
   double2 base = tw(jm * step * tid);  // u^tid
   const double2 cT = tw(jm * step * T);  // u^T
-  if (!FWD) base = c_conj(base);
-  const double2 c = FWD ? cT : c_conj(cT);
-  constexpr int R0 = Plan::R0;
+  *base_out = FWD ? base : c_conj(base);
+  *c_out = FWD ? cT : c_conj(cT);
+}
+template <int R, int V>
+__device__ __forceinline__ void pretwiddle_apply(double2* v, double2 base, const double2 c) {
+  constexpr int R0 = FftPlan<R, V>::R0;
 #pragma unroll
   for (int k = 0; k < V; ++k) {  // base = u^tid (u^T)^k
 #pragma unroll
@@ -261,6 +291,13 @@ __device__ __forceinline__ void pass_pretwiddle(double2* v, int64_t j, int64_t N
       if ((s / R0) + (s % R0) * (V / R0) == k) v[s] = c_mul(v[s], base);
     if (k + 1 < V) base = c_mul(base, c);
   }
+}
+template <int R, int V, bool FWD>
+__device__ __forceinline__ void pass_pretwiddle(double2* v, int64_t j, int64_t Ns, int64_t N, int tid,
+                                                const double2* tw_lo, const double2* tw_hi, int S) {
+  double2 base, c;
+  pretwiddle_uc<R, V, FWD>(j, Ns, N, tid, tw_lo, tw_hi, S, &base, &c);
+  pretwiddle_apply<R, V>(v, base, c);
 }
 // The half inverse's input pieces (FftPassArgs::half): the correlation
 // product X[q] = A conj(B) from the packed spectrum, A = (Z[q] + conj Z[-q]) / 2,
@@ -456,7 +493,46 @@ __global__ __launch_bounds__((PassShape<R>::BLOCK)) void k_fft_pass(FftPassArgs 
           a.out_real[bt * a.out_batch + q] = x * a.scale;
         }
       };
-      if (a.pairs) {
+      if (AD_FFT_RO_VEC && a.remap && a.pairs && Ns >= F && nb % F == 0 && ((a.front_off + a.back_from) & 1) == 0) {
+        // Real pairs into the lag order with 16-B stores.  For fixed rr the
+        // tile's F butterflies give 2F consecutive reals q = 2o, 2o + 1, and
+        // both region maps (q + front_off, q - back_from) shift q by amounts of
+        // one parity (N is even), so whether (2o, 2o+1) lands on a 16-B slot
+        // is the same for every element: `odd` = it does not, and lane jj then
+        // owns the slot (2o - 1, 2o) (its left neighbour's Im and its Re); lane
+        // 0 writes only its Re, lane F - 1 also its Im.  A slot whose two
+        // reals do not land side by side (a region edge) is written per real.
+        auto dst = [&](int64_t q) -> int64_t {
+          return q < a.n_front ? a.front_off + q : (q >= a.back_from ? q - a.back_from : -1);
+        };
+        const bool odd = ((a.front_off + (int64_t)(((uintptr_t)a.out_real >> 3) & 1)) & 1) != 0;
+        typedef double d2v __attribute__((ext_vector_type(2)));
+        const double x = val.x * oscale * oscale2, y = val.y * oscale * oscale2;
+        auto put2 = [&](int64_t ql, double lo, double hi) {  // reals ql, ql + 1
+          const int64_t d0 = dst(ql), d1 = dst(ql + 1);
+          if (d0 >= 0 && d1 == d0 + 1) {
+            *reinterpret_cast<d2v*>(a.out_real + d0) = d2v{lo, hi};
+          } else {
+            if (d0 >= 0) a.out_real[d0] = lo;
+            if (d1 >= 0) a.out_real[d1] = hi;
+          }
+        };
+        if (!odd) {
+          put2(2 * o, x, y);
+        } else {
+          if (jj > 0) {
+            const double py = lds_all[(jj - 1) * MP + lds_slot(rr)].y * oscale * oscale2;
+            put2(2 * o - 1, py, x);
+          } else {
+            const int64_t d0 = dst(2 * o);
+            if (d0 >= 0) a.out_real[d0] = x;
+          }
+          if (jj == F - 1) {
+            const int64_t d1 = dst(2 * o + 1);
+            if (d1 >= 0) a.out_real[d1] = y;
+          }
+        }
+      } else if (a.pairs) {
         emit(2 * o, val.x);
         emit(2 * o + 1, val.y);
       } else {
@@ -470,6 +546,338 @@ __global__ __launch_bounds__((PassShape<R>::BLOCK)) void k_fft_pass(FftPassArgs 
       a.out[bt * a.out_batch + o] = val;
 #endif
     }
+  }
+}
+
+// Workgroup barrier for LDS hand-offs only: __syncthreads() is a workgroup
+// release/acquire fence and waits for every outstanding global load and store
+// of the wave (vmcnt(0)), which would drain the next tile's loads below.
+__device__ __forceinline__ void pass_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+template <int M, int V, bool FWD, int P = 1, class TW>
+__device__ __forceinline__ void run_middle_passes_lb(double2* v, int tid, double2* lds, const TW& twM) {
+  using Plan = FftPlan<M, V>;
+  if constexpr (P < Plan::NPASS) {
+    pass_lds_barrier();
+    pass_load<M, V, P>(v, tid, lds);
+    if constexpr (P + 1 < Plan::NPASS) {
+      pass_lds_barrier();
+      pass_compute_store<M, V, P, FWD, TW>(v, tid, lds, twM);
+      run_middle_passes_lb<M, V, FWD, P + 1, TW>(v, tid, lds, twM);
+    }
+  }
+}
+template <int M, int V, bool FWD, class TW>
+__device__ __forceinline__ void fft_run_lb(double2* v, int tid, double2* lds, const TW& twM) {
+  using Plan = FftPlan<M, V>;
+  if constexpr (Plan::NPASS > 1) {
+    pass_compute_store<M, V, 0, FWD, TW>(v, tid, lds, twM);
+    run_middle_passes_lb<M, V, FWD, 1, TW>(v, tid, lds, twM);
+  }
+  last_pass_compute<M, V, FWD, TW>(v, tid, twM);
+}
+
+// A plain complex pass (not the first of a real-input transform, not the last
+// of a real-output one, not the half inverse's first) as a persistent kernel:
+// workgroup b takes tiles b, b + G, b + 2G, ... and holds the next tile's
+// inputs in registers while it transforms the current one, so its loads stay
+// in flight under the LDS passes (barriers wait on LDS only).  Same
+// arithmetic as k_fft_pass in the same order: bit-identical results.
+// Requires nb % F == 0 (whole tiles) and Ns == 1 or Ns >= F.
+template <int R>
+struct PfShape {  // k_fft_pass_pf: AD_FFT_PF_V values per thread, 16 butterflies per tile
+  static constexpr int V = AD_FFT_PF_V;
+  static constexpr int T = FftPlan<R, V>::T;
+  static constexpr int F = 16;
+  static constexpr int BLOCK = F * T;
+};
+// PACKIN (CorrelateFFT's second forward pass after k_corr_split0, Ns = that
+// pass's radix K0): the input holds each first-pass column's real
+// transforms A, B in the split slot form, and butterfly j = cg K0 + k of
+// this pass reads slot k of its rows, so the butterflies k and K0 - k read
+// the same two slots {k, K0 - k} (A[k] and B[k]).  A tile is 8 butterflies
+// k = kb .. kb+7 (kb < K0/2) and their 8 mirrors K0 - k (K0/2 for k = 0):
+// each pair of loads gives z[k] = sa A + i sb B and z[K0-k] = sa conj(A) +
+// i sb conj(B) (sa, sb from the first pass's max-abs partials), the packed
+// first-pass output the plain form would read.
+template <int R, bool FWD, bool PACKIN = false>
+__global__ __launch_bounds__((PfShape<R>::BLOCK)) __attribute__((amdgpu_waves_per_eu(4))) void k_fft_pass_pf(
+    FftPassArgs a, int tiles) {
+  using Sh = PfShape<R>;
+  using Plan = FftPlan<R, Sh::V>;
+  constexpr int V = Sh::V, T = Plan::T, F = Sh::F, BLOCK = Sh::BLOCK, MP = Plan::MP + (T >= 16 ? 1 : 0);
+  static_assert(BLOCK % R == 0, "k_fft_pass_pf: whole butterflies per store row");
+  static_assert(!PACKIN || (V % 2 == 0 && F == 16), "PACKIN: load pairs, 8 + 8 butterflies per tile");
+  __shared__ __attribute__((aligned(16))) double2 lds_all[F * MP];
+  __shared__ __attribute__((aligned(16))) double2 ltw[TwSplit<R>::N];
+  const int64_t nb = a.N / R, Ns = a.Ns;
+  const double2* in = a.in + blockIdx.y * a.in_batch;
+  double2* out = a.out + blockIdx.y * a.out_batch;
+  const TwLds<R> twr = tw_lds_compute<R>(ltw, (int)threadIdx.x, BLOCK);
+  const int G = (int)gridDim.x;
+  int tile = xcd_remap((int)blockIdx.x, G);
+  typedef double d2v __attribute__((ext_vector_type(2)));  // (a double2 struct copy becomes a memcpy through scratch)
+  d2v pf[V];
+  // PACKIN tiles: column group cg, butterflies kb .. kb+7 and their mirrors
+  const int tpg = PACKIN ? (int)(Ns / 16) : 1;  // tiles per column group
+  auto kmir = [&](int k) { return k == 0 ? (int)(Ns / 2) : (int)Ns - k; };
+  // element (jj, r) of tile t is in[t F + jj + r nb]; idx = i BLOCK + thread
+  // gives jj = thread % F, r = i BLOCK / F + thread / F: a wave-uniform base
+  // per i plus one 32-bit lane offset (global loads with an SGPR base).
+  // PACKIN: e = i BLOCK + thread (i < V/2), jj = e % 8, r = e / 8: slots
+  // kb + jj and kmir(kb + jj) of row cg Ns + r nb.
+#define AD_PF_LOAD(t, tx)                                                                         \
+  {                                                                                               \
+  if constexpr (PACKIN) {                                                                         \
+    const int64_t cg = (t) / tpg;                                                                  \
+    const int kb = 8 * ((t) % tpg), k = kb + (tx) % 8;                                             \
+    const int64_t lane = (int64_t)((tx) / 8) * nb;                                                 \
+    _Pragma("unroll") for (int i = 0; i < V / 2; ++i) {                                           \
+      const d2v* row = reinterpret_cast<const d2v*>(in + cg * Ns + (int64_t)(i * (BLOCK / 8)) * nb + lane); \
+      pf[2 * i] = row[k];                                                                         \
+      pf[2 * i + 1] = row[AD_PACKIN_EXP == 1 ? k + 8 : kmir(k)];                                   \
+    }                                                                                             \
+  } else {                                                                                        \
+    const uint32_t lane_off = (uint32_t)(((int64_t)((tx) % F) + (int64_t)((tx) / F) * nb) * 16);   \
+    _Pragma("unroll") for (int i = 0; i < V; ++i) {                                               \
+      const char* base = reinterpret_cast<const char*>(in + (int64_t)(t) * F + (int64_t)(i * (BLOCK / F)) * nb); \
+      pf[i] = *reinterpret_cast<const d2v*>(base + lane_off);                                     \
+    }                                                                                             \
+  }                                                                                               \
+  }
+  if (tile < tiles) AD_PF_LOAD(tile, (int)threadIdx.x)
+  // PACKIN: the packing scales from the first pass's partials (every
+  // workgroup reduces all of them; workgroup 0 also stores the totals at
+  // amax[0..1] for the last inverse pass)
+  PackScale ps{};
+  if constexpr (PACKIN) {
+    __shared__ unsigned long long wred[2][BLOCK / 64];
+    // 16-B loads, all of a thread's in flight at once (with the first tile's):
+    // one memory round trip, not one per loop trip (every workgroup starts here)
+    unsigned long long ma = 0, mb = 0;
+    const ulonglong2* pa = reinterpret_cast<const ulonglong2*>(a.amax_part);  // amax + 8 words: 16-B aligned
+    const int n2 = a.amax_parts / 2;  // even (host)
+    constexpr int U = 4;
+    for (int b0 = 0; b0 < n2; b0 += U * BLOCK) {
+      ulonglong2 va[U], vb[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {  // clamped, not guarded: a repeated partial leaves the max as it is
+        const int i = min(b0 + u * BLOCK + (int)threadIdx.x, n2 - 1);
+        va[u] = pa[i];
+        vb[u] = pa[n2 + i];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        ma = va[u].x > ma ? va[u].x : ma;
+        ma = va[u].y > ma ? va[u].y : ma;
+        mb = vb[u].x > mb ? vb[u].x : mb;
+        mb = vb[u].y > mb ? vb[u].y : mb;
+      }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      const unsigned long long ta = __shfl_xor(ma, o), tb = __shfl_xor(mb, o);
+      ma = ta > ma ? ta : ma;
+      mb = tb > mb ? tb : mb;
+    }
+    if ((threadIdx.x & 63) == 0) {
+      wred[0][threadIdx.x >> 6] = ma;
+      wred[1][threadIdx.x >> 6] = mb;
+    }
+    __syncthreads();
+    ma = 0;
+    mb = 0;
+    for (int w = 0; w < BLOCK / 64; ++w) {
+      ma = wred[0][w] > ma ? wred[0][w] : ma;
+      mb = wred[1][w] > mb ? wred[1][w] : mb;
+    }
+    ps = pack_scale_bits(ma, mb);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      unsigned long long* tot = const_cast<unsigned long long*>(a.amax);
+      tot[0] = ma;
+      tot[1] = mb;
+    }
+  }
+  for (; tile < tiles; tile += G) {
+    // the thread index through an opaque copy each tile: its LDS and global
+    // offsets are recomputed per tile (a few VALU ops) instead of ~30 of them
+    // staying live across the loop and spilling beside the prefetch registers
+    int tx;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(tx) : "v"((int)threadIdx.x));
+    const int f = tx / T, tid = tx % T;
+    double2* lds = lds_all + f * MP;
+    const int64_t j0 = (int64_t)tile * F;
+    const int64_t cg = PACKIN ? tile / tpg : 0;
+    const int kb = PACKIN ? 8 * (tile % tpg) : 0;
+    // butterfly of tile slot s (PACKIN: kb + s, then the mirrors)
+    auto jbut = [&](int sl) -> int64_t {
+      if constexpr (PACKIN) return cg * Ns + (sl < 8 ? kb + sl : kmir(kb + sl - 8));
+      return j0 + sl;
+    };
+    double2 twb, twc;  // pre-twiddle factors, evaluated before the next tile's loads take their registers
+    if (Ns > 1) pretwiddle_uc<R, V, FWD>(jbut(f), Ns, a.N, tid, a.tw_lo, a.tw_hi, a.S, &twb, &twc);
+    pass_lds_barrier();  // the previous tile's stage-out reads (and the twiddle tables) are done
+    if constexpr (PACKIN) {
+#pragma unroll
+      for (int i = 0; i < V / 2; ++i) {
+        const int e = i * BLOCK + tx, jj = e % 8, r = e / 8;
+        const d2v A = pf[2 * i], B = pf[2 * i + 1];
+        // k > 0: A = A[k], B = B[k]: z[k] = sa A + i sb B, z[K0-k] = sa conj(A) + i sb conj(B).
+        // k = 0: slots 0 and K0/2 hold the real pairs (A[0], B[0]) and (A[K0/2], B[K0/2]).
+        // Selects, not branches (a branch here makes the compiler drain the loads).
+        const bool self = kb + jj == 0;
+        const double ax = ps.a * A.x, ay = ps.a * A.y, bx = ps.b * B.x, by = ps.b * B.y;
+        const double2 zA = self ? make_double2(ax, ps.b * A.y) : make_double2(ax - by, ay + bx);
+        const double2 zB = self ? make_double2(ps.a * B.x, by) : make_double2(ax + by, bx - ay);
+        lds_all[jj * MP + lds_slot(r)] = zA;
+        lds_all[(8 + jj) * MP + lds_slot(r)] = zB;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < V; ++i) {
+        const int idx = i * BLOCK + tx;
+        lds_all[(idx % F) * MP + lds_slot(idx / F)] = make_double2(pf[i].x, pf[i].y);
+      }
+    }
+    if (tile + G < tiles) AD_PF_LOAD(tile + G, tx)
+    pass_lds_barrier();
+    double2 v[V];
+#pragma unroll
+    for (int s = 0; s < V; ++s) v[s] = lds[lds_slot(pass0_index<R, V>(tid, s))];
+    if (Ns > 1) pretwiddle_apply<R, V>(v, twb, twc);
+    pass_lds_barrier();
+    fft_run_lb<R, V, FWD>(v, tid, lds, twr);
+    pass_lds_barrier();
+#pragma unroll
+    for (int s = 0; s < V; ++s) lds[lds_slot(last_pass_index<R, V>(tid, s))] = v[s];
+    pass_lds_barrier();
+    // output rr of butterfly j0 + jj goes to (jo & ~(Ns-1)) R + (jo & (Ns-1)) + rr Ns:
+    // Ns = 1: contiguous (o = j0 R + idx); Ns >= F: the tile sits in one Ns group, so
+    // o = (j0 & ~(Ns-1)) R + (j0 & (Ns-1)) + i (BLOCK/F) Ns + [jj + (thread/F) Ns]
+    if constexpr (PACKIN) {
+#pragma unroll
+      for (int i = 0; i < V; ++i) {
+        const int idx = i * BLOCK + tx, jj = idx % F, rr = idx / F;
+        const int64_t jo = AD_PACKIN_EXP == 2 ? cg * Ns + 2 * kb + jj : jbut(jj);
+        const double2 val = lds_all[jj * MP + lds_slot(rr)];
+        const int64_t o = (jo & ~(Ns - 1)) * R + (jo & (Ns - 1)) + (int64_t)rr * Ns;
+        __builtin_nontemporal_store(d2v{val.x, val.y}, reinterpret_cast<d2v*>(out + o));
+      }
+    } else if (Ns == 1) {
+      d2v* dst = reinterpret_cast<d2v*>(out + j0 * R) + tx;
+#pragma unroll
+      for (int i = 0; i < V; ++i) {
+        const int idx = i * BLOCK + tx;
+        const double2 val = lds_all[(idx / R) * MP + lds_slot(idx % R)];
+        __builtin_nontemporal_store(d2v{val.x, val.y}, dst + i * BLOCK);
+      }
+    } else {
+      const int64_t ob = (j0 & ~(Ns - 1)) * R + (j0 & (Ns - 1)), ostep = (int64_t)(BLOCK / F) * Ns;
+      const uint32_t olane = (uint32_t)((tx % F) + (int64_t)(tx / F) * Ns);
+#pragma unroll
+      for (int i = 0; i < V; ++i) {
+        const int idx = i * BLOCK + tx;
+        const double2 val = lds_all[(idx % F) * MP + lds_slot(idx / F)];
+        __builtin_nontemporal_store(d2v{val.x, val.y}, reinterpret_cast<d2v*>(out + ob + i * ostep) + olane);
+      }
+    }
+  }
+#undef AD_PF_LOAD
+}
+
+// CorrelateFFT's first forward pass with the max-abs folded in (the "split"
+// form; VERDICT r4's CorrelateFFT item: k_absmax2 read a and b, 134 MB, only
+// for the packing scale).  The packed transform Z = FFT(sa a + i sb b) needs
+// sa, sb before the first pass, but the pass is linear: its butterfly j (a
+// column a_j[r] = a[j + r nb] of 256 samples) is computed here as two REAL
+// 256-point transforms A_j = DFT(a_j), B_j = DFT(b_j), unscaled, each paired
+// with its neighbour column in one complex FFT (a_j + i a_{j+1}; the
+// Hermitian split A = (Z_k + conj Z_-k)/2, A' = (Z_k - conj Z_-k)/2i), so a
+// and b never share a transform before the scale is known.  Real inputs give
+// A_j[256 - k] = conj A_j[k]: slot k of the butterfly's 256 outputs holds
+//   k = 1..127:   A_j[k]          k = 129..255: B_j[256 - k]
+//   k = 0:        (A_j[0], B_j[0])   k = 128:   (A_j[128], B_j[128])   (all real)
+// the same 256 complex values as before.  The workgroup's max|a|, max|b| go
+// to amax[8 + blk], amax[8 + gridDim.x + blk]; the second pass
+// (k_fft_pass_pf's PACKIN form) reduces them and forms
+// sa A_j[k] + i sb B_j[k] = the packed pass-0 output at its load.
+template <int R>
+__global__ __launch_bounds__((PassShape<R>::BLOCK)) void k_corr_split0(FftPassArgs a) {
+  using Sh = PassShape<R>;
+  using Plan = FftPlan<R, Sh::V>;
+  constexpr int V = Sh::V, T = Plan::T, F = Sh::F, BLOCK = Sh::BLOCK, MP = Plan::MP + (T >= 16 ? 1 : 0);
+  static_assert(F == 16 && BLOCK % R == 0, "k_corr_split0: 8 column pairs of a and of b per tile");
+  __shared__ __attribute__((aligned(16))) double2 lds_all[F * MP];
+  __shared__ __attribute__((aligned(16))) double2 ltw[TwSplit<R>::N];
+  __shared__ unsigned long long wmax[2][BLOCK / 64];
+  const int64_t nb = a.N / R;
+  const int64_t j0 = (int64_t)xcd_remap((int)blockIdx.x, (int)gridDim.x) * F;
+  const TwLds<R> twr = tw_lds_compute<R>(ltw, (int)threadIdx.x, BLOCK);
+  double* lds_d = reinterpret_cast<double*>(lds_all);
+  // stage in: column jj of a -> FFT jj/2, of b -> FFT 8 + jj/2 (re: even jj, im: odd)
+  unsigned long long mxa = 0, mxb = 0;
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    const int idx = i * BLOCK + (int)threadIdx.x;
+    const int jj = idx % F, r = idx / F;
+    const int64_t g = j0 + jj + (int64_t)r * nb;
+    const double xa = g < a.nr[0] ? a.xb[0][g] : 0.0;
+    const double xb = g < a.nr[1] ? a.xb[1][g] : 0.0;
+    const unsigned long long ua = (unsigned long long)__double_as_longlong(fabs(xa));
+    const unsigned long long ub = (unsigned long long)__double_as_longlong(fabs(xb));
+    mxa = ua > mxa ? ua : mxa;
+    mxb = ub > mxb ? ub : mxb;
+    lds_d[((jj / 2) * MP + lds_slot(r)) * 2 + (jj & 1)] = xa;
+    lds_d[((F / 2 + jj / 2) * MP + lds_slot(r)) * 2 + (jj & 1)] = xb;
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const unsigned long long ta = __shfl_xor(mxa, o), tb = __shfl_xor(mxb, o);
+    mxa = ta > mxa ? ta : mxa;
+    mxb = tb > mxb ? tb : mxb;
+  }
+  if ((threadIdx.x & 63) == 0) {
+    wmax[0][threadIdx.x >> 6] = mxa;
+    wmax[1][threadIdx.x >> 6] = mxb;
+  }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    unsigned long long m = 0;
+    for (int w = 0; w < BLOCK / 64; ++w) m = wmax[threadIdx.x][w] > m ? wmax[threadIdx.x][w] : m;
+    a.amax_part[threadIdx.x * gridDim.x + blockIdx.x] = m;
+  }
+  const int f = threadIdx.x / T, tid = threadIdx.x % T;
+  double2* lds = lds_all + f * MP;
+  double2 v[V];
+#pragma unroll
+  for (int s = 0; s < V; ++s) v[s] = lds[lds_slot(pass0_index<R, V>(tid, s))];
+  __syncthreads();
+  fft_run<R, V, true>(v, tid, lds, twr);
+  __syncthreads();
+#pragma unroll
+  for (int s = 0; s < V; ++s) lds[lds_slot(last_pass_index<R, V>(tid, s))] = v[s];
+  __syncthreads();
+  // stage out (Ns = 1): slot k of column j0 + jj at (j0 + jj) R + k, contiguous
+  auto split = [&](int fi, int k, int second) {  // DFT of FFT fi's re (second = 0) or im input at bin k
+    const double2 zk = lds_all[fi * MP + lds_slot(k)], zm = lds_all[fi * MP + lds_slot((R - k) & (R - 1))];
+    double2 B;
+    const double2 A = corr_ab(zk, zm, &B);
+    return second ? B : A;
+  };
+  typedef double d2v __attribute__((ext_vector_type(2)));
+  d2v* dst = reinterpret_cast<d2v*>(a.out + j0 * R) + threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    const int idx = i * BLOCK + (int)threadIdx.x;
+    const int k = idx % R, jj = idx / R;
+    const int fa = jj / 2, fb = F / 2 + jj / 2, c = jj & 1;
+    double2 val;
+    if (k == 0 || k == R / 2)
+      val = make_double2(split(fa, k, c).x, split(fb, k, c).x);
+    else if (k < R / 2)
+      val = split(fa, k, c);
+    else
+      val = split(fb, R - k, c);
+    __builtin_nontemporal_store(d2v{val.x, val.y}, dst + i * BLOCK);
   }
 }
 
@@ -699,6 +1107,17 @@ void go_pass(const FftPassArgs& a, int batch, hipStream_t s) {
       return;
     }
   }
+#if AD_FFT_PF && AD_FFT_TWC && AD_FFT_NT == 1
+  if constexpr (!RI && !RO && R == 256) {
+    using Pf = PfShape<R>;
+    const int64_t tiles = a.N / R / Pf::F;
+    if (!a.half && (a.N / R) % Pf::F == 0 && (a.Ns == 1 || a.Ns >= Pf::F) && tiles >= 2 * AD_FFT_PF_G) {
+      hipLaunchKernelGGL((k_fft_pass_pf<R, FWD>), dim3(AD_FFT_PF_G, (unsigned)batch), dim3(Pf::BLOCK), 0, s, a,
+                         (int)tiles);
+      return;
+    }
+  }
+#endif
   hipLaunchKernelGGL((k_fft_pass<R, FWD, RI, RO>), grid, dim3(Sh::BLOCK), 0, s, a);
 }
 
@@ -779,13 +1198,24 @@ void BigFft::run(bool forward, const double2* in, const double* xr, int64_t n_re
   run_passes(forward, a, in, xr, in_batch, out, out_real, out_batch, batch, scratch, s);
 }
 
+// The split first pass (k_corr_split0 + k_fft_pass_pf PACKIN) replaces the
+// max-abs kernel when the forward plan is 256 x 256 x 256 (N = 2^24) and the
+// correlation takes the fused path.
+bool BigFft::corr_split(const BigFft& half) const {
+  return AD_CORR_SPLIT && AD_CORR_FUSED && AD_FFT_PF && radix_.size() == 3 && radix_[0] == 256 &&
+         radix_[1] == 256 && radix_[2] == 256 && !half.radix_.empty() && half.radix_.front() == 256 &&
+         half.radix_.size() >= 2 && N_ / 4096 <= kAbsmaxMaxGroups && N_ / 256 / PfShape<256>::F >= 2 * AD_FFT_PF_G;
+}
+
 void BigFft::correlate_half(const BigFft& half, const double* a_, int64_t n, const double* b_, int64_t m,
                             double2* spec, double* out, double2* scratch, unsigned long long* amax,
                             hipStream_t s) const {
-  const int64_t mx = std::max(n, m);
-  const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>(256, (mx / 2 + 1023) / 1024));
-  hipLaunchKernelGGL(k_absmax2, dim3(gx, 2), dim3(256), 0, s, a_, n, b_, m, amax);
-  AD_HIP(hipGetLastError());
+  if (!corr_split(half)) {  // the split first pass takes the max-abs itself
+    const int64_t mx = std::max(n, m);
+    const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>(AD_ABSMAX_G, (mx / 2 + 1023) / 1024));
+    hipLaunchKernelGGL(k_absmax2, dim3(gx, 2), dim3(256), 0, s, a_, n, b_, m, amax);
+    AD_HIP(hipGetLastError());
+  }
   // lags 0..n-1 from the front, -(m-1)..-1 from the back (correlate.go:165-171)
   spectral_half(half, kSpecCorr, 0.0, nullptr, true, a_, n, b_, m, n, m - 1, N_ - m + 1, spec, out, scratch, s, amax);
 }
@@ -813,7 +1243,36 @@ void BigFft::spectral_half(const BigFft& half, int op, double eps, unsigned long
   if (fused) {
     a.pack2 = 1;
     a.amax = amax;
-    const double2* mid = run_passes(true, a, nullptr, a_, 0, nullptr, nullptr, N_, 1, scratch, s, 0, P - 1);
+    const double2* mid = nullptr;
+    if (amax && corr_split(half)) {
+      // the max-abs folded into the first pass (k_corr_split0), the packing
+      // at the second pass's load (k_fft_pass_pf PACKIN); the rest as below
+      FftPassArgs p0 = a;
+      p0.Ns = 1;
+      p0.twR = twR_[0];
+      p0.out = scratch;
+      p0.amax_part = const_cast<unsigned long long*>(amax) + 8;  // the caller's scratch
+      const int nblk = (int)(N_ / 256 / PassShape<256>::F);
+      hipLaunchKernelGGL(k_corr_split0<256>, dim3((unsigned)nblk), dim3(PassShape<256>::BLOCK), 0, s, p0);
+      AD_HIP(hipGetLastError());
+      FftPassArgs p1 = a;
+      p1.pack2 = 0;
+      p1.in = scratch;
+      p1.in_batch = N_;
+      p1.out = scratch + N_;
+      p1.out_batch = N_;
+      p1.Ns = 256;
+      p1.twR = twR_[1];
+      p1.amax_part = const_cast<unsigned long long*>(amax) + 8;
+      p1.amax_parts = nblk;
+      const int tiles = (int)(N_ / 256 / PfShape<256>::F);
+      hipLaunchKernelGGL((k_fft_pass_pf<256, true, true>), dim3(AD_FFT_PF_G), dim3(PfShape<256>::BLOCK), 0, s, p1,
+                         tiles);
+      AD_HIP(hipGetLastError());
+      mid = scratch + N_;
+    } else {
+      mid = run_passes(true, a, nullptr, a_, 0, nullptr, nullptr, N_, 1, scratch, s, 0, P - 1);
+    }
     CorrFusedArgs f{};
     f.in = mid;
     // the half plan's first scratch half (a consumed forward pass output) unless

@@ -49,6 +49,12 @@ struct FftPassArgs {
   // both halves of a + i b have the same scale, and the last pass multiplies
   // the outputs by 2^-e (both exact).  null: no scaling.
   const unsigned long long* amax;
+  // split correlation (k_corr_split0 / k_fft_pass_pf PACKIN): per-workgroup
+  // max-abs partials of the first pass, [2][amax_parts] (a, then b); the
+  // second pass reduces them and stores the totals at amax[0..1] for the last
+  // inverse pass.
+  unsigned long long* amax_part;
+  int amax_parts;
   // half: the inverse of the Hermitian A conj(B) as an N/2-point transform
   // (this plan is N/2 = NF/2): its first pass forms z[k] = E[k] + i O[k] from
   // X[k] and X[k + NF/2] (E = (X[k] + X[k+NF/2])/2, O = (X[k] - X[k+NF/2]) W_NF^-k / 2,
@@ -112,6 +118,7 @@ class BigFft {
   std::vector<double2*> twR_;  // per pass
   double2* tw_lo_ = nullptr;
   double2* tw_hi_ = nullptr;
+  bool corr_split(const BigFft& half) const;
   const double2* run_passes(bool forward, FftPassArgs a, const double2* in, const double* xr, int64_t in_batch,
                             double2* out, double* out_real, int64_t out_batch, int batch, double2* scratch,
                             hipStream_t s, int p_begin = 0, int p_end = -1) const;
@@ -125,7 +132,8 @@ class BigFft {
 enum SpecOp { kSpecCorr = 0, kSpecNaive = 1, kSpecReg = 2, kSpecInvFilt = 3 };
 // Words of device scratch correlate_half's `amax` needs (zeroed once at
 // allocation: the max-abs kernel leaves its counter at zero after each call).
-constexpr int kAbsmaxWords = 8 + 2 * 256;
+constexpr int kAbsmaxMaxGroups = 4096;  // partials per signal, at most (k_absmax2 workgroups; N / 4096 of k_corr_split0)
+constexpr int kAbsmaxWords = 8 + 2 * kAbsmaxMaxGroups;
 void launch_spec_op(int op, double2* a, const double2* b, int64_t n, double eps, unsigned long long* bad,
                     hipStream_t s);
 

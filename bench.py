@@ -642,6 +642,18 @@ def main_stream(args):
     print(json.dumps(line), flush=True)
 
 
+def _plan_radices(N):
+    """Pass radices of the device FFT plan for size N (bigfft.hip BigFft::BigFft)."""
+    k = max(0, N.bit_length() - 1)
+    if k <= 3:
+        return []
+    if k <= 12:
+        return [N]
+    np_ = (k + 8) // 9
+    base, extra = k // np_, k % np_
+    return [1 << (base + (1 if p < extra else 0)) for p in range(np_)]
+
+
 def main_corr(args):
     """conv.CorrelateFFT (correlate.go:111-172) of two n-sample
     signals, one nextPow2(2n-1) = 2^24-point transform pair on the device
@@ -678,19 +690,29 @@ def main_corr(args):
     dt = time.perf_counter() - t0
     ms = e0.elapsed_time(e1) / args.steps
     N = 1 << (2 * n - 2).bit_length()
-    # algorithmic bytes per call (DESIGN.md "spectral row"): one forward
-    # transform of a + i b (the first pass reads the n + m real samples, zero
-    # padding is not read, and writes 16 B per bin); the inverse at half
-    # length, its first pass reading Z once (A conj(B) from Z's mirror pairs;
-    # the mirror re-reads are not counted) and its last pass writing the
-    # n + m - 1 kept lags
-    from algodsp.conv import _fft_pass_count
-    P = _fft_pass_count(N)
-    Ph = _fft_pass_count(N // 2)
-    fwd = 2 * n * 8 + N * 16 + N * 32 * (P - 1)
-    inv = (N * 16 + (2 * n - 1) * 8 if Ph == 1 else
-           N * 16 + (N // 2) * 16 + (N // 2) * 32 * (Ph - 2) + (N // 2) * 16 + (2 * n - 1) * 8)
-    alg = fwd + inv
+    # algorithmic bytes per call (DESIGN.md "spectral row") of the passes the
+    # call runs: the forward transform of a + i b (its first pass reads the
+    # n + m real samples, zero padding is not read, and writes 16 B per bin;
+    # each middle pass reads and writes 16 B per bin), the inverse at half
+    # length (its middle passes 16 + 16 B per half bin, its last pass reading
+    # 16 B per half bin and writing the n + m - 1 kept lags).  With the fused
+    # forward-last / inverse-first pass (plans of 256 x 256 x ... both sides:
+    # k_corr_fwd_last_inv_first) the packed spectrum Z is never stored: that
+    # pass reads 16 B per bin and writes 16 B per half bin.  The max-abs
+    # pre-pass (another read of a and b) is counted where it still runs.
+    rad = _plan_radices(N)
+    rad_h = _plan_radices(N // 2)
+    P, Ph = len(rad), len(rad_h)
+    fused = P >= 2 and Ph >= 2 and rad[-1] == 256 and rad_h[0] == 256 and N // 256 >= 16
+    split = fused and rad == [256, 256, 256]
+    fwd = 2 * n * 8 + N * 16 + N * 32 * (P - 2 if fused else P - 1)
+    if fused:
+        mid = N * 16 + (N // 2) * 16
+        inv = (N // 2) * 32 * (Ph - 2) + (N // 2) * 16 + (2 * n - 1) * 8
+    else:
+        mid = 0
+        inv = N * 16 + (N // 2) * 16 + (N // 2) * 32 * max(0, Ph - 2) + (N // 2) * 16 + (2 * n - 1) * 8
+    alg = fwd + mid + inv + (0 if split else 2 * n * 8)
     gbs = alg / (ms * 1e-3) / 1e9
     cpu = None
     if not args.no_cpu_baseline:
@@ -721,13 +743,14 @@ def main_corr(args):
         "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f64", "data": "synthetic: SplitMix64 white noise",
         "config": {"workload": f"conv.CorrelateFFT n = m = {n}, FFT size {N} (forward: {P} device passes over a + i b; "
-                               f"inverse: {Ph} passes at N/2), device buffers",
+                               f"inverse: {Ph} passes at N/2{'; forward last + inverse first fused' if fused else ''}"
+                               f"{'; max-abs in the first pass' if split else ''}), device-resident (PCIe excluded)",
                    "fft_size": N},
         "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "note": "whole call: algorithmic bytes of all passes (pointwise op and lag order fused) / event "
-                             "time; traffic = HBM bytes per call from PMC (FETCH_SIZE x2 + WRITE_SIZE, the max-abs "
-                             "pre-pass included)"},
+                     "note": "whole call: algorithmic bytes of the passes it runs (pointwise op, lag order and "
+                             "the Z round trip fused away) / event time; traffic = HBM bytes per call from PMC "
+                             "(FETCH_SIZE x2 + WRITE_SIZE, every kernel of the call)"},
         "cpu_baseline": cpu,
         "wall_ms_per_step": round(dt / args.steps * 1e3, 4),
     }

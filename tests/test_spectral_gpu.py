@@ -85,6 +85,28 @@ def test_correlate_fft_unequal_scales(gpu, n, m, sa, sb):
     close(conv.CorrelateFFT(a, b), O.correlate_fft(a, b))
 
 
+def _np_correlate_fft(a, b):  # same lag order as correlate.go:165-171
+    n, m = len(a), len(b)
+    N = 1 << max(0, (n + m - 2).bit_length())
+    r = np.fft.irfft(np.fft.rfft(a, N) * np.conj(np.fft.rfft(b, N)), N)
+    return np.concatenate([r[N - m + 1:], r[:n]])
+
+
+@pytest.mark.parametrize("n,m,sa,sb", [(1 << 23, 1 << 23, 1.0, 1.0), (10_000_000, 3_000_000, 3.0e4, 3.0e-3),
+                                       ((1 << 24) - 9, 10, 2.0**600, 2.0**-600)])
+def test_correlate_fft_2p24(gpu, n, m, sa, sb):
+    """The bench size's plan (n + m - 1 in (2^23, 2^24]: N = 2^24, passes
+    256 x 256 x 256): the first pass with the max-abs folded in
+    (k_corr_split0), the second forming the packed spectrum at its load
+    (k_fft_pass_pf PACKIN), the fused forward-last / inverse-first pass, at
+    equal, 1e7-apart and 2^1200-apart scales.  Checked against numpy's fp64
+    FFT at the spectral bar: the oracle's C restatement takes ~30 s per call
+    at this size, and test_oracle.py::test_correlate_fft_matches_numpy pins it
+    to the same numpy expression at smaller sizes."""
+    a, b = sa * signals.white_noise(n, 5 + n), sb * signals.white_noise(m, 6 + m)
+    close(conv.CorrelateFFT(a, b), _np_correlate_fft(a, b))
+
+
 def test_correlate_fft_empty(gpu):
     with pytest.raises(conv.ErrEmptyInput):
         conv.CorrelateFFT([], [1.0, 2.0])

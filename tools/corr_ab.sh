@@ -2,6 +2,6 @@ cd "${GRAFT_REPO_ROOT:-.}"
 timeout -k 10 300 python -u -m pytest tests/test_spectral_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/t5.log 2>&1; tail -2 gpurun_out/t5.log
 for v in ${CORR_VARIANTS:-ab/head.so - ab/head.so - ab/head.so -}; do
   if [ "$v" = "-" ]; then L=algo-dsp_amd/libalgodsp_hip.so; else L=$v; fi
-  ALGODSP_LIB=$PWD/$L timeout -k 10 120 python bench.py --workload corr --steps 10 --warmup 3 > gpurun_out/corr.json 2>/dev/null || { echo fail $v; exit 1; }
+  ALGODSP_LIB=$PWD/$L timeout -k 10 120 python bench.py --workload corr --steps ${CORR_STEPS:-10} --warmup 3 > gpurun_out/corr.json 2>/dev/null || { echo fail $v; exit 1; }
   python -c "import json;d=json.loads(open('gpurun_out/corr.json').read().strip().splitlines()[-1]); print('$v', d['value'], d['ms_per_step'], d['roofline']['frac'])"
 done
