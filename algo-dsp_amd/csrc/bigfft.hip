@@ -231,7 +231,10 @@ __global__ __launch_bounds__(256) void k_absmax2(const double* __restrict__ a, i
 #define AD_FFT_PF 1  // plain radix-256 passes as a persistent kernel with the next tile's loads in flight
 #endif
 #ifndef AD_CORR_SPLIT
-#define AD_CORR_SPLIT 0  // CorrelateFFT at N = 2^24: the max-abs inside the first pass (k_corr_split0; measured slower, see DESIGN)
+#define AD_CORR_SPLIT 1  // CorrelateFFT at N = 2^24: the max-abs inside the first pass (k_corr_split0)
+#endif
+#ifndef AD_PACKIN_NT
+#define AD_PACKIN_NT 0
 #endif
 #ifndef AD_PACKIN_EXP
 #define AD_PACKIN_EXP 0  // tools/ timing probes only (wrong results): 1 = mirror loads contiguous, 2 = stores contiguous
@@ -760,7 +763,14 @@ __global__ __launch_bounds__((PfShape<R>::BLOCK)) __attribute__((amdgpu_waves_pe
         const int64_t jo = AD_PACKIN_EXP == 2 ? cg * Ns + 2 * kb + jj : jbut(jj);
         const double2 val = lds_all[jj * MP + lds_slot(rr)];
         const int64_t o = (jo & ~(Ns - 1)) * R + (jo & (Ns - 1)) + (int64_t)rr * Ns;
-        __builtin_nontemporal_store(d2v{val.x, val.y}, reinterpret_cast<d2v*>(out + o));
+        // the mirror run [K0-kb-7, K0-kb] is one element off the 128-B lines: its
+        // partial lines are completed by the neighbouring tile (same XCD), so
+        // they are stored through the L2 (write-back merges them) unless
+        // AD_PACKIN_NT (non-temporal: partial-line writes reach memory)
+        if (AD_PACKIN_NT)
+          __builtin_nontemporal_store(d2v{val.x, val.y}, reinterpret_cast<d2v*>(out + o));
+        else
+          *reinterpret_cast<d2v*>(out + o) = d2v{val.x, val.y};
       }
     } else if (Ns == 1) {
       d2v* dst = reinterpret_cast<d2v*>(out + j0 * R) + tx;
