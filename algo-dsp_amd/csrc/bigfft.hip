@@ -822,22 +822,26 @@ __global__ __launch_bounds__((PassShape<R>::BLOCK)) void k_corr_split0(FftPassAr
   const int64_t nb = a.N / R;
   const int64_t j0 = (int64_t)xcd_remap((int)blockIdx.x, (int)gridDim.x) * F;
   const TwLds<R> twr = tw_lds_compute<R>(ltw, (int)threadIdx.x, BLOCK);
-  double* lds_d = reinterpret_cast<double*>(lds_all);
-  // stage in: column jj of a -> FFT jj/2, of b -> FFT 8 + jj/2 (re: even jj, im: odd)
+  // stage in: columns 2p, 2p + 1 of a -> FFT p (re, im), of b -> FFT 8 + p; a
+  // lane takes one column pair of one row (one 16-B LDS write); slots i < V/2
+  // are a's, the rest b's
   unsigned long long mxa = 0, mxb = 0;
 #pragma unroll
   for (int i = 0; i < V; ++i) {
-    const int idx = i * BLOCK + (int)threadIdx.x;
-    const int jj = idx % F, r = idx / F;
-    const int64_t g = j0 + jj + (int64_t)r * nb;
-    const double xa = g < a.nr[0] ? a.xb[0][g] : 0.0;
-    const double xb = g < a.nr[1] ? a.xb[1][g] : 0.0;
-    const unsigned long long ua = (unsigned long long)__double_as_longlong(fabs(xa));
-    const unsigned long long ub = (unsigned long long)__double_as_longlong(fabs(xb));
-    mxa = ua > mxa ? ua : mxa;
-    mxb = ub > mxb ? ub : mxb;
-    lds_d[((jj / 2) * MP + lds_slot(r)) * 2 + (jj & 1)] = xa;
-    lds_d[((F / 2 + jj / 2) * MP + lds_slot(r)) * 2 + (jj & 1)] = xb;
+    const int sg = i / (V / 2);
+    const int pp = (int)threadIdx.x % 8, r = (i % (V / 2)) * (BLOCK / 8) + (int)threadIdx.x / 8;
+    const double* x = a.xb[sg];
+    const int64_t nr = a.nr[sg];
+    const int64_t g = j0 + 2 * pp + (int64_t)r * nb;
+    const double x0 = g < nr ? x[g] : 0.0, x1 = g + 1 < nr ? x[g + 1] : 0.0;
+    const unsigned long long u0 = (unsigned long long)__double_as_longlong(fabs(x0));
+    const unsigned long long u1 = (unsigned long long)__double_as_longlong(fabs(x1));
+    const unsigned long long u = u0 > u1 ? u0 : u1;
+    if (sg == 0)
+      mxa = u > mxa ? u : mxa;
+    else
+      mxb = u > mxb ? u : mxb;
+    lds_all[(sg * (F / 2) + pp) * MP + lds_slot(r)] = make_double2(x0, x1);
   }
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) {
@@ -880,13 +884,15 @@ __global__ __launch_bounds__((PassShape<R>::BLOCK)) void k_corr_split0(FftPassAr
     const int idx = i * BLOCK + (int)threadIdx.x;
     const int k = idx % R, jj = idx / R;
     const int fa = jj / 2, fb = F / 2 + jj / 2, c = jj & 1;
-    double2 val;
-    if (k == 0 || k == R / 2)
-      val = make_double2(split(fa, k, c).x, split(fb, k, c).x);
-    else if (k < R / 2)
-      val = split(fa, k, c);
-    else
-      val = split(fb, R - k, c);
+    // k < R/2: A[k] (k = 0: its pair with B[0] below); k >= R/2: B[R - k]
+    // (k = R/2: its pair with A[R/2]).  Lanes k = 0, R/2 are lane 0 of their
+    // wave: one short divergent step instead of a three-way split of the body.
+    const bool lo = k < R / 2;
+    double2 val = split(lo ? fa : fb, lo ? k : R - k, c);
+    if (k == 0 || k == R / 2) {
+      const double2 o = split(lo ? fb : fa, k, c);
+      val = lo ? make_double2(val.x, o.x) : make_double2(o.x, val.x);
+    }
     __builtin_nontemporal_store(d2v{val.x, val.y}, dst + i * BLOCK);
   }
 }
