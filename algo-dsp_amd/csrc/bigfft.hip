@@ -825,23 +825,31 @@ __global__ __launch_bounds__((PassShape<R>::BLOCK)) void k_corr_split0(FftPassAr
   // stage in: columns 2p, 2p + 1 of a -> FFT p (re, im), of b -> FFT 8 + p; a
   // lane takes one column pair of one row (one 16-B LDS write); slots i < V/2
   // are a's, the rest b's
+  // two 8-B loads per pair (one 16-B load where aligned measured the same:
+  // profiles/r04_split_ab3.txt), all issued before the LDS writes
   unsigned long long mxa = 0, mxb = 0;
+  double2 xv[V];
+  const int pp = (int)threadIdx.x % 8;
+  {
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+      const int sg = i / (V / 2), r = (i % (V / 2)) * (BLOCK / 8) + (int)threadIdx.x / 8;
+      const double* x = a.xb[sg];
+      const int64_t nr = a.nr[sg], g = j0 + 2 * pp + (int64_t)r * nb;
+      xv[i] = make_double2(g < nr ? x[g] : 0.0, g + 1 < nr ? x[g + 1] : 0.0);
+    }
+  }
 #pragma unroll
   for (int i = 0; i < V; ++i) {
-    const int sg = i / (V / 2);
-    const int pp = (int)threadIdx.x % 8, r = (i % (V / 2)) * (BLOCK / 8) + (int)threadIdx.x / 8;
-    const double* x = a.xb[sg];
-    const int64_t nr = a.nr[sg];
-    const int64_t g = j0 + 2 * pp + (int64_t)r * nb;
-    const double x0 = g < nr ? x[g] : 0.0, x1 = g + 1 < nr ? x[g + 1] : 0.0;
-    const unsigned long long u0 = (unsigned long long)__double_as_longlong(fabs(x0));
-    const unsigned long long u1 = (unsigned long long)__double_as_longlong(fabs(x1));
+    const int sg = i / (V / 2), r = (i % (V / 2)) * (BLOCK / 8) + (int)threadIdx.x / 8;
+    const unsigned long long u0 = (unsigned long long)__double_as_longlong(fabs(xv[i].x));
+    const unsigned long long u1 = (unsigned long long)__double_as_longlong(fabs(xv[i].y));
     const unsigned long long u = u0 > u1 ? u0 : u1;
     if (sg == 0)
       mxa = u > mxa ? u : mxa;
     else
       mxb = u > mxb ? u : mxb;
-    lds_all[(sg * (F / 2) + pp) * MP + lds_slot(r)] = make_double2(x0, x1);
+    lds_all[(sg * (F / 2) + pp) * MP + lds_slot(r)] = xv[i];
   }
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) {
