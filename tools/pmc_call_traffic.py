@@ -5,7 +5,8 @@ Usage: python tools/pmc_call_traffic.py <corrprof_dir> [n] > profiles/corr_pmc_t
 
 Sums FETCH_SIZE x 2 (the gfx950 wide-read correction, MI355X_MICROARCH.md) +
 WRITE_SIZE over every adsp:: kernel of the run and divides by the number of
-calls, counted as launches of k_absmax2 (one per call).  Also per kernel
+calls, counted as launches of the call's first kernel: k_corr_split0 (the
+split form at N = 2^24) or k_absmax2 (one per call otherwise).  Also per kernel
 variant (template arguments kept).  bench.py quotes the per-call figure only
 for the same n."""
 import csv
@@ -32,7 +33,7 @@ def load(kind):
 
 ft, fc = load("fetch")
 wt, wc = load("write")
-calls = sum(v for k, v in fc.items() if "k_absmax2" in k)
+calls = sum(v for k, v in fc.items() if "k_corr_split0" in k) or sum(v for k, v in fc.items() if "k_absmax2" in k)
 out = {"per_kernel": {}}
 total = 0.0
 for k in ft:
