@@ -249,7 +249,7 @@ __global__ __launch_bounds__(256) void k_absmax2(const double* __restrict__ a, i
 #define AD_FFT_PF_G 512  // its workgroups (2 per CU)
 #endif
 #ifndef AD_CORR_FUSED_NT
-#define AD_CORR_FUSED_NT 512  // tools/ A/B: 1024 = 8 inverse pairs (128-B input runs), one workgroup per CU
+#define AD_CORR_FUSED_NT 256  // 2 inverse pairs per workgroup, 4 workgroups per CU (512: 0.530 -> 0.522-0.530 ms; 1024 slower)
 #endif
 // Pieces shared by k_fft_pass and the fused CorrelateFFT kernel below, so
 // both round identically.
@@ -917,13 +917,15 @@ __global__ __launch_bounds__((PassShape<R>::BLOCK)) void k_corr_split0(FftPassAr
 // butterflies nbF - j' / nbH - j'.  The inverse butterfly pair {j', nbH - j'}
 // (the mirror tiles of k_fft_pass's PAIR form) needs exactly the four forward
 // butterflies {j', j' + nbH, nbF - j', nbH - j'} (for j' = 0: {0, nbH, nbH/2,
-// 3 nbH/2}, the pair {0, nbH/2}).  A workgroup takes FP = 4 inverse pairs: it
-// loads the 16 forward butterflies' inputs (runs of 4 values), runs the
-// forward pass with k_fft_pass's arithmetic, keeps Z in LDS, forms z with the
-// PAIR form's arithmetic, runs the 8 inverse butterflies (waves 0-3; waves 4-7
-// take the barriers only) and stores their outputs contiguously.  Z never
-// reaches memory, and the values are bit-identical to the two passes run
-// separately (the same operations on the same doubles).
+// 3 nbH/2}, the pair {0, nbH/2}).  A workgroup of NT threads takes
+// FP = NT/128 inverse pairs (NT = 256: 2, four workgroups per CU): it loads
+// the 4 FP forward butterflies' inputs (runs of FP values), runs the forward
+// pass with k_fft_pass's arithmetic, keeps Z in LDS, forms z with the PAIR
+// form's arithmetic, runs the 2 FP inverse butterflies (at 4 values per
+// thread with AD_CORR_INV_V4: every wave busy) and stores their outputs
+// contiguously.  Z never reaches memory.  The forward half is bit-identical
+// to k_fft_pass; the 4-value inverse rounds differently from the 8-value
+// pass (a 4.4.4.4 factoring of the radix-256 butterfly).
 struct CorrFusedArgs {
   const double2* in;  // the forward transform's next-to-last pass output [N]
   double2* out;       // the half inverse's first-pass output [NH]
