@@ -233,6 +233,9 @@ __global__ __launch_bounds__(256) void k_absmax2(const double* __restrict__ a, i
 #ifndef AD_CORR_SPLIT
 #define AD_CORR_SPLIT 1  // CorrelateFFT at N = 2^24: the max-abs inside the first pass (k_corr_split0)
 #endif
+#ifndef AD_SPLIT0_F
+#define AD_SPLIT0_F 16  // k_corr_split0's columns per workgroup (8: 256 threads, 4 workgroups per CU)
+#endif
 #ifndef AD_PACKIN_NT
 #define AD_PACKIN_NT 0
 #endif
@@ -244,6 +247,9 @@ __global__ __launch_bounds__(256) void k_absmax2(const double* __restrict__ a, i
 #endif
 #ifndef AD_FFT_PF_V
 #define AD_FFT_PF_V 8  // its values per thread (4: 1024-thread workgroups)
+#endif
+#ifndef AD_FFT_PF_F
+#define AD_FFT_PF_F 16  // its butterflies per tile (PACKIN: half of them mirrors)
 #endif
 #ifndef AD_FFT_PF_G
 #define AD_FFT_PF_G 512  // its workgroups (2 per CU)
@@ -590,7 +596,7 @@ template <int R>
 struct PfShape {  // k_fft_pass_pf: AD_FFT_PF_V values per thread, 16 butterflies per tile
   static constexpr int V = AD_FFT_PF_V;
   static constexpr int T = FftPlan<R, V>::T;
-  static constexpr int F = 16;
+  static constexpr int F = AD_FFT_PF_F;
   static constexpr int BLOCK = F * T;
 };
 // PACKIN (CorrelateFFT's second forward pass after k_corr_split0, Ns = that
@@ -609,7 +615,8 @@ __global__ __launch_bounds__((PfShape<R>::BLOCK)) __attribute__((amdgpu_waves_pe
   using Plan = FftPlan<R, Sh::V>;
   constexpr int V = Sh::V, T = Plan::T, F = Sh::F, BLOCK = Sh::BLOCK, MP = Plan::MP + (T >= 16 ? 1 : 0);
   static_assert(BLOCK % R == 0, "k_fft_pass_pf: whole butterflies per store row");
-  static_assert(!PACKIN || (V % 2 == 0 && F == 16), "PACKIN: load pairs, 8 + 8 butterflies per tile");
+  static_assert(!PACKIN || (V % 2 == 0 && F % 2 == 0), "PACKIN: load pairs, F/2 butterflies + their mirrors per tile");
+  constexpr int H = F / 2;  // PACKIN: butterflies per half tile
   __shared__ __attribute__((aligned(16))) double2 lds_all[F * MP];
   __shared__ __attribute__((aligned(16))) double2 ltw[TwSplit<R>::N];
   const int64_t nb = a.N / R, Ns = a.Ns;
@@ -621,7 +628,7 @@ __global__ __launch_bounds__((PfShape<R>::BLOCK)) __attribute__((amdgpu_waves_pe
   typedef double d2v __attribute__((ext_vector_type(2)));  // (a double2 struct copy becomes a memcpy through scratch)
   d2v pf[V];
   // PACKIN tiles: column group cg, butterflies kb .. kb+7 and their mirrors
-  const int tpg = PACKIN ? (int)(Ns / 16) : 1;  // tiles per column group
+  const int tpg = PACKIN ? (int)(Ns / F) : 1;  // tiles per column group
   auto kmir = [&](int k) { return k == 0 ? (int)(Ns / 2) : (int)Ns - k; };
   // element (jj, r) of tile t is in[t F + jj + r nb]; idx = i BLOCK + thread
   // gives jj = thread % F, r = i BLOCK / F + thread / F: a wave-uniform base
@@ -632,12 +639,12 @@ __global__ __launch_bounds__((PfShape<R>::BLOCK)) __attribute__((amdgpu_waves_pe
   {                                                                                               \
   if constexpr (PACKIN) {                                                                         \
     const int64_t cg = (t) / tpg;                                                                  \
-    const int kb = 8 * ((t) % tpg), k = kb + (tx) % 8;                                             \
-    const int64_t lane = (int64_t)((tx) / 8) * nb;                                                 \
+    const int kb = H * ((t) % tpg), k = kb + (tx) % H;                                             \
+    const int64_t lane = (int64_t)((tx) / H) * nb;                                                 \
     _Pragma("unroll") for (int i = 0; i < V / 2; ++i) {                                           \
-      const d2v* row = reinterpret_cast<const d2v*>(in + cg * Ns + (int64_t)(i * (BLOCK / 8)) * nb + lane); \
+      const d2v* row = reinterpret_cast<const d2v*>(in + cg * Ns + (int64_t)(i * (BLOCK / H)) * nb + lane); \
       pf[2 * i] = row[k];                                                                         \
-      pf[2 * i + 1] = row[AD_PACKIN_EXP == 1 ? k + 8 : kmir(k)];                                   \
+      pf[2 * i + 1] = row[AD_PACKIN_EXP == 1 ? k + H : kmir(k)];                                   \
     }                                                                                             \
   } else {                                                                                        \
     const uint32_t lane_off = (uint32_t)(((int64_t)((tx) % F) + (int64_t)((tx) / F) * nb) * 16);   \
@@ -659,7 +666,7 @@ __global__ __launch_bounds__((PfShape<R>::BLOCK)) __attribute__((amdgpu_waves_pe
     unsigned long long ma = 0, mb = 0;
     const ulonglong2* pa = reinterpret_cast<const ulonglong2*>(a.amax_part);  // amax + 8 words: 16-B aligned
     const int n2 = a.amax_parts / 2;  // even (host)
-    constexpr int U = 4;
+    constexpr int U = 8;
     for (int b0 = 0; b0 < n2; b0 += U * BLOCK) {
       ulonglong2 va[U], vb[U];
 #pragma unroll
@@ -710,10 +717,10 @@ __global__ __launch_bounds__((PfShape<R>::BLOCK)) __attribute__((amdgpu_waves_pe
     double2* lds = lds_all + f * MP;
     const int64_t j0 = (int64_t)tile * F;
     const int64_t cg = PACKIN ? tile / tpg : 0;
-    const int kb = PACKIN ? 8 * (tile % tpg) : 0;
+    const int kb = PACKIN ? H * (tile % tpg) : 0;
     // butterfly of tile slot s (PACKIN: kb + s, then the mirrors)
     auto jbut = [&](int sl) -> int64_t {
-      if constexpr (PACKIN) return cg * Ns + (sl < 8 ? kb + sl : kmir(kb + sl - 8));
+      if constexpr (PACKIN) return cg * Ns + (sl < H ? kb + sl : kmir(kb + sl - H));
       return j0 + sl;
     };
     double2 twb, twc;  // pre-twiddle factors, evaluated before the next tile's loads take their registers
@@ -722,7 +729,7 @@ __global__ __launch_bounds__((PfShape<R>::BLOCK)) __attribute__((amdgpu_waves_pe
     if constexpr (PACKIN) {
 #pragma unroll
       for (int i = 0; i < V / 2; ++i) {
-        const int e = i * BLOCK + tx, jj = e % 8, r = e / 8;
+        const int e = i * BLOCK + tx, jj = e % H, r = e / H;
         const d2v A = pf[2 * i], B = pf[2 * i + 1];
         // k > 0: A = A[k], B = B[k]: z[k] = sa A + i sb B, z[K0-k] = sa conj(A) + i sb conj(B).
         // k = 0: slots 0 and K0/2 hold the real pairs (A[0], B[0]) and (A[K0/2], B[K0/2]).
@@ -732,7 +739,7 @@ __global__ __launch_bounds__((PfShape<R>::BLOCK)) __attribute__((amdgpu_waves_pe
         const double2 zA = self ? make_double2(ax, ps.b * A.y) : make_double2(ax - by, ay + bx);
         const double2 zB = self ? make_double2(ps.a * B.x, by) : make_double2(ax + by, bx - ay);
         lds_all[jj * MP + lds_slot(r)] = zA;
-        lds_all[(8 + jj) * MP + lds_slot(r)] = zB;
+        lds_all[(H + jj) * MP + lds_slot(r)] = zB;
       }
     } else {
 #pragma unroll
@@ -810,30 +817,29 @@ __global__ __launch_bounds__((PfShape<R>::BLOCK)) __attribute__((amdgpu_waves_pe
 // to amax[8 + blk], amax[8 + gridDim.x + blk]; the second pass
 // (k_fft_pass_pf's PACKIN form) reduces them and forms
 // sa A_j[k] + i sb B_j[k] = the packed pass-0 output at its load.
-template <int R>
-__global__ __launch_bounds__((PassShape<R>::BLOCK)) void k_corr_split0(FftPassArgs a) {
-  using Sh = PassShape<R>;
-  using Plan = FftPlan<R, Sh::V>;
-  constexpr int V = Sh::V, T = Plan::T, F = Sh::F, BLOCK = Sh::BLOCK, MP = Plan::MP + (T >= 16 ? 1 : 0);
-  static_assert(F == 16 && BLOCK % R == 0, "k_corr_split0: 8 column pairs of a and of b per tile");
+template <int R, int FT>
+__global__ __launch_bounds__((FT * FftPlan<R, 8>::T)) void k_corr_split0(FftPassArgs a) {
+  using Plan = FftPlan<R, 8>;
+  constexpr int V = 8, T = Plan::T, F = FT, BLOCK = F * T, MP = Plan::MP + (T >= 16 ? 1 : 0), NP = F / 2;
+  static_assert(F % 2 == 0 && BLOCK % R == 0, "k_corr_split0: column pairs of a and of b, whole output rows");
   __shared__ __attribute__((aligned(16))) double2 lds_all[F * MP];
   __shared__ __attribute__((aligned(16))) double2 ltw[TwSplit<R>::N];
   __shared__ unsigned long long wmax[2][BLOCK / 64];
   const int64_t nb = a.N / R;
   const int64_t j0 = (int64_t)xcd_remap((int)blockIdx.x, (int)gridDim.x) * F;
   const TwLds<R> twr = tw_lds_compute<R>(ltw, (int)threadIdx.x, BLOCK);
-  // stage in: columns 2p, 2p + 1 of a -> FFT p (re, im), of b -> FFT 8 + p; a
+  // stage in: columns 2p, 2p + 1 of a -> FFT p (re, im), of b -> FFT F/2 + p; a
   // lane takes one column pair of one row (one 16-B LDS write); slots i < V/2
   // are a's, the rest b's
   // two 8-B loads per pair (one 16-B load where aligned measured the same:
   // profiles/r04_split_ab3.txt), all issued before the LDS writes
   unsigned long long mxa = 0, mxb = 0;
   double2 xv[V];
-  const int pp = (int)threadIdx.x % 8;
+  const int pp = (int)threadIdx.x % NP;
   {
 #pragma unroll
     for (int i = 0; i < V; ++i) {
-      const int sg = i / (V / 2), r = (i % (V / 2)) * (BLOCK / 8) + (int)threadIdx.x / 8;
+      const int sg = i / (V / 2), r = (i % (V / 2)) * (BLOCK / NP) + (int)threadIdx.x / NP;
       const double* x = a.xb[sg];
       const int64_t nr = a.nr[sg], g = j0 + 2 * pp + (int64_t)r * nb;
       xv[i] = make_double2(g < nr ? x[g] : 0.0, g + 1 < nr ? x[g + 1] : 0.0);
@@ -841,7 +847,7 @@ __global__ __launch_bounds__((PassShape<R>::BLOCK)) void k_corr_split0(FftPassAr
   }
 #pragma unroll
   for (int i = 0; i < V; ++i) {
-    const int sg = i / (V / 2), r = (i % (V / 2)) * (BLOCK / 8) + (int)threadIdx.x / 8;
+    const int sg = i / (V / 2), r = (i % (V / 2)) * (BLOCK / NP) + (int)threadIdx.x / NP;
     const unsigned long long u0 = (unsigned long long)__double_as_longlong(fabs(xv[i].x));
     const unsigned long long u1 = (unsigned long long)__double_as_longlong(fabs(xv[i].y));
     const unsigned long long u = u0 > u1 ? u0 : u1;
@@ -1230,7 +1236,8 @@ void BigFft::run(bool forward, const double2* in, const double* xr, int64_t n_re
 bool BigFft::corr_split(const BigFft& half) const {
   return AD_CORR_SPLIT && AD_CORR_FUSED && AD_FFT_PF && radix_.size() == 3 && radix_[0] == 256 &&
          radix_[1] == 256 && radix_[2] == 256 && !half.radix_.empty() && half.radix_.front() == 256 &&
-         half.radix_.size() >= 2 && N_ / 4096 <= kAbsmaxMaxGroups && N_ / 256 / PfShape<256>::F >= 2 * AD_FFT_PF_G;
+         half.radix_.size() >= 2 && N_ / 256 / AD_SPLIT0_F <= kAbsmaxMaxGroups &&
+         N_ / 256 / PfShape<256>::F >= 2 * AD_FFT_PF_G;
 }
 
 void BigFft::correlate_half(const BigFft& half, const double* a_, int64_t n, const double* b_, int64_t m,
@@ -1278,8 +1285,9 @@ void BigFft::spectral_half(const BigFft& half, int op, double eps, unsigned long
       p0.twR = twR_[0];
       p0.out = scratch;
       p0.amax_part = const_cast<unsigned long long*>(amax) + 8;  // the caller's scratch
-      const int nblk = (int)(N_ / 256 / PassShape<256>::F);
-      hipLaunchKernelGGL(k_corr_split0<256>, dim3((unsigned)nblk), dim3(PassShape<256>::BLOCK), 0, s, p0);
+      constexpr int FT = AD_SPLIT0_F;
+      const int nblk = (int)(N_ / 256 / FT);
+      hipLaunchKernelGGL((k_corr_split0<256, FT>), dim3((unsigned)nblk), dim3(FT * FftPlan<256, 8>::T), 0, s, p0);
       AD_HIP(hipGetLastError());
       FftPassArgs p1 = a;
       p1.pack2 = 0;

@@ -132,7 +132,7 @@ class BigFft {
 enum SpecOp { kSpecCorr = 0, kSpecNaive = 1, kSpecReg = 2, kSpecInvFilt = 3 };
 // Words of device scratch correlate_half's `amax` needs (zeroed once at
 // allocation: the max-abs kernel leaves its counter at zero after each call).
-constexpr int kAbsmaxMaxGroups = 4096;  // partials per signal, at most (k_absmax2 workgroups; N / 4096 of k_corr_split0)
+constexpr int kAbsmaxMaxGroups = 8192;  // partials per signal, at most (k_absmax2 workgroups; k_corr_split0's N / 256 / F)
 constexpr int kAbsmaxWords = 8 + 2 * kAbsmaxMaxGroups;
 void launch_spec_op(int op, double2* a, const double2* b, int64_t n, double eps, unsigned long long* bad,
                     hipStream_t s);
