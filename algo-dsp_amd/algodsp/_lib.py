@@ -177,6 +177,9 @@ def _declare(L: C.CDLL) -> None:
                                        C.c_int]),
         "ad_conv_multi_create": (C.c_int, [c_double_p, C.c_int, i64, i64, C.c_int, C.POINTER(C.c_int32), i64,
                                            C.c_int, C.POINTER(vp)]),
+        "ad_conv_multi_set_schedule": (C.c_int, [vp, C.c_int, i64, i64]),
+        "ad_conv_lowlat_stats": (C.c_int, [vp, c_int64_p, c_int64_p]),
+        "ad_conv_multi_get_schedule": (C.c_int, [vp, C.POINTER(C.c_int), c_int64_p]),
         "ad_conv_multi_process_device": (C.c_int, [vp, vp, i64, i64, vp, i64, i64, vp]),
         "ad_conv_multi_process_device_segment": (C.c_int, [vp, vp, i64, i64, vp, i64, i64, i64, i64, vp]),
         "ad_conv_multi_process_device_mix": (C.c_int, [vp, vp, i64, i64, vp, i64, i64, C.c_int, i64, i64, vp]),
@@ -204,6 +207,7 @@ def _declare(L: C.CDLL) -> None:
         "ad_compressor_default_config": (None, [C.POINTER(CompressorConfig), C.c_double]),
         "ad_fx_chain_create": (C.c_int, [C.c_int, C.c_int, C.POINTER(vp)]),
         "ad_fx_chain_set_eq": (C.c_int, [vp, c_double_p, C.c_int, C.c_int]),
+        "ad_fx_eq_noise": (C.c_int, [c_double_p, C.c_int, C.c_int, c_double_p]),
         "ad_fx_chain_set_compressor": (C.c_int, [vp, C.POINTER(CompressorConfig)]),
         "ad_fx_chain_set_expander": (C.c_int, [vp, C.POINTER(CompressorConfig), C.c_int, C.c_double, C.c_double]),
         "ad_fx_chain_set_freeverb": (C.c_int, [vp, C.c_double, C.c_double, C.c_double, C.c_double, C.c_double]),

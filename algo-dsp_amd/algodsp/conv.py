@@ -60,6 +60,13 @@ class _Handle:
     def FFTSize(self) -> int:
         return int(lib().ad_conv_fft_size(self._h))
 
+    def LowLatencyStats(self):
+        """(calls that took a pre-enqueued launch, pre-enqueued launches that
+        timed out) of a streaming or partitioned handle (ad_conv_lowlat_stats)."""
+        a, b = C.c_int64(), C.c_int64()
+        check(lib().ad_conv_lowlat_stats(self._h, C.byref(a), C.byref(b)))
+        return a.value, b.value
+
     # host-buffer I/O of batch / multi-channel calls (include/algodsp.h ad_conv_set_host_io)
     HOST_IO_AUTO, HOST_IO_STAGE, HOST_IO_REGISTER = 0, 1, 2
 
@@ -362,6 +369,21 @@ class MultiChannelConvolver(_Handle):
         self.kernel_len = K
 
     KERNELS = ("k_window_rfft", "k_fdl_mac", "k_irfft_store")
+    SCHED_SERIAL = 0     # include/algodsp.h AD_CONV_SCHED_*
+    SCHED_PIPELINED = 1
+
+    def set_schedule(self, mode: int, chunk_blocks: int = 0, run_blocks: int = 0) -> None:
+        """Offline schedule of the device calls (ad_conv_multi_set_schedule):
+        SCHED_SERIAL or SCHED_PIPELINED (chunks kept in the Infinity Cache,
+        K2 / K3 on internal streams); bit-identical results."""
+        check(lib().ad_conv_multi_set_schedule(self._h, int(mode), int(chunk_blocks), int(run_blocks)))
+
+    def schedule(self):
+        """(mode, chunk_blocks) the next signal runs with (chunk 0: serial)."""
+        m = C.c_int()
+        c = C.c_int64()
+        check(lib().ad_conv_multi_get_schedule(self._h, C.byref(m), C.byref(c)))
+        return m.value, c.value
 
     def profile_enable(self, on: bool = True, kernels: int = 7) -> None:
         """Event timing of the engine's launches; kernels: bit k = KERNELS[k]."""

@@ -86,6 +86,23 @@ struct DevBuf {
   }
 };
 
+// Library-owned streams (non-blocking), counted process-wide for gate_acquire.
+hipError_t lib_stream_create(hipStream_t* s);
+hipError_t lib_stream_destroy(hipStream_t s);
+
+// Pre-enqueued launches that wait in their stream for a host go word (the
+// streaming chains' gated K1, the partitioned engine's gated emit) hold up
+// every later launch that shares their hardware queue.  HIP maps streams onto
+// GPU_MAX_HW_QUEUES hardware queues (4 on the MI355X boxes): with more
+// streams than that, streams share queues.  So a handle arms such a launch
+// only while no other handle has one armed (gate_acquire takes the one
+// process-wide slot for `owner`; true if owner already holds it) and while
+// the library owns at most kGateMaxStreams streams (one queue left for the
+// caller's); gate_release(owner) frees the slot (no-op for another owner).
+constexpr int kGateMaxStreams = 3;
+bool gate_acquire(const void* owner);
+void gate_release(const void* owner);
+
 // Validates a device index (no CPU fallback: no device is an error).
 inline int pick_device(int device) {
   int n = 0;

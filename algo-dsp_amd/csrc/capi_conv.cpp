@@ -126,6 +126,8 @@ struct ad_conv {
   double gate_gap_ms = 0;
   int gate_misses = 0;
   std::chrono::steady_clock::time_point gate_last{};
+  uint64_t gate_khz = 100000;   // the device's real-time counter, ticks per ms
+  int64_t gate_hits = 0, gate_timeouts = 0;  // ad_conv_lowlat_stats
 
   // time-domain streaming path (blocks of fewer than 64 samples)
   bool direct_stream = false;
@@ -164,6 +166,7 @@ struct ad_conv {
       __atomic_store_n(&ctl->go, kGateAbort, __ATOMIC_RELEASE);
       if (stream) (void)hipStreamSynchronize(stream);
     }
+    gate_release(this);
     pipe.reset();
     if (done) {
       (void)hipEventSynchronize(done);
@@ -175,7 +178,7 @@ struct ad_conv {
     if (pin_in) (void)hipHostFree(pin_in);
     if (pin_out) (void)hipHostFree(pin_out);
     if (ctl) (void)hipHostFree(ctl);
-    if (stream) (void)hipStreamDestroy(stream);
+    if (stream) (void)lib_stream_destroy(stream);
   }
 };
 
@@ -186,7 +189,7 @@ ad_conv* new_handle(Kind k, int device) {
   h->kind = k;
   h->device = device;
   DeviceScope ds(device);
-  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (lib_stream_create(&h->stream) != hipSuccess) {
     delete h;
     AD_FAIL(AD_ERR_DEVICE, "hipStreamCreate failed");
   }
@@ -258,6 +261,7 @@ void gate_setup(ad_conv* h) {
   AD_HIP(hipMemsetAsync(h->gate_word.p, 0, sizeof(uint64_t), h->stream));
   int khz = 0;
   if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, h->device) != hipSuccess || khz <= 0) khz = 100000;
+  h->gate_khz = (uint64_t)khz;
   h->gate_timeout = (uint64_t)khz * 20;  // 20 ms: a later block runs through ordinary launches
 }
 
@@ -286,7 +290,10 @@ void gate_enqueue(ad_conv* h, uint64_t sq, bool wait_for_go, int64_t n) {
     g.go = &h->ctl_dev->go;
     g.k1_state = &h->ctl_dev->k1_state;
     g.gate = h->gate_word.p;
-    g.timeout = h->gate_timeout;
+    // the waiting K1 gives up after 4 call intervals (1 .. 20 ms): whatever
+    // shares its hardware queue waits behind it at most that long
+    const double ms = std::clamp(4.0 * h->gate_gap_ms, 1.0, 20.0);
+    g.timeout = (uint64_t)(ms * (double)h->gate_khz);
   }
   h->eng->set_gate(g);
   h->eng->run(h->pin_in_dev, n, n, h->pin_out_dev, n, n, /*use_hist=*/true, h->stream);
@@ -306,6 +313,7 @@ void gate_cancel(ad_conv* h) {
   if (ctl_load(&h->ctl->k1_state) != p) h->eng->rewind(1);
   __atomic_store_n(&h->ctl->go, 0, __ATOMIC_RELEASE);
   h->chain_pending = 0;
+  gate_release(h);
 }
 
 // Whether the next block's chain is pre-enqueued: only while calls come
@@ -323,7 +331,10 @@ bool gate_pre_enqueue(ad_conv* h) {
   }
   h->gate_last = now;
   const double timeout_ms = 20.0;
-  return h->gate_misses < 3 && h->gate_gap_ms < timeout_ms / 4;
+  // one measured interval first; then the process-wide slot (gate_acquire:
+  // one armed launch at a time, and none while the library's streams could
+  // share the caller's hardware queues)
+  return h->gate_misses < 3 && h->gate_gap_ms > 0 && h->gate_gap_ms < timeout_ms / 4 && gate_acquire(h);
 }
 
 // One block of n = hop samples (already in pin_in) through the chains.
@@ -337,14 +348,17 @@ void gate_block(ad_conv* h, int64_t n) {
       h->chain_pending = sq + 1;
     } else {
       h->chain_pending = 0;
+      gate_release(h);
     }
     // done, or this chain's K1 gave up before go (the caller came late)
     gate_spin(h, [&] { return ctl_load(&h->ctl->done) == sq || ctl_load(&h->ctl->k1_state) == (sq | kGateSkipped); });
     if (ctl_load(&h->ctl->done) == sq) {
       h->gate_misses = 0;
+      ++h->gate_hits;
       return;
     }
     ++h->gate_misses;
+    ++h->gate_timeouts;
     gate_cancel(h);       // the chain behind it
     h->eng->rewind(1);    // this block's skipped chain
     gate_enqueue(h, sq, false, n);
@@ -996,6 +1010,15 @@ int ad_conv_convolve(const double* a, int64_t n, const double* b, int64_t m, int
 
 // --- multi-channel device path ---------------------------------------------------
 
+namespace {
+// The device entry points may run the pipelined schedule (Upols::set_schedule).
+struct PipeCall {
+  Upols* e;
+  explicit PipeCall(Upols* eng) : e(eng) { e->set_pipeline_call(true); }
+  ~PipeCall() { e->set_pipeline_call(false); }
+};
+}  // namespace
+
 int ad_conv_multi_create(const double* kernels, int n_ir, int64_t K, int64_t hop, int channels,
                          const int32_t* ir_index, int64_t max_chunk_blocks, int device, ad_conv** out) {
   return create_guarded(out, [&]() -> ad_conv* {
@@ -1023,6 +1046,46 @@ int ad_conv_multi_create(const double* kernels, int n_ir, int64_t K, int64_t hop
   });
 }
 
+int ad_conv_lowlat_stats(const ad_conv* h, int64_t* pre_enqueued, int64_t* timed_out) {
+  return guard([&] {
+    if (!h) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "null handle");
+    int64_t a = 0, b = 0;
+    if (h->nupd) {
+      h->nupd->lowlat_stats(&a, &b);
+    } else {
+      a = h->gate_hits;
+      b = h->gate_timeouts;
+    }
+    if (pre_enqueued) *pre_enqueued = a;
+    if (timed_out) *timed_out = b;
+  });
+}
+
+int ad_conv_multi_set_schedule(ad_conv* h, int mode, int64_t chunk_blocks, int64_t run_blocks) {
+  return guard([&] {
+    if (!h || h->kind != Kind::Multi) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "not a multi-channel convolver");
+    if (chunk_blocks < 0 || chunk_blocks > (1 << 20) || run_blocks < 0 || run_blocks > (1 << 20))
+      AD_FAIL(AD_ERR_INVALID_ARGUMENT, "schedule: chunk / run length out of range");
+    const int m = mode == AD_CONV_SCHED_PIPELINED ? Upols::kSchedPipelined
+                  : mode == AD_CONV_SCHED_CHUNKED ? Upols::kSchedChunked
+                  : mode == AD_CONV_SCHED_SERIAL  ? Upols::kSchedSerial
+                                                  : -1;
+    if (m < 0) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "schedule: unknown mode");
+    DeviceScope ds(h->device);
+    h->eng->set_schedule(m, (int)chunk_blocks, (int)run_blocks);
+  });
+}
+
+int ad_conv_multi_get_schedule(const ad_conv* h, int* mode, int64_t* chunk_blocks) {
+  return guard([&] {
+    if (!h || h->kind != Kind::Multi) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "not a multi-channel convolver");
+    const int sm = h->eng->schedule();
+    const bool p = sm != Upols::kSchedSerial && h->eng->hop() >= 2048;
+    if (mode) *mode = !p ? AD_CONV_SCHED_SERIAL : sm == Upols::kSchedChunked ? AD_CONV_SCHED_CHUNKED : AD_CONV_SCHED_PIPELINED;
+    if (chunk_blocks) *chunk_blocks = p ? h->eng->pipe_chunk() : 0;
+  });
+}
+
 int ad_conv_multi_process_device(ad_conv* h, const double* d_in, int64_t in_stride, int64_t in_len, double* d_out,
                                  int64_t out_stride, int64_t out_len, void* stream) {
   return guard([&] {
@@ -1034,6 +1097,7 @@ int ad_conv_multi_process_device(ad_conv* h, const double* d_in, int64_t in_stri
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);  // NULL = the default (null) stream
     order_after_last(h, s);
     h->eng->begin_offline(s);
+    PipeCall pc(h->eng.get());
     h->eng->run(d_in, in_stride, in_len, d_out, out_stride, out_len, /*use_hist=*/false, s);
     mark_last(h, s);
     h->seg_next = -1;
@@ -1058,6 +1122,7 @@ int ad_conv_multi_process_device_segment(ad_conv* h, const double* d_in, int64_t
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     order_after_last(h, s);
     if (out_begin == 0) h->eng->begin_offline(s);
+    PipeCall pc(h->eng.get());
     h->eng->run(d_in, in_stride, in_len, d_out, out_stride, out_len, /*use_hist=*/false, s, out_begin / L,
                 (out_end + L - 1) / L);
     mark_last(h, s);
@@ -1087,6 +1152,7 @@ int ad_conv_multi_process_device_mix(ad_conv* h, const double* d_in, int64_t in_
     order_after_last(h, s);
     if (out_begin == 0) h->eng->begin_offline(s);
     const int64_t jb = out_begin / L, je = (out_end + L - 1) / L;
+    PipeCall pc(h->eng.get());
     if (h->eng->can_mix()) {
       const MixOut mix{d_mix, mix_stride, first_parity & 1};
       h->eng->run(d_in, in_stride, in_len, nullptr, 0, out_len, /*use_hist=*/false, s, jb, je, false, &mix);

@@ -157,7 +157,7 @@ struct ad_fx_chain {
     for (hipStream_t x : st)
       if (x) {
         (void)hipStreamSynchronize(x);
-        (void)hipStreamDestroy(x);
+        (void)lib_stream_destroy(x);
       }
     for (auto& e2 : ev)
       for (hipEvent_t e : e2)
@@ -166,7 +166,7 @@ struct ad_fx_chain {
     if (ev_last) (void)hipEventDestroy(ev_last);
     if (stream) {
       (void)hipStreamSynchronize(stream);
-      (void)hipStreamDestroy(stream);
+      (void)lib_stream_destroy(stream);
     }
   }
 };
@@ -260,7 +260,7 @@ void fx_run_staged(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hip
   const bool eq = h->nsec > 0, comp = h->comp_on, verb = h->verb_on;
   const int64_t T = std::min(h->chunk > 0 ? h->chunk : kFxChunk, n);
   if (!h->st[0]) {
-    for (auto& x : h->st) AD_HIP(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
+    for (auto& x : h->st) AD_HIP(lib_stream_create(&x));
     for (auto& e2 : h->ev)
       for (auto& e : e2) AD_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     AD_HIP(hipEventCreateWithFlags(&h->ev_in, hipEventDisableTiming));
@@ -446,8 +446,11 @@ double fx_eq_noise(const std::vector<double>& tab, int sets, int nsec) {
     for (int k = 0; k < nsec; ++k) {
       const double* g = tab.data() + ((size_t)c * nsec + k) * kSecStride;
       const ld a1 = g[4], a2 = g[5];
+      // the stability triangle |a2| < 1, |a1| < 1 + a2 (d alone is
+      // also positive for a2 > 1, |a1| > 1 + a2, e.g. a pole at -3.41)
+      if (!(std::fabs(a2) < 1) || !(std::fabs(a1) < 1 + a2)) return INFINITY;  // not stable: no estimate
       const ld d = (1 - a2) * ((1 + a2) * (1 + a2) - a1 * a1);
-      if (!(d > 0) || !std::isfinite((double)d)) return INFINITY;  // not stable: no estimate
+      if (!(d > 0) || !std::isfinite((double)d)) return INFINITY;
       sum += (1 + a2) / d;
     }
     worst = std::max(worst, (double)(std::sqrt(sum) * std::ldexp(1.0L, -52)));
@@ -577,7 +580,7 @@ void fx_run_tp(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hipStre
   const bool eq = h->nsec > 0, comp = h->comp_on, verb = h->verb_on;
   const int64_t T = std::min(h->chunk > 0 ? h->chunk : kFxTpChunk, n);
   if (!h->st[0]) {
-    for (auto& x : h->st) AD_HIP(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
+    for (auto& x : h->st) AD_HIP(lib_stream_create(&x));
     for (auto& e2 : h->ev)
       for (auto& e : e2) AD_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     AD_HIP(hipEventCreateWithFlags(&h->ev_in, hipEventDisableTiming));
@@ -843,11 +846,19 @@ int ad_fx_chain_create(int channels, int device, ad_fx_chain** out) {
     h->device = dev;
     h->channels = channels;
     h->cpad = (channels + 63) / 64 * 64;
-    AD_HIP(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+    AD_HIP(lib_stream_create(&h->stream));
     raw = h.release();
   });
   if (rc == AD_OK && out) *out = raw;
   return rc;
+}
+
+int ad_fx_eq_noise(const double* sections, int nsec, int sets, double* noise) {
+  return guard([&] {
+    if (nsec < 0 || sets < 1 || (nsec > 0 && !sections) || !noise) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "bad EQ section table");
+    const std::vector<double> tab(sections, sections + (size_t)sets * nsec * kSecStride);
+    *noise = nsec > 0 ? fx_eq_noise(tab, sets, nsec) : 0.0;
+  });
 }
 
 int ad_fx_chain_set_eq(ad_fx_chain* h, const double* sections, int nsec, int per_channel) {
@@ -1121,7 +1132,7 @@ struct ad_fir {
     }
     if (stream) {
       (void)hipStreamSynchronize(stream);
-      (void)hipStreamDestroy(stream);
+      (void)lib_stream_destroy(stream);
     }
   }
 };
@@ -1200,7 +1211,7 @@ int ad_fir_create(const double* coeffs, int64_t n_taps, int channels, int device
     f->device = dev;
     f->channels = channels;
     f->N = n_taps;
-    AD_HIP(hipStreamCreateWithFlags(&f->stream, hipStreamNonBlocking));
+    AD_HIP(lib_stream_create(&f->stream));
     AD_HIP(hipEventCreateWithFlags(&f->done, hipEventDisableTiming));
     if (n_taps > 0) {
       f->h.alloc((size_t)n_taps);

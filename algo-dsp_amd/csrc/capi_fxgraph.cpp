@@ -103,13 +103,13 @@ struct ad_fx_graph {
     for (auto& l : lane)
       if (l) {
         (void)hipStreamSynchronize(l);
-        (void)hipStreamDestroy(l);
+        (void)lib_stream_destroy(l);
       }
     chains.clear();
     convs.clear();
     if (stream) {
       (void)hipStreamSynchronize(stream);
-      (void)hipStreamDestroy(stream);
+      (void)lib_stream_destroy(stream);
     }
   }
 };
@@ -400,10 +400,10 @@ int ad_fx_graph_create(const ad_fx_node* nodes, int n_nodes, int channels, int d
     std::unique_ptr<ad_fx_graph> g(new ad_fx_graph());
     g->device = dev;
     g->channels = channels;
-    AD_HIP(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking));
+    AD_HIP(lib_stream_create(&g->stream));
     compile(g.get(), nodes, n_nodes);
     schedule(g.get());
-    for (int l = 1; l < g->lanes_used; ++l) AD_HIP(hipStreamCreateWithFlags(&g->lane[l], hipStreamNonBlocking));
+    for (int l = 1; l < g->lanes_used; ++l) AD_HIP(lib_stream_create(&g->lane[l]));
     AD_HIP(hipEventCreateWithFlags(&g->start_ev, hipEventDisableTiming));
     g->op_ev.assign(g->ops.size(), nullptr);
     for (size_t i = 0; i < g->ops.size(); ++i)

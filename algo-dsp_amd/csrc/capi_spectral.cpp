@@ -13,6 +13,7 @@
 #include <cstring>
 #include <map>
 #include <memory>
+#include <exception>
 #include <mutex>
 #include <string>
 
@@ -47,6 +48,37 @@ struct DeviceCache {
   DevBuf<double2> spec, scratch;
   DevBuf<double> xr, res;
   DevBuf<unsigned long long> bad, amax;
+  // The work buffers (and the first pass's max-abs counter, which the kernel
+  // resets itself) are shared by every call on the device, whatever its
+  // stream: a call waits for the previous call's last launch when that was
+  // enqueued on another stream (two CorrelateFFT calls on two
+  // streams interleaved the counter's increments).
+  hipEvent_t last = nullptr;
+  hipStream_t last_stream = nullptr;
+  bool pending = false;  // `last` covers a device call that may still run
+};
+
+// Orders a call on stream s after the previous call on the device; on
+// destruction records the call's end (device calls) or, for host calls that
+// synchronised s, clears it.
+struct CallOrder {
+  DeviceCache& dc;
+  hipStream_t s;
+  bool async;
+  CallOrder(DeviceCache& c, hipStream_t st, bool device_call) : dc(c), s(st), async(device_call) {
+    if (dc.pending && dc.last_stream != s) AD_HIP(hipStreamWaitEvent(s, dc.last, 0));
+  }
+  ~CallOrder() {
+    if (!async) {
+      if (std::uncaught_exceptions() == 0) dc.pending = false;
+      return;
+    }
+    if (!dc.last && hipEventCreateWithFlags(&dc.last, hipEventDisableTiming) != hipSuccess) return;
+    if (hipEventRecord(dc.last, s) == hipSuccess) {
+      dc.last_stream = s;
+      dc.pending = true;
+    }
+  }
 };
 DeviceCache& cache(int dev) {
   static std::mutex m;
@@ -141,6 +173,7 @@ int ad_correlate_fft(const double* a, int64_t n, const double* b, int64_t m, dou
     DeviceCache& dc = cache(dev);
     std::lock_guard<std::mutex> g(dc.mu);
     hipStream_t s = nullptr;
+    CallOrder order(dc, s, /*device_call=*/false);
     const int64_t N = next_pow2(n + m - 1);  // correlate.go:119
     SpectralRun run(dc, N);
     // the caller's arrays page-locked for the call: DMA, not pageable staging
@@ -183,6 +216,7 @@ int ad_correlate_fft_device(const double* a, int64_t n, const double* b, int64_t
     DeviceCache& dc = cache(dev);
     std::lock_guard<std::mutex> g(dc.mu);
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    CallOrder order(dc, s, /*device_call=*/true);
     const int64_t N = next_pow2(n + m - 1);
     SpectralRun run(dc, N);
     if (run.fused()) {
@@ -203,7 +237,7 @@ int ad_correlate_fft_device(const double* a, int64_t n, const double* b, int64_t
       AD_HIP(hipMemcpyAsync(out, run.res() + (N - m + 1), (size_t)(m - 1) * sizeof(double), hipMemcpyDeviceToDevice,
                             s));
     // asynchronous on the caller's stream: the cached work buffers are reused
-    // only by later calls, which the lock and stream order serialise
+    // only by later calls, which the lock and CallOrder serialise
   });
 }
 
@@ -247,6 +281,7 @@ int ad_deconvolve(const double* signal, int64_t n, const double* kernel, int64_t
     DeviceCache& dc = cache(dev);
     std::lock_guard<std::mutex> g(dc.mu);
     hipStream_t s = nullptr;
+    CallOrder order(dc, s, /*device_call=*/false);
     SpectralRun run(dc, N);
     const HostPin ps(signal, (size_t)n * 8), pk(kernel, (size_t)m * 8), po(out, (size_t)olen * 8);
     if (run.fused()) {
@@ -310,6 +345,7 @@ int ad_inverse_filter(const double* kernel, int64_t m, int64_t length, double ep
     DeviceCache& dc = cache(dev);
     std::lock_guard<std::mutex> g(dc.mu);
     hipStream_t s = nullptr;
+    CallOrder order(dc, s, /*device_call=*/false);
     SpectralRun run(dc, N);
     const int64_t mk = m < N ? m : N;  // kernel truncated to the transform (:367)
     const HostPin pk(kernel, (size_t)mk * 8), po(out, (size_t)length * 8);

@@ -192,8 +192,8 @@ HostPin::~HostPin() {
 }
 
 HostPipeline::HostPipeline(int) {
-  AD_HIP(hipStreamCreateWithFlags(&s_in_, hipStreamNonBlocking));
-  AD_HIP(hipStreamCreateWithFlags(&s_out_, hipStreamNonBlocking));
+  AD_HIP(lib_stream_create(&s_in_));
+  AD_HIP(lib_stream_create(&s_out_));
   for (int i = 0; i < 2; ++i) {
     AD_HIP(hipEventCreateWithFlags(&ev_in_[i], hipEventDisableTiming));
     AD_HIP(hipEventCreateWithFlags(&ev_out_[i], hipEventDisableTiming));
@@ -211,8 +211,8 @@ HostPipeline::~HostPipeline() {
     if (ev_out_[i]) (void)hipEventDestroy(ev_out_[i]);
   }
   if (ev_comp_) (void)hipEventDestroy(ev_comp_);
-  if (s_in_) (void)hipStreamDestroy(s_in_);
-  if (s_out_) (void)hipStreamDestroy(s_out_);
+  if (s_in_) (void)lib_stream_destroy(s_in_);
+  if (s_out_) (void)lib_stream_destroy(s_out_);
 }
 
 void HostPipeline::ensure_pinned(int64_t doubles) {

@@ -297,8 +297,12 @@ void ctl_spin(hipStream_t s, Pred&& pred) {
 // (interval EMA under 5 ms, fewer than 3 timed-out emits in a row): a paced
 // caller gets ordinary launches, not a workgroup polling through its period.
 void NupolsDev::gate_arm(int64_t n, bool mix, double wet, double dry, hipStream_t s) {
-  if (C_ != 1 || n > 256 || gp_.on || gmiss_ >= 3 || gap_ms_ >= 5.0) return;
+  // one measured call interval first (gap_ms_ > 0), and back-to-back calls only
+  if (C_ != 1 || n > 256 || gp_.on || gmiss_ >= 3 || gap_ms_ <= 0 || gap_ms_ >= 5.0) return;
   if (emitted_ + n - lambda_ > complete_upto()) return;
+  // the process-wide slot (ad_common.hpp): no other handle's launch waiting,
+  // and no more library streams than hardware queues to spare
+  if (!gate_acquire(this)) return;
   if (!gctl_) {
     AD_HIP(hipHostMalloc(reinterpret_cast<void**>(&gctl_), sizeof(GateCtl), hipHostMallocMapped | hipHostMallocCoherent));
     std::memset(gctl_, 0, sizeof(GateCtl));
@@ -306,8 +310,11 @@ void NupolsDev::gate_arm(int64_t n, bool mix, double wet, double dry, hipStream_
     int dev = 0, khz = 0;
     AD_HIP(hipGetDevice(&dev));
     if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0) khz = 100000;
-    gtimeout_ = (uint64_t)khz * 20;  // 20 ms
+    gkhz_ = (uint64_t)khz;
   }
+  // the emit gives up after 4 call intervals (1 .. 20 ms): work that shares
+  // its hardware queue waits behind it at most that long
+  gtimeout_ = (uint64_t)(std::clamp(4.0 * gap_ms_, 1.0, 20.0) * (double)gkhz_);
   const int slot = in_slot_;
   in_slot_ ^= 1;
   if (in_used_[slot]) AD_HIP(hipEventSynchronize(ev_in_[slot]));
@@ -351,6 +358,7 @@ void NupolsDev::gate_cancel(hipStream_t s) {
   }
   __atomic_store_n(&gctl_->go, 0, __ATOMIC_RELEASE);
   gp_.on = false;
+  gate_release(this);
 }
 
 void NupolsDev::process_host(const double* in, double* out, int64_t n, bool mix, double wet, double dry,
@@ -379,8 +387,10 @@ void NupolsDev::process_host(const double* in, double* out, int64_t n, bool mix,
       return v == sq || v == (sq | kGateSkipped);
     });
     gp_.on = false;
+    gate_release(this);
     if (ctl_load(&gctl_->state) == sq) {
       gmiss_ = 0;
+      ++ghits_;
       run_stages(emitted_, s);
       gate_arm(n, mix, wet, dry, s);
       ctl_spin(s, [&] { return ctl_load(&gctl_->done) == sq; });
@@ -388,6 +398,7 @@ void NupolsDev::process_host(const double* in, double* out, int64_t n, bool mix,
       return;
     }
     ++gmiss_;  // it gave up before this call came: roll back and run the ordinary path
+    ++gtimeouts_;
     AD_HIP(hipStreamSynchronize(s));
     emitted_ -= n;
     received_ -= n;
@@ -425,6 +436,7 @@ void NupolsDev::process_host(const double* in, double* out, int64_t n, bool mix,
     AD_HIP(hipEventRecord(ev_emit_, s));
   }
   in_used_[slot] = true;
+  if (gmiss_ >= 3 && gap_ms_ > 0 && gap_ms_ < 1.0) gmiss_ = 0;  // back to back again: retry (as gate_block)
   gate_arm(n, mix, wet, dry, s);
   AD_HIP(hipEventSynchronize(ev_emit_));
   std::memcpy(out, out_h_, (size_t)n * C_ * sizeof(double));
@@ -432,6 +444,7 @@ void NupolsDev::process_host(const double* in, double* out, int64_t n, bool mix,
 
 NupolsDev::~NupolsDev() {
   if (gp_.on && gctl_) __atomic_store_n(&gctl_->go, kGateAbort, __ATOMIC_RELEASE);  // release the waiting emit
+  gate_release(this);
   if (gctl_) {
     (void)hipDeviceSynchronize();
     (void)hipHostFree(gctl_);

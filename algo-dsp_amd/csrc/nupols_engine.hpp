@@ -47,6 +47,11 @@ class NupolsDev {
   void process_host(const double* in, double* out, int64_t n, bool mix, double wet, double dry, hipStream_t s);
   void reset(hipStream_t s);
   int channels() const { return C_; }
+  // host calls that took a pre-enqueued emit / whose pre-enqueued emit timed out
+  void lowlat_stats(int64_t* hits, int64_t* timeouts) const {
+    if (hits) *hits = ghits_;
+    if (timeouts) *timeouts = gtimeouts_;
+  }
   ~NupolsDev();
 
  private:
@@ -86,6 +91,8 @@ class NupolsDev {
   } gp_;
   double gap_ms_ = 0;
   int gmiss_ = 0;
+  uint64_t gkhz_ = 100000;               // the device's real-time counter, ticks per ms
+  int64_t ghits_ = 0, gtimeouts_ = 0;    // pre-enqueued emits taken / timed out (lowlat_stats)
   std::chrono::steady_clock::time_point glast_{};
   void gate_arm(int64_t n, bool mix, double wet, double dry, hipStream_t s);
   void gate_cancel(hipStream_t s);

@@ -97,6 +97,14 @@ Upols::Upols(int device, const double* kernels, int n_ir, int64_t K, int L, int 
 }
 
 Upols::~Upols() {
+  for (auto st : ps_)
+    if (st) {
+      (void)hipStreamSynchronize(st);
+      (void)lib_stream_destroy(st);
+    }
+  for (auto& row : pev_)
+    for (auto e : row)
+      if (e) (void)hipEventDestroy(e);
   for (auto& r : prof_recs_) {
     (void)hipEventDestroy(r.start);
     (void)hipEventDestroy(r.stop);
@@ -180,6 +188,153 @@ void Upols::begin_offline(hipStream_t) {
   // Spectra with logical index < 0 read as zeros inside k_fdl_mac, so a new
   // signal only restarts the logical block counter (no memset).
   g_next_ = 0;
+  sig_pipe_ = sched_mode_ != kSchedSerial && M_ >= 2048;
+  if (sig_pipe_) ensure_pipe();
+}
+
+void Upols::set_schedule(int mode, int chunk, int run) {
+  if (mode != kSchedSerial && mode != kSchedPipelined && mode != kSchedChunked) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "unknown schedule");
+  if (chunk < 0 || run < 0) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "schedule: negative chunk or run length");
+  sched_mode_ = mode;
+  // auto chunk: 128 blocks per channel of two channels keep the live rings
+  // (two chunks of block spectra + two of Z rows, ~64 MiB each at hop 8192)
+  // inside the 256 MiB Infinity Cache
+  pipe_jc_ = chunk > 0 ? chunk : (int)std::max<int64_t>(32, std::min<int64_t>(jc_max_, 256 / std::max(1, C_)));
+  pipe_jc_ = std::min(pipe_jc_, jc_max_);
+  pipe_run_ = run;
+}
+
+void Upols::ensure_pipe() {
+  const int Qp = 2 * pipe_jc_ + P_ + 2 * PC_ + 1;
+  const int zr = pipe_jc_ + 16;
+  if (Qp != Qp_ || !Xp_.p) {
+    // a resized ring: no kernel of an earlier call may still read the old one
+    for (auto st : ps_)
+      if (st) AD_HIP(hipStreamSynchronize(st));
+    Xp_.alloc((size_t)C_ * (Qp + 1) * MS_);
+    // the zero rows (row Qp of each channel) must read as zeros; every other
+    // row is written by K1 before any kernel reads it
+    AD_HIP(hipMemsetAsync(Xp_.p, 0, Xp_.n * sizeof(double2), stream_));
+    AD_HIP(hipStreamSynchronize(stream_));  // the memset precedes any call stream's use
+    Qp_ = Qp;
+  }
+  if (zr != zrows_p_ || !Zp_.p) {
+    for (auto st : ps_)
+      if (st) AD_HIP(hipStreamSynchronize(st));
+    Zp_.alloc((size_t)2 * C_ * zr * MS_);
+    zrows_p_ = zr;
+  }
+  for (auto& st : ps_)
+    if (!st) AD_HIP(lib_stream_create(&st));
+  for (auto& row : pev_)
+    for (auto& e : row)
+      if (!e) AD_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+}
+
+void Upols::k1(const Chunk& ck, const Rings& rg, const Io& io, const StreamGate& sg, bool ordered, int runR,
+               int runNy, hipStream_t s) {
+  RfftArgs a{};
+  a.x = io.in;
+  a.x_stride = io.in_stride;
+  a.n = io.n;
+  a.s0 = ck.cs * L_;
+  a.jc = ck.jin;
+  a.channels = C_;
+  a.aligned = io.in_aligned;
+  a.X = rg.X;
+  a.x_ch_stride = (int64_t)(rg.Q + 1) * MS_;
+  a.Q = rg.Q;
+  a.slot0 = (int)(ck.g0 % rg.Q);
+  a.MS = MS_;
+  a.twM = tw_.p;
+  a.twN = tw_.p + M_;
+  if (ordered) {
+    a.ord_R = runR;
+    a.ord_ny = runNy;
+    a.ord_pc = PC_;
+  }
+  a.sg = sg;
+  hipEvent_t e0;
+  prof_begin(s, &e0, 0);
+  launch_window_rfft(M_, a, s);
+  // algorithmic bytes per launch: unique input samples in, M+1
+  // complex128 bins out, per (channel, block)
+  prof_end(s, e0, 0, (double)C_ * ck.jin * ((double)L_ * 8 + (double)M_ * 16));
+}
+
+void Upols::k2(const Chunk& ck, const Rings& rg, const StreamGate& sg, int runR, hipStream_t s) {
+  MacArgs m{};
+  m.X = rg.X;
+  m.x_ch_stride = (int64_t)(rg.Q + 1) * MS_;
+  m.Q = rg.Q;
+  m.g0 = ck.g0;
+  m.gend = ck.gend;
+  m.MS = MS_;
+  m.H = H_.p;
+  m.h_ir_stride = (int64_t)P_ * MS_;
+  m.ir_index = irmap_.p;
+  m.n_ir = n_ir_;
+  m.Y = rg.Z;
+  m.y_ch_stride = (int64_t)rg.zrows * MS_;
+  m.jc = ck.jc;
+  m.R = runR;
+  m.P = P_;
+  m.M = M_;
+  m.twN = tw_.p + M_;
+  // Z[M/2] from K3 (split sizes, few partitions): K2 then runs pair waves only
+  m.mid_in_k3 = (M_ >= 2048 && P_ <= 256) ? 1 : 0;
+  m.sg = sg;
+  hipEvent_t e0;
+  prof_begin(s, &e0, 1);
+  launch_fdl_mac(PC_, NH_, m, C_, s);
+  prof_end(s, e0, 1, (double)C_ * ck.jc * (double)(M_ + 1) * 32 + (double)n_ir_ * P_ * (M_ + 1) * 16);
+}
+
+void Upols::k3(const Chunk& ck, const Rings& rg, const Io& io, const StreamGate& sg, bool ordered, int runR,
+               int runNy, hipStream_t s) {
+  IrfftArgs b{};
+  b.Y = rg.Z;
+  b.y_ch_stride = (int64_t)rg.zrows * MS_;
+  b.MS = MS_;
+  b.out = io.mix ? io.mix->p : io.out;
+  b.out_stride = io.mix ? io.mix->stride : io.out_stride;
+  b.out_len = io.out_len;
+  b.o0 = ck.cs * L_;
+  b.jc = ck.jc;
+  b.channels = C_;
+  b.aligned = io.out_aligned;
+  b.accumulate = io.accumulate ? 1 : 0;
+  b.twM = tw_.p;
+  b.twN = tw_.p + M_;
+  if (ordered) {
+    b.ord_R = runR;
+    b.ord_ny = runNy;
+  }
+  if (M_ >= 2048 && P_ <= 256) {
+    b.mid.on = 1;
+    b.mid.X = rg.X;
+    b.mid.x_ch_stride = (int64_t)(rg.Q + 1) * MS_;
+    b.mid.Q = rg.Q;
+    b.mid.g0 = ck.g0;
+    b.mid.gend = ck.gend;
+    b.mid.H = H_.p;
+    b.mid.h_ir_stride = (int64_t)P_ * MS_;
+    b.mid.ir_index = irmap_.p;
+    b.mid.n_ir = n_ir_;
+    b.mid.P = P_;
+  }
+  b.sg = sg;
+  const double blocks = (double)C_ * ck.jc;
+  hipEvent_t e0;
+  prof_begin(s, &e0, 2);
+  if (io.mix) {  // every channel's Z rows in, the two mix rows out
+    b.mix_parity = io.mix->first_parity & 1;
+    launch_irfft_mix(M_, b, s);
+    prof_end(s, e0, 2, blocks * (double)(M_ + 1) * 16 + 2.0 * ck.jc * L_ * 8);
+  } else {
+    launch_irfft_store(M_, b, s);
+    prof_end(s, e0, 2, blocks * ((double)(M_ + 1) * 16 + (double)L_ * 8));
+  }
 }
 
 void Upols::run(const double* d_in, int64_t in_stride, int64_t n, double* d_out, int64_t out_stride, int64_t out_len,
@@ -189,140 +344,113 @@ void Upols::run(const double* d_in, int64_t in_stride, int64_t n, double* d_out,
   if (je < 0) je = (out_len + L_ - 1) / L_;
   const int64_t J = je - jb;
   if (J <= 0) return;
-  const int in_aligned = ((reinterpret_cast<uintptr_t>(d_in) & 15) == 0) && (in_stride % 2 == 0);
-  if (mix) {
-    d_out = mix->p;
-    out_stride = mix->stride;
-  }
-  const int out_aligned = ((reinterpret_cast<uintptr_t>(d_out) & 15) == 0) && (out_stride % 2 == 0);
+  Io io{};
+  io.in = d_in;
+  io.in_stride = in_stride;
+  io.n = n;
+  io.in_aligned = ((reinterpret_cast<uintptr_t>(d_in) & 15) == 0) && (in_stride % 2 == 0);
+  io.out = d_out;
+  io.out_stride = out_stride;
+  io.out_len = out_len;
+  io.accumulate = accumulate;
+  io.mix = mix;
+  const double* op = mix ? mix->p : d_out;
+  const int64_t ostr = mix ? mix->stride : out_stride;
+  io.out_aligned = ((reinterpret_cast<uintptr_t>(op) & 15) == 0) && (ostr % 2 == 0);
   // call blocks holding input samples: [0, nb_in); K1 transforms only those,
   // K2 reads every later block as zeros
   const int64_t nb_in = (std::max<int64_t>(n, 0) + L_ - 1) / L_;
-  // balanced chunks of at most jc_max blocks (no tiny tail launch)
+  if (sig_pipe_ && pipe_call_ && !use_hist && !accumulate && !gate_on_) {
+    run_pipelined(io, s, jb, J, nb_in);
+    return;
+  }
   StreamGate sg{};
   if (gate_on_) {
     if (J != 1 || C_ != 1 || M_ < 2048) AD_FAIL(AD_ERR_INTERNAL, "gated run: one block of one channel, hop >= 2048");
     sg = gate_;
     gate_on_ = false;
   }
+  const Rings rg{X_.p, Q_, Y_.p, jc_max_ + 16};
+  // balanced chunks of at most jc_max blocks (no tiny tail launch)
   const int64_t nchunks = (J + jc_max_ - 1) / jc_max_;
   const int64_t jc_even = (J + nchunks - 1) / nchunks;
   for (int64_t cr = 0; cr < J; cr += jc_even) {
-    const int jc = (int)std::min<int64_t>(jc_even, J - cr);
-    const int64_t cs = jb + cr;  // first output block of this chunk
-    const int slot0 = (int)(g_next_ % Q_);
-    const int jin = (int)std::clamp<int64_t>(nb_in - cs, 0, jc);  // K1 items per channel
-
-    RfftArgs a{};
-    a.x = d_in;
-    a.x_stride = in_stride;
-    a.n = n;
-    a.s0 = cs * L_;
-    a.jc = jin;
-    a.channels = C_;
-    a.aligned = in_aligned;
-    a.X = X_.p;
-    a.x_ch_stride = (int64_t)(Q_ + 1) * MS_;
-    a.Q = Q_;
-    a.slot0 = slot0;
-    a.MS = MS_;
-    a.twM = tw_.p;
-    a.twN = tw_.p + M_;
-    // algorithmic bytes per launch: unique input samples in,
-    // M+1 complex128 bins out, per (channel, block)
-    const double blocks = (double)C_ * jc;
+    Chunk ck{};
+    ck.jc = (int)std::min<int64_t>(jc_even, J - cr);
+    ck.cs = jb + cr;
+    ck.jin = (int)std::clamp<int64_t>(nb_in - ck.cs, 0, ck.jc);
+    ck.g0 = g_next_;
+    ck.gend = g_next_ - ck.cs + nb_in - 1;
     // K2's run geometry, decided here so K1 and K3 can order their items by it
     // (newest rows first for the kernel that reads them next; see RfftArgs)
     int runR = R_, runNy = 0;
-    mac_run_geometry(PC_, NH_, M_, M_ >= 2048 && P_ <= 256 ? 1 : 0, C_, jc, R_, &runR, &runNy);
+    mac_run_geometry(PC_, NH_, M_, M_ >= 2048 && P_ <= 256 ? 1 : 0, C_, ck.jc, R_, &runR, &runNy);
     // worth it when the Infinity Cache (256 MiB) holds the rows of a good
     // part of a run: stereo at hop 8192 ~81 of R = 176 steps (step 0.5751 ->
     // 0.5686 ms); the 8-channel shard ~81 of R = 688 (no gain, +0.7 %)
     const int64_t rows_per_step = (int64_t)C_ * runNy;
     const int64_t steps_cached = (int64_t(256) << 20) / ((int64_t)MS_ * 16 * std::max<int64_t>(1, rows_per_step));
-    const bool ordered = M_ >= 2048 && !(NH_ == 1 && jc <= 2) && runNy > 1 &&
-                         steps_cached * 4 >= runR && !mix;
-    if (ordered) {
-      a.ord_R = runR;
-      a.ord_ny = runNy;
-      a.ord_pc = PC_;
-    }
-    a.sg = sg;
-    hipEvent_t e0;
-    prof_begin(s, &e0, 0);
-    launch_window_rfft(M_, a, s);
-    prof_end(s, e0, 0, (double)C_ * jin * ((double)L_ * 8 + (double)M_ * 16));
-
-    MacArgs m{};
-    m.X = X_.p;
-    m.x_ch_stride = (int64_t)(Q_ + 1) * MS_;
-    m.Q = Q_;
-    m.g0 = g_next_;
-    m.gend = g_next_ - cs + nb_in - 1;
-    m.MS = MS_;
-    m.H = H_.p;
-    m.h_ir_stride = (int64_t)P_ * MS_;
-    m.ir_index = irmap_.p;
-    m.n_ir = n_ir_;
-    m.Y = Y_.p;
-    m.y_ch_stride = (int64_t)(jc_max_ + 16) * MS_;
-    m.jc = jc;
-    m.R = runR;
-    m.P = P_;
-    m.M = M_;
-    m.twN = tw_.p + M_;
-    // Z[M/2] from K3 (split sizes, few partitions): K2 then runs pair waves only
-    const bool mid_k3 = M_ >= 2048 && P_ <= 256;
-    m.mid_in_k3 = mid_k3 ? 1 : 0;
-    m.sg = sg;
-    prof_begin(s, &e0, 1);
-    launch_fdl_mac(PC_, NH_, m, C_, s);
-    prof_end(s, e0, 1, blocks * (double)(M_ + 1) * 32 + (double)n_ir_ * P_ * (M_ + 1) * 16);
-
-    IrfftArgs b{};
-    b.Y = Y_.p;
-    b.y_ch_stride = (int64_t)(jc_max_ + 16) * MS_;
-    b.MS = MS_;
-    b.out = d_out;
-    b.out_stride = out_stride;
-    b.out_len = out_len;
-    b.o0 = cs * L_;
-    b.jc = jc;
-    b.channels = C_;
-    b.aligned = out_aligned;
-    b.accumulate = accumulate ? 1 : 0;
-    b.twM = tw_.p;
-    b.twN = tw_.p + M_;
-    if (ordered) {
-      b.ord_R = runR;
-      b.ord_ny = runNy;
-    }
-    if (mid_k3) {
-      b.mid.on = 1;
-      b.mid.X = X_.p;
-      b.mid.x_ch_stride = (int64_t)(Q_ + 1) * MS_;
-      b.mid.Q = Q_;
-      b.mid.g0 = m.g0;
-      b.mid.gend = m.gend;
-      b.mid.H = H_.p;
-      b.mid.h_ir_stride = (int64_t)P_ * MS_;
-      b.mid.ir_index = irmap_.p;
-      b.mid.n_ir = n_ir_;
-      b.mid.P = P_;
-    }
-    b.sg = sg;
-    prof_begin(s, &e0, 2);
-    if (mix) {  // every channel's Z rows in, the two mix rows out
-      b.mix_parity = mix->first_parity & 1;
-      launch_irfft_mix(M_, b, s);
-      prof_end(s, e0, 2, blocks * (double)(M_ + 1) * 16 + 2.0 * jc * L_ * 8);
-    } else {
-      launch_irfft_store(M_, b, s);
-      prof_end(s, e0, 2, blocks * ((double)(M_ + 1) * 16 + (double)L_ * 8));
-    }
+    const bool ordered = M_ >= 2048 && !(NH_ == 1 && ck.jc <= 2) && runNy > 1 && steps_cached * 4 >= runR && !mix;
+    k1(ck, rg, io, sg, ordered, runR, runNy, s);
+    k2(ck, rg, sg, runR, s);
+    k3(ck, rg, io, sg, ordered, runR, runNy, s);
     AD_HIP(hipGetLastError());
-    g_next_ += jc;
+    g_next_ += ck.jc;
   }
+}
+
+// The pipelined offline schedule (set_schedule): chunk k's K1 on the caller's
+// stream s, its K2 on ps_[0], its K3 on ps_[1].  Ring reuse:
+//   - K1(k) overwrites block-spectrum rows that K2 and K3's middle bin of
+//     chunk k-2 read: s waits for K3(k-2) (which follows K2(k-2)); the rows
+//     chunk k-1's kernels read (its blocks and the P + PC rows before them)
+//     are disjoint from chunk k's in a ring of Qp >= 2 chunk + P + 2 PC + 1;
+//   - K2(k) writes Z half k mod 2, which K3(k-2) read: ps_[0] waits for it;
+//   - K2(k) waits for K1(k), K3(k) for K2(k);
+//   - the caller's stream waits for the last K3, so the call's outputs are
+//     complete when s passes it, as in the serial schedule, and the next
+//     call's K1 (on s) follows every kernel of this one.
+void Upols::run_pipelined(const Io& io, hipStream_t s, int64_t jb, int64_t J, int64_t nb_in) {
+  const int jp = pipe_jc_;
+  const int64_t nchunks = (J + jp - 1) / jp;
+  const int64_t jc_even = (J + nchunks - 1) / nchunks;
+  int64_t k = 0;
+  for (int64_t cr = 0; cr < J; cr += jc_even, ++k) {
+    Chunk ck{};
+    ck.jc = (int)std::min<int64_t>(jc_even, J - cr);
+    ck.cs = jb + cr;
+    ck.jin = (int)std::clamp<int64_t>(nb_in - ck.cs, 0, ck.jc);
+    ck.g0 = g_next_;
+    ck.gend = g_next_ - ck.cs + nb_in - 1;
+    const Rings rg{Xp_.p, Qp_, Zp_.p + (size_t)(k & 1) * C_ * zrows_p_ * MS_, zrows_p_};
+    hipEvent_t* e1 = &pev_[0][k & 3];
+    hipEvent_t* e2 = &pev_[1][k & 3];
+    hipEvent_t* e3 = &pev_[2][k & 3];
+    const hipEvent_t e3_prev2 = k >= 2 ? pev_[2][(k - 2) & 3] : nullptr;
+    int runR = pipe_run_, runNy = 0;
+    mac_run_geometry(PC_, NH_, M_, M_ >= 2048 && P_ <= 256 ? 1 : 0, C_, ck.jc, pipe_run_, &runR, &runNy);
+    if (sched_mode_ == kSchedChunked) {
+      k1(ck, rg, io, StreamGate{}, false, runR, runNy, s);
+      k2(ck, rg, StreamGate{}, runR, s);
+      k3(ck, rg, io, StreamGate{}, false, runR, runNy, s);
+      AD_HIP(hipGetLastError());
+      g_next_ += ck.jc;
+      continue;
+    }
+    if (e3_prev2) AD_HIP(hipStreamWaitEvent(s, e3_prev2, 0));
+    k1(ck, rg, io, StreamGate{}, false, runR, runNy, s);
+    AD_HIP(hipEventRecord(*e1, s));
+    AD_HIP(hipStreamWaitEvent(ps_[0], *e1, 0));
+    if (e3_prev2) AD_HIP(hipStreamWaitEvent(ps_[0], e3_prev2, 0));
+    k2(ck, rg, StreamGate{}, runR, ps_[0]);
+    AD_HIP(hipEventRecord(*e2, ps_[0]));
+    AD_HIP(hipStreamWaitEvent(ps_[1], *e2, 0));
+    k3(ck, rg, io, StreamGate{}, false, runR, runNy, ps_[1]);
+    AD_HIP(hipEventRecord(*e3, ps_[1]));
+    AD_HIP(hipGetLastError());
+    g_next_ += ck.jc;
+  }
+  if (sched_mode_ != kSchedChunked) AD_HIP(hipStreamWaitEvent(s, pev_[2][(k - 1) & 3], 0));
 }
 
 void Upols::save_history(const double*, int64_t, int64_t n, hipStream_t) {

@@ -69,6 +69,26 @@ class Upols {
            bool use_hist, hipStream_t s, int64_t jb = 0, int64_t je = -1, bool accumulate = false,
            const MixOut* mix = nullptr);
   bool can_mix() const { return M_ >= 2048; }
+
+  // Offline schedule of the device entry points (ad_conv_multi_set_schedule).
+  // SERIAL: each chunk's K1 -> K2 -> K3 on the caller's stream, chunks of up
+  // to jc_max blocks.  PIPELINED (hop >= 2048): chunks of `chunk` blocks per
+  // channel whose block spectra and Z rows live in small rings that the
+  // Infinity Cache holds; K1 runs on the caller's stream, K2 and K3 on two
+  // internal streams, so K1 of chunk k+1, K2 of chunk k and K3 of chunk k-1
+  // run concurrently (events order the ring reuse), and the caller's stream
+  // waits for the last K3 before the call returns (the ABI's ordering holds).
+  // `run`: K2's run length in blocks (0: auto).  Takes effect at the next
+  // signal start (begin_offline): the segments of one signal share a ring.
+  static constexpr int kSchedSerial = 0;
+  static constexpr int kSchedPipelined = 1;
+  static constexpr int kSchedChunked = 2;  // the pipelined rings and chunks, every kernel on the caller's stream
+  void set_schedule(int mode, int chunk, int run);
+  int schedule() const { return sched_mode_; }
+  int pipe_chunk() const { return pipe_jc_; }
+  // the device entry points opt in (the host-buffer pipeline and the
+  // partitioned stages call run() with their own streams and stay serial)
+  void set_pipeline_call(bool on) { pipe_call_ = on; }
   // Kept for API symmetry: the ring already holds the last block's spectrum
   // (checks that a streaming call covers at least one hop).
   void save_history(const double* d_in, int64_t in_stride, int64_t n, hipStream_t s);
@@ -93,6 +113,47 @@ class Upols {
   DevBuf<double2> X_;    // [C][Q][MS]
   DevBuf<double2> Y_;    // [C][jc_max][MS]
   DevBuf<int> irmap_;    // [C]
+
+  // One chunk of output blocks and the buffers its kernels use.
+  struct Chunk {
+    int64_t cs;     // first output block (call-relative)
+    int jc;         // output blocks per channel
+    int jin;        // K1 items per channel (blocks holding input)
+    int64_t g0;     // logical block of chunk block 0
+    int64_t gend;   // last logical block holding input
+  };
+  struct Rings {
+    double2* X;     // block-spectrum ring [C][Q+1][MS] (row Q: zeros)
+    int Q;
+    double2* Z;     // Z rows [C][zrows][MS]
+    int zrows;
+  };
+  struct Io {
+    const double* in;
+    int64_t in_stride, n;
+    int in_aligned;
+    double* out;
+    int64_t out_stride, out_len;
+    int out_aligned;
+    bool accumulate;
+    const MixOut* mix;
+  };
+  void k1(const Chunk& ck, const Rings& rg, const Io& io, const StreamGate& sg, bool ordered, int runR, int runNy,
+          hipStream_t s);
+  void k2(const Chunk& ck, const Rings& rg, const StreamGate& sg, int runR, hipStream_t s);
+  void k3(const Chunk& ck, const Rings& rg, const Io& io, const StreamGate& sg, bool ordered, int runR, int runNy,
+          hipStream_t s);
+  void run_pipelined(const Io& io, hipStream_t s, int64_t jb, int64_t J, int64_t nb_in);
+
+  int sched_mode_ = kSchedSerial, pipe_jc_ = 0, pipe_run_ = 0;
+  bool pipe_call_ = false;  // this call may pipeline (device entry points)
+  bool sig_pipe_ = false;   // the current signal runs pipelined (fixed at begin_offline)
+  int Qp_ = 0, zrows_p_ = 0;
+  DevBuf<double2> Xp_;      // pipelined block-spectrum ring [C][Qp+1][MS]
+  DevBuf<double2> Zp_;      // pipelined Z rows, two halves [2][C][zrows_p][MS]
+  hipStream_t ps_[2] = {nullptr, nullptr};  // K2, K3 streams
+  hipEvent_t pev_[3][4] = {};               // K1 / K2 / K3 done, per chunk mod 4
+  void ensure_pipe();
 
   struct ProfRec {
     hipEvent_t start, stop;

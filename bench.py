@@ -43,6 +43,12 @@ def parse():
                    help="samples per channel per step (default 2^24)")
     p.add_argument("--hop", type=int, default=8192)
     p.add_argument("--chunk", type=int, default=0, help="blocks per channel per engine chunk (0 = auto)")
+    p.add_argument("--schedule", choices=["serial", "pipelined", "chunked"], default="serial",
+                   help="conv: the engine's offline schedule (ad_conv_multi_set_schedule): serial chunks on the "
+                        "caller's stream, or Infinity-Cache-sized chunks with K1 / K2 / K3 of consecutive chunks "
+                        "overlapped on three streams")
+    p.add_argument("--pipe-chunk", type=int, default=0, help="pipelined schedule: blocks per channel per chunk (0 = auto)")
+    p.add_argument("--pipe-run", type=int, default=0, help="pipelined schedule: K2 run length in blocks (0 = auto)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-sample", type=int, default=1 << 24, help="samples per channel (per host thread) for the CPU leg")
     p.add_argument("--mixdown", choices=["auto", "on", "off"], default="auto")
@@ -368,6 +374,7 @@ def main():
                 "kernel_taps": K,
                 "hop": args.hop,
                 "partitions": (K + args.hop - 1) // args.hop,
+                "schedule": {"mode": ["serial", "pipelined", "chunked"][r["schedule"][0]], "chunk_blocks": r["schedule"][1]},
                 "parallelism": f"channel-group per GPU x{world}" + (" + RCCL reduce mixdown" if mixdown else ""),
             },
             "roofline": {
@@ -492,9 +499,11 @@ def run_conv(args, world, rank, local, dev, ir, C, shard_cfg, mixdown, steps, wa
 
     eng = conv.MultiChannelConvolver(ir, hop=args.hop, channels=C, ir_index=shard.ir_index(ids),
                                      chunk_blocks=args.chunk, device=local)
+    if args.schedule != "serial":
+        eng.set_schedule(["serial", "pipelined", "chunked"].index(args.schedule), args.pipe_chunk, args.pipe_run)
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
-    side = torch.cuda.Stream(dev)  # mixdown + reduce
+    side = torch.cuda.Stream(dev) if mixdown else None  # mixdown + reduce
     blocks = -(-out_len // args.hop)
     cuts = [min(out_len, args.hop * (blocks * i // args.segments)) for i in range(args.segments + 1)]
     segs = [(b, e) for b, e in zip(cuts[:-1], cuts[1:]) if e > b]
@@ -580,7 +589,7 @@ def run_conv(args, world, rank, local, dev, ir, C, shard_cfg, mixdown, steps, wa
         elapsed = float(t.item())
 
     return {"elapsed": elapsed, "prof": prof, "prof_live": prof_live, "ids": ids, "x_host": x_host, "eng": eng,
-            "ys": ys, "mixes": mixes, "last": last, "comm": comm, "out_len": out_len}
+            "ys": ys, "mixes": mixes, "last": last, "comm": comm, "out_len": out_len, "schedule": eng.schedule()}
 
 
 def main_stream(args):

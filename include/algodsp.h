@@ -143,6 +143,16 @@ int ad_conv_reverb_process_inplace(ad_conv* h, double* block, int64_t n);
 int ad_conv_set_host_io(ad_conv* h, int mode, int workers);
 int ad_conv_host_io_profile(const ad_conv* h, double* register_ms, double* transfer_ms, double* unregister_ms);
 
+/* Low-latency host calls (streaming blocks of hop >= 2048, partitioned calls
+ * of <= 256 samples): how many calls took a pre-enqueued launch and how many
+ * pre-enqueued launches timed out (the call then ran ordinary launches).  A
+ * handle pre-enqueues only for back-to-back callers, while no other handle
+ * has a launch waiting and while the library owns at most 3 streams (they
+ * would otherwise share the device's 4 hardware queues with the caller's);
+ * a waiting launch gives up after 4 call intervals (1..20 ms).  No reference
+ * counterpart (diagnostics).                                              */
+int ad_conv_lowlat_stats(const ad_conv* h, int64_t* pre_enqueued, int64_t* timed_out);
+
 /* ---- common handle API -------------------------------------------------- */
 int ad_conv_reset(ad_conv* h);   /* Reset(): clears history/tail/FDL state */
 int64_t ad_conv_block_size(const ad_conv* h);
@@ -175,6 +185,22 @@ int ad_conv_convolve(const double* a, int64_t n, const double* b, int64_t m, int
  * max_chunk_blocks: blocks per channel per internal chunk (0 = auto).     */
 int ad_conv_multi_create(const double* kernels, int n_ir, int64_t kernel_len, int64_t hop, int channels,
                          const int32_t* ir_index, int64_t max_chunk_blocks, int device, ad_conv** out);
+/* Offline schedule of the device calls below (no reference counterpart: how
+ * OverlapSave.Process, overlap_save.go:126-254, is laid out on the GPU).
+ * SERIAL: each internal chunk's forward transforms, delay-line MAC and inverse
+ * transforms run in turn on the caller's stream.  PIPELINED (hop >= 2048;
+ * smaller hops stay serial): chunks of chunk_blocks blocks per channel (0:
+ * auto) whose spectra stay in the Infinity Cache, the MAC and the inverse
+ * transforms on two internal streams, so consecutive chunks' kernels overlap;
+ * the caller's stream still passes the call only when every output is
+ * written.  run_blocks: the MAC's run length (0: auto).  Results are
+ * bit-identical in both schedules.  Applies from the next signal start (a
+ * process_device call, or a segment / mix call with out_begin == 0).       */
+#define AD_CONV_SCHED_SERIAL 0
+#define AD_CONV_SCHED_PIPELINED 1
+#define AD_CONV_SCHED_CHUNKED 2 /* PIPELINED's chunks and rings, every kernel on the caller's stream */
+int ad_conv_multi_set_schedule(ad_conv* h, int mode, int64_t chunk_blocks, int64_t run_blocks);
+int ad_conv_multi_get_schedule(const ad_conv* h, int* mode, int64_t* chunk_blocks);
 /* Full linear convolution of every channel (ModeFull semantics per channel):
  * d_in  [channels][in_stride] (first in_len used),
  * d_out [channels][out_stride] (first out_len written; out_len <= in_len+K-1).
@@ -346,6 +372,11 @@ void ad_compressor_default_config(ad_compressor_config* cfg, double sample_rate)
 
 int ad_fx_chain_create(int channels, int device, ad_fx_chain** out);
 int ad_fx_chain_set_eq(ad_fx_chain* h, const double* sections, int nsec, int per_channel);
+/* The EQ round-off noise estimate ad_fx_chain_set_eq computes for the engine
+ * choice (eps sqrt(sum NG) of the worst of `sets` tables [nsec][6]; +inf when
+ * a section is unstable: |a2| >= 1 or |a1| >= 1 + a2).  Host only, no device
+ * needed; no reference counterpart (diagnostics).                         */
+int ad_fx_eq_noise(const double* sections, int nsec, int sets, double* noise);
 int ad_fx_chain_set_compressor(ad_fx_chain* h, const ad_compressor_config* cfg); /* NULL: stage off */
 /* dynamics.Expander / dynamics.Gate (expander.go, gate.go) as the chain's
  * dynamics stage instead of the compressor: cfg gives threshold, ratio, knee,

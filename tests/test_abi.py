@@ -95,3 +95,35 @@ def test_comm_rejects_bad_arguments_without_gpu():
     assert L.ad_comm_create(uid, 2, 5, 0, C.byref(h)) == _lib.AD_ERR_INVALID_ARGUMENT
     assert not h.value
     assert L.ad_mixdown_reduce(None, None, 2, 10, 10, 0, None, 10, 0, None) == _lib.AD_ERR_INVALID_ARGUMENT
+
+
+def test_eq_noise_estimate_host_only():
+    """ad_fx_eq_noise (the engine-choice estimate of ad_fx_chain_set_eq) runs
+    on the host: config 5's EQ at 48 kHz estimates 3.6e-13 (under the
+    time-parallel engine's 4.5e-13 gate); an unstable section gives +inf,
+    including ADVICE r4's a1 = 4, a2 = 2 (pole at -3.41), for which the old
+    test d = (1 - a2)((1 + a2)^2 - a1^2) > 0 still held."""
+    from algodsp import design
+
+    L = _lib.lib()
+
+    def noise(secs):
+        tab = np.ascontiguousarray(np.asarray(secs, dtype=np.float64))
+        out = C.c_double()
+        _lib.check(L.ad_fx_eq_noise(tab.ctypes.data_as(C.POINTER(C.c_double)), tab.shape[0], 1, C.byref(out)))
+        return out.value
+
+    from algodsp.processors import section_table
+
+    eq = design.config5_eq(48000.0)
+    tab = np.concatenate([section_table(co, g) for co, g in eq])
+    assert 3.0e-13 < noise(tab) < 4.5e-13
+    unstable = tab.copy()
+    unstable[0, 4:6] = [4.0, 2.0]
+    assert noise(unstable) == float("inf")
+    edge = tab.copy()
+    edge[1, 5] = 1.0
+    assert noise(edge) == float("inf")
+    with pytest.raises(_lib.ErrInvalidArgument):
+        bad = C.c_double()
+        _lib.check(L.ad_fx_eq_noise(None, 2, 1, C.byref(bad)))

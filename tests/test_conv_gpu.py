@@ -319,6 +319,71 @@ def test_partitioned_pre_enqueued_calls(gpu, lo, n):
     assert np.max(np.abs(got - want)) < 1e-9
 
 
+def test_partitioned_gate_after_pause(gpu):
+    """a caller that pauses longer than the pre-enqueued emit's
+    timeout (4 call intervals, at least 1 ms) between two equal calls gets the
+    timed-out emit rolled back and an ordinary call, with correct outputs;
+    after three timeouts in a row pre-enqueueing stops, and it resumes once
+    calls come back to back again."""
+    import time
+
+    h = irlib.large_church()[0, :30000].copy()
+    g = conv.NewPartitionedConvolution(h, 7, 13)
+    o = O.Partitioned(h, 7, 13)
+    x = signals.white_noise(200_000, 91)
+    plan = [128] * 20 + ["sleep"] + [128] * 3 + ["sleep", 128, "sleep", 128, "sleep", 128, "sleep"] + [128] * 40
+    pos, got, want = 0, [], []
+    for m in plan:
+        if m == "sleep":
+            time.sleep(0.03)  # > 20 ms, the longest timeout
+            continue
+        blk = x[pos:pos + m]
+        out = np.empty(m)
+        g.ProcessBlock(blk, out)
+        got.append(out)
+        want.append(o.process_block(blk))
+        pos += m
+    got, want = np.concatenate(got), np.concatenate(want)
+    assert rms(got, want) < FFT_RMS_TOL
+    assert np.max(np.abs(got - want)) < 1e-9
+    hits, timeouts = g.LowLatencyStats()
+    assert timeouts >= 1, (hits, timeouts)
+    assert hits >= 30, (hits, timeouts)  # resumed after the pauses
+
+
+def test_partitioned_two_handles_alternating(gpu):
+    """two low-latency handles called alternately.  Only one
+    pre-enqueued emit may wait at a time (the process-wide slot), so neither
+    handle's call queues behind the other's waiting emit: no call takes as long
+    as a timeout, and both outputs match the oracle."""
+    import time
+
+    h = irlib.large_church()[0, :30000].copy()
+    gs = [conv.NewPartitionedConvolution(h, 7, 13) for _ in range(2)]
+    os_ = [O.Partitioned(h, 7, 13) for _ in range(2)]
+    xs = [signals.white_noise(64 * 128, 95 + i) for i in range(2)]
+    got = [[], []]
+    lat = []
+    for b in range(64):
+        for i in range(2):
+            blk = xs[i][b * 128:(b + 1) * 128]
+            out = np.empty(128)
+            t0 = time.perf_counter()
+            gs[i].ProcessBlock(blk, out)
+            lat.append(time.perf_counter() - t0)
+            got[i].append(out)
+    for i in range(2):
+        a = np.concatenate(got[i])
+        w = np.concatenate([os_[i].process_block(xs[i][b * 128:(b + 1) * 128]) for b in range(64)])
+        assert rms(a, w) < FFT_RMS_TOL
+        assert np.max(np.abs(a - w)) < 1e-9
+    lat = np.sort(np.array(lat[8:]))
+    # no call waits out another handle's 20-ms emit timeout
+    assert lat[-1] < 0.010 and lat[int(0.95 * lat.size)] < 0.002, lat[-10:]
+    hits = [g.LowLatencyStats()[0] for g in gs]
+    assert sum(hits) > 0, hits
+
+
 def test_partitioned_dirac(gpu):
     c = KATS["partitioned_dirac"]
     x = signals.white_noise(c["signal_len"], 3)

@@ -68,6 +68,35 @@ def test_correlate_fft_device_matches_host(gpu, n, m):
     close(got, O.correlate_fft(a, b))
 
 
+def test_correlate_fft_device_two_streams(gpu):
+    """device calls alternating between two streams share the
+    per-device work buffers and the first pass's max-abs counter; each call
+    waits for the previous one when that ran on another stream, so every
+    result equals the single-stream result bit for bit (and a later call on
+    the first stream is not corrupted either)."""
+    import ctypes as C
+
+    import torch
+
+    from algodsp._lib import check, lib
+
+    n = m = 1 << 20  # the split first pass with the max-abs partials (N = 2^21)
+    pairs = [(signals.white_noise(n, 300 + i), 10.0 ** (3 * i) * signals.white_noise(m, 400 + i)) for i in range(6)]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    outs = []
+    devs = [(torch.from_numpy(a).cuda(), torch.from_numpy(b).cuda()) for a, b in pairs]
+    torch.cuda.synchronize()
+    for i, (da, db) in enumerate(devs):
+        st = streams[i % 2]
+        dout = torch.full((n + m - 1,), np.nan, dtype=torch.float64, device="cuda")
+        check(lib().ad_correlate_fft_device(C.c_void_p(da.data_ptr()), n, C.c_void_p(db.data_ptr()), m,
+                                            C.c_void_p(dout.data_ptr()), 0, C.c_void_p(st.cuda_stream)))
+        outs.append(dout)
+    torch.cuda.synchronize()
+    for (a, b), dout in zip(pairs, outs):
+        assert np.array_equal(dout.cpu().numpy(), conv.CorrelateFFT(a, b))
+
+
 @pytest.mark.parametrize("sa,sb", [(3.0e4, 3.0e-3), (1.0e-4, 2.0e3), (1.0, 1.0e-9), (2.0**600, 2.0**-600),
                                    (2.0**-600, 2.0**560)])
 @pytest.mark.parametrize("n,m", [(40000, 25000), (1 << 17, 4096)])
