@@ -42,6 +42,28 @@ def reduce_mix(mix_tensor, dist, async_op: bool = False):
     return dist.reduce(mix_tensor, dst=0, op=dist.ReduceOp.SUM, async_op=async_op)
 
 
+def scaling_diagnostics(step_ms: float, conv_ms: float, reduce_ms: float, reduce_bytes: float) -> dict:
+    """What an N > 1 bench line needs to tell whether the mixdown reduce hides
+    under the convolution (every input already the max over ranks):
+    step_ms   the timed step (convolution + reduce on the side stream, pipelined);
+    conv_ms   the same step with the reduce off;
+    reduce_ms the reduce alone (events around it on the side stream);
+    reduce_bytes the partial mix each rank contributes (2 rows x out_len x 8 B).
+    overlap = the share of the reduce that the step did not pay for,
+    (conv + reduce - step) / reduce, clipped to [0, 1]; hide_GBps = the rate the
+    reduce needs to fit under the convolution."""
+    hidden = conv_ms + reduce_ms - step_ms
+    return {
+        "conv_ms_per_step": round(conv_ms, 4),
+        "reduce_ms": round(reduce_ms, 4),
+        "reduce_bytes_per_rank": int(reduce_bytes),
+        "reduce_GBps": round(reduce_bytes / (reduce_ms * 1e-3) / 1e9, 2) if reduce_ms > 0 else None,
+        "hide_GBps": round(reduce_bytes / (conv_ms * 1e-3) / 1e9, 2) if conv_ms > 0 else None,
+        "overlap": round(min(1.0, max(0.0, hidden / reduce_ms)), 3) if reduce_ms > 0 else None,
+        "step_over_conv": round(step_ms / conv_ms, 4) if conv_ms > 0 else None,
+    }
+
+
 class Comm:
     """The library's own RCCL communicator (include/algodsp.h ad_comm_*): the
     path a cgo caller takes to shard without torch.distributed.  `bootstrap`

@@ -449,6 +449,148 @@ __global__ __launch_bounds__(192) void k_fxtp_det(FxStageArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// K_det, one wave (the bare detector: peak level, no side-chain filters, the
+// config-5 compressor).  The three-wave form above spends
+// 43 clocks per sample against the envelope chain's 24.5: one barrier per
+// batch and the LDS hand-offs between its waves.  Here one wave does it all
+// for kDetCh channels, with no barrier:
+//   - batch k's rows (32 rows x 8 channels, 2 KiB) arrive in an LDS ring by
+//     LDS-DMA (global_load_lds_dwordx4: lane l fetches 16 B of row l / 4, so
+//     two instructions fill a batch), issued kDet1D batches ahead;
+//   - the wave reads batch k + 1 out of the ring (lane = channel) before it
+//     runs the chain over batch k, puts batch k's envelopes into a small LDS
+//     staging area and stores batch k - 1's from there as four full-width
+//     stores (lane l: row l / 8 + 8 i, channel l % 8);
+//   - the vector-memory counter retires in issue order and the wave issues 4
+//     stores then 2 DMAs per step (4 dummy DMAs into a scratch line stand in
+//     for the stores before the first step), so "batch k + 1 has landed" is
+//     the constant wait vmcnt(6 (kDet1D - 1)) at every step (the DMAs are inline asm,
+//     as K2's X ring: hipcc would drain them with vmcnt(0) before the first LDS
+//     read).  A slot is refilled kDet1D + 1 steps after it was read.
+// Same operations per sample as the three-wave kernel (env_step), so the same
+// bits.  Full batches only; a chunk's last partial batch runs lane-serially
+// after a vmcnt(0).
+// ---------------------------------------------------------------------------
+// Measured (round 5, one box, tools/fx_iso_prof.sh on AD_FX_TP_SERIAL builds,
+// profiles/r05_det_onewave.txt): 1646 us per 64K-sample chunk at 256 channels
+// against 1144 us for the three-wave kernel (60 against 42 clocks per
+// sample), config 5 8.1 against 10.9 Gsamples/s: the chain wave also issuing
+// the ring DMAs, their address arithmetic, the masked envelope writes and the
+// stores costs more than the barrier it saves.  Kept for A/B builds only.
+#ifndef AD_DET_ONEWAVE  // tools/ A/B builds: 1 = this kernel for the bare detector
+#define AD_DET_ONEWAVE 0
+#endif
+typedef __attribute__((address_space(3))) void lds_void_t;
+constexpr int kDet1D = 8;                 // batches in flight (DMA issued this many batches ahead)
+constexpr int kDet1Slots = kDet1D + 2;    // ring slots
+constexpr int kDet1Wait = 6 * (kDet1D - 1);  // ops issued after batch k + 1's DMAs, at step k
+static_assert(kDetB == 32 && kDetCh == 8, "one-wave detector: 32-row batches of 8 channels (two 1-KiB DMAs)");
+static_assert(kDet1Wait <= 63, "vmcnt holds 6 bits");
+
+__device__ __forceinline__ void det1_dma(const double* g, unsigned lds) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(g), "s"(lds)
+               : "memory");
+}
+
+__global__ __launch_bounds__(64) void k_fxtp_det1(FxStageArgs a) {
+#pragma clang fp contract(off)
+  __shared__ __attribute__((aligned(16))) double ring[kDet1Slots][kDetB][kDetCh];
+  __shared__ __attribute__((aligned(16))) double evr[2][kDetB][kDetCh];
+  __shared__ __attribute__((aligned(16))) double scratch[128];  // the dummy DMAs' target (1 KiB)
+  const int l = threadIdx.x;
+  const int li = l & (kDetCh - 1);
+  const int c0 = blockIdx.x * kDetCh;
+  const int cp = a.cpad;
+  const int64_t len = a.len;
+  const int64_t nbf = len / kDetB;  // full batches
+  const CompParams& p = a.cp;
+  const int c = c0 + li;
+  const int cc = c < a.channels ? c : a.channels - 1;
+  CompChState cs = a.cs[cc];
+  const double* vin = a.vT;
+  double* eo = a.envT;
+  // this lane's 16 B of a DMA: row (l >> 2), channels c0 + 2 (l & 3) .. + 1
+  const double* gl = vin + (int64_t)(l >> 2) * cp + c0 + 2 * (l & 3);
+  auto dma = [&](int64_t b) {  // batch b into its slot (rows past the chunk re-read its last row)
+    const int slot = (int)(b % kDet1Slots);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int64_t row = min(b * kDetB + 16 * h + (l >> 2), len - 1) - (l >> 2);
+      det1_dma(gl + row * cp, (unsigned)(uintptr_t)(lds_void_t*)&ring[slot][16 * h][0]);
+    }
+  };
+  auto dummy4 = [&]() {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) det1_dma(vin + c0, (unsigned)(uintptr_t)(lds_void_t*)&scratch[0]);
+  };
+  // envelopes of batch b from the staging area to memory (four full-width stores)
+  auto flush = [&](int64_t b) {
+    double v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = evr[b & 1][(l >> 3) + 8 * i][l & 7];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) eo[(b * kDetB + (l >> 3) + 8 * i) * cp + c0 + (l & 7)] = v[i];
+  };
+  __builtin_amdgcn_s_waitcnt(0);  // the state load has landed: from here on only counted ops
+  if (nbf > 0) {
+    dma(0);
+    for (int j = 1; j <= kDet1D; ++j) {
+      dummy4();
+      dma(j);
+    }
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kDet1Wait + 6) : "memory");  // batch 0
+    double xa[kDetB], xb[kDetB];
+#pragma unroll
+    for (int d = 0; d < kDetB; ++d) xa[d] = ring[0][d][li];
+    auto step = [&](int64_t k, double (&cur)[kDetB], double (&nxt)[kDetB]) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kDet1Wait) : "memory");  // batch k + 1 has landed
+      const int sn = (int)((k + 1) % kDet1Slots);
+      double ev[kDetB];
+      // the chain over batch k with batch k + 1's ring reads interleaved (they
+      // issue in the chain's dependency stalls; one wave issues in order)
+#pragma unroll
+      for (int d = 0; d < kDetB; ++d) {
+        cs.env = env_step(p, cs.env, fabs(cur[d]));
+        ev[d] = cs.env;
+        nxt[d] = ring[sn][d][li];
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (l < kDetCh) {
+#pragma unroll
+        for (int d = 0; d < kDetB; ++d) evr[k & 1][d][li] = ev[d];
+      }
+      // per step: 4 stores, then 2 DMAs (the order kDet1Wait counts)
+      if (k > 0)
+        flush(k - 1);
+      else
+        dummy4();
+      dma(k + 1 + kDet1D);
+    };
+    int64_t k = 0;
+    for (; k + 1 < nbf; k += 2) {
+      step(k, xa, xb);
+      step(k + 1, xb, xa);
+    }
+    if (k < nbf) step(k, xa, xb);
+    flush(nbf - 1);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // the chunk's last partial batch, lane-serially from memory
+  for (int64_t r = nbf * kDetB; r < len; ++r) {
+    const double x = vin[r * cp + cc];
+    cs.env = env_step(p, cs.env, fabs(x));
+    if (l < kDetCh && c < a.channels) eo[r * cp + c] = cs.env;
+  }
+  if (l < kDetCh && c < a.channels) {
+    CompChState* o = a.cs + c;
+    o->env = cs.env;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // K_verb: Freeverb for one channel per workgroup (reverb.go:57-189), every
 // delay line of the channel in LDS for the whole chunk (12587 positions,
 // 98 KiB): no delay-line traffic to memory inside the chunk, and the comb
@@ -671,7 +813,12 @@ void launch_fxtp_carry(const FxTpEqArgs& a, hipStream_t s) {
 
 void launch_fxtp_det(const FxStageArgs& a, hipStream_t s) {
   if (a.len <= 0) return;
-  hipLaunchKernelGGL(k_fxtp_det, dim3((unsigned)((a.channels + kDetCh - 1) / kDetCh)), dim3(192), 0, s, a);
+  const CompParams& p = a.cp;
+  const bool bare = !p.lp_on && !p.hp_on && !p.detector_rms;
+  if (AD_DET_ONEWAVE && bare)
+    hipLaunchKernelGGL(k_fxtp_det1, dim3((unsigned)((a.channels + kDetCh - 1) / kDetCh)), dim3(64), 0, s, a);
+  else
+    hipLaunchKernelGGL(k_fxtp_det, dim3((unsigned)((a.channels + kDetCh - 1) / kDetCh)), dim3(192), 0, s, a);
 }
 
 void launch_fxtp_verb(const FxStageArgs& a, const double* xC, int64_t xstride, double* vbufC, double* coC, int wu,

@@ -57,6 +57,12 @@ def parse():
     p.add_argument("--shard-sub", choices=["on", "off"], default="on",
                    help="N = 1 conv: also measure config 4's per-GPU shard (8 ch x 2^24 + the stereo mixdown "
                         "through the ABI at world 1), the like-for-like base of the N > 1 curve")
+    p.add_argument("--fx-leg", choices=["on", "off"], default="on",
+                   help="N = 1 conv: also time config 5 (256 ch x 2^20 effect chain, AUTO engine, 5 steps, "
+                        "with its parity and CPU baseline) as the line's config5 key")
+    p.add_argument("--stream-leg", choices=["on", "off"], default="on",
+                   help="N = 1 conv: also time config 2 (StreamingOverlapSave, 4096-sample host blocks, "
+                        "1024 blocks: p50 / p99 per block) as the line's config2_stream key")
     p.add_argument("--pipeline", choices=["on", "off"], default="on",
                    help="N > 1: overlap step i's mixdown reduce with step i+1's convolution (two output buffers)")
     p.add_argument("--mix-fused", choices=["on", "off"], default="on",
@@ -104,14 +110,19 @@ def launch_ranks(n: int) -> int:
     return subprocess.call(cmd, stdout=sys.stdout)  # the JSON channel, not the fd-1 banner sink
 
 
+def affinity_cores() -> int:
+    """Cores this process's CPU affinity allows (os.cpu_count() on the GPU box
+    reports the whole machine)."""
+    try:
+        return max(1, len(os.sched_getaffinity(0)))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
 def host_cores() -> int:
     """Host cores this process may use, capped at the GPU box's per-GPU CPU
-    share (16): os.cpu_count() there reports the whole machine."""
-    try:
-        n = len(os.sched_getaffinity(0))
-    except AttributeError:
-        n = os.cpu_count() or 1
-    return max(1, min(16, n))
+    share (16)."""
+    return max(1, min(16, affinity_cores()))
 
 
 def cpu_baseline(ir, sample_len):
@@ -142,16 +153,36 @@ def cpu_baseline(ir, sample_len):
         list(ex.map(one, range(T)))
         dtT = time.perf_counter() - t0
     fast = cpu_fast_fft(ir, xs, T)
+    del xs
+    # every core the affinity mask allows (capped at 64 threads, a shorter
+    # channel each): the box's whole-machine figure beside the per-GPU share
+    A = affinity_cores()
+    wide = None
+    if A > T:
+        TA = min(A, 64)
+        la = max(1 << 20, sample_len // 8)
+        xa = [signals.white_noise(la, 0x7000 + c) for c in range(TA)]
+        with ThreadPoolExecutor(TA) as ex:
+            t0 = time.perf_counter()
+            list(ex.map(lambda c: O.OverlapSave(ir[c % 2], 0).process(xa[c]).size, range(TA)))
+            dtA = time.perf_counter() - t0
+        del xa
+        wide = {"value": round(TA * la / dtA / 1e6, 3), "unit": "Msamples/s", "threads": TA, "affinity_cores": A,
+                "sample": f"one channel of {la} samples per thread on {TA} threads ({dtA:.1f} s)"}
     return {
         "value": T * sample_len / dtT / 1e6,
         "unit": "Msamples/s",
         "cores": T,
         "kind": "port",
+        "per_gpu_share_cores": T,
+        "affinity_cores": A,
+        "affinity_wide": wide,
         "single_core": sample_len / dt1 / 1e6,
         "optimized_fft": fast,
         "sample": f"oracle OverlapSave.Process (N=262144, Large Church 131072 taps) on {T} host threads, one "
                   f"channel of {sample_len} white-noise samples each ({dtT:.1f} s; host cpu_count "
-                  f"{os.cpu_count()}, affinity share capped at 16); single_core: 1 channel on 1 thread ({dt1:.1f} s)",
+                  f"{os.cpu_count()}, affinity {A}; `value` uses the per-GPU share of 16 cores, affinity_wide every "
+                  f"allowed core up to 64); single_core: 1 channel on 1 thread ({dt1:.1f} s)",
     }
 
 
@@ -328,9 +359,28 @@ def main():
                                      "RCCL reduce through ad_mixdown_reduce (world 1), the per-GPU work of every "
                                      "rank at N > 1",
                          "kernels_avg_us": {k: round(v[0] / max(v[1], 1) * 1e3, 1) for k, v in r8["prof"].items()},
+                         "mixdown_reduce": r8["reduce_diag"],
                          "parity": output_parity(args, r8, ir, 8, True)}
             r8["comm"].close()
             del r8
+        legs_on = world == 1 and args.workload == "conv" and not shard_cfg
+        if legs_on:
+            # the legs get the process to themselves: the conv handle's stream
+            # would share the device's 4 hardware queues with the effect chain's
+            # three, and the low-latency streaming path pre-enqueues only while
+            # the library owns at most 3 streams (include/algodsp.h)
+            import gc
+
+            r["eng"] = eng = None
+            gc.collect()
+        config5 = None
+        if legs_on and args.fx_leg == "on":
+            ys.clear(), mixes.clear()
+            config5 = fx_measure(args, 1, 0, local, dev, 5, 2, not args.no_cpu_baseline, n=1 << 20)
+            torch.cuda.empty_cache()
+        config2 = None
+        if legs_on and args.stream_leg == "on":
+            config2 = stream_measure(1024, 32, not args.no_cpu_baseline)
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(ir, args.cpu_sample)
@@ -398,6 +448,18 @@ def main():
             "shard_per_gpu": shard_sub,
             "cpu_baseline": cpu,
         }
+        if config5 is not None:
+            line["config5"] = config5
+        if config2 is not None:
+            line["config2_stream"] = config2
+        if r["reduce_diag"] is not None:
+            line["mixdown_reduce"] = dict(r["reduce_diag"], note=(
+                "max over ranks; conv_ms_per_step: the same step with the reduce off; reduce_ms: RCCL reduce "
+                "of the stereo partial mix (ad_mixdown_reduce) event-timed on the side stream; overlap: the share "
+                "of reduce_ms the step did not pay; hide_GBps: the reduce rate that fits under the convolution"))
+        if world > 1:
+            line["like_for_like_base"] = ("shard_per_gpu of the N = 1 line: the same 8 ch x 2^24 per GPU with "
+                                          "the mixdown fused into K3, at world 1")
         if cpu:
             line["speedup_vs_cpu"] = round(value / cpu["value"], 1)
         print(json.dumps(line), flush=True)
@@ -509,6 +571,8 @@ def run_conv(args, world, rank, local, dev, ir, C, shard_cfg, mixdown, steps, wa
     segs = [(b, e) for b, e in zip(cuts[:-1], cuts[1:]) if e > b]
     red_done = [None] * nbuf
     it = [0]
+    reduce_on = [True]   # off: the conv-only steps after the timed region (N > 1 diagnostics)
+    red_ev = []          # (start, end) timing events around each reduce on the side stream
 
     def step():
         i = it[0] % nbuf
@@ -523,14 +587,18 @@ def run_conv(args, world, rank, local, dev, ir, C, shard_cfg, mixdown, steps, wa
                 eng.process_device(x.data_ptr(), n, n, yb.data_ptr(), out_len, out_len, sptr)
             else:
                 eng.process_device_segment(x.data_ptr(), n, n, yb.data_ptr(), out_len, out_len, b, e, sptr)
-            if mixdown:
+            if mixdown and reduce_on[0]:
                 done = torch.cuda.Event()
                 done.record(stream)
                 side.wait_event(done)
+                r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                r0.record(side)
                 # stereo group or fused mix: mb already holds the partial mix (no k_mixdown)
                 comm.mixdown_reduce(yb.data_ptr() + 8 * b, 0 if (C == 2 or fused) else C, out_len, e - b,
                                     mb.data_ptr() + 8 * b, out_len, ids[0] % 2, 0, side.cuda_stream)
-        if mixdown:
+                r1.record(side)
+                red_ev.append((r0, r1))
+        if mixdown and reduce_on[0]:
             ev = torch.cuda.Event()
             ev.record(side)
             red_done[i] = ev
@@ -558,6 +626,7 @@ def run_conv(args, world, rank, local, dev, ir, C, shard_cfg, mixdown, steps, wa
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    red_ev.clear()
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
@@ -567,6 +636,9 @@ def run_conv(args, world, rank, local, dev, ir, C, shard_cfg, mixdown, steps, wa
         dist.barrier()
     elapsed = time.perf_counter() - t0
     last = (it[0] - 1) % nbuf
+    # the reduces of the timed steps, event-timed on the side stream
+    reduce_ms = sum(a.elapsed_time(b) for a, b in red_ev) / steps if red_ev else 0.0
+    red_ev.clear()
     prof_live = eng.profile_read() if mode != "off" else {}
     if mode != "on":  # the kernels not timed live: a separate event-timed pass
         eng.profile_enable(True)
@@ -583,38 +655,72 @@ def run_conv(args, world, rank, local, dev, ir, C, shard_cfg, mixdown, steps, wa
         prof = prof_live
     eng.profile_enable(False)
 
+    conv_elapsed = None
+    if mixdown:
+        # the same step with the reduce off: what the convolution alone takes
+        # (N > 1 diagnostics: does the reduce hide?)
+        reduce_on[0] = False
+        ksteps = min(steps, 5)
+        step()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        tc = time.perf_counter()
+        for _ in range(ksteps):
+            step()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        conv_elapsed = (time.perf_counter() - tc) / ksteps * steps
+        reduce_on[0] = True
+        red_done[:] = [None] * nbuf
+        # one full step again, so the buffers the parity check reads hold a
+        # reduced (whole-job) mix
+        step()
+        drain()
+        torch.cuda.synchronize(dev)
+        last = (it[0] - 1) % nbuf
+    conv_elapsed = conv_elapsed if conv_elapsed is not None else 0.0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, conv_elapsed, reduce_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed, conv_elapsed, reduce_ms = (float(v) for v in t.tolist())
+    diag = None
+    if mixdown:
+        diag = shard.scaling_diagnostics(elapsed / steps * 1e3, conv_elapsed / steps * 1e3, reduce_ms,
+                                         2 * out_len * 8)
 
     return {"elapsed": elapsed, "prof": prof, "prof_live": prof_live, "ids": ids, "x_host": x_host, "eng": eng,
-            "ys": ys, "mixes": mixes, "last": last, "comm": comm, "out_len": out_len, "schedule": eng.schedule()}
+            "ys": ys, "mixes": mixes, "last": last, "comm": comm, "out_len": out_len, "schedule": eng.schedule(),
+            "reduce_diag": diag}
 
 
-def main_stream(args):
+def stream_measure(nblk: int, warmup_blocks: int, cpu_leg: bool) -> dict:
     """BASELINE config 2: StreamingOverlapSave(K=16384, B=4096) driven block by
     block through the host-buffer ABI, as a Go caller would (ProcessBlockTo per
-    block: PCIe in, UPOLS on the GPU, PCIe out, synchronous).  Replicas only."""
+    block: PCIe in, UPOLS on the GPU, PCIe out, synchronous; reference
+    streaming_overlap_save.go:100-164).  Per-block wall times give p50 / p99;
+    parity: the measured output's first blocks against exact float64 products."""
     import numpy as np
 
     from algodsp import conv, irlib, signals
 
     ir = irlib.large_church()[0, :16384]
     B = 4096
-    nblk = max(1, args.samples // B) if args.samples else 2048
     x = signals.white_noise(nblk * B, 0x5EED)
     y = np.empty_like(x)
     s = conv.NewStreamingOverlapSave(ir, B)
-    for i in range(min(args.warmup * 8, nblk)):
+    for i in range(min(warmup_blocks, nblk)):
         s.ProcessBlockTo(y[i * B:(i + 1) * B], x[i * B:(i + 1) * B])
     s.Reset()
+    lat = np.empty(nblk)
     t0 = time.perf_counter()
     for i in range(nblk):
+        tb = time.perf_counter()
         s.ProcessBlockTo(y[i * B:(i + 1) * B], x[i * B:(i + 1) * B])
+        lat[i] = time.perf_counter() - tb
     dt = time.perf_counter() - t0
-    # parity: the measured output's first blocks against exact float64 dot
-    # products (numpy) of the same input (zero history before block 0)
+    hits, timeouts = s.LowLatencyStats()
     nchk = min(nblk, 4) * B
     ref = np.convolve(x[:nchk], ir)[:nchk]
     err = y[:nchk] - ref
@@ -622,9 +728,9 @@ def main_stream(args):
               "outputs_checked": int(nchk), "against": "exact float64 convolution (numpy) of the first blocks",
               "tolerance_rms": 1e-7}
     if parity["rms"] > 1e-7:
-        print(f"bench.py: PARITY FAILURE {parity}", file=sys.stderr)
+        print(f"bench.py: PARITY FAILURE (config 2) {parity}", file=sys.stderr)
     cpu = None
-    if not args.no_cpu_baseline:
+    if cpu_leg:
         sys.path.insert(0, str(ROOT / "tests"))
         import oracle_lib as O
 
@@ -636,17 +742,33 @@ def main_stream(args):
         dtc = time.perf_counter() - tc
         cpu = {"value": m * B / dtc / 1e6, "unit": "Msamples/s", "cores": 1, "kind": "port",
                "sample": f"{m} blocks of {B}, oracle StreamingOverlapSave (N=32768); {dtc:.1f} s"}
+    us = lat * 1e6
+    return {"value": round(nblk * B / dt / 1e6, 3), "unit": "Msamples/s", "blocks": nblk, "block": B,
+            "kernel_taps": 16384, "ms_per_block": round(dt / nblk * 1e3, 4),
+            "p50_us": round(float(np.percentile(us, 50)), 1), "p99_us": round(float(np.percentile(us, 99)), 1),
+            "mean_us": round(float(us.mean()), 1), "max_us": round(float(us.max()), 1),
+            "pre_enqueued_blocks": hits, "timed_out_blocks": timeouts,
+            "workload": "config 2: StreamingOverlapSave mono K=16384 B=4096, host buffers in and out, one "
+                        "synchronous ProcessBlockTo per block (PCIe + 3 kernels + completion wait per block)",
+            "parity": parity, "cpu_baseline": cpu}
+
+
+def main_stream(args):
+    """BASELINE config 2 as its own line (replicas only)."""
+    nblk = max(1, args.samples // 4096) if args.samples else 2048
+    r = stream_measure(nblk, args.warmup * 8, not args.no_cpu_baseline)
     line = {
         "metric": "Msamples/sec, streaming overlap-save 16384-tap IR, 4096-sample blocks (config 2)",
-        "value": round(nblk * B / dt / 1e6, 3), "unit": "Msamples/s", "n_gpus": 1, "steps": nblk,
-        "warmup": args.warmup, "ms_per_step": round(dt / nblk * 1e3, 4), "higher_is_better": True,
+        "value": r["value"], "unit": "Msamples/s", "n_gpus": 1, "steps": nblk,
+        "warmup": args.warmup, "ms_per_step": r["ms_per_block"], "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic: SplitMix64 white noise x Large Church L (first 16384 taps)",
         "config": {"workload": "StreamingOverlapSave mono K=16384 B=4096, host buffers, one block per step",
-                   "block": B, "kernel_taps": 16384},
+                   "block": 4096, "kernel_taps": 16384},
+        "latency_us": {k: r[k] for k in ("p50_us", "p99_us", "mean_us", "max_us")},
         "note": "latency-bound: each block = H2D copy + 3 kernels + D2H copy + sync",
-        "parity": parity,
-        "cpu_baseline": cpu,
+        "parity": r["parity"],
+        "cpu_baseline": r["cpu_baseline"],
     }
     print(json.dumps(line), flush=True)
 
@@ -766,50 +888,104 @@ def main_corr(args):
     print(json.dumps(line), flush=True)
 
 
-def main_fx(args):
+def fx_chain_oracle(eq, comp_cfg, verb, fs, v):
+    """One channel through the oracle chain (chain_process.go:11-33: biquad
+    chains with the avx2 registry kernel's 4x-unrolled DF-II-T, Compressor,
+    Freeverb); ctypes releases the GIL."""
+    sys.path.insert(0, str(ROOT / "tests"))
+    import numpy as np
+
+    import oracle_lib as O
+
+    for co, g in eq:
+        v, _ = O.biquad_chain_block(np.ravel(co), np.zeros(2 * len(co)), g, v)
+    v = O.Compressor(fs, **comp_cfg).process_in_place(v)
+    o = O.Freeverb()
+    o.set(*verb)
+    return o.process_in_place(v)
+
+
+def fx_cpu_baseline(eq, comp_cfg, verb, fs, m):
+    """The oracle chain on the host cores (one channel per thread, m/4 samples
+    each), on one core (m samples), and the EQ alone on one core: five
+    sections of the avx2 registry kernel's 4x-unrolled DF-II-T
+    (internal/arch/amd64/avx2/register.go:23-66, oracle/or_filters.c), north
+    star's "AVX2 biquad"."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    import numpy as np
+
+    sys.path.insert(0, str(ROOT / "tests"))
+    import oracle_lib as O
+    from algodsp import signals
+
+    T = host_cores()
+    vs = [0.5 * signals.white_noise(m // 4, 0x5EED + c) for c in range(T)]
+    x1 = 0.5 * signals.white_noise(m, 0x5EED)
+    tc = time.perf_counter()
+    fx_chain_oracle(eq, comp_cfg, verb, fs, x1)
+    dt = time.perf_counter() - tc
+    with ThreadPoolExecutor(T) as ex:
+        tc = time.perf_counter()
+        list(ex.map(lambda v: fx_chain_oracle(eq, comp_cfg, verb, fs, v).size, vs))
+        dtT = time.perf_counter() - tc
+    coeffs = np.concatenate([np.ravel(co) for co, _ in eq])
+    tq = time.perf_counter()
+    O.biquad_chain_block(coeffs, np.zeros(2 * (coeffs.size // 5)), 1.0, x1)
+    dtq = time.perf_counter() - tq
+    return {"value": T * (m // 4) / dtT / 1e6, "unit": "Msamples/s", "cores": T, "kind": "port",
+            "single_core": m / dt / 1e6,
+            "eq_avx2_biquad_single_core": {"value": round(m / dtq / 1e6, 3), "unit": "Msamples/s",
+                                           "sections": coeffs.size // 5,
+                                           "sample": f"{m} samples through the config-5 EQ's 5 sections, "
+                                                     f"oracle avx2 registry kernel (4x-unrolled DF-II-T), "
+                                                     f"{dtq:.2f} s"},
+            "sample": f"oracle biquad chains + Compressor + Freeverb, one channel of {m // 4} samples per "
+                      f"host thread on {T} threads ({dtT:.2f} s); single_core: 1 channel x {m} samples "
+                      f"({dt:.2f} s)"}
+
+
+def fx_measure(args, world, rank, local, dev, steps, warmup, cpu_leg, graph=None, n=None, parity_on=True) -> dict:
     """BASELINE config 5: effectchain filter(x5 RBJ) -> dyn-compressor ->
-    reverb-freeverb on 256 channels x 2^20 samples, fused per sample (one
-    lane per channel), buffers resident in HBM.  Replicas only for N > 1."""
+    reverb-freeverb on 256 channels x 2^20 samples (device buffers, the
+    engine AUTO picks), `steps` timed calls after `warmup`; barrier +
+    synchronize around them, max over ranks.  Parity: a fresh chain over the
+    same input against the oracle chain on channels 0 and 255 (a 2^17-sample
+    prefix: the chain is causal)."""
     import numpy as np
     import torch
     import torch.distributed as dist
 
     from algodsp import design, processors, signals
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
     fs = 48000.0
     C = 256
-    n = args.samples or (1 << 20)
+    n = n or (1 << 20)
     eq = design.config5_eq(fs)
     comp_cfg = {"auto_makeup": 0, "makeup_db": 0.0}  # runtime_dynamics.go:46-54
     verb = (0.22, 1.0, 0.72, 0.45, 0.015)
-    x = torch.from_numpy(np.stack([0.5 * signals.white_noise(n, 0x5EED + c) for c in range(C)])).to(dev)
+    x_host = np.stack([0.5 * signals.white_noise(n, 0x5EED + c) for c in range(C)])
+    x = torch.from_numpy(x_host).to(dev)
     sptr = torch.cuda.current_stream(dev).cuda_stream
-    if args.graph:  # the batched effectchain graph runtime (SURVEY 8(f)4)
+    if graph:  # the batched effectchain graph runtime (SURVEY 8(f)4)
         from algodsp import effectchain
 
         fx = effectchain.Chain(fs, C, designer=design.RBJDesigner(), device=local)
-        fx.LoadGraph(effectchain.EXAMPLE_GRAPHS[args.graph])
+        fx.LoadGraph(effectchain.EXAMPLE_GRAPHS[graph])
     else:
         fx = processors.EffectChain(C, eq, comp_cfg, verb, fs, device=local)
 
     def step():
         fx.process_device(x.data_ptr(), n, n, sptr)
 
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         step()
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -819,68 +995,87 @@ def main_fx(args):
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    value = world * C * n * args.steps / elapsed / 1e6
+    value = world * C * n * steps / elapsed / 1e6
+    engine = None
+    if not graph:
+        eng_id, noise = fx.LastEngine()
+        engine = {"id": eng_id, "name": {1: "fused", 2: "staged_nosplit", 3: "staged", 4: "time_parallel"}.get(
+            eng_id, str(eng_id)), "eq_noise_estimate": noise}
+    parity = None
+    if parity_on and not graph and rank == 0:
+        fx.Reset()
+        x.copy_(torch.from_numpy(x_host))
+        step()
+        torch.cuda.synchronize(dev)
+        m0 = min(n, 1 << 17)
+        errs = []
+        for c in (0, C - 1):
+            got = x[c, :m0].cpu().numpy()
+            want = fx_chain_oracle(eq, comp_cfg, verb, fs, x_host[c, :m0].copy())
+            errs.append(got - want)
+        err = np.concatenate(errs)
+        ref_rms = float(np.sqrt(np.mean(np.concatenate([x_host[0, :m0], x_host[-1, :m0]]) ** 2)))
+        parity = {"rms": float(np.sqrt(np.mean(err ** 2))), "max_abs": float(np.max(np.abs(err))),
+                  "outputs_checked": int(err.size),
+                  "against": f"oracle chain (biquad chains -> Compressor -> Freeverb) on channels 0 and {C - 1}, "
+                             f"first {m0} samples, fresh chain state",
+                  "tolerance_rms": 1e-12, "input_rms": ref_rms}
+        if parity["rms"] > 1e-12:
+            print(f"bench.py: PARITY FAILURE (config 5) {parity}", file=sys.stderr)
+    cpu = fx_cpu_baseline(eq, comp_cfg, verb, fs, 1 << 25) if cpu_leg and world == 1 and rank == 0 else None
+    # The bound is the one serial recurrence left, not HBM (16 B/sample of
+    # input and output moves 0.5 % of peak): the time-parallel engine cuts the
+    # EQ sections and the Freeverb combs into time segments, but the envelope
+    # follower (attack or release by the sign of src - env) is serial per
+    # channel, 24.5 clocks per sample (tools/chain_latency.hip).
+    # Ceiling = clock x channels / 24.5.
+    ceiling = FX_CLOCK_HZ * C / FX_CHAIN_CLK / 1e6
+    return {
+        "value": round(value, 3), "unit": "Msamples/s", "steps": steps, "warmup": warmup,
+        "ms_per_step": round(elapsed / steps * 1e3, 3), "channels_per_gpu": C, "samples_per_channel": n,
+        "workload": (f"effectchain graph '{graph}' through the batched graph runtime ({fx.op_count()[0]} device "
+                     f"ops per call), {C} ch x {n} samples per GPU per step" if graph else
+                     f"effectchain filter x5 (RBJ) -> dyn-compressor -> reverb-freeverb, {C} ch x {n} samples "
+                     f"per GPU per step, device buffers, engine AUTO"),
+        "engine": engine,
+        "roofline": {"bound": "serial-recurrence latency (compressor envelope)", "achieved": round(value, 3),
+                     "peak": round(ceiling, 1), "unit": "Msamples/s", "frac": round(value / ceiling, 4),
+                     "traffic": None, "hbm_GBps": round(value * 16e6 / 1e9, 3),
+                     "note": f"ceiling = {FX_CLOCK_HZ / 1e9} GHz x {C} channels / {FX_CHAIN_CLK} clk per sample "
+                             f"(the envelope follower's dependency chain, each channel's own); HBM carries "
+                             f"16 B/sample of input and output"},
+        "parity": parity, "cpu_baseline": cpu,
+    }
+
+
+def main_fx(args):
+    """BASELINE config 5 as its own line.  Replicas only for N > 1."""
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    r = fx_measure(args, world, rank, local, dev, args.steps, args.warmup, not args.no_cpu_baseline,
+                   graph=args.graph, n=args.samples)
     if rank == 0:
-        cpu = None
-        if not args.no_cpu_baseline and world == 1:
-            sys.path.insert(0, str(ROOT / "tests"))
-            import oracle_lib as O
-
-            from concurrent.futures import ThreadPoolExecutor
-
-            def chain(v):  # one channel through the oracle chain (ctypes releases the GIL)
-                for co, g in eq:
-                    v, _ = O.biquad_chain_block(np.ravel(co), np.zeros(2 * len(co)), g, v)
-                v = O.Compressor(fs, **comp_cfg).process_in_place(v)
-                o = O.Freeverb()
-                o.set(*verb)
-                o.process_in_place(v)
-                return v.size
-
-            m = 1 << 25
-            T = host_cores()
-            vs = [0.5 * signals.white_noise(m // 4, 0x5EED + c) for c in range(T)]
-            tc = time.perf_counter()
-            chain(0.5 * signals.white_noise(m, 0x5EED))
-            dt = time.perf_counter() - tc
-            with ThreadPoolExecutor(T) as ex:
-                tc = time.perf_counter()
-                list(ex.map(chain, vs))
-                dtT = time.perf_counter() - tc
-            cpu = {"value": T * (m // 4) / dtT / 1e6, "unit": "Msamples/s", "cores": T, "kind": "port",
-                   "single_core": m / dt / 1e6,
-                   "sample": f"oracle biquad chains + Compressor + Freeverb, one channel of {m // 4} samples per "
-                             f"host thread on {T} threads ({dtT:.2f} s); single_core: 1 channel x {m} samples "
-                             f"({dt:.2f} s)"}
         line = {
             "metric": "Msamples/sec, effectchain biquad EQ + Compressor + Freeverb (config 5)",
-            "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+            "value": r["value"], "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": r["ms_per_step"], "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic: 0.5 x SplitMix64 white noise, 48 kHz",
-            "config": {"workload": (f"effectchain graph '{args.graph}' through the batched graph runtime "
-                                    f"({fx.op_count()[0]} device ops per call), {C} ch x {n} samples per GPU per step"
-                                    if args.graph else
-                                    f"effectchain filter x5 (RBJ) -> dyn-compressor -> reverb-freeverb, {C} ch x "
-                                    f"{n} samples per GPU per step, fused per sample"),
-                       "channels_per_gpu": C, "samples_per_channel": n,
+            "config": {"workload": r["workload"], "channels_per_gpu": r["channels_per_gpu"],
+                       "samples_per_channel": r["samples_per_channel"],
                        "parallelism": "replicas" if world > 1 else "single GPU"},
-            # The bound is the one serial recurrence left, not HBM (16 B/sample
-            # of input and output moves 0.5 % of peak): the time-parallel engine
-            # cuts the EQ sections and the Freeverb combs into time segments,
-            # but the envelope follower (attack or release by the sign of
-            # src - env) is serial per channel, 24.5 clocks per sample
-            # (tools/chain_latency.hip).  Ceiling = clock x channels / 24.5.
-            "roofline": {"bound": "serial-recurrence latency (compressor envelope)", "achieved": round(value, 3),
-                         "peak": round(FX_CLOCK_HZ * C / FX_CHAIN_CLK / 1e6, 1),
-                         "unit": "Msamples/s",
-                         "frac": round(value / (FX_CLOCK_HZ * C / FX_CHAIN_CLK / 1e6), 4),
-                         "traffic": None,
-                         "hbm_GBps": round(value * 16e6 / 1e9, 3),
-                         "note": f"ceiling = {FX_CLOCK_HZ / 1e9} GHz x {C} channels / {FX_CHAIN_CLK} clk per sample "
-                                 f"(the envelope follower's dependency chain, each channel's own); HBM carries "
-                                 f"16 B/sample of input and output"},
-            "cpu_baseline": cpu,
+            "engine": r["engine"],
+            "roofline": r["roofline"],
+            "parity": r["parity"],
+            "cpu_baseline": r["cpu_baseline"],
         }
         print(json.dumps(line), flush=True)
     if world > 1:

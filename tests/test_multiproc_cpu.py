@@ -51,6 +51,13 @@ def _worker(rank, world, port, q):
             w.wait()
         if rank == 0:
             q.put([b.numpy() for b in bufs])
+        # bench.py's N > 1 diagnostics: per-rank step / conv-only / reduce
+        # times, max over ranks, then the assembled fields on rank 0
+        t = torch.tensor([2.30 + 0.05 * rank, 2.10 + 0.10 * rank, 1.00 - 0.20 * rank], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        step_ms, conv_ms, reduce_ms = t.tolist()
+        if rank == 0:
+            q.put(shard.scaling_diagnostics(step_ms, conv_ms, reduce_ms, 2 * (N + K - 1) * 8))
         dist.barrier()
     finally:
         dist.destroy_process_group()
@@ -67,6 +74,7 @@ def test_channel_shard_reduce_world2():
         p.start()
     got = q.get(timeout=240)
     piped = q.get(timeout=240)
+    diag = q.get(timeout=240)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -74,6 +82,13 @@ def test_channel_shard_reduce_world2():
     np.testing.assert_allclose(got, full, rtol=0, atol=1e-12 * np.max(np.abs(full)))
     for s, b in enumerate(piped):
         np.testing.assert_allclose(b, full * (s + 1), rtol=0, atol=1e-12 * np.max(np.abs(full)) * (s + 1))
+    # max over ranks: step 2.35, conv 2.20, reduce 1.00 ms -> 0.85 of the reduce hidden
+    assert diag["conv_ms_per_step"] == 2.2 and diag["reduce_ms"] == 1.0
+    assert diag["overlap"] == 0.85
+    nbytes = 2 * (N + K - 1) * 8
+    assert diag["reduce_bytes_per_rank"] == nbytes
+    assert diag["reduce_GBps"] == round(nbytes / 1e-3 / 1e9, 2)
+    assert diag["hide_GBps"] == round(nbytes / 2.2e-3 / 1e9, 2)
 
 
 def test_channel_groups_partition():

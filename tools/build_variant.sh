@@ -6,11 +6,11 @@ set -eu
 cd "$(dirname "$0")/../algo-dsp_amd"
 name=$1; flags=$2; shift 2
 make -s >/dev/null
-mkdir -p ../ab/$name
+mkdir -p ../${ABDIR:-ab}/$name
 objs=""
 for src in "$@"; do
   b=$(basename "$src"); b=${b%.*}
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -Wno-unused-parameter $flags -c csrc/$src -o ../ab/$name/$b.o
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -Wno-unused-parameter $flags -c csrc/$src -o ../${ABDIR:-ab}/$name/$b.o
   objs="$objs $b.o"
 done
 link=""
@@ -18,5 +18,5 @@ for o in build/*.o; do
   skip=0; for x in $objs; do [ "$(basename $o)" = "$x" ] && skip=1; done
   [ $skip = 0 ] && link="$link $o"
 done
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -Wl,--no-undefined $link ../ab/$name/*.o -ldl -lpthread -o ../ab/$name.so
-echo built ab/$name.so
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -Wl,--no-undefined $link ../${ABDIR:-ab}/$name/*.o -ldl -lpthread -o ../${ABDIR:-ab}/$name.so
+echo built ${ABDIR:-ab}/$name.so
