@@ -272,14 +272,18 @@ __device__ __forceinline__ void pretwiddle_uc(int64_t j, int64_t Ns, int64_t N, 
   using Plan = FftPlan<R, V>;
   constexpr int T = Plan::T;
   const int64_t jm = j & (Ns - 1);
-  const int64_t step = N / (Ns * R);
+  // N, Ns and R are powers of two: shifts and an exact power-of-two scale
+  // instead of a 64-bit integer division and a float64 division per call
+  // (the same values: N / (Ns R) and e / N are exact either way)
+  const int lgN = __builtin_ctzll((unsigned long long)N);
+  const int64_t step = N >> (__builtin_ctzll((unsigned long long)Ns) + ilog2c(R));
   const int64_t mask = ((int64_t)1 << S) - 1;
   auto tw = [&](int64_t e) {
     e &= N - 1;
 #if AD_FFT_TWC
     (void)mask;
     double sn, cs;
-    sincospi(-2.0 * (double)e / (double)N, &sn, &cs);  // e / N exact (N a power of two)
+    sincospi(ldexp(-2.0 * (double)e, -lgN), &sn, &cs);  // -2 e / N, exact
     return make_double2(cs, sn);
 #else
     return c_mul(tw_lo[e & mask], tw_hi[e >> S]);
@@ -325,7 +329,7 @@ __device__ __forceinline__ double2 half_wneg(int64_t g, int64_t NF, const double
 #if AD_FFT_TWC
   (void)ftw_lo, (void)ftw_hi, (void)fS;
   double sn, cs;
-  sincospi(2.0 * (double)g / (double)NF, &sn, &cs);  // g / NF exact (NF a power of two)
+  sincospi(ldexp(2.0 * (double)g, -__builtin_ctzll((unsigned long long)NF)), &sn, &cs);  // 2 g / NF, exact
   return make_double2(cs, sn);
 #else
   const int64_t fm = ((int64_t)1 << fS) - 1;

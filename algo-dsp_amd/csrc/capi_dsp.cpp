@@ -130,6 +130,9 @@ struct ad_fx_chain {
   hipEvent_t ev[3][kFxSlots] = {};
   DevBuf<double> xT[kFxSlots], vT[kFxSlots], envT[kFxSlots], inT[kFxSlots], coT[kFxSlots];
   DevBuf<double> midT[kFxSlots];  // split K_eq: the first part's output rows
+  // EQ-only chains, one K_eq part per section (fx_run_staged): section k's
+  // output rows of chunk c in secT[k][c & 1], read by section k + 1 one launch later
+  DevBuf<double> secT[kMaxSecPerPass][2];
   // time-parallel engine (fx_tp.hip): K_eq segment states
   DevBuf<double> tp_zs, tp_carry;
   // K_carry's segment maps per (seg, nseg): M = A^seg and M^Q per section and
@@ -230,6 +233,16 @@ int fx_eq_split(const ad_fx_chain* h) {
   return (h->nsec + 2) / 2;  // part waves (s1 + loader) vs (ns - s1 + detector + loader)
 }
 
+// EQ-only chains (no compressor) run one K_eq part per section (see
+// fx_run_staged); STAGED_NOSPLIT keeps the one-workgroup pipeline.
+#ifndef AD_FX_EQ_PER_SECTION  // tools/ A/B builds
+#define AD_FX_EQ_PER_SECTION 1
+#endif
+bool fx_eq_per_section(const ad_fx_chain* h) {
+  return AD_FX_EQ_PER_SECTION && h->engine != AD_FX_ENGINE_STAGED_NOSPLIT && !h->comp_on && h->nsec >= 2 &&
+         h->nsec <= kMaxSecPerPass;
+}
+
 constexpr int64_t kFxChunk = 16384;  // staged engine: samples per stage chunk
 constexpr int kFxProfWords = 32;
 
@@ -253,6 +266,9 @@ void fx_grow_tmax(ad_fx_chain* h, int64_t t) {
       if (b->p && b->n < r) b->release();
     if (h->coT[k].p && h->coT[k].n < r * kVerbCombs) h->coT[k].release();
   }
+  for (auto& sk : h->secT)
+    for (auto& b : sk)
+      if (b.p && b.n < r) b.release();
   h->tmax = t;
 }
 
@@ -332,6 +348,56 @@ void fx_run_staged(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hip
     a.vbuf = h->vbuf.p;
     return a;
   };
+  if (fx_eq_per_section(h)) {
+    // EQ-only chain (a12-a14), one K_eq part per section: launch i runs section
+    // k of chunk i - k for every k, each part a workgroup of its own (one
+    // section wave and a loader: the section has a SIMD and a CU to itself),
+    // reading section k - 1's rows of that chunk, which the previous launch
+    // wrote into secT[k - 1][chunk & 1]; the last section writes vT (inT with
+    // Freeverb), and that chunk's later stages follow the launch.  The bits
+    // are the single-part kernel's: every section runs the reference
+    // operations on the same samples, its state carried across chunks.
+    const int ns = h->nsec;
+    const size_t r = (size_t)h->cpad * std::max(T, h->tmax);
+    for (int k = 0; k + 1 < ns; ++k)
+      for (auto& b : h->secT[k]) b.reserve(r);
+    const int64_t nch = (n + T - 1) / T;
+    int kl = 0;
+    for (int64_t li = 0; li < nch + ns - 1; ++li) {
+      const int64_t cd = li - (ns - 1);  // the chunk whose last section runs in this launch
+      if (li < nch) launch_fx_transpose_in(chunk_args(li), chunk_args(li).xT, s);
+      // inT / coT of slot cd % kFxSlots: chunk cd - kFxSlots's allpasses are done
+      if (verb && cd >= kFxSlots) AD_HIP(hipStreamWaitEvent(s, h->ev[EA][cd % kFxSlots], 0));
+      FxStageArgs e = chunk_args(std::min(li, nch - 1));
+      e.nparts = 0;
+      for (int k = 0; k < ns; ++k) {
+        const int64_t c = li - k;
+        if (c < 0 || c >= nch) continue;
+        const FxStageArgs ac = chunk_args(c);
+        const double* in = k == 0 ? ac.xT : h->secT[k - 1][c & 1].p;
+        double* out = k == ns - 1 ? (verb ? ac.inT : ac.vT) : h->secT[k][c & 1].p;
+        e.part[e.nparts++] = FxEqPart{k, 1, 0, ac.len, in, out, nullptr};
+      }
+      launch_fx_eq_sec(e, s);
+      if (cd < 0) continue;
+      const FxStageArgs b = chunk_args(cd);
+      if (!verb) {
+        launch_fx_transpose_out(b, b.vT, s);
+        continue;
+      }
+      kl = (int)(cd % kFxSlots);
+      AD_HIP(hipEventRecord(h->ev[EE][kl], s));
+      AD_HIP(hipStreamWaitEvent(sc, h->ev[EE][kl], 0));
+      launch_fx_comb(b, sc);
+      AD_HIP(hipEventRecord(h->ev[EC][kl], sc));
+      AD_HIP(hipStreamWaitEvent(sa, h->ev[EC][kl], 0));
+      launch_fx_allpass(b, sa);
+      AD_HIP(hipEventRecord(h->ev[EA][kl], sa));
+    }
+    AD_HIP(hipGetLastError());
+    if (verb) AD_HIP(hipStreamWaitEvent(s, h->ev[EA][kl], 0));
+    return;
+  }
   if (s1) {
     // Split K_eq: launch i runs part A (sections 0 .. s1-1) of chunk i and
     // part B (sections s1 .. ns-1 + detector) of chunk i - 1, which read A's
@@ -754,7 +820,7 @@ void fx_run(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hipStream_
       h->last_engine = AD_FX_ENGINE_TIME_PARALLEL;
     } else {
       fx_run_staged(h, d_buf, stride, n, s);
-      h->last_engine = fx_eq_split(h) ? AD_FX_ENGINE_STAGED : AD_FX_ENGINE_STAGED_NOSPLIT;
+      h->last_engine = (fx_eq_split(h) || fx_eq_per_section(h)) ? AD_FX_ENGINE_STAGED : AD_FX_ENGINE_STAGED_NOSPLIT;
     }
     AD_HIP(hipEventRecord(h->ev_last, s));
     return;

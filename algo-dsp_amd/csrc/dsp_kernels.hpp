@@ -124,12 +124,14 @@ struct FxStageArgs {
   VerbChState* vs;
   double* vbuf;
   unsigned long long* prof;  // diagnostics only (AD_FX_PROF): K_eq per wave {compute, barrier wait} clock ticks
-  FxEqPart part[2];          // K_eq parts (launch_fx_eq_parts)
+  FxEqPart part[kMaxSecPerPass];  // K_eq parts (launch_fx_eq_parts)
   int nparts;
 };
 // stage kernels; `mode` selects where a stage writes (see fx_staged.hip)
 void launch_fx_eq(const FxStageArgs& a, bool comp, int out_mode, hipStream_t s);
 void launch_fx_eq_parts(const FxStageArgs& a, hipStream_t s);  // a.part[0 .. nparts)
+// one section per part (part.s0, ns = 1, no detector), a workgroup each (EQ-only pipeline)
+void launch_fx_eq_sec(const FxStageArgs& a, hipStream_t s);
 void launch_fx_gain(const FxStageArgs& a, bool to_user, hipStream_t s);
 void launch_fx_transpose_in(const FxStageArgs& a, double* dstT, hipStream_t s);   // user -> dstT
 void launch_fx_transpose_out(const FxStageArgs& a, const double* srcT, hipStream_t s);  // srcT -> user

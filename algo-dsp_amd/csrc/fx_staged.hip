@@ -339,6 +339,128 @@ __global__ __launch_bounds__(64 * (kMaxSecPerPass + 2)) void k_fx_eq(FxStageArgs
 }
 
 // ---------------------------------------------------------------------------
+// K_sec: one EQ section of 64 channels per workgroup (the EQ-only chains'
+// per-section pipeline, fx_run_staged): part blockIdx.y runs section
+// part.s0 over its own chunk, so the sections of a cascade run on different
+// CUs in one launch.  Two waves:
+//   wave 0 (section) only reads its input rows out of an LDS ring, runs the
+//          DF-II-T recurrence with the reference operations (eq_section_step)
+//          and writes its outputs into a second ring; on its SIMD alone, its
+//          time is the section's dependency chain;
+//   wave 1 (I/O) loads input rows kSecPF steps ahead (16-B loads: lanes
+//          0-31 row r, lanes 32-63 row r + 1, two channels each), puts them
+//          into the ring one step ahead, and stores the section's outputs of
+//          the previous step.
+// One LDS-only barrier per step of kSecP samples.  Rows past the chunk are
+// re-read (loads) and never stored.
+// ---------------------------------------------------------------------------
+constexpr int kSecP = 32;   // samples per step
+constexpr int kSecPF = 2;   // I/O wave: steps of input loads in flight
+__global__ __launch_bounds__(128) void k_fx_eq_sec(FxStageArgs a) {
+#pragma clang fp contract(off)
+  __shared__ __attribute__((aligned(16))) double xr[2][kSecP][64];
+  __shared__ __attribute__((aligned(16))) double yr[2][kSecP][64];
+  const FxEqPart& P = a.part[blockIdx.y];
+  const int wid = wave_id();
+  const int l = threadIdx.x & 63;
+  const int g0 = blockIdx.x * 64;  // first channel of the group
+  const int64_t len = P.len;
+  const int64_t nst = (len + kSecP - 1) / kSecP;
+  const int cp = a.cpad;
+  if (wid == 0) {
+    const int c = g0 + l;
+    const int cc = c < a.channels ? c : a.channels - 1;
+    const int gs = P.s0;
+    const AD_GLOBAL double* sec = glob(a.eq.sec) + (int64_t)cc * a.eq.sec_ch_stride + gs * kSecStride;
+    double q[kSecStride];
+#pragma unroll
+    for (int k = 0; k < kSecStride; ++k) q[k] = sec[k];
+    AD_GLOBAL double* st = glob(a.eq.state) + ((int64_t)cc * a.eq.nsec + gs) * 2;
+    double d0 = st[0], d1 = st[1];
+    __builtin_amdgcn_s_waitcnt(0);
+    lds_barrier();  // step 0's rows are in xr[0]
+    for (int64_t k = 0; k <= nst; ++k) {
+      if (k < nst) {
+        const int nreal = (int)min((int64_t)kSecP, len - k * kSecP);
+        double x[kSecP], y[kSecP];
+#pragma unroll
+        for (int d = 0; d < kSecP; ++d) x[d] = xr[k & 1][d][l];
+        if (nreal == kSecP) {
+#pragma unroll
+          for (int h = 0; h < kSecP / kEqP; ++h)
+            eq_section_step<true>(q, d0, d1, *reinterpret_cast<const double(*)[kEqP]>(x + h * kEqP),
+                                  *reinterpret_cast<double(*)[kEqP]>(y + h * kEqP), kEqP);
+        } else {
+#pragma unroll
+          for (int h = 0; h < kSecP / kEqP; ++h)
+            eq_section_step<false>(q, d0, d1, *reinterpret_cast<const double(*)[kEqP]>(x + h * kEqP),
+                                   *reinterpret_cast<double(*)[kEqP]>(y + h * kEqP), nreal - h * kEqP);
+        }
+#pragma unroll
+        for (int d = 0; d < kSecP; ++d) yr[k & 1][d][l] = y[d];
+      }
+      lds_barrier();
+    }
+    if (c < a.channels) {
+      st[0] = d0;
+      st[1] = d1;
+    }
+  } else {
+    // I/O wave: lane l covers channels g0 + 2 (l & 31) .. + 1 of row 2 i + (l >> 5)
+    const AD_GLOBAL double* xin = glob(P.in);
+    AD_GLOBAL double* yo = glob(P.out);
+    const int cl = 2 * (l & 31), rh = l >> 5;
+    typedef double d2 __attribute__((ext_vector_type(2)));
+    d2 buf[kSecPF][kSecP / 2];
+    auto fetch = [&](d2 (&dst)[kSecP / 2], int64_t step) {  // branch-free: rows past the chunk re-read its last
+#pragma unroll
+      for (int i = 0; i < kSecP / 2; ++i) {
+        const int64_t row = min(step * kSecP + 2 * i + rh, len - 1);
+        dst[i] = *reinterpret_cast<const AD_GLOBAL d2*>(xin + row * cp + g0 + cl);
+      }
+    };
+    auto put = [&](const d2 (&src)[kSecP / 2], int64_t step) {
+#pragma unroll
+      for (int i = 0; i < kSecP / 2; ++i) *reinterpret_cast<d2*>(&xr[step & 1][2 * i + rh][cl]) = src[i];
+    };
+    auto flush = [&](int64_t step) {  // the section's outputs of `step`
+      const int64_t r0 = step * kSecP;
+      const int nreal = (int)min((int64_t)kSecP, len - r0);
+      d2 v[kSecP / 2];
+#pragma unroll
+      for (int i = 0; i < kSecP / 2; ++i) v[i] = *reinterpret_cast<const d2*>(&yr[step & 1][2 * i + rh][cl]);
+      if (nreal == kSecP) {
+#pragma unroll
+        for (int i = 0; i < kSecP / 2; ++i) *reinterpret_cast<AD_GLOBAL d2*>(yo + (r0 + 2 * i + rh) * cp + g0 + cl) = v[i];
+      } else {
+#pragma unroll
+        for (int i = 0; i < kSecP / 2; ++i)
+          if (2 * i + rh < nreal) *reinterpret_cast<AD_GLOBAL d2*>(yo + (r0 + 2 * i + rh) * cp + g0 + cl) = v[i];
+      }
+    };
+#pragma unroll
+    for (int b = 0; b < kSecPF; ++b) fetch(buf[b], b);
+    put(buf[0], 0);
+    fetch(buf[0], kSecPF);
+    lds_barrier();
+    // step k: rows of step k + 1 into xr, loads of step k + 1 + PF, outputs of step k - 1
+    for (int64_t k = 0; k <= nst; k += kSecPF) {
+#pragma unroll
+      for (int u = 0; u < kSecPF; ++u) {
+        const int64_t kk = k + u;
+        if (kk <= nst) {
+          const int b = (u + 1) % kSecPF;
+          if (kk + 1 < nst) put(buf[b], kk + 1);
+          fetch(buf[b], kk + 1 + kSecPF);
+          if (kk >= 1) flush(kk - 1);
+          lds_barrier();
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // K_gain: out = v * g(env) * makeup per (channel, sample), parallel.  A
 // workgroup takes a 64-sample x 64-channel tile (lane = channel, wave w =
 // samples 16w .. 16w+15).  to_user: the tile is transposed through LDS and
@@ -692,6 +814,12 @@ void launch_fx_eq_parts(const FxStageArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_fx_eq<true>, grid, block, dyn, s, a);
   else
     hipLaunchKernelGGL(k_fx_eq<false>, grid, block, dyn, s, a);
+}
+
+void launch_fx_eq_sec(const FxStageArgs& a, hipStream_t s) {
+  if (a.nparts <= 0) return;
+  const dim3 grid((unsigned)((a.channels + 63) / 64), (unsigned)a.nparts);
+  hipLaunchKernelGGL(k_fx_eq_sec, grid, dim3(128), 0, s, a);
 }
 
 void launch_fx_eq(const FxStageArgs& a, bool comp, int out_mode, hipStream_t s) {

@@ -716,3 +716,30 @@ def test_convolution_reverb(gpu, min_order):
     wet = np.concatenate([pc.process_block(x[a:b]) for a, b in blocks])
     want = 0.9 * x + 0.4 * wet
     assert rms(got, want) <= 1e-7
+
+
+def test_eq_only_per_section_pipeline_bit_exact(gpu):
+    """EQ-only chains (a12-a14) run one K_sec workgroup per section, each on
+    its own chunk (fx_run_staged): bit-exact against the oracle's
+    biquad.Chain.ProcessBlock (chain.go:59-70, section.go:47-53) over several
+    16384-sample chunks, calls that end mid-step and mid-chunk, a partial
+    channel group (130 channels), and the EQ state afterwards."""
+    fs = 48000.0
+    eq = design.config5_eq(fs)
+    C, n = 130, 40000
+    x = np.stack([0.5 * signals.white_noise(n, 1300 + c) for c in range(C)])
+    fx = P.EffectChain(C, eq, None, None, fs)
+    y = x.copy()
+    parts = []
+    for lo, hi in [(0, 17001), (17001, 17040), (17040, n)]:
+        b = y[:, lo:hi].copy()
+        fx.Process(b)
+        parts.append(b)
+    y = np.concatenate(parts, axis=1)
+    engine, _ = fx.LastEngine()
+    assert engine == P.EffectChain.ENGINE_STAGED, engine
+    for c in (0, 63, 64, 129):
+        v = x[c].copy()
+        for co, g in eq:
+            v, _ = O.biquad_chain_block(np.ravel(co), np.zeros(2 * len(co)), g, v)
+        assert np.array_equal(y[c], v), (c, float(np.max(np.abs(y[c] - v))))
