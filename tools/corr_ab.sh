@@ -3,5 +3,5 @@ timeout -k 10 300 python -u -m pytest tests/test_spectral_gpu.py -m gpu -x -q --
 for v in ${CORR_VARIANTS:-ab/head.so - ab/head.so - ab/head.so -}; do
   if [ "$v" = "-" ]; then L=algo-dsp_amd/libalgodsp_hip.so; else L=$v; fi
   ALGODSP_LIB=$PWD/$L timeout -k 10 120 python bench.py --workload corr --steps ${CORR_STEPS:-10} --warmup 3 > gpurun_out/corr.json 2>/dev/null || { echo fail $v; exit 1; }
-  python -c "import json;d=json.loads(open('gpurun_out/corr.json').read().strip().splitlines()[-1]); print('$v', d['value'], d['ms_per_step'], d['roofline']['frac'])"
+  python -c "import json;d=json.loads(open('gpurun_out/corr.json').read().strip().splitlines()[-1]); print('$v', d['value'], d['ms_per_step'], d['roofline']['frac'], d.get('parity'))"
 done
