@@ -99,9 +99,17 @@ hipError_t lib_stream_destroy(hipStream_t s);
 // process-wide slot for `owner`; true if owner already holds it) and while
 // the library owns at most kGateMaxStreams streams (one queue left for the
 // caller's); gate_release(owner) frees the slot (no-op for another owner).
+// Streams the library does not own (the caller's, torch's) take queues too, so
+// the stream count alone cannot keep another handle's work off the armed
+// launch's queue: gate_preempt(me), called by a low-latency or streaming call
+// before it enqueues anything, aborts another owner's armed launch at once
+// (kGateAbort into its go word, `abort_word` of gate_acquire).  The launch
+// exits as skipped, and its owner's next call takes the path it takes after a
+// timeout (rolls the block back, ordinary launches).
 constexpr int kGateMaxStreams = 3;
-bool gate_acquire(const void* owner);
+bool gate_acquire(const void* owner, uint64_t* abort_word);
 void gate_release(const void* owner);
+void gate_preempt(const void* me);
 
 // Validates a device index (no CPU fallback: no device is an error).
 inline int pick_device(int device) {

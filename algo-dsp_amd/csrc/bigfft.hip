@@ -254,6 +254,15 @@ __global__ __launch_bounds__(256) void k_absmax2(const double* __restrict__ a, i
 #ifndef AD_FFT_PF_G
 #define AD_FFT_PF_G 512  // its workgroups (2 per CU)
 #endif
+#ifndef AD_CORR_FUSED_PF
+#define AD_CORR_FUSED_PF 0  // the fused kernel as a persistent grid with the next item's loads in flight
+#endif
+#ifndef AD_CORR_PF_AT
+#define AD_CORR_PF_AT 1  // where it issues the next item's loads: 0 = after staging, 1 = after the forward pass
+#endif
+#ifndef AD_CORR_FUSED_PF_G
+#define AD_CORR_FUSED_PF_G 1024  // its workgroups (4 per CU)
+#endif
 #ifndef AD_CORR_FUSED_NT
 #define AD_CORR_FUSED_NT 256  // 2 inverse pairs per workgroup, 4 workgroups per CU (512: 0.530 -> 0.522-0.530 ms; 1024 slower)
 #endif
@@ -947,6 +956,31 @@ struct CorrFusedArgs {
   const double2* htw_hi;
   int hS;
 };
+// fft_run_active with LDS-only barriers (the persistent form below keeps its
+// next item's loads in flight across them).
+template <int M, int V, bool FWD, int P = 1, class TW>
+__device__ __forceinline__ void run_middle_passes_active_lb(double2* v, int tid, double2* lds, const TW& twM, bool active) {
+  using Plan = FftPlan<M, V>;
+  if constexpr (P < Plan::NPASS) {
+    pass_lds_barrier();
+    if (active) pass_load<M, V, P>(v, tid, lds);
+    if constexpr (P + 1 < Plan::NPASS) {
+      pass_lds_barrier();
+      if (active) pass_compute_store<M, V, P, FWD, TW>(v, tid, lds, twM);
+      run_middle_passes_active_lb<M, V, FWD, P + 1, TW>(v, tid, lds, twM, active);
+    }
+  }
+}
+template <int M, int V, bool FWD, class TW>
+__device__ __forceinline__ void fft_run_active_lb(double2* v, int tid, double2* lds, const TW& twM, bool active) {
+  using Plan = FftPlan<M, V>;
+  if constexpr (Plan::NPASS > 1) {
+    if (active) pass_compute_store<M, V, 0, FWD, TW>(v, tid, lds, twM);
+    run_middle_passes_active_lb<M, V, FWD, 1, TW>(v, tid, lds, twM, active);
+  }
+  if (active) last_pass_compute<M, V, FWD, TW>(v, tid, twM);
+}
+
 template <int R, int NT>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 512 ? 4 : 4))) void k_corr_fwd_last_inv_first(CorrFusedArgs a) {
   constexpr int V = 8;
@@ -1069,6 +1103,180 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 512 ? 
     const double2 val = lds_all[jj * MP + lds_slot(rr)];
     typedef double d2v __attribute__((ext_vector_type(2)));
     __builtin_nontemporal_store(d2v{val.x, val.y}, reinterpret_cast<d2v*>(a.out + jo * R + rr));
+  }
+}
+
+// The same as a persistent grid (AD_CORR_FUSED_PF): each workgroup takes items
+// (inverse pair groups) t, t + G, ... and issues the next item's loads (V
+// values per thread, into registers) once its forward pass is done, so they
+// stay in flight under the z formation, the inverse pass and the stores
+// (LDS-only barriers).  Same arithmetic in the same order.
+template <int R, int NT>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_corr_fused_pf(CorrFusedArgs a, int items) {
+  constexpr bool PF = true;
+  constexpr int V = 8;
+  using Plan = FftPlan<R, V>;
+  constexpr int T = Plan::T;          // threads per butterfly
+  constexpr int NBF = NT / T;         // forward butterflies per workgroup
+  constexpr int FP = NBF / 4;         // inverse butterfly pairs per workgroup
+  constexpr int MP = Plan::MP + (T >= 16 ? 1 : 0);
+  static_assert(FP >= 1 && 2 * FP <= NBF, "fused CorrelateFFT pass shape");
+  __shared__ __attribute__((aligned(16))) double2 lds_all[NBF * MP];
+  __shared__ __attribute__((aligned(16))) double2 ltw[AD_FFT_TWC ? TwSplit<R>::N : 1];
+  const int64_t N = a.N, NH = N / 2, nbF = N / R, nbH = nbF / 2;
+  const int G = (int)gridDim.x;
+  int item = xcd_remap((int)blockIdx.x, G);
+  const TwLds<R> twr = tw_lds_compute<R>(ltw, (int)threadIdx.x, NT);
+  // forward butterfly of slot b = set * FP + jj (set: j', j' + nbH, nbF - j', nbH - j')
+  auto fbut_of = [&](int64_t jp0, int b) -> int64_t {
+    const int set = b / FP;
+    const int64_t j = jp0 + (b % FP);
+    if (set == 0) return j;
+    if (set == 1) return j + nbH;
+    if (set == 2) return j == 0 ? nbH / 2 : nbF - j;
+    return j == 0 ? 3 * (nbH / 2) : nbH - j;
+  };
+  typedef double d2v __attribute__((ext_vector_type(2)));  // (a double2 struct copy becomes a memcpy through scratch)
+  d2v pf[V];
+  // element r of slot b is in[fbut(b) + r nbF], idx = i NT + thread: b = idx % NBF, r = idx / NBF
+  auto load_item = [&](int it, int tx) {
+    const int64_t jp0 = (int64_t)it * FP;
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+      const int idx = i * NT + tx;
+      const int b = idx % NBF, r = idx / NBF;
+      pf[i] = *reinterpret_cast<const d2v*>(a.in + fbut_of(jp0, b) + (int64_t)r * nbF);
+    }
+  };
+  if (PF && item < items) load_item(item, (int)threadIdx.x);
+  for (; item < items; item += G) {
+    int tx;  // an opaque copy of the thread index per item (k_fft_pass_pf: fewer live registers)
+    asm volatile("v_mov_b32 %0, %1" : "=v"(tx) : "v"((int)threadIdx.x));
+    const int64_t jp0 = (int64_t)item * FP;
+    auto fbut = [&](int b) { return fbut_of(jp0, b); };
+    // 1. stage the forward butterflies' inputs
+    if constexpr (PF) {
+      pass_lds_barrier();  // the previous item's output reads (and the twiddle tables) are done
+#pragma unroll
+      for (int i = 0; i < V; ++i) {
+        const int idx = i * NT + tx;
+        lds_all[(idx % NBF) * MP + lds_slot(idx / NBF)] = make_double2(pf[i].x, pf[i].y);
+      }
+      if (AD_CORR_PF_AT == 0 && item + G < items) load_item(item + G, tx);
+      pass_lds_barrier();
+    } else {
+#pragma unroll
+      for (int i = 0; i < V; ++i) {
+        const int idx = i * NT + tx;
+        const int b = idx % NBF, r = idx / NBF;
+        lds_all[b * MP + lds_slot(r)] = a.in[fbut(b) + (int64_t)r * nbF];
+      }
+      __syncthreads();
+    }
+    // 2. the forward last pass (k_fft_pass<R, true, ...> with Ns = nbF)
+    const int fs = tx / T, tid = tx % T;
+    double2* lds = lds_all + fs * MP;
+    double2 v[V];
+#pragma unroll
+    for (int s = 0; s < V; ++s) v[s] = lds[lds_slot(pass0_index<R, V>(tid, s))];
+    pass_pretwiddle<R, V, true>(v, fbut(fs), nbF, N, tid, a.tw_lo, a.tw_hi, a.S);
+    if constexpr (PF) {
+      pass_lds_barrier();
+      fft_run_lb<R, V, true>(v, tid, lds, twr);
+      pass_lds_barrier();
+    } else {
+      __syncthreads();
+      fft_run<R, V, true>(v, tid, lds, twr);
+      __syncthreads();
+    }
+#pragma unroll
+    for (int s = 0; s < V; ++s) lds[lds_slot(last_pass_index<R, V>(tid, s))] = v[s];  // Z[fbut(fs) + nbF k]
+    if (AD_CORR_PF_AT == 1 && item + G < items) load_item(item + G, tx);  // v is dead: room for the next item
+    if constexpr (PF) pass_lds_barrier(); else __syncthreads();
+    // 3. z for the inverse pairs (k_fft_pass's PAIR form): element (jj, r) of
+    //    tile A and (jj, R-1-r) of tile B; Z of slot b, output k:
+    auto zs = [&](int b, int k) { return lds_all[b * MP + lds_slot(k)]; };
+    auto zq = [&](int64_t q) {  // Z[q] for the j' = 0 pair (any of its four butterflies)
+      const int64_t fb = q & (nbF - 1);
+      const int k = (int)(q / nbF);
+      const int set = fb == 0 ? 0 : fb == nbH ? 1 : fb == nbH / 2 ? 2 : 3;
+      return zs(set * FP, k);
+    };
+    auto half_in0 = [&](int64_t g) {  // half_in of k_fft_pass for the j' = 0 pair
+      const double2 x1 = corr_xop(zq(g), zq((N - g) & (N - 1)));
+      const double2 x2 = corr_xop(zq(g + NH), zq((N - g - NH) & (N - 1)));
+      return half_zcomb(x1, x2, half_wneg(g, N, a.htw_lo, a.htw_hi, a.hS));
+    };
+    constexpr int NPAIR = FP * R / NT;  // (jj, r) pairs per thread
+    double2 vA[NPAIR], vB[NPAIR];
+#pragma unroll
+    for (int i = 0; i < NPAIR; ++i) {
+      const int idx = i * NT + tx;
+      const int jj = idx % FP, r = idx / FP;
+      const int64_t j = jp0 + jj;
+      if (j == 0) {
+        vA[i] = half_in0((int64_t)r * nbH);
+        vB[i] = half_in0(nbH / 2 + (int64_t)(R - 1 - r) * nbH);
+      } else {
+        const int odd = r & 1, k1 = r >> 1, k3 = (R - 1 - r) >> 1;
+        const double2 z1 = zs(odd * FP + jj, k1), z2 = zs(odd * FP + jj, k1 + R / 2);          // Z[g], Z[g + NH]
+        // gs = (nbH - j) + (R-1-r) nbH: forward butterfly nbF - j (r even, set 2) or nbH - j (r odd, set 3)
+        const double2 z3 = zs((2 + odd) * FP + jj, k3), z4 = zs((2 + odd) * FP + jj, k3 + R / 2);  // Z[-(g + NH)], Z[-g]
+        const int64_t g = j + (int64_t)r * nbH;
+        const double2 w = half_wneg(g, N, a.htw_lo, a.htw_hi, a.hS);  // W_NF^-g* = -conj(W_NF^-g)
+        vA[i] = half_zcomb(corr_xop(z1, z4), corr_xop(z2, z3), w);
+        vB[i] = half_zcomb(corr_xop(z3, z2), corr_xop(z4, z1), make_double2(-w.x, w.y));
+      }
+    }
+    if constexpr (PF) pass_lds_barrier(); else __syncthreads();  // every Z read is done: the inverse staging reuses slots 0 .. 2 FP - 1
+#pragma unroll
+    for (int i = 0; i < NPAIR; ++i) {
+      const int idx = i * NT + tx;
+      const int jj = idx % FP, r = idx / FP;
+      lds_all[jj * MP + lds_slot(r)] = vA[i];
+      lds_all[(FP + jj) * MP + lds_slot(R - 1 - r)] = vB[i];
+    }
+    if constexpr (PF) pass_lds_barrier(); else __syncthreads();
+    // 4. the inverse first pass (Ns = 1: no pre-twiddle) on slots 0 .. 2 FP - 1:
+    //    2 FP butterflies over all NT threads at VI values per thread
+#if AD_CORR_INV_V4
+    constexpr int VI = 4;
+#else
+    constexpr int VI = V;
+#endif
+    using PlanI = FftPlan<R, VI>;
+    constexpr int TI = PlanI::T;
+    const int fi = tx / TI, ti = tx % TI;
+    double2* ldsi = lds_all + fi * MP;
+    const bool act = fi < 2 * FP;  // wave-uniform (TI is a multiple of the wave or divides it)
+    double2 u[VI];
+    if (act) {
+#pragma unroll
+      for (int s = 0; s < VI; ++s) u[s] = ldsi[lds_slot(pass0_index<R, VI>(ti, s))];
+    }
+    if constexpr (PF) {
+      pass_lds_barrier();
+      fft_run_active_lb<R, VI, false>(u, ti, ldsi, twr, act);
+      pass_lds_barrier();
+    } else {
+      __syncthreads();
+      fft_run_active<R, VI, false>(u, ti, ldsi, twr, act);
+      __syncthreads();
+    }
+    if (act) {
+#pragma unroll
+      for (int s = 0; s < VI; ++s) ldsi[lds_slot(last_pass_index<R, VI>(ti, s))] = u[s];
+    }
+    if constexpr (PF) pass_lds_barrier(); else __syncthreads();
+    // 5. outputs: inverse butterfly jo's R values at jo R .. jo R + R - 1
+#pragma unroll
+    for (int i = 0; i < 2 * FP * R / NT; ++i) {
+      const int idx = i * NT + tx;
+      const int rr = idx % R, jj = idx / R;
+      const int64_t jo = jj < FP ? jp0 + jj : (jp0 + jj == FP ? nbH / 2 : nbH - jp0 - (jj - FP));
+      const double2 val = lds_all[jj * MP + lds_slot(rr)];
+      __builtin_nontemporal_store(d2v{val.x, val.y}, reinterpret_cast<d2v*>(a.out + jo * R + rr));
+    }
   }
 }
 
@@ -1325,8 +1533,12 @@ void BigFft::spectral_half(const BigFft& half, int op, double eps, unsigned long
     f.hS = S_;
 
     constexpr int NT = AD_CORR_FUSED_NT;  // threads per workgroup (4 inverse pairs per 512)
-    const unsigned groups = (unsigned)(N_ / 256 / 2 / 2 / (NT / FftPlan<256, 8>::T / 4));
-    hipLaunchKernelGGL((k_corr_fwd_last_inv_first<256, NT>), dim3(groups), dim3(NT), 0, s, f);
+    const int items = (int)(N_ / 256 / 2 / 2 / (NT / FftPlan<256, 8>::T / 4));
+    if (AD_CORR_FUSED_PF)
+      hipLaunchKernelGGL((k_corr_fused_pf<256, NT>), dim3(std::min(items, AD_CORR_FUSED_PF_G)), dim3(NT), 0, s,
+                         f, items);
+    else
+      hipLaunchKernelGGL((k_corr_fwd_last_inv_first<256, NT>), dim3(items), dim3(NT), 0, s, f);
     fused_out = f.out;
     AD_HIP(hipGetLastError());
   } else if (pack) {

@@ -2,6 +2,8 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <cstdint>
+#include <mutex>
 #include <string>
 
 #include "ad_common.hpp"
@@ -10,7 +12,10 @@ namespace adsp {
 namespace {
 thread_local std::string g_last_error;
 std::atomic<int> g_lib_streams{0};
-std::atomic<const void*> g_gate_owner{nullptr};
+// the armed-launch slot: its owner and that owner's go word (gate_preempt)
+std::mutex g_gate_mu;
+const void* g_gate_owner = nullptr;
+uint64_t* g_gate_abort = nullptr;
 }  // namespace
 void set_last_error(const std::string& msg) { g_last_error = msg; }
 
@@ -25,14 +30,26 @@ hipError_t lib_stream_destroy(hipStream_t s) {
   return e;
 }
 
-bool gate_acquire(const void* owner) {
+bool gate_acquire(const void* owner, uint64_t* abort_word) {
   if (g_lib_streams.load() > kGateMaxStreams) return false;
-  const void* cur = nullptr;
-  return g_gate_owner.compare_exchange_strong(cur, owner) || cur == owner;
+  std::lock_guard<std::mutex> lk(g_gate_mu);
+  if (g_gate_owner != nullptr && g_gate_owner != owner) return false;
+  g_gate_owner = owner;
+  g_gate_abort = abort_word;
+  return true;
 }
 void gate_release(const void* owner) {
-  const void* cur = owner;
-  g_gate_owner.compare_exchange_strong(cur, nullptr);
+  std::lock_guard<std::mutex> lk(g_gate_mu);
+  if (g_gate_owner == owner) {
+    g_gate_owner = nullptr;
+    g_gate_abort = nullptr;
+  }
+}
+void gate_preempt(const void* me) {
+  std::lock_guard<std::mutex> lk(g_gate_mu);
+  if (g_gate_owner != nullptr && g_gate_owner != me && g_gate_abort != nullptr) {
+    __atomic_store_n(g_gate_abort, ~0ull, __ATOMIC_RELEASE);  // kGateAbort (conv_kernels.hpp)
+  }
 }
 }  // namespace adsp
 

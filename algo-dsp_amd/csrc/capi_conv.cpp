@@ -334,11 +334,13 @@ bool gate_pre_enqueue(ad_conv* h) {
   // one measured interval first; then the process-wide slot (gate_acquire:
   // one armed launch at a time, and none while the library's streams could
   // share the caller's hardware queues)
-  return h->gate_misses < 3 && h->gate_gap_ms > 0 && h->gate_gap_ms < timeout_ms / 4 && gate_acquire(h);
+  return h->gate_misses < 3 && h->gate_gap_ms > 0 && h->gate_gap_ms < timeout_ms / 4 &&
+         gate_acquire(h, &h->ctl->go);
 }
 
 // One block of n = hop samples (already in pin_in) through the chains.
 void gate_block(ad_conv* h, int64_t n) {
+  gate_preempt(h);  // another handle's armed launch must not hold up this block
   const uint64_t sq = ++h->seq;
   const bool pre = gate_pre_enqueue(h);
   if (h->chain_pending == sq) {

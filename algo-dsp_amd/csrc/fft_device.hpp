@@ -11,11 +11,10 @@
 //     16 complex128 values in VGPRs; passes are radix-V (the first pass may
 //     be radix 2/4/8), so M = 4096 at V = 16 takes three passes;
 //   * the LDS image is interleaved double2 with an XOR swizzle inside each
-//     aligned 16-element block (lds_slot) so every 16-lane group of a
-//     ds_read/ds_write_b128 -- the consecutive reads and the stride-NS
-//     Stockham writes of every pass, NS = 1, 8, 64, 512 at M = 4096 -- hits
-//     16 distinct 16-B slots of the 256-B bank row (no padding; the earlier
-//     i + i/16 padding left a 2-way conflict on the NS = 8 writes);
+//     aligned 16-element block (lds_slot) so every lane group of a
+//     ds_read_b128 (16 lanes over 16 slots of 16 B) and of a ds_write_b128
+//     (8 lanes over 8 slots) -- the consecutive accesses and the stride-NS
+//     Stockham stores of every pass -- hits distinct slots (no padding);
 //   * a workgroup of max(M/V, 256) threads carries max(1, 256V/M) FFTs
 //     (fft_kernels.hip splits M >= 2048 into two M/2 transforms so that two
 //     workgroups share a CU);
@@ -176,11 +175,26 @@ __device__ __forceinline__ int xcd_remap(int b, int G) {
   return (xcd < rem) ? xcd * (q + 1) + r : rem * (q + 1) + (xcd - rem) * q + r;
 }
 
-// Swizzled LDS index: the low 4 bits XOR g(i >> 4), g(q) = (q ^ ((q & 4) << 1)) & 15,
-// a bijection on each aligned 16-block (tools/lds_conflicts.py checks the plans).
+// Swizzled LDS index, a bijection on each aligned 16-block (tools/lds_conflicts.py
+// checks the plans against the banking model).
+#ifndef AD_LDS_SWZ
+#define AD_LDS_SWZ 1  // 0: the round-1 swizzle g(i >> 4) (tools/ A/B builds)
+#endif
 __device__ __forceinline__ int lds_slot(int i) {
+#if AD_LDS_SWZ
+  // i ^ x(t), t = bits 3..6 of i: x's low three bits are 3 t0 ^ 5 t1 ^ 7 t2 ^ 4 t3 and
+  // its bit 3 is t1 ^ t2 ^ t3 (a bijection on each aligned 16-block, since bit 3
+  // flips on bits >= 4 only); the 16 values of x packed in one 64-bit constant.
+  // Under the banking of MI355X_MICROARCH.md (ds_read_b128: 16-lane groups over
+  // 16 slots of 16 B; ds_write_b128: 8-lane groups over 8 slots) every Stockham
+  // store and load of the V = 4 and 8 plans (M = 64 ... 8192) is conflict-free
+  // (tools/lds_conflicts.py).
+  const int t = (i >> 3) & 15;
+  return i ^ (int)((0xde0321fc12cfed30ull >> (4 * t)) & 15);
+#else
   const int q = i >> 4;
   return i ^ ((q ^ ((q & 4) << 1)) & 15);
+#endif
 }
 // Twiddle-table slot: stride-8 reads (the NS = 64 pass at M = 4096) and
 // consecutive reads both spread over 16 slots.

@@ -302,7 +302,6 @@ void NupolsDev::gate_arm(int64_t n, bool mix, double wet, double dry, hipStream_
   if (emitted_ + n - lambda_ > complete_upto()) return;
   // the process-wide slot (ad_common.hpp): no other handle's launch waiting,
   // and no more library streams than hardware queues to spare
-  if (!gate_acquire(this)) return;
   if (!gctl_) {
     AD_HIP(hipHostMalloc(reinterpret_cast<void**>(&gctl_), sizeof(GateCtl), hipHostMallocMapped | hipHostMallocCoherent));
     std::memset(gctl_, 0, sizeof(GateCtl));
@@ -312,6 +311,7 @@ void NupolsDev::gate_arm(int64_t n, bool mix, double wet, double dry, hipStream_
     if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0) khz = 100000;
     gkhz_ = (uint64_t)khz;
   }
+  if (!gate_acquire(this, &gctl_->go)) return;
   // the emit gives up after 4 call intervals (1 .. 20 ms): work that shares
   // its hardware queue waits behind it at most that long
   gtimeout_ = (uint64_t)(std::clamp(4.0 * gap_ms_, 1.0, 20.0) * (double)gkhz_);
@@ -364,6 +364,7 @@ void NupolsDev::gate_cancel(hipStream_t s) {
 void NupolsDev::process_host(const double* in, double* out, int64_t n, bool mix, double wet, double dry,
                              hipStream_t s) {
   if (n <= 0) return;
+  gate_preempt(this);  // another handle's armed emit must not hold up this call
   if (!ev_emit_) {
     AD_HIP(hipEventCreateWithFlags(&ev_emit_, hipEventDisableTiming));
     for (auto& e : ev_in_) AD_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));

@@ -353,9 +353,12 @@ def test_partitioned_gate_after_pause(gpu):
 
 def test_partitioned_two_handles_alternating(gpu):
     """two low-latency handles called alternately.  Only one
-    pre-enqueued emit may wait at a time (the process-wide slot), so neither
-    handle's call queues behind the other's waiting emit: no call takes as long
-    as a timeout, and both outputs match the oracle."""
+    pre-enqueued emit may wait at a time (the process-wide slot), and a call
+    aborts the other handle's armed emit before it enqueues anything
+    (gate_preempt), so neither handle's call queues behind the other's waiting
+    emit whichever hardware queues their streams share (streams created
+    earlier in the process, torch's included, shift that mapping): no call
+    takes as long as a timeout, and both outputs match the oracle."""
     import time
 
     h = irlib.large_church()[0, :30000].copy()
@@ -380,8 +383,6 @@ def test_partitioned_two_handles_alternating(gpu):
     lat = np.sort(np.array(lat[8:]))
     # no call waits out another handle's 20-ms emit timeout
     assert lat[-1] < 0.010 and lat[int(0.95 * lat.size)] < 0.002, lat[-10:]
-    hits = [g.LowLatencyStats()[0] for g in gs]
-    assert sum(hits) > 0, hits
 
 
 def test_partitioned_dirac(gpu):
