@@ -72,6 +72,9 @@ def parse():
     p.add_argument("--segments", type=int, default=1,
                    help="output segments per step (ad_conv_multi_process_device_segment); each segment's "
                         "mixdown reduce starts as soon as it is computed")
+    p.add_argument("--settle-steps", type=int, default=60,
+                   help="N = 1: after the timed region, this many more steps event-timed one by one (the line's "
+                        "`settled` key: the step once the board's clock has recovered from its load-onset dip)")
     p.add_argument("--kernel-timing", choices=["dominant", "on", "off"], default="dominant",
                    help="HIP events inside the timed region around the dominant kernel's launches only "
                         "(dominant: picked by a profiled warm-up pass, the other kernels timed in a pass "
@@ -284,7 +287,7 @@ def main():
         args.samples = 1 << 24
     ir = irlib.large_church()                       # [2][131072], Large Church zero padded
     r = run_conv(args, world, rank, local, dev, ir, args.channels, shard_cfg, mixdown, args.steps, args.warmup,
-                 args.kernel_timing)
+                 args.kernel_timing, args.settle_steps)
     C, n, K, out_len = args.channels, args.samples, ir.shape[1], r["out_len"]
     elapsed, prof, prof_live, mode = r["elapsed"], r["prof"], r["prof_live"], args.kernel_timing
     ids, x_host, eng, ys, mixes, last = r["ids"], r["x_host"], r["eng"], r["ys"], r["mixes"], r["last"]
@@ -448,6 +451,13 @@ def main():
             "shard_per_gpu": shard_sub,
             "cpu_baseline": cpu,
         }
+        if r["step_ms"]:
+            line["step_ms"] = r["step_ms"]  # each timed step, event-timed on the launch stream
+        if r["settled"]:
+            line["settled"] = dict(r["settled"], value=round(C * n / (r["settled"]["median_ms_last_half"] * 1e-3) / 1e6, 3),
+                                   note="the same step after the timed region once the board's clock has recovered "
+                                        "from its load-onset dip (median of the last half of the settle steps); "
+                                        "not `value`")
         if config5 is not None:
             line["config5"] = config5
         if config2 is not None:
@@ -515,7 +525,7 @@ def output_parity(args, r, ir, C_total, mixdown):
     return parity
 
 
-def run_conv(args, world, rank, local, dev, ir, C, shard_cfg, mixdown, steps, warmup, mode):
+def run_conv(args, world, rank, local, dev, ir, C, shard_cfg, mixdown, steps, warmup, mode, settle_steps=0):
     """One conv measurement: C channels x args.samples per GPU per step (IR[c mod 2]),
     optionally with the RCCL stereo mixdown; `steps` timed steps after `warmup`,
     bracketed by barrier + synchronize, max over ranks.  Returns the timing, the
@@ -627,14 +637,21 @@ def run_conv(args, world, rank, local, dev, ir, C, shard_cfg, mixdown, steps, wa
         dist.barrier()
     torch.cuda.synchronize(dev)
     red_ev.clear()
+    # per-step events on the launch stream (record only: no host wait inside the loop)
+    sev = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)] if world == 1 else None
     t0 = time.perf_counter()
-    for _ in range(steps):
+    if sev:
+        sev[0].record(stream)
+    for i in range(steps):
         step()
+        if sev:
+            sev[i + 1].record(stream)
     drain()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    step_ms = [round(sev[i].elapsed_time(sev[i + 1]), 4) for i in range(steps)] if sev else None
     last = (it[0] - 1) % nbuf
     # the reduces of the timed steps, event-timed on the side stream
     reduce_ms = sum(a.elapsed_time(b) for a, b in red_ev) / steps if red_ev else 0.0
@@ -690,9 +707,27 @@ def run_conv(args, world, rank, local, dev, ir, C, shard_cfg, mixdown, steps, wa
         diag = shard.scaling_diagnostics(elapsed / steps * 1e3, conv_elapsed / steps * 1e3, reduce_ms,
                                          2 * out_len * 8)
 
+    settled = None
+    if world == 1 and not mixdown and settle_steps > 0:
+        # The board's clock dips for a few ms once the load turns sustained and then
+        # recovers (tools/step_curve.py): the same step after
+        # the timed region, event-timed per step, median of the last half.  Reported
+        # beside `value`, never as it.
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(settle_steps + 1)]
+        ev[0].record(stream)
+        for i in range(settle_steps):
+            step()
+            ev[i + 1].record(stream)
+        torch.cuda.synchronize(dev)
+        per = [ev[i].elapsed_time(ev[i + 1]) for i in range(settle_steps)]
+        tail = sorted(per[settle_steps // 2:])
+        settled = {"steps": settle_steps, "median_ms_last_half": round(tail[len(tail) // 2], 4),
+                   "max_ms": round(max(per), 4), "min_ms": round(min(per), 4)}
+        last = (it[0] - 1) % nbuf
+
     return {"elapsed": elapsed, "prof": prof, "prof_live": prof_live, "ids": ids, "x_host": x_host, "eng": eng,
             "ys": ys, "mixes": mixes, "last": last, "comm": comm, "out_len": out_len, "schedule": eng.schedule(),
-            "reduce_diag": diag}
+            "reduce_diag": diag, "step_ms": step_ms, "settled": settled}
 
 
 def stream_measure(nblk: int, warmup_blocks: int, cpu_leg: bool) -> dict:
