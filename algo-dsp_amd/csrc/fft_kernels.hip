@@ -261,9 +261,15 @@ struct SplitPlan {
   static constexpr int LDS = Sub::MP + TwSplit<M2>::N + TwSplit<M>::N;  // double2 elements
 };
 
-template <int M>
-__global__ __launch_bounds__((SplitPlan<M>::T)) __attribute__((amdgpu_waves_per_eu(4))) void k_window_rfft_split(RfftArgs a) {
-  using SP = SplitPlan<M>;
+#ifndef AD_K1_V
+#define AD_K1_V 8  // K1's values per thread in the split transforms (16: 256-lane workgroups, 2 waves/SIMD)
+#endif
+#ifndef AD_K3_V
+#define AD_K3_V 8  // K3's (k_irfft_store_split)
+#endif
+template <int M, int VV = AD_K1_V>
+__global__ __launch_bounds__((SplitPlan<M, VV>::T)) __attribute__((amdgpu_waves_per_eu(32 / VV))) void k_window_rfft_split(RfftArgs a) {
+  using SP = SplitPlan<M, VV>;
   constexpr int M2 = SP::M2, V = SP::V, T = SP::T, L = M;
   __shared__ __attribute__((aligned(16))) double2 lds[SP::LDS];
   const int tid = threadIdx.x;
@@ -323,9 +329,9 @@ __global__ __launch_bounds__((SplitPlan<M>::T)) __attribute__((amdgpu_waves_per_
 }
 
 // NT: non-temporal Z loads and output stores (large launches, see k3_nt).
-template <int M, bool NT>
-__global__ __launch_bounds__((SplitPlan<M>::T)) __attribute__((amdgpu_waves_per_eu(4))) void k_irfft_store_split(IrfftArgs a) {
-  using SP = SplitPlan<M>;
+template <int M, bool NT, int VV = AD_K3_V>
+__global__ __launch_bounds__((SplitPlan<M, VV>::T)) __attribute__((amdgpu_waves_per_eu(32 / VV))) void k_irfft_store_split(IrfftArgs a) {
+  using SP = SplitPlan<M, VV>;
   constexpr int M2 = SP::M2, V = SP::V, T = SP::T, L = M;
   __shared__ __attribute__((aligned(16))) double2 lds[SP::LDS];
   const int tid = threadIdx.x;
@@ -515,7 +521,7 @@ void rfft_go(const RfftArgs& a, hipStream_t s) {
 template <int M>
 void rfft_split_go(const RfftArgs& a, hipStream_t s) {
   const int64_t items = a.ord_R > 0 ? (int64_t)a.channels * (a.ord_ny + 1) * a.ord_R : (int64_t)a.channels * a.jc;
-  const dim3 g((unsigned)items), b(SplitPlan<M>::T);
+  const dim3 g((unsigned)items), b(SplitPlan<M, AD_K1_V>::T);
   timed_launch(k_window_rfft_split<M>, g, b, s, a);
 }
 template <int M, int V>
@@ -527,7 +533,7 @@ void irfft_go(const IrfftArgs& a, hipStream_t s) {
 template <int M>
 void irfft_split_go(const IrfftArgs& a, hipStream_t s) {
   const int64_t items = a.ord_R > 0 ? (int64_t)a.channels * a.ord_ny * a.ord_R : (int64_t)a.channels * a.jc;
-  const dim3 g((unsigned)items), b(SplitPlan<M>::T);
+  const dim3 g((unsigned)items), b(SplitPlan<M, AD_K3_V>::T);
   if (k3_nt(items))
     timed_launch(k_irfft_store_split<M, true>, g, b, s, a);
   else

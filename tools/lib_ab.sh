@@ -13,6 +13,6 @@ for r in $(seq 1 ${ROUNDS:-2}); do
         --host-io off --shard-sub off --fx-leg off --stream-leg off ${BENCH_ARGS:-} > gpurun_out/libab.json 2> gpurun_out/libab.err
     rc=$?
     if [ $rc -ne 0 ]; then echo "lib $v rc=$rc"; tail -5 gpurun_out/libab.err; exit $rc; fi
-    python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], d['value'], d['ms_per_step'], {k:round(x['avg_us'],1) for k,x in d.get('kernels',{}).items()})" gpurun_out/libab.json "$v"
+    python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], d['value'], d['ms_per_step'], 'settled', (d.get('settled') or {}).get('median_ms_last_half'), {k:round(x['avg_us'],1) for k,x in d.get('kernels',{}).items()})" gpurun_out/libab.json "$v"
   done
 done
