@@ -538,6 +538,12 @@ constexpr int64_t kFxTpChunk = AD_FX_TP_CHUNK;
 #define AD_FX_TP_SERIAL_TAIL 0
 #endif
 constexpr bool kFxTpSerialTail = AD_FX_TP_SERIAL_TAIL;  // gain + Freeverb on the caller's stream (fx_run_tp)
+#ifndef AD_FX_TP_GAIN_ON_S  // tools/ A/B builds
+#define AD_FX_TP_GAIN_ON_S 1
+#endif
+// chunk i - 1's gain on the caller's stream behind chunk i's EQ, its Freeverb on
+// st[1] after it: the detector's stream runs detectors back to back (fx_run_tp)
+constexpr bool kFxTpGainOnS = AD_FX_TP_GAIN_ON_S;
 constexpr int kFxTpSeg = 64;     // K_eq segment (samples), at least
 constexpr size_t kFxTpMatsCached = 8;  // segment lengths whose maps stay cached
 
@@ -706,6 +712,22 @@ void fx_run_tp(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hipStre
     launch_fx_gain(b, true, s);
     launch_fxtp_verb(p, h->inC[kp].p, h->tmax, h->vbufC.p, h->coC.p, wu, s);
   };
+  // kFxTpGainOnS: chunk i - 1's gain on s (it waits there for its detector,
+  // by then chunk i's EQ is queued ahead of it) and its Freeverb on sv behind
+  // the gain; EE[kp] is re-recorded after the gain (the detector's wait on the
+  // EQ's record was already enqueued)
+  auto gain_verb = [&](const FxStageArgs& p, int kp) {
+    AD_HIP(hipStreamWaitEvent(s, h->ev[ED][kp], 0));
+    FxStageArgs b = p;
+    b.buf = h->inC[kp].p;
+    b.stride = h->tmax;
+    launch_fx_gain(b, true, s);
+    AD_HIP(hipEventRecord(h->ev[EE][kp], s));
+    AD_HIP(hipStreamWaitEvent(sv, h->ev[EE][kp], 0));
+    launch_fxtp_verb(p, h->inC[kp].p, h->tmax, h->vbufC.p, h->coC.p, wu, sv);
+    AD_HIP(hipEventRecord(h->ev[EA][kp], sv));
+  };
+  const bool gain_on_s = kFxTpGainOnS && !kFxTpSerialTail && comp && verb;
   int64_t i = 0;
   int k = 0;
   for (int64_t t0 = 0; t0 < n; t0 += T, ++i) {
@@ -764,6 +786,14 @@ void fx_run_tp(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hipStre
       prev = a;
       continue;
     }
+    if (gain_on_s) {
+      AD_HIP(hipStreamWaitEvent(sd, h->ev[EE][k], 0));
+      launch_fxtp_det(a, sd);
+      AD_HIP(hipEventRecord(h->ev[ED][k], sd));
+      if (i > 0) gain_verb(prev, (int)((i - 1) % kFxSlots));
+      prev = a;
+      continue;
+    }
     if (comp) {
       AD_HIP(hipStreamWaitEvent(sd, h->ev[EE][k], 0));
       launch_fxtp_det(a, sd);
@@ -795,6 +825,7 @@ void fx_run_tp(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hipStre
     AD_HIP(hipGetLastError());
     return;
   }
+  if (gain_on_s) gain_verb(prev, k);  // the last chunk's
   AD_HIP(hipGetLastError());
   AD_HIP(hipStreamWaitEvent(s, h->ev[EA][k], 0));  // the last chunk's reverb / output follows all work
 }
