@@ -11,7 +11,7 @@ from algodsp import design, processors as P  # noqa: E402
 fs = 48000.0
 C, n = 256, 1 << 20
 x = torch.randn(C, n, dtype=torch.float64, device="cuda") * 0.3
-for chunk in (32768, 65536, 98304, 131072, 262144):
+for chunk in [int(c) for c in (sys.argv[1:] or (16384, 32768, 49152, 65536, 98304, 131072))]:
     fx = P.EffectChain(C, design.config5_eq(fs), {"auto_makeup": 0, "makeup_db": 0.0},
                        (0.22, 1.0, 0.72, 0.45, 0.015), fs)
     fx.SetEngine(P.EffectChain.ENGINE_AUTO, chunk)
