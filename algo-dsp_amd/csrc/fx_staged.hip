@@ -478,32 +478,50 @@ __device__ __forceinline__ void atomic_min_pos(double* p, double v) {
 }
 
 template <bool TO_USER>
-__global__ __launch_bounds__(256) void k_fx_gain(FxStageArgs a) {
+__global__ __launch_bounds__(256) void k_fx_gain(FxStageArgs a, int tiles_per_wg) {
 #pragma clang fp contract(off)
   __shared__ double tile[64][65];
   __shared__ double red[3][4][64];
   const int w = wave_id();
   const int l = threadIdx.x & 63;
   const int c = blockIdx.y * 64 + l;
-  const int64_t t0 = (int64_t)blockIdx.x * 64;
   const CompParams& p = a.cp;
   double ip = 0.0, op = 0.0, gr = 1.0;
+  // tiles_per_wg consecutive 64-sample tiles: one set of metric atomics per
+  // workgroup and channel for all of them (the atomics on a channel's three
+  // words serialise in the L2)
+  for (int q = 0; q < tiles_per_wg; ++q) {
+    const int64_t t0 = ((int64_t)blockIdx.x * tiles_per_wg + q) * 64;
+    if (t0 >= a.len) break;  // uniform
 #pragma unroll 4
-  for (int j = 0; j < 16; ++j) {
-    const int tl = w * 16 + j;
-    const int64_t t = t0 + tl;
-    double out = 0.0;
-    if (t < a.len) {
-      const double v = a.vT[t * a.cpad + c];
-      const double g = gain_for_level(p, a.envT[t * a.cpad + c]);
-      out = v * g * p.makeup_lin;
-      const double il = fabs(v), ol = fabs(out);
-      if (il > ip) ip = il;
-      if (ol > op) op = ol;
-      if (g < gr) gr = g;
-      if (!TO_USER) a.inT[t * a.cpad + c] = out;
+    for (int j = 0; j < 16; ++j) {
+      const int tl = w * 16 + j;
+      const int64_t t = t0 + tl;
+      double out = 0.0;
+      if (t < a.len) {
+        const double v = a.vT[t * a.cpad + c];
+        const double g = gain_for_level(p, a.envT[t * a.cpad + c]);
+        out = v * g * p.makeup_lin;
+        const double il = fabs(v), ol = fabs(out);
+        if (il > ip) ip = il;
+        if (ol > op) op = ol;
+        if (g < gr) gr = g;
+        if (!TO_USER) a.inT[t * a.cpad + c] = out;
+      }
+      if (TO_USER) tile[tl][l] = out;
     }
-    if (TO_USER) tile[tl][l] = out;
+    if (TO_USER) {
+      __syncthreads();
+      // lane = sample, wave w = channels 16w .. 16w+15 of the tile
+      const int64_t t = t0 + l;
+#pragma unroll 4
+      for (int j = 0; j < 16; ++j) {
+        const int cl = w * 16 + j;
+        const int ch = blockIdx.y * 64 + cl;
+        if (ch < a.channels && t < a.len) a.buf[(int64_t)ch * a.stride + t] = tile[l][cl];
+      }
+      __syncthreads();  // the tile's reads before the next tile's writes
+    }
   }
   red[0][w][l] = ip;
   red[1][w][l] = op;
@@ -520,16 +538,6 @@ __global__ __launch_bounds__(256) void k_fx_gain(FxStageArgs a) {
     if (ip > 0.0) atomic_max_pos(&cs->in_peak, ip);
     if (op > 0.0) atomic_max_pos(&cs->out_peak, op);
     if (gr < 1.0) atomic_min_pos(&cs->gr, gr);
-  }
-  if (TO_USER) {
-    // lane = sample, wave w = channels 16w .. 16w+15 of the tile
-    const int64_t t = t0 + l;
-#pragma unroll 4
-    for (int j = 0; j < 16; ++j) {
-      const int cl = w * 16 + j;
-      const int ch = blockIdx.y * 64 + cl;
-      if (ch < a.channels && t < a.len) a.buf[(int64_t)ch * a.stride + t] = tile[l][cl];
-    }
   }
 }
 
@@ -830,13 +838,23 @@ void launch_fx_eq(const FxStageArgs& a, bool comp, int out_mode, hipStream_t s) 
   launch_fx_eq_parts(b, s);
 }
 
+#ifndef AD_FX_GAIN_TPW
+#define AD_FX_GAIN_TPW 8  // 64-sample tiles per K_gain workgroup, at most
+#endif
+#ifndef AD_FX_GAIN_MINWG
+#define AD_FX_GAIN_MINWG 1024  // while the grid keeps at least this many workgroups
+#endif
 void launch_fx_gain(const FxStageArgs& a, bool to_user, hipStream_t s) {
   if (a.len <= 0) return;
-  const dim3 grid((unsigned)((a.len + 63) / 64), (unsigned)((a.channels + 63) / 64));
+  const int64_t tiles = (a.len + 63) / 64, cgroups = (a.channels + 63) / 64;
+  // several tiles per workgroup while the grid keeps AD_FX_GAIN_MINWG workgroups
+  int tpw = 1;
+  while (tpw < AD_FX_GAIN_TPW && (tiles / (2 * tpw)) * cgroups >= AD_FX_GAIN_MINWG) tpw *= 2;
+  const dim3 grid((unsigned)((tiles + tpw - 1) / tpw), (unsigned)cgroups);
   if (to_user)
-    hipLaunchKernelGGL(k_fx_gain<true>, grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_fx_gain<true>, grid, dim3(256), 0, s, a, tpw);
   else
-    hipLaunchKernelGGL(k_fx_gain<false>, grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_fx_gain<false>, grid, dim3(256), 0, s, a, tpw);
 }
 
 void launch_fx_transpose_in(const FxStageArgs& a, double* dstT, hipStream_t s) {
