@@ -388,6 +388,7 @@ def main():
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(ir, args.cpu_sample)
         traffic = None
+        step_pmc = None
         tfile = ROOT / "profiles" / "pmc_traffic.json"
         if tfile.exists():
             try:
@@ -396,6 +397,10 @@ def main():
                 same = tab.get("_config") == {"channels": C, "samples": n, "hop": args.hop}
                 key = next((k for k in tab if k == dom or k.startswith(dom)), None)
                 traffic = tab[key]["hbm_bytes_per_launch"] if key and same else None
+                if same and world == 1 and not shard_cfg:
+                    # the whole step: K1 + K2 + K3's PMC bytes (one launch each per step at N = 1)
+                    ks = [k for k in tab if k.startswith(("k_window_rfft", "k_fdl_mac", "k_irfft_store"))]
+                    step_pmc = sum(tab[k]["hbm_bytes_per_launch"] for k in ks) if len(ks) == 3 else None
             except Exception:
                 traffic = None
         workload = ("OverlapSave partitioned conv, stereo, 131072-tap IR, full linear convolution, "
@@ -451,6 +456,15 @@ def main():
             "shard_per_gpu": shard_sub,
             "cpu_baseline": cpu,
         }
+        if step_pmc:
+            alg = 80 * C * n  # x in, y out, X and Z written and read: 8 + 8 + 32 + 32 B per sample
+            sec = elapsed / args.steps
+            line["step_hbm"] = {"pmc_bytes": step_pmc, "alg_bytes": alg,
+                                "frac_pmc": round(step_pmc / sec / 1e9 / HBM_PEAK_GBS, 4),
+                                "frac_alg": round(alg / sec / 1e9 / HBM_PEAK_GBS, 4),
+                                "note": "whole step at ms_per_step against 8 TB/s: PMC bytes of K1 + K2 + K3 "
+                                        "(profiles/pmc_traffic.json, FETCH_SIZE x 2 + WRITE_SIZE) and the 80 B/sample "
+                                        "algorithmic figure"}
         if r["step_ms"]:
             line["step_ms"] = r["step_ms"]  # each timed step, event-timed on the launch stream
         if r["settled"]:
