@@ -254,6 +254,9 @@ __global__ __launch_bounds__(256) void k_absmax2(const double* __restrict__ a, i
 #ifndef AD_FFT_PF_G
 #define AD_FFT_PF_G 512  // its workgroups (2 per CU)
 #endif
+#ifndef AD_CORR_TW_EARLY
+#define AD_CORR_TW_EARLY 1  // the fused kernel's twiddles from the tables, loaded ahead of its data
+#endif
 #ifndef AD_CORR_FUSED_PF
 #define AD_CORR_FUSED_PF 0  // the fused kernel as a persistent grid with the next item's loads in flight
 #endif
@@ -1004,6 +1007,27 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 512 ? 
     if (set == 2) return j == 0 ? nbH / 2 : nbF - j;
     return j == 0 ? 3 * (nbH / 2) : nbH - j;
   };
+  constexpr int NPAIR = FP * R / NT;  // (jj, r) pairs per thread in step 3
+#if AD_CORR_TW_EARLY
+  // The twiddles of steps 2 and 3 from the W_N table pair, loaded ahead of the
+  // data (vmcnt retires in order: they land with it), instead of four FP64
+  // sincospi per thread on the VALU.  Step 2's pre-twiddle (Ns = nbF, so
+  // j mod Ns = j and N / (Ns R) = 1): u^tid and u^T with u = W_N^j; step 3's
+  // W_N^-g, g = j' + r nbH.
+  const int64_t tmask = ((int64_t)1 << a.S) - 1, hmask = ((int64_t)1 << a.hS) - 1;
+  const int64_t jf = fbut((int)threadIdx.x / T);
+  const int64_t e1 = (jf * ((int)threadIdx.x % T)) & (N - 1), e2 = (jf * T) & (N - 1);
+  const double2 tl1 = a.tw_lo[e1 & tmask], th1 = a.tw_hi[e1 >> a.S];
+  const double2 tl2 = a.tw_lo[e2 & tmask], th2 = a.tw_hi[e2 >> a.S];
+  double2 zl[NPAIR], zh[NPAIR];
+#pragma unroll
+  for (int i = 0; i < NPAIR; ++i) {
+    const int idx = i * NT + (int)threadIdx.x;
+    const int64_t g = jp0 + idx % FP + (int64_t)(idx / FP) * nbH;
+    zl[i] = a.htw_lo[g & hmask];
+    zh[i] = a.htw_hi[g >> a.hS];
+  }
+#endif
   // 1. stage the forward butterflies' inputs: element r of slot b is in[fbut(b) + r nbF]
 #pragma unroll
   for (int i = 0; i < V; ++i) {
@@ -1018,7 +1042,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 512 ? 
   double2 v[V];
 #pragma unroll
   for (int s = 0; s < V; ++s) v[s] = lds[lds_slot(pass0_index<R, V>(tid, s))];
+#if AD_CORR_TW_EARLY
+  pretwiddle_apply<R, V>(v, c_mul(tl1, th1), c_mul(tl2, th2));
+#else
   pass_pretwiddle<R, V, true>(v, fbut(fs), nbF, N, tid, a.tw_lo, a.tw_hi, a.S);
+#endif
   __syncthreads();
   fft_run<R, V, true>(v, tid, lds, twr);
   __syncthreads();
@@ -1039,7 +1067,6 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 512 ? 
     const double2 x2 = corr_xop(zq(g + NH), zq((N - g - NH) & (N - 1)));
     return half_zcomb(x1, x2, half_wneg(g, N, a.htw_lo, a.htw_hi, a.hS));
   };
-  constexpr int NPAIR = FP * R / NT;  // (jj, r) pairs per thread
   double2 vA[NPAIR], vB[NPAIR];
 #pragma unroll
   for (int i = 0; i < NPAIR; ++i) {
@@ -1054,8 +1081,12 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 512 ? 
       const double2 z1 = zs(odd * FP + jj, k1), z2 = zs(odd * FP + jj, k1 + R / 2);          // Z[g], Z[g + NH]
       // gs = (nbH - j) + (R-1-r) nbH: forward butterfly nbF - j (r even, set 2) or nbH - j (r odd, set 3)
       const double2 z3 = zs((2 + odd) * FP + jj, k3), z4 = zs((2 + odd) * FP + jj, k3 + R / 2);  // Z[-(g + NH)], Z[-g]
+#if AD_CORR_TW_EARLY
+      const double2 w = c_conj(c_mul(zl[i], zh[i]));  // W_N^-g, g = j + r nbH
+#else
       const int64_t g = j + (int64_t)r * nbH;
       const double2 w = half_wneg(g, N, a.htw_lo, a.htw_hi, a.hS);  // W_NF^-g* = -conj(W_NF^-g)
+#endif
       vA[i] = half_zcomb(corr_xop(z1, z4), corr_xop(z2, z3), w);
       vB[i] = half_zcomb(corr_xop(z3, z2), corr_xop(z4, z1), make_double2(-w.x, w.y));
     }
