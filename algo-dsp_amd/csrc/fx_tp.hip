@@ -264,12 +264,13 @@ __global__ __launch_bounds__(kFxTpMaxSeg) void k_fxtp_carry(FxTpEqArgs a) {
 // wave 0; the other lanes repeat them): a 64-channel group would need
 // ~40 GB/s of row traffic into one CU at the detector's pace.  Three waves:
 //   wave 1 (loader) keeps kDetNB batches of row loads in flight in registers
-//          (every load covers 64 / kDetCh rows of kDetCh channels; <= 63
-//          outstanding) and puts each batch into a small LDS ring two steps
-//          before the detector consumes it;
+//          (every load covers 64 / kDetCh rows of kDetCh channels; 64
+//          outstanding at 8 batches of 64 rows: the 64th issue waits for the
+//          6-bit vmcnt) and puts each batch into a small LDS ring two steps
+//          before the detector consumes it (kDetNB even: the steps run in pairs);
 //   wave 0 (detector) reads batch k + 1 out of the ring before it runs the
 //          envelope chain over batch k (the LDS latency hides under the
-//          chain) and puts the 16 envelopes into a second ring;
+//          chain) and puts the batch's envelopes into a second ring;
 //   wave 2 (storer) writes the envelopes of batch k - 1 to memory with two
 //          full-width stores (no selects or address arithmetic on the
 //          detector's issue slots, and no stores in the loader's vmcnt).
@@ -278,8 +279,11 @@ __global__ __launch_bounds__(kFxTpMaxSeg) void k_fxtp_carry(FxTpEqArgs a) {
 // ---------------------------------------------------------------------------
 constexpr int kDetCh = 8;      // channels per workgroup
 #ifndef AD_DET_B  // tools/ A/B builds may override
-#define AD_DET_B 32
-#define AD_DET_NB 14
+// round 5, with the detector's stream running detectors only (config 5, same
+// box, profiles/r05_fx_det_batch_ab.txt): 16 rows 11.39, 32 rows 12.16,
+// 64 rows 12.29-12.31 Gsamples/s (14 or 8 batches in flight alike)
+#define AD_DET_B 64
+#define AD_DET_NB 8
 #endif
 constexpr int kDetB = AD_DET_B;  // rows per batch
 constexpr int kDetLd = kDetB * kDetCh / 64;  // loads per batch (2)
@@ -484,6 +488,7 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 constexpr int kDet1D = 8;                 // batches in flight (DMA issued this many batches ahead)
 constexpr int kDet1Slots = kDet1D + 2;    // ring slots
 constexpr int kDet1Wait = 6 * (kDet1D - 1);  // ops issued after batch k + 1's DMAs, at step k
+#if AD_DET_B == 32  // the one-wave form needs 32-row batches of 8 channels (two 1-KiB DMAs)
 static_assert(kDetB == 32 && kDetCh == 8, "one-wave detector: 32-row batches of 8 channels (two 1-KiB DMAs)");
 static_assert(kDet1Wait <= 63, "vmcnt holds 6 bits");
 
@@ -589,6 +594,8 @@ __global__ __launch_bounds__(64) void k_fxtp_det1(FxStageArgs a) {
     o->env = cs.env;
   }
 }
+
+#endif  // AD_DET_B == 32
 
 // ---------------------------------------------------------------------------
 // K_verb: Freeverb for one channel per workgroup (reverb.go:57-189), every
@@ -815,9 +822,11 @@ void launch_fxtp_det(const FxStageArgs& a, hipStream_t s) {
   if (a.len <= 0) return;
   const CompParams& p = a.cp;
   const bool bare = !p.lp_on && !p.hp_on && !p.detector_rms;
+#if AD_DET_B == 32
   if (AD_DET_ONEWAVE && bare)
     hipLaunchKernelGGL(k_fxtp_det1, dim3((unsigned)((a.channels + kDetCh - 1) / kDetCh)), dim3(64), 0, s, a);
   else
+#endif
     hipLaunchKernelGGL(k_fxtp_det, dim3((unsigned)((a.channels + kDetCh - 1) / kDetCh)), dim3(192), 0, s, a);
 }
 
