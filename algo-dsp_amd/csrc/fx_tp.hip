@@ -484,11 +484,11 @@ __global__ __launch_bounds__(192) void k_fxtp_det(FxStageArgs a) {
 #ifndef AD_DET_ONEWAVE  // tools/ A/B builds: 1 = this kernel for the bare detector
 #define AD_DET_ONEWAVE 0
 #endif
+#if AD_DET_B == 32  // the one-wave form needs 32-row batches of 8 channels (two 1-KiB DMAs)
 typedef __attribute__((address_space(3))) void lds_void_t;
 constexpr int kDet1D = 8;                 // batches in flight (DMA issued this many batches ahead)
 constexpr int kDet1Slots = kDet1D + 2;    // ring slots
 constexpr int kDet1Wait = 6 * (kDet1D - 1);  // ops issued after batch k + 1's DMAs, at step k
-#if AD_DET_B == 32  // the one-wave form needs 32-row batches of 8 channels (two 1-KiB DMAs)
 static_assert(kDetB == 32 && kDetCh == 8, "one-wave detector: 32-row batches of 8 channels (two 1-KiB DMAs)");
 static_assert(kDet1Wait <= 63, "vmcnt holds 6 bits");
 
@@ -820,9 +820,9 @@ void launch_fxtp_carry(const FxTpEqArgs& a, hipStream_t s) {
 
 void launch_fxtp_det(const FxStageArgs& a, hipStream_t s) {
   if (a.len <= 0) return;
+#if AD_DET_B == 32
   const CompParams& p = a.cp;
   const bool bare = !p.lp_on && !p.hp_on && !p.detector_rms;
-#if AD_DET_B == 32
   if (AD_DET_ONEWAVE && bare)
     hipLaunchKernelGGL(k_fxtp_det1, dim3((unsigned)((a.channels + kDetCh - 1) / kDetCh)), dim3(64), 0, s, a);
   else
