@@ -251,6 +251,12 @@ __global__ __launch_bounds__(256) void k_absmax2(const double* __restrict__ a, i
 #ifndef AD_FFT_PF_F
 #define AD_FFT_PF_F 16  // its butterflies per tile (PACKIN: half of them mirrors)
 #endif
+#ifndef AD_FFT_PF_RO
+#define AD_FFT_PF_RO 0  // the last inverse pass (real outputs) persistent too: measured slower (0.551 -> 0.566-0.578 ms per call, profiles/r05_corr_pf_ro_ab.txt)
+#endif
+#ifndef AD_FFT_PF_RO_G
+#define AD_FFT_PF_RO_G 1024  // its workgroups (R = 128: 33 KiB of LDS, four per CU)
+#endif
 #ifndef AD_FFT_PF_G
 #define AD_FFT_PF_G 512  // its workgroups (2 per CU)
 #endif
@@ -352,6 +358,69 @@ __device__ __forceinline__ double2 half_zcomb(double2 x1, double2 x2, double2 w)
   const double2 e = make_double2(0.5 * (x1.x + x2.x), 0.5 * (x1.y + x2.y));
   const double2 o = c_mul(make_double2(0.5 * (x1.x - x2.x), 0.5 * (x1.y - x2.y)), w);
   return make_double2(e.x - o.y, e.y + o.x);
+}
+
+// The last inverse pass's real outputs (REALOUT): element rr of butterfly jj
+// of a tile of F butterflies, output index o, value val (LDS row stride MP).
+template <int F>
+__device__ __forceinline__ void realout_store(const FftPassArgs& a, const double2* lds_all, int MP, int jj, int rr,
+                                              int64_t o, double2 val, int bt, double oscale, double oscale2,
+                                              int64_t Ns, int64_t nb) {
+  auto emit = [&](int64_t q, double x) {
+    if (a.remap) {
+      if (q < a.n_front)
+        a.out_real[a.front_off + q] = x * oscale * oscale2;
+      else if (q >= a.back_from)
+        a.out_real[q - a.back_from] = x * oscale * oscale2;
+    } else {
+      a.out_real[bt * a.out_batch + q] = x * a.scale;
+    }
+  };
+  if (AD_FFT_RO_VEC && a.remap && a.pairs && Ns >= F && nb % F == 0 && ((a.front_off + a.back_from) & 1) == 0) {
+    // Real pairs into the lag order with 16-B stores.  For fixed rr the
+    // tile's F butterflies give 2F consecutive reals q = 2o, 2o + 1, and
+    // both region maps (q + front_off, q - back_from) shift q by amounts of
+    // one parity (N is even), so whether (2o, 2o+1) lands on a 16-B slot
+    // is the same for every element: `odd` = it does not, and lane jj then
+    // owns the slot (2o - 1, 2o) (its left neighbour's Im and its Re); lane
+    // 0 writes only its Re, lane F - 1 also its Im.  A slot whose two
+    // reals do not land side by side (a region edge) is written per real.
+    auto dst = [&](int64_t q) -> int64_t {
+      return q < a.n_front ? a.front_off + q : (q >= a.back_from ? q - a.back_from : -1);
+    };
+    const bool odd = ((a.front_off + (int64_t)(((uintptr_t)a.out_real >> 3) & 1)) & 1) != 0;
+    typedef double d2v __attribute__((ext_vector_type(2)));
+    const double x = val.x * oscale * oscale2, y = val.y * oscale * oscale2;
+    auto put2 = [&](int64_t ql, double lo, double hi) {  // reals ql, ql + 1
+      const int64_t d0 = dst(ql), d1 = dst(ql + 1);
+      if (d0 >= 0 && d1 == d0 + 1) {
+        *reinterpret_cast<d2v*>(a.out_real + d0) = d2v{lo, hi};
+      } else {
+        if (d0 >= 0) a.out_real[d0] = lo;
+        if (d1 >= 0) a.out_real[d1] = hi;
+      }
+    };
+    if (!odd) {
+      put2(2 * o, x, y);
+    } else {
+      if (jj > 0) {
+        const double py = lds_all[(jj - 1) * MP + lds_slot(rr)].y * oscale * oscale2;
+        put2(2 * o - 1, py, x);
+      } else {
+        const int64_t d0 = dst(2 * o);
+        if (d0 >= 0) a.out_real[d0] = x;
+      }
+      if (jj == F - 1) {
+        const int64_t d1 = dst(2 * o + 1);
+        if (d1 >= 0) a.out_real[d1] = y;
+      }
+    }
+  } else if (a.pairs) {
+    emit(2 * o, val.x);
+    emit(2 * o + 1, val.y);
+  } else {
+    emit(o, val.x);
+  }
 }
 
 template <int R>
@@ -508,61 +577,7 @@ __global__ __launch_bounds__((PassShape<R>::BLOCK)) void k_fft_pass(FftPassArgs 
     const double2 val = lds_all[jj * MP + lds_slot(rr)];
     const int64_t o = (jo & ~(Ns - 1)) * R + (jo & (Ns - 1)) + (int64_t)rr * Ns;
     if constexpr (REALOUT) {
-      auto emit = [&](int64_t q, double x) {
-        if (a.remap) {
-          if (q < a.n_front)
-            a.out_real[a.front_off + q] = x * oscale * oscale2;
-          else if (q >= a.back_from)
-            a.out_real[q - a.back_from] = x * oscale * oscale2;
-        } else {
-          a.out_real[bt * a.out_batch + q] = x * a.scale;
-        }
-      };
-      if (AD_FFT_RO_VEC && a.remap && a.pairs && Ns >= F && nb % F == 0 && ((a.front_off + a.back_from) & 1) == 0) {
-        // Real pairs into the lag order with 16-B stores.  For fixed rr the
-        // tile's F butterflies give 2F consecutive reals q = 2o, 2o + 1, and
-        // both region maps (q + front_off, q - back_from) shift q by amounts of
-        // one parity (N is even), so whether (2o, 2o+1) lands on a 16-B slot
-        // is the same for every element: `odd` = it does not, and lane jj then
-        // owns the slot (2o - 1, 2o) (its left neighbour's Im and its Re); lane
-        // 0 writes only its Re, lane F - 1 also its Im.  A slot whose two
-        // reals do not land side by side (a region edge) is written per real.
-        auto dst = [&](int64_t q) -> int64_t {
-          return q < a.n_front ? a.front_off + q : (q >= a.back_from ? q - a.back_from : -1);
-        };
-        const bool odd = ((a.front_off + (int64_t)(((uintptr_t)a.out_real >> 3) & 1)) & 1) != 0;
-        typedef double d2v __attribute__((ext_vector_type(2)));
-        const double x = val.x * oscale * oscale2, y = val.y * oscale * oscale2;
-        auto put2 = [&](int64_t ql, double lo, double hi) {  // reals ql, ql + 1
-          const int64_t d0 = dst(ql), d1 = dst(ql + 1);
-          if (d0 >= 0 && d1 == d0 + 1) {
-            *reinterpret_cast<d2v*>(a.out_real + d0) = d2v{lo, hi};
-          } else {
-            if (d0 >= 0) a.out_real[d0] = lo;
-            if (d1 >= 0) a.out_real[d1] = hi;
-          }
-        };
-        if (!odd) {
-          put2(2 * o, x, y);
-        } else {
-          if (jj > 0) {
-            const double py = lds_all[(jj - 1) * MP + lds_slot(rr)].y * oscale * oscale2;
-            put2(2 * o - 1, py, x);
-          } else {
-            const int64_t d0 = dst(2 * o);
-            if (d0 >= 0) a.out_real[d0] = x;
-          }
-          if (jj == F - 1) {
-            const int64_t d1 = dst(2 * o + 1);
-            if (d1 >= 0) a.out_real[d1] = y;
-          }
-        }
-      } else if (a.pairs) {
-        emit(2 * o, val.x);
-        emit(2 * o + 1, val.y);
-      } else {
-        emit(o, val.x);
-      }
+      realout_store<F>(a, lds_all, MP, jj, rr, o, val, bt, oscale, oscale2, Ns, nb);
     } else {
 #if AD_FFT_NT  // non-temporal pass outputs (AD_FFT_NT above)
       typedef double d2v __attribute__((ext_vector_type(2)));
@@ -624,7 +639,7 @@ struct PfShape {  // k_fft_pass_pf: AD_FFT_PF_V values per thread, 16 butterflie
 // each pair of loads gives z[k] = sa A + i sb B and z[K0-k] = sa conj(A) +
 // i sb conj(B) (sa, sb from the first pass's max-abs partials), the packed
 // first-pass output the plain form would read.
-template <int R, bool FWD, bool PACKIN = false>
+template <int R, bool FWD, bool PACKIN = false, bool REALOUT = false>
 __global__ __launch_bounds__((PfShape<R>::BLOCK)) __attribute__((amdgpu_waves_per_eu(4))) void k_fft_pass_pf(
     FftPassArgs a, int tiles) {
   using Sh = PfShape<R>;
@@ -632,6 +647,11 @@ __global__ __launch_bounds__((PfShape<R>::BLOCK)) __attribute__((amdgpu_waves_pe
   constexpr int V = Sh::V, T = Plan::T, F = Sh::F, BLOCK = Sh::BLOCK, MP = Plan::MP + (T >= 16 ? 1 : 0);
   static_assert(BLOCK % R == 0, "k_fft_pass_pf: whole butterflies per store row");
   static_assert(!PACKIN || (V % 2 == 0 && F % 2 == 0), "PACKIN: load pairs, F/2 butterflies + their mirrors per tile");
+  static_assert(!(PACKIN && REALOUT), "PACKIN is a forward pass, REALOUT the last inverse one");
+  // REALOUT (the last pass of a real-output inverse, Ns >= F): the scales of
+  // the packed pair (pack_scale of the first pass's max-abs) once per workgroup
+  const PackScale ops = REALOUT ? pack_scale(a.amax) : PackScale{};
+  const double oscale = a.scale * ops.o1, oscale2 = ops.o2;
   constexpr int H = F / 2;  // PACKIN: butterflies per half tile
   __shared__ __attribute__((aligned(16))) double2 lds_all[F * MP];
   __shared__ __attribute__((aligned(16))) double2 ltw[TwSplit<R>::N];
@@ -779,7 +799,16 @@ __global__ __launch_bounds__((PfShape<R>::BLOCK)) __attribute__((amdgpu_waves_pe
     // output rr of butterfly j0 + jj goes to (jo & ~(Ns-1)) R + (jo & (Ns-1)) + rr Ns:
     // Ns = 1: contiguous (o = j0 R + idx); Ns >= F: the tile sits in one Ns group, so
     // o = (j0 & ~(Ns-1)) R + (j0 & (Ns-1)) + i (BLOCK/F) Ns + [jj + (thread/F) Ns]
-    if constexpr (PACKIN) {
+    if constexpr (REALOUT) {  // Ns >= F (launch condition): jj = idx % F, rr = idx / F
+#pragma unroll
+      for (int i = 0; i < V; ++i) {
+        const int idx = i * BLOCK + tx, jj = idx % F, rr = idx / F;
+        const int64_t jo = j0 + jj;
+        const double2 val = lds_all[jj * MP + lds_slot(rr)];
+        const int64_t o = (jo & ~(Ns - 1)) * R + (jo & (Ns - 1)) + (int64_t)rr * Ns;
+        realout_store<F>(a, lds_all, MP, jj, rr, o, val, (int)blockIdx.y, oscale, oscale2, Ns, nb);
+      }
+    } else if constexpr (PACKIN) {
 #pragma unroll
       for (int i = 0; i < V; ++i) {
         const int idx = i * BLOCK + tx, jj = idx % F, rr = idx / F;
@@ -1383,6 +1412,15 @@ void go_pass(const FftPassArgs& a, int batch, hipStream_t s) {
     }
   }
 #if AD_FFT_PF && AD_FFT_TWC && AD_FFT_NT == 1
+  if constexpr (!RI && RO && !FWD && (R == 128 || R == 256)) {  // the last inverse pass, persistent
+    using Pf = PfShape<R>;
+    const int64_t tiles = a.N / R / Pf::F;
+    if (AD_FFT_PF_RO && !a.half && (a.N / R) % Pf::F == 0 && a.Ns >= Pf::F && tiles >= 2 * AD_FFT_PF_RO_G) {
+      hipLaunchKernelGGL((k_fft_pass_pf<R, false, false, true>), dim3(AD_FFT_PF_RO_G, (unsigned)batch), dim3(Pf::BLOCK),
+                         0, s, a, (int)tiles);
+      return;
+    }
+  }
   if constexpr (!RI && !RO && R == 256) {
     using Pf = PfShape<R>;
     const int64_t tiles = a.N / R / Pf::F;
