@@ -13,7 +13,9 @@ if [ "${SKIP_SUITE:-0}" != "1" ]; then
   tail -1 gpurun_out/${T}_pytest_gpu.log
   timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" || exit 1
 fi
-timeout -k 10 400 python3 -u bench.py > gpurun_out/${T}_bench.json 2> gpurun_out/${T}_bench.err || { tail gpurun_out/${T}_bench.err; exit 1; }
+t0=$(date +%s.%N)
+timeout -k 10 400 python3 -u bench.py --steps 20 --warmup 5 > gpurun_out/${T}_bench.json 2> gpurun_out/${T}_bench.err || { tail gpurun_out/${T}_bench.err; exit 1; }
+echo "bench wall s: $(python3 -c "import sys; print(round(float(sys.argv[2]) - float(sys.argv[1]), 1))" $t0 $(date +%s.%N))"
 tail -c 300 gpurun_out/${T}_bench.json; echo
 timeout -k 10 300 python3 -u bench.py --workload corr --steps 40 --warmup 3 > gpurun_out/${T}_corr_bench.json 2> gpurun_out/${T}_corr_bench.err || { tail gpurun_out/${T}_corr_bench.err; exit 1; }
 tail -c 300 gpurun_out/${T}_corr_bench.json; echo
