@@ -72,6 +72,8 @@ def parse():
     p.add_argument("--segments", type=int, default=1,
                    help="output segments per step (ad_conv_multi_process_device_segment); each segment's "
                         "mixdown reduce starts as soon as it is computed")
+    p.add_argument("--step-events", choices=["on", "off"], default="on",
+                   help="N = 1: an event between the timed steps (the line's step_ms)")
     p.add_argument("--settle-steps", type=int, default=60,
                    help="N = 1: after the timed region, this many more steps event-timed one by one (the line's "
                         "`settled` key: the step once the board's clock has recovered from its load-onset dip)")
@@ -652,7 +654,8 @@ def run_conv(args, world, rank, local, dev, ir, C, shard_cfg, mixdown, steps, wa
     torch.cuda.synchronize(dev)
     red_ev.clear()
     # per-step events on the launch stream (record only: no host wait inside the loop)
-    sev = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)] if world == 1 else None
+    sev = ([torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+           if world == 1 and args.step_events == "on" else None)
     t0 = time.perf_counter()
     if sev:
         sev[0].record(stream)
