@@ -689,7 +689,6 @@ void fx_run_tp(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hipStre
 #else
   hipStream_t sd = h->st[0], sv = h->st[1];
 #endif
-  const hipStream_t sg = s;  // the gain's stream (kFxTpGainOnS); CU-masked streams for the detector and the gain measured 2x slower
   enum { EE = 0, ED = 1, EA = 2 };
   if (verb && !h->verb_cm) {  // the delay lines into K_verb's channel-major layout
     h->vbufC.reserve((size_t)kVerbLen * h->channels);
@@ -699,7 +698,6 @@ void fx_run_tp(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hipStre
   AD_HIP(hipEventRecord(h->ev_in, s));
   AD_HIP(hipStreamWaitEvent(sd, h->ev_in, 0));
   AD_HIP(hipStreamWaitEvent(sv, h->ev_in, 0));
-  if (sg != s) AD_HIP(hipStreamWaitEvent(sg, h->ev_in, 0));
   const int wu = verb ? fx_comb_warmup(h->vp) : 0;
   // kFxTpSerialTail: the gain + Freeverb of a chunk on the caller's stream
   // (see the loop); slot reuse then follows from that stream's order: chunk i's
@@ -718,16 +716,16 @@ void fx_run_tp(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hipStre
   // by then chunk i's EQ is queued ahead of it) and its Freeverb on sv behind
   // the gain; EE[kp] is re-recorded after the gain (the detector's wait on the
   // EQ's record was already enqueued)
-  auto gain_verb = [&](const FxStageArgs& p, int kp, int64_t ip) {
-    AD_HIP(hipStreamWaitEvent(sg, h->ev[ED][kp], 0));
-    // on its own stream the gain also waits until inC[kp]'s previous reader
-    // (chunk ip - kFxSlots's Freeverb) is done; on s that order is implied
-    if (sg != s && ip >= kFxSlots) AD_HIP(hipStreamWaitEvent(sg, h->ev[EA][kp], 0));
+  // (inC[kp]'s previous reader, chunk i - 1 - kFxSlots's Freeverb, is ordered
+  // before the gain by s's own wait on that slot at the top of the loop; on
+  // CU-masked streams of their own, the detector and the gain measured 2x slower)
+  auto gain_verb = [&](const FxStageArgs& p, int kp) {
+    AD_HIP(hipStreamWaitEvent(s, h->ev[ED][kp], 0));
     FxStageArgs b = p;
     b.buf = h->inC[kp].p;
     b.stride = h->tmax;
-    launch_fx_gain(b, true, sg);
-    AD_HIP(hipEventRecord(h->ev[EE][kp], sg));
+    launch_fx_gain(b, true, s);
+    AD_HIP(hipEventRecord(h->ev[EE][kp], s));
     AD_HIP(hipStreamWaitEvent(sv, h->ev[EE][kp], 0));
     launch_fxtp_verb(p, h->inC[kp].p, h->tmax, h->vbufC.p, h->coC.p, wu, sv);
     AD_HIP(hipEventRecord(h->ev[EA][kp], sv));
@@ -795,7 +793,7 @@ void fx_run_tp(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hipStre
       AD_HIP(hipStreamWaitEvent(sd, h->ev[EE][k], 0));
       launch_fxtp_det(a, sd);
       AD_HIP(hipEventRecord(h->ev[ED][k], sd));
-      if (i > 0) gain_verb(prev, (int)((i - 1) % kFxSlots), i - 1);
+      if (i > 0) gain_verb(prev, (int)((i - 1) % kFxSlots));
       prev = a;
       continue;
     }
@@ -830,7 +828,7 @@ void fx_run_tp(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hipStre
     AD_HIP(hipGetLastError());
     return;
   }
-  if (gain_on_s) gain_verb(prev, k, i - 1);  // the last chunk's
+  if (gain_on_s) gain_verb(prev, k);  // the last chunk's
   AD_HIP(hipGetLastError());
   AD_HIP(hipStreamWaitEvent(s, h->ev[EA][k], 0));  // the last chunk's reverb / output follows all work
 }
