@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--steps", type=int, default=60)
     ap.add_argument("--gap-ms", type=float, default=20.0)
     a = ap.parse_args()
+    import numpy as np
     import torch
 
     from algodsp import conv, irlib, signals
@@ -38,7 +39,7 @@ def main():
     n, C, hop = 1 << 24, 2, 8192
     ir = irlib.large_church()
     out_len = n + ir.shape[1] - 1
-    x = torch.from_numpy(__import__("numpy").stack([signals.white_noise(n, 0x5EED + c) for c in range(C)])).cuda()
+    x = torch.from_numpy(np.stack([signals.white_noise(n, 0x5EED + c) for c in range(C)])).cuda()
     y = torch.empty((C, out_len), dtype=torch.float64, device="cuda")
     eng = conv.MultiChannelConvolver(ir, hop=hop, channels=C, ir_index=[0, 1], chunk_blocks=0, device=0)
     s = torch.cuda.current_stream()
