@@ -531,7 +531,7 @@ double fx_eq_noise(const std::vector<double>& tab, int sets, int nsec) {
 // i-2's reverb.  A slot is reused only after st[1] is done with it (the
 // detector and the gain precede st[1]'s work on every chunk).
 #ifndef AD_FX_TP_CHUNK  // tools/ A/B builds only
-#define AD_FX_TP_CHUNK 32768  // config 5 (tools/fx_chunk_sweep.py, round 5 schedule): 16384 10.6, 32768 12.0, 65536 11.9, 131072 11.5 Gsamples/s
+#define AD_FX_TP_CHUNK 49152  // config 5 (tools/fx_chunk_sweep.py, round 5 schedule + 64-row detector batches): 24576 11.7, 32768 12.3-12.4, 49152 12.5-12.6, 65536 12.4-12.5 Gsamples/s
 #endif
 constexpr int64_t kFxTpChunk = AD_FX_TP_CHUNK;
 #ifndef AD_FX_TP_SERIAL_TAIL  // tools/ A/B builds
