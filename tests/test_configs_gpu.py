@@ -132,10 +132,10 @@ def test_config5_chain(gpu):
     """configs[4] at the shape bench.py --workload fx times: 256 channels,
     device buffers, the engine AUTO picks for a chain with a compressor -- the
     time-parallel engine (fx_tp.hip; the EQ's noise estimate, 3.6e-13 at
-    48 kHz, is under its 4.5e-13 gate) -- 2^18 samples = 8 of its 32768-sample
-    chunks (each chunk's gain runs on the caller's stream behind the next
-    chunk's EQ, and the four chunk slots are reused), in two calls (the
-    second starts mid-chunk); channels 0, 63, 64
+    48 kHz, is under its 4.5e-13 gate) -- 2^18 samples = 5 1/3 of its
+    49152-sample chunks (each chunk's gain runs on the caller's stream behind
+    the next chunk's EQ, and the four chunk slots are reused), in two calls
+    (the second starts mid-chunk); channels 0, 63, 64
     (the first of the second 64-channel group) and 255 against the oracle
     chain (chain_process.go:11-33: biquad chains -> Compressor -> Freeverb)."""
     import torch

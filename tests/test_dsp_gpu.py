@@ -361,7 +361,7 @@ def test_time_parallel_per_channel_eq(gpu, chunk, nsec):
     """The time-parallel engine with a coefficient table per channel
     (ad_fx_chain_set_eq per_channel = 1: one set of segment maps per channel
     in K_carry) against the fused kernels: <= 1e-12 relative RMS, over a full
-    65536-sample chunk (256 segments, every scan step) and a partial one
+    49152-sample chunk (256 segments, every scan step) and a partial one
     (chunk 0 = the engine's default), or 4096-sample chunks; 1, 5 (config 5)
     and 8 (the most a pass takes) sections with a chain gain != 1, every
     table's noise estimate under the engine's gate (<= 4.4e-13 at the highest
@@ -454,7 +454,7 @@ def test_time_parallel_engine_on_request(gpu, what):
     time-parallel engine too (EQ-only, Freeverb-only -- the per-channel
     K_verb in place on the caller's buffer -- and EQ + Freeverb): outputs
     within 1e-12 relative RMS of the fused kernels and EQ end states within
-    the serial recurrence's noise, over a full 65536-sample chunk and a
+    the serial recurrence's noise, over a full 49152-sample chunk and a
     partial one; then the fused engine continues from the state the
     time-parallel one left (the delay lines move back to its layout)."""
     fs = 48000.0
