@@ -132,10 +132,10 @@ def test_config5_chain(gpu):
     """configs[4] at the shape bench.py --workload fx times: 256 channels,
     device buffers, the engine AUTO picks for a chain with a compressor -- the
     time-parallel engine (fx_tp.hip; the EQ's noise estimate, 3.6e-13 at
-    48 kHz, is under its 4.5e-13 gate) -- 2^18 samples = 5 1/3 of its
+    48 kHz, is under its 4.5e-13 gate) -- 2^19 samples = 10 2/3 of its
     49152-sample chunks (each chunk's gain runs on the caller's stream behind
-    the next chunk's EQ, and the four chunk slots are reused), in two calls
-    (the second starts mid-chunk); channels 0, 63, 64
+    the next chunk's EQ, and the second call reuses the four chunk slots
+    twice), in two calls (the second starts mid-chunk); channels 0, 63, 64
     (the first of the second 64-channel group) and 255 against the oracle
     chain (chain_process.go:11-33: biquad chains -> Compressor -> Freeverb)."""
     import torch
@@ -144,7 +144,7 @@ def test_config5_chain(gpu):
     eq = design.config5_eq(fs)
     comp_cfg = {"auto_makeup": 0, "makeup_db": 0.0}
     verb = (0.22, 1.0, 0.72, 0.45, 0.015)
-    C, n = 256, 1 << 18
+    C, n = 256, 1 << 19
     x = np.stack([0.5 * signals.white_noise(n, 0x5EED + c) for c in range(C)])
     fx = P.EffectChain(C, eq, comp_cfg, verb, fs)
     dx = torch.from_numpy(x).cuda()
