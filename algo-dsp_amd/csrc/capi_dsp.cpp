@@ -238,9 +238,15 @@ int fx_eq_split(const ad_fx_chain* h) {
 #ifndef AD_FX_EQ_PER_SECTION  // tools/ A/B builds
 #define AD_FX_EQ_PER_SECTION 1
 #endif
+#ifndef AD_FX_EQ_PER_SECTION_MAXCH
+// above this many channels the one-workgroup-per-group kernel fills the chip and
+// wins (tools/eq_cross.py, profiles/r05_eq_cross.txt: per-section / whole-chain
+// Msamples/s at 4096 ch 39.4 / 38.2, 8192 ch 44.9 / 60.7, 16384 ch 47.9 / 85.2)
+#define AD_FX_EQ_PER_SECTION_MAXCH 4096
+#endif
 bool fx_eq_per_section(const ad_fx_chain* h) {
   return AD_FX_EQ_PER_SECTION && h->engine != AD_FX_ENGINE_STAGED_NOSPLIT && !h->comp_on && h->nsec >= 2 &&
-         h->nsec <= kMaxSecPerPass;
+         h->nsec <= kMaxSecPerPass && h->cpad <= AD_FX_EQ_PER_SECTION_MAXCH;
 }
 
 constexpr int64_t kFxChunk = 16384;  // staged engine: samples per stage chunk
