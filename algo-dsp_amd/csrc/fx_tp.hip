@@ -278,21 +278,27 @@ __global__ __launch_bounds__(kFxTpMaxSeg) void k_fxtp_carry(FxTpEqArgs a) {
 // memory latency: 10 batches of 16 measured 481 us per chunk, 14 370 us.
 // ---------------------------------------------------------------------------
 constexpr int kDetCh = 8;      // channels per workgroup
-#ifndef AD_DET_B  // tools/ A/B builds may override
-// round 5, with the detector's stream running detectors only (config 5, same
-// box, profiles/r05_fx_det_batch_ab.txt): 16 rows 11.39, 32 rows 12.16,
-// 64 rows 12.29-12.31 Gsamples/s (14 or 8 batches in flight alike)
-#define AD_DET_B 64
-#define AD_DET_NB 8
+#ifndef AD_DET_B  // tools/ A/B builds may override (the one-wave form's batch; the three-wave
+                  // kernel below is instantiated at 64 and 32 rows, launch_fxtp_det picks)
+#define AD_DET_B 32
 #endif
-constexpr int kDetB = AD_DET_B;  // rows per batch
-constexpr int kDetLd = kDetB * kDetCh / 64;  // loads per batch (2)
-constexpr int kDetNB = AD_DET_NB;  // batches in flight in the loader (56 loads outstanding)
+constexpr int kDetB = AD_DET_B;  // rows per batch of the one-wave form (k_fxtp_det1)
 constexpr int kDetSlots = 4;   // input ring slots (put two steps ahead, read one step ahead)
 __device__ __forceinline__ void lds_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// DB rows per batch, DNB batches in flight (DNB even: the steps run in pairs).
+// Round 5, with the detector's stream running detectors only (config 5, same
+// box, profiles/r05_fx_det_batch_ab.txt): 16 rows 11.39, 32 rows 12.16, 64
+// rows 12.29-12.31 Gsamples/s; but 64-row batches take 256 VGPRs, and where
+// the channel groups outnumber the CUs occupancy wins (16384 channels:
+// 63.2 -> 56.4 Gsamples/s on the compressor-only chain), so launch_fxtp_det
+// takes 64 rows for up to 256 groups and 32 above.
+template <int DB, int DNB>
 __global__ __launch_bounds__(192) void k_fxtp_det(FxStageArgs a) {
 #pragma clang fp contract(off)
+  constexpr int kDetB = DB, kDetNB = DNB;
+  constexpr int kDetLd = kDetB * kDetCh / 64;  // loads per batch
+  static_assert(kDetNB % 2 == 0 && kDetLd * kDetNB <= 64, "detector batches: an even count, <= 64 loads in flight");
   __shared__ double ring[kDetSlots][kDetB][kDetCh];
   __shared__ double evr[2][kDetB][kDetCh];  // envelopes of a bare full batch, for the storer
   const int w = wave_of_thread();
@@ -827,7 +833,13 @@ void launch_fxtp_det(const FxStageArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_fxtp_det1, dim3((unsigned)((a.channels + kDetCh - 1) / kDetCh)), dim3(64), 0, s, a);
   else
 #endif
-    hipLaunchKernelGGL(k_fxtp_det, dim3((unsigned)((a.channels + kDetCh - 1) / kDetCh)), dim3(192), 0, s, a);
+  {
+    const unsigned groups = (unsigned)((a.channels + kDetCh - 1) / kDetCh);
+    if (groups <= 256)
+      hipLaunchKernelGGL((k_fxtp_det<64, 8>), dim3(groups), dim3(192), 0, s, a);
+    else
+      hipLaunchKernelGGL((k_fxtp_det<32, 14>), dim3(groups), dim3(192), 0, s, a);
+  }
 }
 
 void launch_fxtp_verb(const FxStageArgs& a, const double* xC, int64_t xstride, double* vbufC, double* coC, int wu,
