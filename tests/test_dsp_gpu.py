@@ -743,3 +743,35 @@ def test_eq_only_per_section_pipeline_bit_exact(gpu):
         for co, g in eq:
             v, _ = O.biquad_chain_block(np.ravel(co), np.zeros(2 * len(co)), g, v)
         assert np.array_equal(y[c], v), (c, float(np.max(np.abs(y[c] - v))))
+
+
+def test_eq_only_many_channels_whole_chain_bit_exact(gpu):
+    """Above 4096 channels an EQ-only chain runs the one-workgroup-per-channel-
+    group kernel again (the per-section pipeline's hand-offs cost more than
+    they gain once the groups fill the chip; AD_FX_EQ_PER_SECTION_MAXCH):
+    still bit-exact against the oracle's biquad.Chain.ProcessBlock
+    (chain.go:59-70) at 4160 channels (a partial last group), device buffers,
+    over a chunk boundary, on the first and last channels of the groups at
+    both ends."""
+    import torch
+
+    fs = 48000.0
+    eq = design.config5_eq(fs)
+    C, n = 4160, 20000
+    base = np.stack([0.5 * signals.white_noise(n, 4160 + c) for c in range(4)])
+    x = np.concatenate([base] * (C // 4))
+    fx = P.EffectChain(C, eq, None, None, fs)
+    dx = torch.from_numpy(x).cuda()
+    s = torch.cuda.current_stream()
+    fx.process_device(dx.data_ptr(), n, n, s.cuda_stream)
+    s.synchronize()
+    y = dx.cpu().numpy()
+    engine, _ = fx.LastEngine()
+    # not the per-section pipeline (ENGINE_STAGED); the staged one-workgroup form or the fused kernels
+    assert engine in (P.EffectChain.ENGINE_STAGED_NOSPLIT, P.EffectChain.ENGINE_FUSED), engine
+    for c in (0, 63, 4097, 4159):
+        v = x[c].copy()
+        for co, g in eq:
+            v, _ = O.biquad_chain_block(np.ravel(co), np.zeros(2 * len(co)), g, v)
+        assert np.array_equal(y[c], v), (c, float(np.max(np.abs(y[c] - v))))
+    fx.close()
