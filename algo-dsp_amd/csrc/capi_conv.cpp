@@ -393,6 +393,7 @@ void stream_reset(ad_conv* h) {
 // multiple of the hop on the FFT path.  Writes n linear-conv samples to out.
 void stream_convolve(ad_conv* h, const double* in, int64_t n, double* out) {
   if (n == 0) return;
+  gate_preempt(h);  // every streaming path, gated or not: no other handle's armed launch ahead of this block
   hipStream_t s = h->stream;
   if (h->direct_stream) {
     const int64_t K = h->conv_len;

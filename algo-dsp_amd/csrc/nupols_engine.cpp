@@ -243,6 +243,7 @@ void NupolsDev::emit(const double* d_in, int64_t in_stride, double* d_out, int64
 void NupolsDev::process(const double* d_in, int64_t in_stride, double* d_out, int64_t out_stride, int64_t n,
                         bool mix, double wet, double dry, hipStream_t s) {
   if (n <= 0) return;
+  gate_preempt(this);  // another handle's armed emit must not hold up this call either
   gate_cancel(s);
   append(d_in, in_stride, n, false, s);           // 1. the block joins the input FIFO
   run_stages(emitted_ + n, s);                    // 2. every complete block of every stage (K3 adds at +T)
