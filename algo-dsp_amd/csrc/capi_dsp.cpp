@@ -141,7 +141,7 @@ struct ad_fx_chain {
   std::map<int, std::unique_ptr<DevBuf<double>>> tp_mats;  // by segment length
   DevBuf<double> inC[kFxSlots];  // reverb input, channel-major [cpad][tmax]
   DevBuf<double> vbufC;          // Freeverb lines channel-major [channels][kVerbLen] (K_verb)
-  DevBuf<double> coC;            // K_verb comb outputs [channels][8][kFxVerbSB] (scratch, stream st[1] only)
+  DevBuf<double> coC;            // K_verb comb outputs [channels][2][8][kFxVerbSB] (scratch, stream st[1] only)
   bool verb_cm = false;          // vbufC (not vbuf) holds the current delay lines
   int64_t tmax = 0;
   // engine selection (ad_fx_chain_set_engine) and per-wave clock counters of
@@ -668,7 +668,7 @@ void fx_run_tp(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hipStre
     // staged engine, which may have raised it; see fx_run_staged)
     const size_t r = (size_t)h->cpad * std::max(T, h->tmax);
     auto shortb = [](const DevBuf<double>& b, size_t want) { return !b.p || b.n < want; };
-    bool grow = (verb && shortb(h->coC, (size_t)h->channels * kVerbCombs * kFxVerbSB)) ||
+    bool grow = (verb && shortb(h->coC, (size_t)h->channels * 2 * kVerbCombs * kFxVerbSB)) ||
                 (eq && shortb(h->tp_zs, (size_t)kFxTpMaxSeg * h->nsec * h->cpad * 2));
     for (int k = 0; k < kFxSlots; ++k)
       grow = grow || shortb(h->xT[k], r) || (eq && shortb(h->vT[k], r)) || (comp && shortb(h->envT[k], r)) ||
@@ -683,7 +683,7 @@ void fx_run_tp(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hipStre
         if (comp) h->envT[k].reserve(r);
         if (comp && verb) h->inC[k].reserve(r);
       }
-      if (verb) h->coC.reserve((size_t)h->channels * kVerbCombs * kFxVerbSB);
+      if (verb) h->coC.reserve((size_t)h->channels * 2 * kVerbCombs * kFxVerbSB);  // two halves (k_fxtp_verb_pipe)
       if (eq) {
         h->tp_zs.reserve((size_t)kFxTpMaxSeg * h->nsec * h->cpad * 2);
         h->tp_carry.reserve((size_t)kFxTpMaxSeg * h->nsec * h->cpad * 4);

@@ -625,6 +625,9 @@ __global__ __launch_bounds__(64) void k_fxtp_det1(FxStageArgs a) {
 //               window's comb outputs loaded during the current one
 // ---------------------------------------------------------------------------
 constexpr int kVbSB = kFxVerbSB;
+#ifndef AD_VB_PIPE
+#define AD_VB_PIPE 1  // k_fxtp_verb_pipe: comb and allpass phases of consecutive sub-blocks overlapped
+#endif
 constexpr int kVbSeg = 32;  // comb segments per piece, at most
 constexpr int kVbThreads = 64 * (kVerbCombs + 4);
 constexpr int kVbXr = (kVbSB + kVbThreads - 1) / kVbThreads;  // input values per thread per sub-block
@@ -794,6 +797,182 @@ __global__ __launch_bounds__(kVbThreads) void k_fxtp_verb(FxStageArgs a, const d
   }
 }
 
+// K_verb with its two phases overlapped across sub-blocks (AD_VB_PIPE): in
+// step b the comb waves run sub-block b while the allpass waves run sub-block
+// b - 1 (the comb and allpass delay lines are separate LDS regions).  The comb
+// outputs alternate between two halves of coC ([2][comb][kVbSB] per channel);
+// the allpass waves read the dry input of their sub-block from the input
+// buffer (each lane reads its sample before it writes the output there, so the
+// in-place call stays exact), and order their 225-sample windows among
+// themselves with an LDS counter instead of the workgroup barrier, which the
+// comb waves only meet once per step.  Same operations per sample in the same
+// order as k_fxtp_verb: the same bits.
+__global__ __launch_bounds__(kVbThreads) void k_fxtp_verb_pipe(FxStageArgs a, const double* __restrict__ xC,
+                                                               int64_t xstride, double* __restrict__ vbufC,
+                                                               double* __restrict__ coC, int wu) {
+#pragma clang fp contract(off)
+  __shared__ double lines[kVerbLen];
+  __shared__ double xs[kVbSB];
+  __shared__ unsigned apbar;  // allpass windows done x 4 (one increment per allpass wave and window)
+  const int w = wave_of_thread();
+  const int l = threadIdx.x & 63;
+  const int tid = threadIdx.x;
+  const int c = xcd_remap((int)blockIdx.x, (int)gridDim.x);
+  const VerbParams& p = a.vp;
+  const int64_t len = a.len;
+  double* vl = vbufC + (int64_t)c * kVerbLen;
+  for (int e = tid; e < kVerbLen; e += kVbThreads) lines[e] = vl[e];
+  if (tid == 0) apbar = 0u;
+  const double* xc = xC + (int64_t)c * xstride;
+  double* cocb = coC + (int64_t)c * 2 * kVerbCombs * kVbSB;  // [2][comb][kVbSB]
+  double xr[kVbXr];
+#pragma unroll
+  for (int q = 0; q < kVbXr; ++q) {
+    const int e = q * kVbThreads + tid;
+    xr[q] = e < kVbSB && e < len ? xc[e] : 0.0;
+  }
+  const int ci = w < kVerbCombs ? w : 0;
+  int idx = a.vs[c].comb_idx[ci];
+  double carry = a.vs[c].filter_store[ci];
+  int apx[kVerbAllpass];
+#pragma unroll
+  for (int i = 0; i < kVerbAllpass; ++i) apx[i] = a.vs[c].ap_idx[i];
+  unsigned nwin = 0;  // allpass windows this wave has finished
+  const int64_t nsb = (len + kVbSB - 1) / kVbSB;
+  for (int64_t b = 0; b <= nsb; ++b) {
+    const int64_t t0 = b * kVbSB;
+    const int sb = b < nsb ? (int)min((int64_t)kVbSB, len - t0) : 0;
+    __syncthreads();  // step b - 1's comb reads of xs and comb outputs are done (the first time: the lines)
+    if (sb > 0) {
+#pragma unroll
+      for (int q = 0; q < kVbXr; ++q) {
+        const int e = q * kVbThreads + tid;
+        if (e < sb) xs[e] = xr[q];
+      }
+#pragma unroll
+      for (int q = 0; q < kVbXr; ++q) {  // the next sub-block's input, in flight during this step
+        const int e = q * kVbThreads + tid;
+        if (e < kVbSB && t0 + kVbSB + e < len) xr[q] = xc[t0 + kVbSB + e];
+      }
+    }
+    __syncthreads();  // xs holds sub-block b
+    if (w < kVerbCombs) {
+      if (sb > 0) {
+        const int D = kCombLen[w];
+        double* L = lines + comb_off(w);
+        double* cw = cocb + ((int64_t)(b & 1) * kVerbCombs + w) * kVbSB;
+        for (int r = 0; r < sb;) {
+          const int pos0 = idx;
+          const int m = min(sb - r, D - pos0);
+          const int nw = wu > 0 ? max(1, min(kVbSeg, m / wu)) : min(kVbSeg, m);
+          const int Lw = ((m + nw - 1) / nw) | 1;
+          const int s0 = l * Lw, s1 = min(m, s0 + Lw);
+          const bool mine = l < nw && s0 < s1;
+          double fs = l == 0 ? carry : 0.0;
+          if (mine && l > 0) {
+            int j = s0 - wu;
+            for (; j + 8 <= s0; j += 8) {
+              double ov[8];
+#pragma unroll
+              for (int t = 0; t < 8; ++t) ov[t] = L[pos0 + j + t];
+#pragma unroll
+              for (int t = 0; t < 8; ++t) fs = comb_fs(p, ov[t], fs);
+            }
+            for (; j < s0; ++j) fs = comb_fs(p, L[pos0 + j], fs);
+          }
+          if (mine) {
+            int j = s0;
+            for (; j + 8 <= s1; j += 8) {
+              double ov[8], xv[8];
+#pragma unroll
+              for (int t = 0; t < 8; ++t) {
+                ov[t] = L[pos0 + j + t];
+                xv[t] = xs[r + j + t];
+              }
+#pragma unroll
+              for (int t = 0; t < 8; ++t) {
+                fs = comb_fs(p, ov[t], fs);
+                L[pos0 + j + t] = p.gain * xv[t] + fs * p.feedback;
+              }
+#pragma unroll
+              for (int t = 0; t < 8; ++t) cw[r + j + t] = ov[t];
+            }
+            for (; j < s1; ++j) {
+              const double out = L[pos0 + j];
+              fs = comb_fs(p, out, fs);
+              L[pos0 + j] = p.gain * xs[r + j] + fs * p.feedback;
+              cw[r + j] = out;
+            }
+          }
+          const int lastl = (m - 1) / Lw;
+          carry = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(fs), lastl),
+                                   __builtin_amdgcn_readlane(__double2loint(fs), lastl));
+          idx = pos0 + m == D ? 0 : pos0 + m;
+          r += m;
+        }
+      }
+    } else if (b > 0) {  // the allpass waves: sub-block b - 1
+      const int64_t tp = (b - 1) * kVbSB;
+      const int sbp = (int)min((int64_t)kVbSB, len - tp);
+      const double* coc = cocb + (int64_t)((b - 1) & 1) * kVerbCombs * kVbSB;
+      const int j = (w - kVerbCombs) * 64 + l;
+      const bool apw = j < 225;
+      double cv[kVerbCombs], xd = 0.0;
+      auto loadc = [&](int r) {
+        const int e = min(r + j, sbp - 1);
+#pragma unroll
+        for (int i = 0; i < kVerbCombs; ++i) cv[i] = coc[(int64_t)i * kVbSB + e];
+        xd = xc[tp + e];
+      };
+      if (apw) loadc(0);
+      for (int r = 0; r < sbp; r += 225) {
+        const int m = min(225, sbp - r);
+        if (apw && j < m) {
+          double acc = 0.0;
+#pragma unroll
+          for (int i = 0; i < kVerbCombs; ++i) acc += cv[i];
+          int off = comb_off(kVerbCombs);
+#pragma unroll
+          for (int i = 0; i < kVerbAllpass; ++i) {
+            int q = apx[i] + j;
+            if (q >= kApLen[i]) q -= kApLen[i];
+            const double bo = lines[off + q];
+            const double output = bo - acc;
+            lines[off + q] = acc + bo * p.ap_feedback;
+            acc = output;
+            off += kApLen[i];
+          }
+          a.buf[(int64_t)c * a.stride + tp + r + j] = acc * p.wet + xd * p.dry;
+        }
+        if (apw && r + 225 < sbp) loadc(r + 225);
+#pragma unroll
+        for (int i = 0; i < kVerbAllpass; ++i) {
+          apx[i] += m;
+          if (apx[i] >= kApLen[i]) apx[i] -= kApLen[i];
+        }
+        // the four allpass waves' window barrier (LDS counter; bounded spin)
+        ++nwin;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (l == 0) __hip_atomic_fetch_add(&apbar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        for (int it = 0; it < (1 << 22); ++it) {
+          if (__hip_atomic_load(&apbar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= 4u * nwin) break;
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  for (int e = tid; e < kVerbLen; e += kVbThreads) vl[e] = lines[e];
+  if (w < kVerbCombs && l == 0) {
+    a.vs[c].comb_idx[w] = idx;
+    a.vs[c].filter_store[w] = carry;
+  }
+  if (w == kVerbCombs && l == 0) {
+#pragma unroll
+    for (int i = 0; i < kVerbAllpass; ++i) a.vs[c].ap_idx[i] = apx[i];
+  }
+}
+
 // Freeverb delay lines between the engines' layouts: position-major
 // vbuf [pos][cpad] (fused and staged kernels) <-> channel-major vbufC
 // [channels][kVerbLen] (K_verb).
@@ -845,7 +1024,11 @@ void launch_fxtp_det(const FxStageArgs& a, hipStream_t s) {
 void launch_fxtp_verb(const FxStageArgs& a, const double* xC, int64_t xstride, double* vbufC, double* coC, int wu,
                       hipStream_t s) {
   if (a.len <= 0) return;
-  hipLaunchKernelGGL(k_fxtp_verb, dim3((unsigned)a.channels), dim3(kVbThreads), 0, s, a, xC, xstride, vbufC, coC, wu);
+  if (AD_VB_PIPE)
+    hipLaunchKernelGGL(k_fxtp_verb_pipe, dim3((unsigned)a.channels), dim3(kVbThreads), 0, s, a, xC, xstride, vbufC, coC,
+                       wu);
+  else
+    hipLaunchKernelGGL(k_fxtp_verb, dim3((unsigned)a.channels), dim3(kVbThreads), 0, s, a, xC, xstride, vbufC, coC, wu);
 }
 
 void launch_vbuf_layout(double* vbuf, double* vbufC, int cpad, int channels, bool to_cm, hipStream_t s) {
