@@ -733,7 +733,7 @@ void fx_run_tp(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hipStre
     launch_fx_gain(b, true, s);
     AD_HIP(hipEventRecord(h->ev[EE][kp], s));
     AD_HIP(hipStreamWaitEvent(sv, h->ev[EE][kp], 0));
-    launch_fxtp_verb(p, h->inC[kp].p, h->tmax, h->vbufC.p, h->coC.p, wu, sv);
+    launch_fxtp_verb(p, h->inC[kp].p, h->tmax, h->vbufC.p, h->coC.p, wu, sv, true);
     AD_HIP(hipEventRecord(h->ev[EA][kp], sv));
   };
   const bool gain_on_s = kFxTpGainOnS && !kFxTpSerialTail && comp && verb;

@@ -170,8 +170,11 @@ void launch_fxtp_det(const FxStageArgs& a, hipStream_t s);           // vT -> en
 // Freeverb, one channel per workgroup: xC [channels][xstride] (channel-major
 // reverb input) -> user buffer, delay lines in vbufC [channels][kVerbLen],
 // comb outputs through coC [channels][8][kFxVerbSB] (scratch)
+// pipe: k_fxtp_verb_pipe, the comb and allpass phases of consecutive
+// sub-blocks overlapped (faster beside the config-5 pipeline's other stages:
+// 12.5 -> 13.0 Gsamples/s; slower alone: Freeverb-only 22.3 -> 20.1)
 void launch_fxtp_verb(const FxStageArgs& a, const double* xC, int64_t xstride, double* vbufC, double* coC, int wu,
-                      hipStream_t s);
+                      hipStream_t s, bool pipe = false);
 void launch_vbuf_layout(double* vbuf, double* vbufC, int cpad, int channels, bool to_cm, hipStream_t s);
 
 // Fan-in average of an effect-chain graph node (mixParentEdgesInto,

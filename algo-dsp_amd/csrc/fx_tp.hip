@@ -626,7 +626,7 @@ __global__ __launch_bounds__(64) void k_fxtp_det1(FxStageArgs a) {
 // ---------------------------------------------------------------------------
 constexpr int kVbSB = kFxVerbSB;
 #ifndef AD_VB_PIPE
-#define AD_VB_PIPE 1  // k_fxtp_verb_pipe: comb and allpass phases of consecutive sub-blocks overlapped
+#define AD_VB_PIPE 1  // k_fxtp_verb_pipe (where the caller asks): comb and allpass phases of consecutive sub-blocks overlapped
 #endif
 constexpr int kVbSeg = 32;  // comb segments per piece, at most
 constexpr int kVbThreads = 64 * (kVerbCombs + 4);
@@ -1022,9 +1022,9 @@ void launch_fxtp_det(const FxStageArgs& a, hipStream_t s) {
 }
 
 void launch_fxtp_verb(const FxStageArgs& a, const double* xC, int64_t xstride, double* vbufC, double* coC, int wu,
-                      hipStream_t s) {
+                      hipStream_t s, bool pipe) {
   if (a.len <= 0) return;
-  if (AD_VB_PIPE)
+  if (AD_VB_PIPE && pipe)
     hipLaunchKernelGGL(k_fxtp_verb_pipe, dim3((unsigned)a.channels), dim3(kVbThreads), 0, s, a, xC, xstride, vbufC, coC,
                        wu);
   else
