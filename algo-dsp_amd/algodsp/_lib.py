@@ -205,6 +205,7 @@ def _declare(L: C.CDLL) -> None:
         "ad_conv_profile_kernels": (C.c_int, [vp, C.c_int]),
         "ad_conv_profile_read": (C.c_int, [vp, c_double_p, c_int64_p, c_double_p]),
         "ad_compressor_default_config": (None, [C.POINTER(CompressorConfig), C.c_double]),
+        "ad_compressor_validate": (C.c_int, [C.POINTER(CompressorConfig)]),
         "ad_fx_chain_create": (C.c_int, [C.c_int, C.c_int, C.POINTER(vp)]),
         "ad_fx_chain_set_eq": (C.c_int, [vp, c_double_p, C.c_int, C.c_int]),
         "ad_fx_eq_noise": (C.c_int, [c_double_p, C.c_int, C.c_int, c_double_p]),

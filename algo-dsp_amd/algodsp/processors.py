@@ -149,34 +149,49 @@ class Compressor(_FxChain):
     def _apply(self):
         check(lib().ad_fx_chain_set_compressor(self._h, C.byref(self.cfg)))
 
-    # setters (compressor.go:130-305)
+    def _set(self, **kv):
+        # a setter the reference rejects returns its error and leaves the
+        # config as it was (core.go:131-198): restore the fields, then raise
+        old = {k: getattr(self.cfg, k) for k in kv}
+        for k, v in kv.items():
+            setattr(self.cfg, k, v)
+        try:
+            self._apply()
+        except Exception:
+            for k, v in old.items():
+                setattr(self.cfg, k, v)
+            raise
+
+    # setters (compressor.go:130-305, core.go:131-250)
     def SetThreshold(self, db):
-        self.cfg.threshold_db = db
-        self._apply()
+        self._set(threshold_db=db)
 
     def SetRatio(self, r):
-        self.cfg.ratio = r
-        self._apply()
+        self._set(ratio=r)
 
     def SetKnee(self, db):
-        self.cfg.knee_db = db
-        self._apply()
+        self._set(knee_db=db)
 
     def SetAttack(self, ms):
-        self.cfg.attack_ms = ms
-        self._apply()
+        self._set(attack_ms=ms)
 
     def SetRelease(self, ms):
-        self.cfg.release_ms = ms
-        self._apply()
+        self._set(release_ms=ms)
+
+    def SetRMSWindow(self, ms):
+        self._set(rms_window_ms=ms)
+
+    def SetSidechainLowCut(self, hz):
+        self._set(sidechain_low_cut_hz=hz)
+
+    def SetSidechainHighCut(self, hz):
+        self._set(sidechain_high_cut_hz=hz)
 
     def SetAutoMakeup(self, on: bool):
-        self.cfg.auto_makeup = int(bool(on))
-        self._apply()
+        self._set(auto_makeup=int(bool(on)))
 
     def SetMakeupGain(self, db):
-        self.cfg.makeup_db = db
-        self._apply()
+        self._set(makeup_db=db)
 
     def ProcessInPlace(self, buf):  # compressor.go:362-366
         self._process(buf)

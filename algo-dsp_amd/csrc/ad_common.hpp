@@ -97,8 +97,9 @@ hipError_t lib_stream_destroy(hipStream_t s);
 // streams than that, streams share queues.  So a handle arms such a launch
 // only while no other handle has one armed (gate_acquire takes the one
 // process-wide slot for `owner`; true if owner already holds it) and while
-// the library owns at most kGateMaxStreams streams (one queue left for the
-// caller's); gate_release(owner) frees the slot (no-op for another owner).
+// the library owns at most kGateMaxStreams streams on the device of `s`, the
+// stream the armed launch goes to (one queue left for the caller's; other
+// devices' streams take other queues and do not count); gate_release(owner) frees the slot (no-op for another owner).
 // Streams the library does not own (the caller's, torch's) take queues too, so
 // the stream count alone cannot keep another handle's work off the armed
 // launch's queue: gate_preempt(me), called by a low-latency or streaming call
@@ -107,7 +108,7 @@ hipError_t lib_stream_destroy(hipStream_t s);
 // exits as skipped, and its owner's next call takes the path it takes after a
 // timeout (rolls the block back, ordinary launches).
 constexpr int kGateMaxStreams = 3;
-bool gate_acquire(const void* owner, uint64_t* abort_word);
+bool gate_acquire(const void* owner, uint64_t* abort_word, hipStream_t s);
 void gate_release(const void* owner);
 void gate_preempt(const void* me);
 

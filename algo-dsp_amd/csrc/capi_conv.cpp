@@ -311,9 +311,12 @@ void gate_cancel(ad_conv* h) {
   });
   AD_HIP(hipStreamSynchronize(h->stream));
   if (ctl_load(&h->ctl->k1_state) != p) h->eng->rewind(1);
+  // release the slot before clearing go: a gate_preempt from another thread
+  // writes the abort only while this handle owns the slot, so no stale abort
+  // can land in go after the clear
+  gate_release(h);
   __atomic_store_n(&h->ctl->go, 0, __ATOMIC_RELEASE);
   h->chain_pending = 0;
-  gate_release(h);
 }
 
 // Whether the next block's chain is pre-enqueued: only while calls come
@@ -335,7 +338,7 @@ bool gate_pre_enqueue(ad_conv* h) {
   // one armed launch at a time, and none while the library's streams could
   // share the caller's hardware queues)
   return h->gate_misses < 3 && h->gate_gap_ms > 0 && h->gate_gap_ms < timeout_ms / 4 &&
-         gate_acquire(h, &h->ctl->go);
+         gate_acquire(h, &h->ctl->go, h->stream);
 }
 
 // One block of n = hop samples (already in pin_in) through the chains.

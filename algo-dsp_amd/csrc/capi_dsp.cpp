@@ -64,14 +64,35 @@ CompParams comp_params(const ad_compressor_config& g) {
 }
 
 void check_comp_config(const ad_compressor_config& g) {
-  // validation of the setters (compressor.go:130-305, core.go validate*)
-  if (!(g.sample_rate > 0) || !std::isfinite(g.sample_rate))
+  // the setters' validation: SetRatio / SetKnee / SetAttack / SetRelease /
+  // SetRMSWindow / SetThreshold / SetManualMakeupGain (core.go:131-198,
+  // ranges compressor.go:16-23, core.go:10-12), SetMakeupGain, SetTopology /
+  // SetDetectorMode (core.go:106-124) and recalculatePrefilter's side-chain
+  // cut rules (core.go:542-564); a config any setter would reject is rejected
+  // whole, before anything changes
+  auto fin = [](double v) { return std::isfinite(v); };
+  if (!(g.sample_rate > 0) || !fin(g.sample_rate))
     AD_FAIL(AD_ERR_INVALID_ARGUMENT, "dynamics: sample rate must be positive and finite");
-  if (!(g.ratio >= 1) || !std::isfinite(g.ratio)) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "dynamics: ratio must be >= 1");
-  if (!(g.knee_db >= 0)) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "dynamics: knee must be >= 0");
-  if (!(g.attack_ms > 0) || !(g.release_ms > 0))
-    AD_FAIL(AD_ERR_INVALID_ARGUMENT, "dynamics: attack/release must be positive");
-  if (!(g.rms_window_ms > 0)) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "dynamics: rms window must be positive");
+  if (!fin(g.threshold_db)) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "dynamics: threshold must be finite");
+  if (!(g.ratio >= 1.0 && g.ratio <= 100.0)) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "dynamics: ratio must be in [1, 100]");
+  if (!(g.knee_db >= 0.0 && g.knee_db <= 24.0)) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "dynamics: knee must be in [0, 24] dB");
+  if (!(g.attack_ms >= 0.1 && g.attack_ms <= 1000.0))
+    AD_FAIL(AD_ERR_INVALID_ARGUMENT, "dynamics: attack must be in [0.1, 1000] ms");
+  if (!(g.release_ms >= 1.0 && g.release_ms <= 5000.0))
+    AD_FAIL(AD_ERR_INVALID_ARGUMENT, "dynamics: release must be in [1, 5000] ms");
+  if (!(g.rms_window_ms >= 1.0 && g.rms_window_ms <= 1000.0))
+    AD_FAIL(AD_ERR_INVALID_ARGUMENT, "dynamics: rms window must be in [1, 1000] ms");
+  if (!fin(g.makeup_db)) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "dynamics: makeup gain must be finite");
+  if (g.topology != 0 && g.topology != 1) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "dynamics: invalid topology");
+  if (g.detector_mode != 0 && g.detector_mode != 1) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "dynamics: invalid detector mode");
+  // side-chain cuts: <= 0 is off (the setters reject negatives; the ABI's
+  // "<= 0: off" keeps 0 and maps nothing else), on: [1 Hz, Nyquist), low < high
+  const double lo = g.sidechain_low_cut_hz, hi = g.sidechain_high_cut_hz, nyq = g.sample_rate * 0.5;
+  if (!fin(lo) || !fin(hi) || lo < 0 || hi < 0)
+    AD_FAIL(AD_ERR_INVALID_ARGUMENT, "dynamics: side-chain cuts must be non-negative and finite");
+  if (lo > 0 && !(lo >= 1.0 && lo < nyq)) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "dynamics: side-chain low-cut must be in [1, nyquist)");
+  if (hi > 0 && !(hi >= 1.0 && hi < nyq)) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "dynamics: side-chain high-cut must be in [1, nyquist)");
+  if (lo > 0 && hi > 0 && lo >= hi) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "dynamics: side-chain low-cut must be below high-cut");
 }
 
 // EQ state on the device is kept per pass of <= kMaxSecPerPass sections,
@@ -939,6 +960,13 @@ void ad_compressor_default_config(ad_compressor_config* c, double sample_rate) {
   c->makeup_db = 0.0;
   c->auto_makeup = 1;
   c->feedback_ratio_scale = 1;
+}
+
+int ad_compressor_validate(const ad_compressor_config* cfg) {
+  return guard([&] {
+    if (!cfg) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "nil compressor config");
+    check_comp_config(*cfg);
+  });
 }
 
 int ad_fx_chain_create(int channels, int device, ad_fx_chain** out) {

@@ -838,6 +838,10 @@ __global__ __launch_bounds__(kVbThreads) void k_fxtp_verb_pipe(FxStageArgs a, co
 #pragma unroll
   for (int i = 0; i < kVerbAllpass; ++i) apx[i] = a.vs[c].ap_idx[i];
   unsigned nwin = 0;  // allpass windows this wave has finished
+  // set if a window barrier's spin ever expires (cannot happen with all waves
+  // resident in one workgroup): every later output of the wave is NaN, so a
+  // broken barrier shows as an error instead of silently stale allpass lines
+  bool spin_lost = false;
   const int64_t nsb = (len + kVbSB - 1) / kVbSB;
   for (int64_t b = 0; b <= nsb; ++b) {
     const int64_t t0 = b * kVbSB;
@@ -942,7 +946,7 @@ __global__ __launch_bounds__(kVbThreads) void k_fxtp_verb_pipe(FxStageArgs a, co
             acc = output;
             off += kApLen[i];
           }
-          a.buf[(int64_t)c * a.stride + tp + r + j] = acc * p.wet + xd * p.dry;
+          a.buf[(int64_t)c * a.stride + tp + r + j] = spin_lost ? __builtin_nan("") : acc * p.wet + xd * p.dry;
         }
         if (apw && r + 225 < sbp) loadc(r + 225);
 #pragma unroll
@@ -950,14 +954,20 @@ __global__ __launch_bounds__(kVbThreads) void k_fxtp_verb_pipe(FxStageArgs a, co
           apx[i] += m;
           if (apx[i] >= kApLen[i]) apx[i] -= kApLen[i];
         }
-        // the four allpass waves' window barrier (LDS counter; bounded spin)
+        // the four allpass waves' window barrier (LDS counter; bounded spin,
+        // an expiry poisons the wave's outputs, see spin_lost)
         ++nwin;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if (l == 0) __hip_atomic_fetch_add(&apbar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        bool met = false;
         for (int it = 0; it < (1 << 22); ++it) {
-          if (__hip_atomic_load(&apbar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= 4u * nwin) break;
+          if (__hip_atomic_load(&apbar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= 4u * nwin) {
+            met = true;
+            break;
+          }
           __builtin_amdgcn_s_sleep(1);
         }
+        spin_lost |= !met;
       }
     }
   }

@@ -312,7 +312,7 @@ void NupolsDev::gate_arm(int64_t n, bool mix, double wet, double dry, hipStream_
     if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0) khz = 100000;
     gkhz_ = (uint64_t)khz;
   }
-  if (!gate_acquire(this, &gctl_->go)) return;
+  if (!gate_acquire(this, &gctl_->go, s)) return;
   // the emit gives up after 4 call intervals (1 .. 20 ms): work that shares
   // its hardware queue waits behind it at most that long
   gtimeout_ = (uint64_t)(std::clamp(4.0 * gap_ms_, 1.0, 20.0) * (double)gkhz_);
@@ -357,9 +357,9 @@ void NupolsDev::gate_cancel(hipStream_t s) {
     emitted_ -= gp_.n;
     received_ -= gp_.n;
   }
+  gate_release(this);  // before clearing go: no stale gate_preempt abort after the clear
   __atomic_store_n(&gctl_->go, 0, __ATOMIC_RELEASE);
   gp_.on = false;
-  gate_release(this);
 }
 
 void NupolsDev::process_host(const double* in, double* out, int64_t n, bool mix, double wet, double dry,

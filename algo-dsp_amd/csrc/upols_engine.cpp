@@ -188,6 +188,12 @@ void Upols::begin_offline(hipStream_t) {
   // Spectra with logical index < 0 read as zeros inside k_fdl_mac, so a new
   // signal only restarts the logical block counter (no memset).
   g_next_ = 0;
+  // the schedule is fixed per signal: a request made between two segments of
+  // one signal waits for the next signal, so the rings never change size
+  // under a signal in flight
+  sched_mode_ = req_mode_;
+  pipe_jc_ = req_jc_;
+  pipe_run_ = req_run_;
   sig_pipe_ = sched_mode_ != kSchedSerial && M_ >= 2048;
   if (sig_pipe_) ensure_pipe();
 }
@@ -195,13 +201,13 @@ void Upols::begin_offline(hipStream_t) {
 void Upols::set_schedule(int mode, int chunk, int run) {
   if (mode != kSchedSerial && mode != kSchedPipelined && mode != kSchedChunked) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "unknown schedule");
   if (chunk < 0 || run < 0) AD_FAIL(AD_ERR_INVALID_ARGUMENT, "schedule: negative chunk or run length");
-  sched_mode_ = mode;
+  req_mode_ = mode;
   // auto chunk: 128 blocks per channel of two channels keep the live rings
   // (two chunks of block spectra + two of Z rows, ~64 MiB each at hop 8192)
   // inside the 256 MiB Infinity Cache
-  pipe_jc_ = chunk > 0 ? chunk : (int)std::max<int64_t>(32, std::min<int64_t>(jc_max_, 256 / std::max(1, C_)));
-  pipe_jc_ = std::min(pipe_jc_, jc_max_);
-  pipe_run_ = run;
+  req_jc_ = chunk > 0 ? chunk : (int)std::max<int64_t>(32, std::min<int64_t>(jc_max_, 256 / std::max(1, C_)));
+  req_jc_ = std::min(req_jc_, jc_max_);
+  req_run_ = run;
 }
 
 void Upols::ensure_pipe() {
@@ -412,6 +418,9 @@ void Upols::run(const double* d_in, int64_t in_stride, int64_t n, double* d_out,
 //     call's K1 (on s) follows every kernel of this one.
 void Upols::run_pipelined(const Io& io, hipStream_t s, int64_t jb, int64_t J, int64_t nb_in) {
   const int jp = pipe_jc_;
+  // the rings were sized for this signal's schedule at begin_offline
+  if (jp < 1 || jp + 16 > zrows_p_ || 2 * jp + P_ + 2 * PC_ + 1 > Qp_)
+    AD_FAIL(AD_ERR_INTERNAL, "pipelined schedule: rings smaller than the chunk");
   const int64_t nchunks = (J + jp - 1) / jp;
   const int64_t jc_even = (J + nchunks - 1) / nchunks;
   int64_t k = 0;

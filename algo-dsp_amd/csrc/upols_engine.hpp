@@ -75,17 +75,19 @@ class Upols {
   // to jc_max blocks.  PIPELINED (hop >= 2048): chunks of `chunk` blocks per
   // channel whose block spectra and Z rows live in small rings that the
   // Infinity Cache holds; K1 runs on the caller's stream, K2 and K3 on two
-  // internal streams, so K1 of chunk k+1, K2 of chunk k and K3 of chunk k-1
-  // run concurrently (events order the ring reuse), and the caller's stream
-  // waits for the last K3 before the call returns (the ABI's ordering holds).
-  // `run`: K2's run length in blocks (0: auto).  Takes effect at the next
-  // signal start (begin_offline): the segments of one signal share a ring.
+  // internal streams.  K1 of chunk k+1 overlaps K2 and K3 of chunk k; it does
+  // not overlap K3 of chunk k-1, because the caller's stream waits on K3(k-1)
+  // before K1(k+1) (the X-ring sizing 2*jc + P + 2*PC + 1 depends on that
+  // wait).  The caller's stream waits for the last K3 before the call returns
+  // (the ABI's ordering holds).  `run`: K2's run length in blocks (0: auto).
+  // Takes effect at the next signal start (begin_offline copies the request):
+  // the segments of one signal share a ring sized for the schedule it began with.
   static constexpr int kSchedSerial = 0;
   static constexpr int kSchedPipelined = 1;
   static constexpr int kSchedChunked = 2;  // the pipelined rings and chunks, every kernel on the caller's stream
   void set_schedule(int mode, int chunk, int run);
-  int schedule() const { return sched_mode_; }
-  int pipe_chunk() const { return pipe_jc_; }
+  int schedule() const { return req_mode_; }
+  int pipe_chunk() const { return req_jc_; }
   // the device entry points opt in (the host-buffer pipeline and the
   // partitioned stages call run() with their own streams and stay serial)
   void set_pipeline_call(bool on) { pipe_call_ = on; }
@@ -145,7 +147,8 @@ class Upols {
           hipStream_t s);
   void run_pipelined(const Io& io, hipStream_t s, int64_t jb, int64_t J, int64_t nb_in);
 
-  int sched_mode_ = kSchedSerial, pipe_jc_ = 0, pipe_run_ = 0;
+  int sched_mode_ = kSchedSerial, pipe_jc_ = 0, pipe_run_ = 0;  // in force for the current signal
+  int req_mode_ = kSchedSerial, req_jc_ = 0, req_run_ = 0;        // requested, applied at begin_offline
   bool pipe_call_ = false;  // this call may pipeline (device entry points)
   bool sig_pipe_ = false;   // the current signal runs pipelined (fixed at begin_offline)
   int Qp_ = 0, zrows_p_ = 0;

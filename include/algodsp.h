@@ -361,7 +361,7 @@ int ad_mixdown_reduce(ad_comm* comm, const double* d_chan, int channels, int64_t
 typedef struct ad_fx_chain ad_fx_chain;
 typedef struct ad_compressor_config {
   double sample_rate, threshold_db, ratio, knee_db, attack_ms, release_ms, rms_window_ms, makeup_db;
-  double sidechain_low_cut_hz, sidechain_high_cut_hz; /* <= 0: off */
+  double sidechain_low_cut_hz, sidechain_high_cut_hz; /* 0: off; else [1 Hz, Nyquist), low < high */
   int topology;             /* 0 feed-forward, 1 feedback */
   int detector_mode;        /* 0 peak, 1 RMS */
   int feedback_ratio_scale; /* 1: feedback topology scales time constants and ratio */
@@ -369,6 +369,16 @@ typedef struct ad_compressor_config {
 } ad_compressor_config;
 /* NewCompressor(sampleRate) defaults (compressor.go:77-127). */
 void ad_compressor_default_config(ad_compressor_config* cfg, double sample_rate);
+/* The setters' validation of a whole config, host only (no device needed):
+ * AD_OK, or AD_ERR_INVALID_ARGUMENT for any value a reference setter rejects:
+ * ratio outside [1, 100], knee outside [0, 24] dB, attack outside [0.1, 1000]
+ * ms, release outside [1, 5000] ms, RMS window outside [1, 1000] ms
+ * (compressor.go:16-23, core.go:10-12, 131-198), a non-finite threshold or
+ * makeup, a bad sample rate, topology or detector mode, a side-chain cut
+ * that is negative or not in [1 Hz, Nyquist), or low >= high when both are on
+ * (core.go:542-564).  ad_fx_chain_set_compressor and the graph's COMPRESSOR
+ * node run the same check and change nothing on failure. */
+int ad_compressor_validate(const ad_compressor_config* cfg);
 
 int ad_fx_chain_create(int channels, int device, ad_fx_chain** out);
 int ad_fx_chain_set_eq(ad_fx_chain* h, const double* sections, int nsec, int per_channel);

@@ -127,3 +127,56 @@ def test_eq_noise_estimate_host_only():
     with pytest.raises(_lib.ErrInvalidArgument):
         bad = C.c_double()
         _lib.check(L.ad_fx_eq_noise(None, 2, 1, C.byref(bad)))
+
+
+# Each value a reference setter rejects (compressor.go:16-23; core.go:10-12,
+# 131-198, 542-564), applied to NewCompressor's defaults at 48 kHz.
+BAD_COMPRESSOR_VALUES = [
+    ("ratio", 100.5), ("ratio", 0.5), ("ratio", float("nan")),
+    ("knee_db", 24.5), ("knee_db", -0.1),
+    ("attack_ms", 0.05), ("attack_ms", 1000.5),
+    ("release_ms", 0.5), ("release_ms", 5001.0),
+    ("rms_window_ms", 0.5), ("rms_window_ms", 1001.0),
+    ("threshold_db", float("nan")), ("threshold_db", float("inf")),
+    ("makeup_db", float("nan")), ("makeup_db", float("-inf")),
+    ("sidechain_low_cut_hz", 0.5), ("sidechain_high_cut_hz", 0.5),
+    ("sidechain_low_cut_hz", 24000.0), ("sidechain_high_cut_hz", 30000.0),
+    ("sidechain_low_cut_hz", -1.0), ("sidechain_high_cut_hz", float("nan")),
+    ("sample_rate", 0.0), ("topology", 2), ("detector_mode", -1),
+]
+GOOD_COMPRESSOR_EDGES = [
+    ("ratio", 1.0), ("ratio", 100.0), ("knee_db", 0.0), ("knee_db", 24.0),
+    ("attack_ms", 0.1), ("attack_ms", 1000.0), ("release_ms", 1.0), ("release_ms", 5000.0),
+    ("rms_window_ms", 1.0), ("rms_window_ms", 1000.0),
+    ("sidechain_low_cut_hz", 1.0), ("sidechain_high_cut_hz", 23999.0),
+]
+
+
+def _comp_cfg(**kv):
+    cfg = _lib.CompressorConfig()
+    _lib.lib().ad_compressor_default_config(C.byref(cfg), 48000.0)
+    for k, v in kv.items():
+        setattr(cfg, k, v)
+    return cfg
+
+
+@pytest.mark.parametrize("field,value", BAD_COMPRESSOR_VALUES)
+def test_compressor_validation_rejects_setter_ranges(field, value):
+    rc = _lib.lib().ad_compressor_validate(C.byref(_comp_cfg(**{field: value})))
+    assert rc == _lib.AD_ERR_INVALID_ARGUMENT, (field, value)
+
+
+def test_compressor_validation_low_must_be_below_high():
+    L = _lib.lib()
+    assert L.ad_compressor_validate(C.byref(_comp_cfg(sidechain_low_cut_hz=6000.0, sidechain_high_cut_hz=6000.0))) \
+        == _lib.AD_ERR_INVALID_ARGUMENT
+    assert L.ad_compressor_validate(C.byref(_comp_cfg(sidechain_low_cut_hz=7000.0, sidechain_high_cut_hz=80.0))) \
+        == _lib.AD_ERR_INVALID_ARGUMENT
+    assert L.ad_compressor_validate(C.byref(_comp_cfg(sidechain_low_cut_hz=80.0, sidechain_high_cut_hz=6000.0))) \
+        == _lib.AD_OK
+    assert L.ad_compressor_validate(None) == _lib.AD_ERR_INVALID_ARGUMENT
+
+
+@pytest.mark.parametrize("field,value", GOOD_COMPRESSOR_EDGES)
+def test_compressor_validation_accepts_range_edges(field, value):
+    assert _lib.lib().ad_compressor_validate(C.byref(_comp_cfg(**{field: value}))) == _lib.AD_OK

@@ -184,6 +184,40 @@ def test_compressor_vs_oracle(gpu, cfg):
         np.testing.assert_allclose(gm, om, rtol=METRIC_RTOL, atol=0)
 
 
+def test_compressor_setters_reject_out_of_range(gpu):
+    """Every value a reference setter rejects (compressor.go:16-23, core.go:131-198,
+    542-564) makes ad_fx_chain_set_compressor return AD_ERR_INVALID_ARGUMENT,
+    and the stage keeps its previous config: the output afterwards equals an
+    untouched compressor's bit for bit."""
+    from algodsp import _lib
+    from test_abi import BAD_COMPRESSOR_VALUES
+
+    n = 4096
+    x = np.stack([legacy_signal(n), 0.5 * signals.white_noise(n, 77)])
+    comp = P.Compressor(48000.0, channels=2)
+    setters = {"ratio": comp.SetRatio, "knee_db": comp.SetKnee, "attack_ms": comp.SetAttack,
+               "release_ms": comp.SetRelease, "rms_window_ms": comp.SetRMSWindow,
+               "threshold_db": comp.SetThreshold, "makeup_db": comp.SetMakeupGain,
+               "sidechain_low_cut_hz": comp.SetSidechainLowCut, "sidechain_high_cut_hz": comp.SetSidechainHighCut}
+    for field, value in BAD_COMPRESSOR_VALUES:
+        with pytest.raises(_lib.ADError) as e:
+            if field in setters:
+                setters[field](value)
+            else:
+                comp._set(**{field: value})
+        assert e.value.code == _lib.AD_ERR_INVALID_ARGUMENT, (field, value)
+    comp.SetSidechainHighCut(6000.0)
+    with pytest.raises(_lib.ADError) as e:
+        comp.SetSidechainLowCut(6000.0)  # low >= high
+    assert e.value.code == _lib.AD_ERR_INVALID_ARGUMENT
+    comp.SetSidechainHighCut(0.0)
+    a = x.copy()
+    comp.ProcessInPlace(a)
+    b = x.copy()
+    P.Compressor(48000.0, channels=2).ProcessInPlace(b)
+    assert np.array_equal(a, b)
+
+
 # ------------------------------------------------------------------ Expander / Gate
 @pytest.mark.parametrize("kind,cfg", [
     ("expander", {}),

@@ -122,3 +122,40 @@ def test_schedule_rejects_bad_arguments(gpu):
     small = conv.MultiChannelConvolver(ir[:, :4096], hop=1024, channels=1)
     small.set_schedule(small.SCHED_PIPELINED)
     assert small.schedule() == (small.SCHED_SERIAL, 0)
+
+
+@pytest.mark.parametrize("first,second", [
+    ((1, 12, 0), (0, 0, 0)),     # pipelined signal, serial requested mid-signal
+    ((1, 12, 0), (1, 64, 0)),    # a larger chunk requested mid-signal
+    ((0, 0, 0), (1, 12, 0)),     # serial signal, pipelined requested mid-signal
+])
+def test_schedule_change_between_segments(gpu, first, second):
+    """A set_schedule between two segments of one signal applies from the next
+    signal start (begin_offline): the signal in flight keeps the rings it began
+    with, so its output equals the serial schedule bit for bit, and the next
+    signal runs the new schedule, also bit for bit."""
+    import torch
+
+    ir = irlib.large_church()
+    C_, n, hop = 4, 1 << 20, 8192
+    out_len = n + ir.shape[1] - 1
+    x = np.stack([signals.white_noise(n, 0xC4A7 + c) for c in range(C_)])
+    dx = torch.from_numpy(x).cuda()
+    ids = [c % 2 for c in range(C_)]
+    ref = conv.MultiChannelConvolver(ir, hop=hop, channels=C_, ir_index=ids)
+    want, _ = _run(ref, x, out_len)
+    eng = conv.MultiChannelConvolver(ir, hop=hop, channels=C_, ir_index=ids)
+    eng.set_schedule(*first)
+    blocks = -(-out_len // hop)
+    cuts = [min(out_len, hop * (blocks * i // 3)) for i in range(4)]
+    y = torch.full((C_, out_len), np.nan, dtype=torch.float64, device="cuda")
+    for i, (b, e) in enumerate(zip(cuts[:-1], cuts[1:])):
+        if i == 1:
+            eng.set_schedule(*second)
+            assert eng.schedule()[0] == (second[0] if second[0] == 0 else eng.SCHED_PIPELINED)
+        eng.process_device_segment(dx.data_ptr(), n, n, y.data_ptr(), out_len, out_len, b, e)
+    torch.cuda.synchronize()
+    assert torch.equal(y, want)
+    y2, _ = _run(eng, x, out_len)
+    torch.cuda.synchronize()
+    assert torch.equal(y2, want)
