@@ -34,7 +34,7 @@ FX_CHAIN_CLK = 24.5     # config 5's serial chain per sample, clocks: the compre
                         # so the envelope is the one recurrence left serial per channel
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
@@ -93,7 +93,58 @@ def parse():
                         "fx: config 5 effect chain (256 ch); "
                         "stream: config 2 streaming OLS (mono, 16384 taps, 4096-sample host blocks); "
                         "corr: CorrelateFFT of two 2^23-sample signals (SURVEY 8(f)3, device buffers)")
-    return p.parse_args()
+    return p.parse_args(argv)
+
+
+class GpuRuntime:
+    """What run_conv needs from the machine: torch.cuda streams and events, the
+    HIP engine (conv.MultiChannelConvolver) and the library's RCCL communicator
+    (shard.Comm, ad_comm_* / ad_mixdown_reduce).  The product path.  The N > 1
+    orchestration around it (bootstrap, two-buffer reduce pipeline, conv-only
+    pass, max over ranks, rank 0's parity) is plain Python over this interface,
+    so tests/test_bench_orchestration.py runs the same code at world 2 over gloo
+    with CPU stand-ins for these members."""
+
+    dist_backend = "nccl"  # RCCL on ROCm
+
+    def __init__(self, local: int):
+        import torch
+
+        self.torch = torch
+        torch.cuda.set_device(local)
+        self.dev = torch.device("cuda", local)
+        self.local = local
+
+    def init_dist(self):
+        import torch.distributed as dist
+
+        dist.init_process_group(self.dist_backend, device_id=self.dev)
+
+    def current_stream(self):
+        return self.torch.cuda.current_stream(self.dev)
+
+    def new_stream(self):
+        return self.torch.cuda.Stream(self.dev)
+
+    def event(self, timing: bool = False):
+        return self.torch.cuda.Event(enable_timing=timing)
+
+    def synchronize(self):
+        self.torch.cuda.synchronize(self.dev)
+
+    def engine(self, ir, hop, channels, ir_index, chunk_blocks):
+        from algodsp import conv
+
+        return conv.MultiChannelConvolver(ir, hop=hop, channels=channels, ir_index=ir_index,
+                                          chunk_blocks=chunk_blocks, device=self.local)
+
+    def comm(self, rank, world, bootstrap):
+        from algodsp import shard
+
+        return shard.Comm(rank, world, self.local, bootstrap)
+
+    def empty_cache(self):
+        self.torch.cuda.empty_cache()
 
 
 def _free_port() -> int:
@@ -265,30 +316,37 @@ def main():
         return main_corr(args)
     if args.workload == "stream":
         return main_stream(args)
-    import numpy as np
-    import torch
-    import torch.distributed as dist
-
-    from algodsp import conv, irlib, signals
-
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    rt = GpuRuntime(local)
+    if world > 1:
+        rt.init_dist()
+    return conv_main(args, rt, world, rank, local)
+
+
+def conv_main(args, rt, world, rank, local):
+    """The conv / shard workload on this rank (the BASELINE metric): measure
+    with run_conv, then rank 0 assembles and prints the JSON line.  `rt` is a
+    GpuRuntime (or a test's CPU stand-in with the same members); a world > 1
+    process group is already initialised."""
+    import numpy as np
+    import torch.distributed as dist
+
+    from algodsp import irlib
+
+    dev = rt.dev
     # config 4's shard (8 ch x 2^24 per GPU + the stereo mixdown) at N > 1, or
     # at any N with --workload shard; config 3 (stereo x 2^24) at N = 1
     shard_cfg = world > 1 or args.workload == "shard"
     mixdown = shard_cfg if args.mixdown == "auto" else args.mixdown == "on"
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
 
     if args.channels is None:
         args.channels = 8 if shard_cfg else 2
     if args.samples is None:
         args.samples = 1 << 24
     ir = irlib.large_church()                       # [2][131072], Large Church zero padded
-    r = run_conv(args, world, rank, local, dev, ir, args.channels, shard_cfg, mixdown, args.steps, args.warmup,
+    r = run_conv(args, world, rank, rt, ir, args.channels, shard_cfg, mixdown, args.steps, args.warmup,
                  args.kernel_timing, args.settle_steps)
     C, n, K, out_len = args.channels, args.samples, ir.shape[1], r["out_len"]
     elapsed, prof, prof_live, mode = r["elapsed"], r["prof"], r["prof_live"], args.kernel_timing
@@ -354,7 +412,7 @@ def main():
         shard_sub = None
         if world == 1 and args.workload == "conv" and args.shard_sub == "on" and not shard_cfg:
             ys.clear(), mixes.clear()
-            r8 = run_conv(args, 1, 0, local, dev, ir, 8, True, True, min(args.steps, 5), 2, "off")
+            r8 = run_conv(args, 1, 0, rt, ir, 8, True, True, min(args.steps, 5), 2, "off")
             fused = args.mix_fused == "on"
             shard_sub = {"value": round(8 * n * min(args.steps, 5) / r8["elapsed"] / 1e6, 3), "unit": "Msamples/s",
                          "ms_per_step": round(r8["elapsed"] / min(args.steps, 5) * 1e3, 4),
@@ -382,7 +440,7 @@ def main():
         if legs_on and args.fx_leg == "on":
             ys.clear(), mixes.clear()
             config5 = fx_measure(args, 1, 0, local, dev, 5, 2, not args.no_cpu_baseline, n=1 << 20)
-            torch.cuda.empty_cache()
+            rt.empty_cache()
         config2 = None
         if legs_on and args.stream_leg == "on":
             config2 = stream_measure(1024, 32, not args.no_cpu_baseline)
@@ -541,23 +599,25 @@ def output_parity(args, r, ir, C_total, mixdown):
     return parity
 
 
-def run_conv(args, world, rank, local, dev, ir, C, shard_cfg, mixdown, steps, warmup, mode, settle_steps=0):
+def run_conv(args, world, rank, rt, ir, C, shard_cfg, mixdown, steps, warmup, mode, settle_steps=0):
     """One conv measurement: C channels x args.samples per GPU per step (IR[c mod 2]),
     optionally with the RCCL stereo mixdown; `steps` timed steps after `warmup`,
     bracketed by barrier + synchronize, max over ranks.  Returns the timing, the
-    per-kernel event profile and the buffers for the parity check."""
+    per-kernel event profile and the buffers for the parity check.  `rt`
+    supplies the device, streams, events, the engine and the communicator
+    (GpuRuntime; a CPU stand-in in tests/test_bench_orchestration.py)."""
     import numpy as np
     import torch
     import torch.distributed as dist
 
-    from algodsp import conv, shard, signals
+    from algodsp import shard, signals
+
+    dev = rt.dev
 
     K = ir.shape[1]
     n = args.samples
     comm = None
     out_len = n + K - 1                             # full linear convolution (OverlapSave.Process)
-    from algodsp import shard
-
     if mixdown and C % 2 and world > 1:
         raise SystemExit("--channels must be even for the multi-GPU stereo mixdown")
     ids = list(shard.channel_group(rank, world, C * world))  # this rank's global channel ids
@@ -578,20 +638,19 @@ def run_conv(args, world, rank, local, dev, ir, C, shard_cfg, mixdown, steps, wa
             dist.broadcast_object_list(obj, src=0)
             return obj[0]
 
-        comm = shard.Comm(rank, world, local, bootstrap)
+        comm = rt.comm(rank, world, bootstrap)
     nbuf = 2 if (mixdown and args.pipeline == "on") else 1
     # fused: the engine writes the stereo mix directly (no per-channel rows)
     fused = mixdown and C != 2 and args.mix_fused == "on"
     ys = [torch.empty((2 if fused else C, out_len), dtype=torch.float64, device=dev) for _ in range(nbuf)]
     mixes = [y if (C == 2 or fused) else torch.empty((2, out_len), dtype=torch.float64, device=dev) for y in ys]
 
-    eng = conv.MultiChannelConvolver(ir, hop=args.hop, channels=C, ir_index=shard.ir_index(ids),
-                                     chunk_blocks=args.chunk, device=local)
+    eng = rt.engine(ir, args.hop, C, shard.ir_index(ids), args.chunk)
     if args.schedule != "serial":
         eng.set_schedule(["serial", "pipelined", "chunked"].index(args.schedule), args.pipe_chunk, args.pipe_run)
-    stream = torch.cuda.current_stream(dev)
+    stream = rt.current_stream()
     sptr = stream.cuda_stream
-    side = torch.cuda.Stream(dev) if mixdown else None  # mixdown + reduce
+    side = rt.new_stream() if mixdown else None  # mixdown + reduce
     blocks = -(-out_len // args.hop)
     cuts = [min(out_len, args.hop * (blocks * i // args.segments)) for i in range(args.segments + 1)]
     segs = [(b, e) for b, e in zip(cuts[:-1], cuts[1:]) if e > b]
@@ -614,10 +673,10 @@ def run_conv(args, world, rank, local, dev, ir, C, shard_cfg, mixdown, steps, wa
             else:
                 eng.process_device_segment(x.data_ptr(), n, n, yb.data_ptr(), out_len, out_len, b, e, sptr)
             if mixdown and reduce_on[0]:
-                done = torch.cuda.Event()
+                done = rt.event()
                 done.record(stream)
                 side.wait_event(done)
-                r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                r0, r1 = rt.event(True), rt.event(True)
                 r0.record(side)
                 # stereo group or fused mix: mb already holds the partial mix (no k_mixdown)
                 comm.mixdown_reduce(yb.data_ptr() + 8 * b, 0 if (C == 2 or fused) else C, out_len, e - b,
@@ -625,7 +684,7 @@ def run_conv(args, world, rank, local, dev, ir, C, shard_cfg, mixdown, steps, wa
                 r1.record(side)
                 red_ev.append((r0, r1))
         if mixdown and reduce_on[0]:
-            ev = torch.cuda.Event()
+            ev = rt.event()
             ev.record(side)
             red_done[i] = ev
 
@@ -636,7 +695,7 @@ def run_conv(args, world, rank, local, dev, ir, C, shard_cfg, mixdown, steps, wa
     for _ in range(warmup):
         step()
     drain()
-    torch.cuda.synchronize(dev)
+    rt.synchronize()
     eng.profile_read()  # clear
 
     dom_mask = 7
@@ -645,16 +704,16 @@ def run_conv(args, world, rank, local, dev, ir, C, shard_cfg, mixdown, steps, wa
         for _ in range(2):
             step()
         drain()
-        torch.cuda.synchronize(dev)
+        rt.synchronize()
         pw = eng.profile_read()
         dom_mask = 1 << list(pw).index(max(pw, key=lambda k: pw[k][0]))
     eng.profile_enable(mode != "off", kernels=dom_mask if mode == "dominant" else 7)
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize(dev)
+    rt.synchronize()
     red_ev.clear()
     # per-step events on the launch stream (record only: no host wait inside the loop)
-    sev = ([torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+    sev = ([rt.event(True) for _ in range(steps + 1)]
            if world == 1 and args.step_events == "on" else None)
     t0 = time.perf_counter()
     if sev:
@@ -664,7 +723,7 @@ def run_conv(args, world, rank, local, dev, ir, C, shard_cfg, mixdown, steps, wa
         if sev:
             sev[i + 1].record(stream)
     drain()
-    torch.cuda.synchronize(dev)
+    rt.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -679,7 +738,7 @@ def run_conv(args, world, rank, local, dev, ir, C, shard_cfg, mixdown, steps, wa
         for _ in range(max(2, steps // 2)):
             step()
         drain()
-        torch.cuda.synchronize(dev)
+        rt.synchronize()
         last = (it[0] - 1) % nbuf
         prof = eng.profile_read()
         for k, v in prof_live.items():  # live (timed-region) numbers win
@@ -696,13 +755,13 @@ def run_conv(args, world, rank, local, dev, ir, C, shard_cfg, mixdown, steps, wa
         reduce_on[0] = False
         ksteps = min(steps, 5)
         step()
-        torch.cuda.synchronize(dev)
+        rt.synchronize()
         if world > 1:
             dist.barrier()
         tc = time.perf_counter()
         for _ in range(ksteps):
             step()
-        torch.cuda.synchronize(dev)
+        rt.synchronize()
         if world > 1:
             dist.barrier()
         conv_elapsed = (time.perf_counter() - tc) / ksteps * steps
@@ -712,7 +771,7 @@ def run_conv(args, world, rank, local, dev, ir, C, shard_cfg, mixdown, steps, wa
         # reduced (whole-job) mix
         step()
         drain()
-        torch.cuda.synchronize(dev)
+        rt.synchronize()
         last = (it[0] - 1) % nbuf
     conv_elapsed = conv_elapsed if conv_elapsed is not None else 0.0
     if world > 1:
@@ -730,12 +789,12 @@ def run_conv(args, world, rank, local, dev, ir, C, shard_cfg, mixdown, steps, wa
         # recovers (tools/step_curve.py): the same step after
         # the timed region, event-timed per step, median of the last half.  Reported
         # beside `value`, never as it.
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(settle_steps + 1)]
+        ev = [rt.event(True) for _ in range(settle_steps + 1)]
         ev[0].record(stream)
         for i in range(settle_steps):
             step()
             ev[i + 1].record(stream)
-        torch.cuda.synchronize(dev)
+        rt.synchronize()
         per = [ev[i].elapsed_time(ev[i + 1]) for i in range(settle_steps)]
         tail = sorted(per[settle_steps // 2:])
         settled = {"steps": settle_steps, "median_ms_last_half": round(tail[len(tail) // 2], 4),
