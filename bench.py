@@ -63,6 +63,9 @@ def parse(argv=None):
     p.add_argument("--stream-leg", choices=["on", "off"], default="on",
                    help="N = 1 conv: also time config 2 (StreamingOverlapSave, 4096-sample host blocks, "
                         "1024 blocks: p50 / p99 per block) as the line's config2_stream key")
+    p.add_argument("--corr-leg", choices=["on", "off"], default="on",
+                   help="N = 1 conv: also time CorrelateFFT of two 2^23-sample signals (SURVEY 8(f)3, device "
+                        "buffers, 40 calls, parity + CPU leg) as the line's correlate key")
     p.add_argument("--pipeline", choices=["on", "off"], default="on",
                    help="N > 1: overlap step i's mixdown reduce with step i+1's convolution (two output buffers)")
     p.add_argument("--mix-fused", choices=["on", "off"], default="on",
@@ -74,7 +77,11 @@ def parse(argv=None):
                         "mixdown reduce starts as soon as it is computed")
     p.add_argument("--step-events", choices=["on", "off"], default="on",
                    help="N = 1: an event between the timed steps (the line's step_ms)")
-    p.add_argument("--settle-steps", type=int, default=60,
+    p.add_argument("--clock-settle", type=int, default=60,
+                   help="untimed steps before the W warm-up steps: the board's clock dips for ~10 ms once the load "
+                        "turns sustained and recovers after ~30-45 steps (profiles/r05_step_curve.json, DESIGN.md "
+                        "section 2), so the timed region measures the steady state (the line's clock_settle_steps)")
+    p.add_argument("--settle-steps", type=int, default=0,
                    help="N = 1: after the timed region, this many more steps event-timed one by one (the line's "
                         "`settled` key: the step once the board's clock has recovered from its load-onset dip)")
     p.add_argument("--kernel-timing", choices=["dominant", "on", "off"], default="dominant",
@@ -347,7 +354,7 @@ def conv_main(args, rt, world, rank, local):
         args.samples = 1 << 24
     ir = irlib.large_church()                       # [2][131072], Large Church zero padded
     r = run_conv(args, world, rank, rt, ir, args.channels, shard_cfg, mixdown, args.steps, args.warmup,
-                 args.kernel_timing, args.settle_steps)
+                 args.kernel_timing, args.settle_steps, args.clock_settle)
     C, n, K, out_len = args.channels, args.samples, ir.shape[1], r["out_len"]
     elapsed, prof, prof_live, mode = r["elapsed"], r["prof"], r["prof_live"], args.kernel_timing
     ids, x_host, eng, ys, mixes, last = r["ids"], r["x_host"], r["eng"], r["ys"], r["mixes"], r["last"]
@@ -444,6 +451,10 @@ def conv_main(args, rt, world, rank, local):
         config2 = None
         if legs_on and args.stream_leg == "on":
             config2 = stream_measure(1024, 32, not args.no_cpu_baseline)
+        correlate = None
+        if legs_on and args.corr_leg == "on":
+            correlate = corr_measure(40, 3, not args.no_cpu_baseline)
+            rt.empty_cache()
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(ir, args.cpu_sample)
@@ -478,6 +489,7 @@ def conv_main(args, rt, world, rank, local):
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "clock_settle_steps": args.clock_settle,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -536,6 +548,8 @@ def conv_main(args, rt, world, rank, local):
             line["config5"] = config5
         if config2 is not None:
             line["config2_stream"] = config2
+        if correlate is not None:
+            line["correlate"] = correlate
         if r["reduce_diag"] is not None:
             line["mixdown_reduce"] = dict(r["reduce_diag"], note=(
                 "max over ranks; conv_ms_per_step: the same step with the reduce off; reduce_ms: RCCL reduce "
@@ -599,7 +613,7 @@ def output_parity(args, r, ir, C_total, mixdown):
     return parity
 
 
-def run_conv(args, world, rank, rt, ir, C, shard_cfg, mixdown, steps, warmup, mode, settle_steps=0):
+def run_conv(args, world, rank, rt, ir, C, shard_cfg, mixdown, steps, warmup, mode, settle_steps=0, pre_steps=0):
     """One conv measurement: C channels x args.samples per GPU per step (IR[c mod 2]),
     optionally with the RCCL stereo mixdown; `steps` timed steps after `warmup`,
     bracketed by barrier + synchronize, max over ranks.  Returns the timing, the
@@ -692,7 +706,7 @@ def run_conv(args, world, rank, rt, ir, C, shard_cfg, mixdown, steps, warmup, mo
         if mixdown:
             side.synchronize()
 
-    for _ in range(warmup):
+    for _ in range(pre_steps + warmup):  # pre_steps: the clock settle (--clock-settle)
         step()
     drain()
     rt.synchronize()
@@ -896,10 +910,11 @@ def _plan_radices(N):
     return [1 << (base + (1 if p < extra else 0)) for p in range(np_)]
 
 
-def main_corr(args):
+def corr_measure(steps: int, warmup: int, cpu_leg: bool, n: int | None = None) -> dict:
     """conv.CorrelateFFT (correlate.go:111-172) of two n-sample
     signals, one nextPow2(2n-1) = 2^24-point transform pair on the device
-    (device-resident inputs/outputs; plans and work buffers cached).  Replicas only."""
+    (device-resident inputs/outputs; plans and work buffers cached), with the
+    parity of the measured output and the CPU leg.  Replicas only."""
     import ctypes as C
 
     import numpy as np
@@ -908,10 +923,11 @@ def main_corr(args):
     from algodsp import _lib, signals
 
     dev = torch.device("cuda", 0)
-    n = args.samples or (1 << 23)
-    a = torch.from_numpy(signals.white_noise(n, 0x5EED)).to(dev)
-    b = torch.from_numpy(signals.white_noise(n, 0x5EEE)).to(dev)
-    out = torch.empty(2 * n - 1, dtype=torch.float64, device=dev)
+    n = n or (1 << 23)
+    ah, bh = signals.white_noise(n, 0x5EED), signals.white_noise(n, 0x5EEE)
+    a = torch.from_numpy(ah).to(dev)
+    b = torch.from_numpy(bh).to(dev)
+    out = torch.full((2 * n - 1,), float("nan"), dtype=torch.float64, device=dev)
     stream = torch.cuda.current_stream(dev)
     L = _lib.lib()
 
@@ -919,18 +935,40 @@ def main_corr(args):
         _lib.check(L.ad_correlate_fft_device(C.c_void_p(a.data_ptr()), n, C.c_void_p(b.data_ptr()), n,
                                              C.c_void_p(out.data_ptr()), 0, C.c_void_p(stream.cuda_stream)))
 
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step()
     torch.cuda.synchronize(dev)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     e0.record(stream)
-    for _ in range(args.steps):
+    for _ in range(steps):
         step()
     e1.record(stream)
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
-    ms = e0.elapsed_time(e1) / args.steps
+    ms = e0.elapsed_time(e1) / steps
+    # parity of the measured output: 16-lag windows (result[j] = sum_i a[i + j - (n-1)] b[i],
+    # correlate.go:176-185) at the most negative lags, around lag 0, two middles and the
+    # most positive lags, against exact float64 dot products (numpy)
+    got = out.cpu().numpy()
+    wins = [0, n // 3, n - 1 - 8, n - 1 + n // 2, 2 * n - 2 - 15]
+    errs, refs = [], []
+    for j0 in wins:
+        for j in range(j0, j0 + 16):
+            lag = j - (n - 1)
+            ref = float(np.dot(ah[lag:], bh[:n - lag])) if lag >= 0 else float(np.dot(ah[:n + lag], bh[-lag:]))
+            errs.append(got[j] - ref)
+            refs.append(ref)
+    errs, refs = np.array(errs), np.array(refs)
+    scale = max(1.0, float(np.max(np.abs(refs))))
+    parity = {"max_abs": float(np.max(np.abs(errs))), "rms": float(np.sqrt(np.mean(errs ** 2))),
+              "max_rel": float(np.max(np.abs(errs)) / scale), "outputs_checked": int(errs.size),
+              "no_nan": bool(not np.isnan(got).any()),
+              "against": "exact float64 dot products (numpy) at lags " + ", ".join(str(j - (n - 1)) for j in wins) +
+                         " (+0..15)",
+              "tolerance": "max |err| <= 1e-10 max(1, max |ref|) (tests/test_spectral_gpu.py)"}
+    if not (parity["max_rel"] <= 1e-10 and parity["no_nan"]):
+        print(f"bench.py: CORRELATE PARITY FAILURE {parity}", file=sys.stderr)
     N = 1 << (2 * n - 2).bit_length()
     # algorithmic bytes per call (DESIGN.md "spectral row") of the passes the
     # call runs: the forward transform of a + i b (its first pass reads the
@@ -957,7 +995,7 @@ def main_corr(args):
     alg = fwd + mid + inv + (0 if split else 2 * n * 8)
     gbs = alg / (ms * 1e-3) / 1e9
     cpu = None
-    if not args.no_cpu_baseline:
+    if cpu_leg:
         sys.path.insert(0, str(ROOT / "tests"))
         import oracle_lib as O
 
@@ -979,22 +1017,35 @@ def main_corr(args):
                 traffic = tab["hbm_bytes_per_call"]
         except Exception:
             traffic = None
-    line = {
-        "metric": "Msamples/sec, CorrelateFFT of two 2^23-sample signals (input samples per second)",
-        "value": round(2 * n / (ms * 1e-3) / 1e6, 3), "unit": "Msamples/s", "n_gpus": 1, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "f64", "data": "synthetic: SplitMix64 white noise",
-        "config": {"workload": f"conv.CorrelateFFT n = m = {n}, FFT size {N} (forward: {P} device passes over a + i b; "
-                               f"inverse: {Ph} passes at N/2{'; forward last + inverse first fused' if fused else ''}"
-                               f"{'; max-abs in the first pass' if split else ''}), device-resident (PCIe excluded)",
-                   "fft_size": N},
+    return {
+        "value": round(2 * n / (ms * 1e-3) / 1e6, 3), "unit": "Msamples/s", "steps": steps, "warmup": warmup,
+        "ms_per_call": round(ms, 4),
+        "workload": f"conv.CorrelateFFT n = m = {n}, FFT size {N} (forward: {P} device passes over a + i b; "
+                    f"inverse: {Ph} passes at N/2{'; forward last + inverse first fused' if fused else ''}"
+                    f"{'; max-abs in the first pass' if split else ''}), device-resident (PCIe excluded), "
+                    f"event-timed over {steps} back-to-back calls",
+        "fft_size": N,
         "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "note": "whole call: algorithmic bytes of the passes it runs (pointwise op, lag order and "
                              "the Z round trip fused away) / event time; traffic = HBM bytes per call from PMC "
                              "(FETCH_SIZE x2 + WRITE_SIZE, every kernel of the call)"},
+        "parity": parity,
         "cpu_baseline": cpu,
-        "wall_ms_per_step": round(dt / args.steps * 1e3, 4),
+        "wall_ms_per_call": round(dt / steps * 1e3, 4),
+    }
+
+
+def main_corr(args):
+    r = corr_measure(args.steps, args.warmup, not args.no_cpu_baseline, args.samples)
+    line = {
+        "metric": "Msamples/sec, CorrelateFFT of two 2^23-sample signals (input samples per second)",
+        "value": r["value"], "unit": "Msamples/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": r["ms_per_call"], "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f64", "data": "synthetic: SplitMix64 white noise",
+        "config": {"workload": r["workload"], "fft_size": r["fft_size"]},
+        "roofline": r["roofline"], "parity": r["parity"], "cpu_baseline": r["cpu_baseline"],
+        "wall_ms_per_step": r["wall_ms_per_call"],
     }
     print(json.dumps(line), flush=True)
 

@@ -221,7 +221,7 @@ def _run_world(argv, world=2):
     return res
 
 
-BASE = ["--gpus", "2", "--steps", "3", "--warmup", "1", "--samples", "8192", "--no-cpu-baseline",
+BASE = ["--gpus", "2", "--steps", "3", "--warmup", "1", "--clock-settle", "2", "--samples", "8192", "--no-cpu-baseline",
         "--host-io", "off", "--shard-sub", "off", "--fx-leg", "off", "--stream-leg", "off"]
 
 
