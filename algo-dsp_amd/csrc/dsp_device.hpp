@@ -26,19 +26,6 @@ __device__ __forceinline__ double env_step(const CompParams& p, double env, doub
   return __builtin_fma(p.env_c2, fabs(src - env), __builtin_fma(p.env_k1, env, p.env_c1 * src));
 }
 
-// env_step carried in the difference dd = src_t - env_{t-1} (same map, other
-// rounding): env_t = src_t - k1 dd + c2 |dd|, and with ds = src_{t+1} - src_t
-//   dd' = src_{t+1} - env_t = fma(-c2, |dd|, fma(k1, dd, ds)),
-// so the chain is two FMAs with nothing beside them on it (env_step issues
-// the |src - env| subtraction and the k1 env FMA back to back, both waiting
-// on env); the envelope itself is src_{t+1} - dd', off the chain.
-__device__ __forceinline__ double env_dstep(const CompParams& p, double dd, double ds) {
-  return __builtin_fma(-p.env_c2, fabs(dd), __builtin_fma(p.env_k1, dd, ds));
-}
-__device__ __forceinline__ double env_from_d(const CompParams& p, double dd, double src) {
-  return __builtin_fma(p.env_c2, fabs(dd), __builtin_fma(-p.env_k1, dd, src));
-}
-
 __device__ __forceinline__ double go_log2(double x) {
 #pragma clang fp contract(off)
   int e;

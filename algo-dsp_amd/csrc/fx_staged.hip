@@ -357,151 +357,8 @@ __global__ __launch_bounds__(64 * (kMaxSecPerPass + 2)) void k_fx_eq(FxStageArgs
 #ifndef AD_SEC_P
 #define AD_SEC_P 32
 #endif
-#ifndef AD_SEC_PRE
-#define AD_SEC_PRE 0
-#endif
 constexpr int kSecP = AD_SEC_P;   // samples per step
 constexpr int kSecPF = 2;   // I/O wave: steps of input loads in flight
-#if AD_SEC_PRE
-// K_sec with the section's input products formed by the I/O wave: v = x g,
-// b0 v, b1 v, b2 v depend on the input only, so the I/O wave computes them
-// (the same IEEE operations on the same operands: the same bits) and puts
-// (b0 v, b1 v) and b2 v into the ring; the section wave issues only the
-// recurrence's six operations per sample (yy = b0v + d0, a1 yy, b1v - a1 yy,
-// + d1, a2 yy, b2v - a2 yy) plus two ring reads and one write.
-__global__ __launch_bounds__(128) void k_fx_eq_sec(FxStageArgs a) {
-#pragma clang fp contract(off)
-  __shared__ __attribute__((aligned(16))) double2 pr[2][kSecP][64];  // (b0 v, b1 v)
-  __shared__ __attribute__((aligned(16))) double p2[2][kSecP][64];   // b2 v
-  __shared__ __attribute__((aligned(16))) double yr[2][kSecP][64];
-  const FxEqPart& P = a.part[blockIdx.y];
-  const int wid = wave_id();
-  const int l = threadIdx.x & 63;
-  const int g0 = blockIdx.x * 64;  // first channel of the group
-  const int64_t len = P.len;
-  const int64_t nst = (len + kSecP - 1) / kSecP;
-  const int cp = a.cpad;
-  const int gs = P.s0;
-  if (wid == 0) {
-    const int c = g0 + l;
-    const int cc = c < a.channels ? c : a.channels - 1;
-    const AD_GLOBAL double* sec = glob(a.eq.sec) + (int64_t)cc * a.eq.sec_ch_stride + gs * kSecStride;
-    const double a1 = sec[4], a2 = sec[5];
-    AD_GLOBAL double* st = glob(a.eq.state) + ((int64_t)cc * a.eq.nsec + gs) * 2;
-    double d0 = st[0], d1 = st[1];
-    __builtin_amdgcn_s_waitcnt(0);
-    lds_barrier();  // step 0's rows are in the ring
-    for (int64_t k = 0; k <= nst; ++k) {
-      if (k < nst) {
-        const int nreal = (int)min((int64_t)kSecP, len - k * kSecP);
-        double y[kSecP];
-        if (nreal == kSecP) {
-#pragma unroll
-          for (int d = 0; d < kSecP; ++d) {
-            const double2 bb = pr[k & 1][d][l];
-            const double b2v = p2[k & 1][d][l];
-            const double yy = bb.x + d0;
-            const double n0 = bb.y - a1 * yy + d1;
-            const double n1 = b2v - a2 * yy;
-            d0 = n0;
-            d1 = n1;
-            y[d] = yy;
-          }
-        } else {
-#pragma unroll
-          for (int d = 0; d < kSecP; ++d) {
-            const double2 bb = pr[k & 1][d][l];
-            const double b2v = p2[k & 1][d][l];
-            const double yy = bb.x + d0;
-            const double n0 = bb.y - a1 * yy + d1;
-            const double n1 = b2v - a2 * yy;
-            if (d < nreal) {  // padding leaves the state untouched
-              d0 = n0;
-              d1 = n1;
-            }
-            y[d] = yy;
-          }
-        }
-#pragma unroll
-        for (int d = 0; d < kSecP; ++d) yr[k & 1][d][l] = y[d];
-      }
-      lds_barrier();
-    }
-    if (c < a.channels) {
-      st[0] = d0;
-      st[1] = d1;
-    }
-  } else {
-    // I/O wave: lane l covers channels g0 + 2 (l & 31) .. + 1 of row 2 i + (l >> 5)
-    const AD_GLOBAL double* xin = glob(P.in);
-    AD_GLOBAL double* yo = glob(P.out);
-    const int cl = 2 * (l & 31), rh = l >> 5;
-    double qg[2], qb0[2], qb1[2], qb2[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int c = g0 + cl + h;
-      const int cc = c < a.channels ? c : a.channels - 1;
-      const AD_GLOBAL double* sec = glob(a.eq.sec) + (int64_t)cc * a.eq.sec_ch_stride + gs * kSecStride;
-      qg[h] = sec[0];
-      qb0[h] = sec[1];
-      qb1[h] = sec[2];
-      qb2[h] = sec[3];
-    }
-    typedef double d2 __attribute__((ext_vector_type(2)));
-    d2 buf[kSecPF][kSecP / 2];
-    auto fetch = [&](d2 (&dst)[kSecP / 2], int64_t step) {  // branch-free: rows past the chunk re-read its last
-#pragma unroll
-      for (int i = 0; i < kSecP / 2; ++i) {
-        const int64_t row = min(step * kSecP + 2 * i + rh, len - 1);
-        dst[i] = *reinterpret_cast<const AD_GLOBAL d2*>(xin + row * cp + g0 + cl);
-      }
-    };
-    auto put = [&](const d2 (&src)[kSecP / 2], int64_t step) {
-#pragma unroll
-      for (int i = 0; i < kSecP / 2; ++i) {
-        const double v0 = src[i].x * qg[0], v1 = src[i].y * qg[1];  // eq_section_step: v = x q[0]
-        pr[step & 1][2 * i + rh][cl] = make_double2(qb0[0] * v0, qb1[0] * v0);
-        pr[step & 1][2 * i + rh][cl + 1] = make_double2(qb0[1] * v1, qb1[1] * v1);
-        *reinterpret_cast<d2*>(&p2[step & 1][2 * i + rh][cl]) = d2{qb2[0] * v0, qb2[1] * v1};
-      }
-    };
-    auto flush = [&](int64_t step) {  // the section's outputs of `step`
-      const int64_t r0 = step * kSecP;
-      const int nreal = (int)min((int64_t)kSecP, len - r0);
-      d2 v[kSecP / 2];
-#pragma unroll
-      for (int i = 0; i < kSecP / 2; ++i) v[i] = *reinterpret_cast<const d2*>(&yr[step & 1][2 * i + rh][cl]);
-      if (nreal == kSecP) {
-#pragma unroll
-        for (int i = 0; i < kSecP / 2; ++i) *reinterpret_cast<AD_GLOBAL d2*>(yo + (r0 + 2 * i + rh) * cp + g0 + cl) = v[i];
-      } else {
-#pragma unroll
-        for (int i = 0; i < kSecP / 2; ++i)
-          if (2 * i + rh < nreal) *reinterpret_cast<AD_GLOBAL d2*>(yo + (r0 + 2 * i + rh) * cp + g0 + cl) = v[i];
-      }
-    };
-#pragma unroll
-    for (int b = 0; b < kSecPF; ++b) fetch(buf[b], b);
-    put(buf[0], 0);
-    fetch(buf[0], kSecPF);
-    lds_barrier();
-    // step k: rows of step k + 1 into the ring, loads of step k + 1 + PF, outputs of step k - 1
-    for (int64_t k = 0; k <= nst; k += kSecPF) {
-#pragma unroll
-      for (int u = 0; u < kSecPF; ++u) {
-        const int64_t kk = k + u;
-        if (kk <= nst) {
-          const int b = (u + 1) % kSecPF;
-          if (kk + 1 < nst) put(buf[b], kk + 1);
-          fetch(buf[b], kk + 1 + kSecPF);
-          if (kk >= 1) flush(kk - 1);
-          lds_barrier();
-        }
-      }
-    }
-  }
-}
-#else
 __global__ __launch_bounds__(128) void k_fx_eq_sec(FxStageArgs a) {
 #pragma clang fp contract(off)
   __shared__ __attribute__((aligned(16))) double xr[2][kSecP][64];
@@ -605,8 +462,6 @@ __global__ __launch_bounds__(128) void k_fx_eq_sec(FxStageArgs a) {
     }
   }
 }
-
-#endif  // AD_SEC_PRE
 
 // ---------------------------------------------------------------------------
 // K_gain: out = v * g(env) * makeup per (channel, sample), parallel.  A

@@ -293,16 +293,8 @@ __device__ __forceinline__ void lds_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n
 // the channel groups outnumber the CUs occupancy wins (16384 channels:
 // 63.2 -> 56.4 Gsamples/s on the compressor-only chain), so launch_fxtp_det
 // takes 64 rows for up to 256 groups and 32 above.
-#ifdef AD_DET_WPE  // tools/ A/B builds: cap the detector's VGPRs (waves per SIMD) so it co-resides with K_verb
-#define AD_DET_ATTR __attribute__((amdgpu_waves_per_eu(AD_DET_WPE)))
-#else
-#define AD_DET_ATTR
-#endif
-#ifndef AD_DET_DFORM
-#define AD_DET_DFORM 0  // tools/ A/B builds: the detector chain carried as src - env (env_dstep)
-#endif
 template <int DB, int DNB>
-__global__ __launch_bounds__(192) AD_DET_ATTR void k_fxtp_det(FxStageArgs a) {
+__global__ __launch_bounds__(192) void k_fxtp_det(FxStageArgs a) {
 #pragma clang fp contract(off)
   constexpr int kDetB = DB, kDetNB = DNB;
   constexpr int kDetLd = kDetB * kDetCh / 64;  // loads per batch
@@ -343,25 +335,11 @@ __global__ __launch_bounds__(192) AD_DET_ATTR void k_fxtp_det(FxStageArgs a) {
 #pragma unroll
         for (int d = 0; d < kDetB; ++d) nxt[d] = ring[sn][d][li];
         double ev[kDetB];
-#if AD_DET_DFORM
-        // the same map carried as dd = src - env (env_dstep): one FMA pair
-        // per sample on the chain, the envelope formed beside it
-        double dd = fabs(cur[0]) - cs.env;
-#pragma unroll
-        for (int d = 0; d + 1 < kDetB; ++d) {
-          const double sn = fabs(cur[d + 1]);
-          dd = env_dstep(p, dd, sn - fabs(cur[d]));
-          ev[d] = sn - dd;
-        }
-        ev[kDetB - 1] = env_from_d(p, dd, fabs(cur[kDetB - 1]));
-        cs.env = ev[kDetB - 1];
-#else
 #pragma unroll
         for (int d = 0; d < kDetB; ++d) {
           cs.env = env_step(p, cs.env, fabs(cur[d]));
           ev[d] = cs.env;
         }
-#endif
         // one masked region per batch: lanes >= kDetCh would write the same
         // addresses again (8-way conflicts on every write)
         if (l < kDetCh) {
@@ -829,12 +807,7 @@ __global__ __launch_bounds__(kVbThreads) void k_fxtp_verb(FxStageArgs a, const d
 // themselves with an LDS counter instead of the workgroup barrier, which the
 // comb waves only meet once per step.  Same operations per sample in the same
 // order as k_fxtp_verb: the same bits.
-#ifdef AD_VB_NUMVGPR  // tools/ A/B builds: cap K_verb's VGPRs so a detector workgroup co-resides
-#define AD_VB_ATTR __attribute__((amdgpu_waves_per_eu(AD_VB_NUMVGPR)))
-#else
-#define AD_VB_ATTR
-#endif
-__global__ __launch_bounds__(kVbThreads) AD_VB_ATTR void k_fxtp_verb_pipe(FxStageArgs a, const double* __restrict__ xC,
+__global__ __launch_bounds__(kVbThreads) void k_fxtp_verb_pipe(FxStageArgs a, const double* __restrict__ xC,
                                                                int64_t xstride, double* __restrict__ vbufC,
                                                                double* __restrict__ coC, int wu) {
 #pragma clang fp contract(off)
@@ -1040,13 +1013,6 @@ void launch_fxtp_carry(const FxTpEqArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_fxtp_carry, dim3((unsigned)a.channels), dim3(kFxTpMaxSeg), 0, s, a);
 }
 
-#ifndef AD_DET_SMALL_B  // the detector above 256 channel groups (and AD_DET_FORCE32): rows per batch, batches in flight
-#define AD_DET_SMALL_B 32
-#define AD_DET_SMALL_NB 14
-#endif
-#ifndef AD_DET_FORCE32
-#define AD_DET_FORCE32 0  // tools/ A/B builds: the 32-row detector at any channel count
-#endif
 void launch_fxtp_det(const FxStageArgs& a, hipStream_t s) {
   if (a.len <= 0) return;
 #if AD_DET_B == 32
@@ -1058,10 +1024,10 @@ void launch_fxtp_det(const FxStageArgs& a, hipStream_t s) {
 #endif
   {
     const unsigned groups = (unsigned)((a.channels + kDetCh - 1) / kDetCh);
-    if (groups <= 256 && !AD_DET_FORCE32)
+    if (groups <= 256)
       hipLaunchKernelGGL((k_fxtp_det<64, 8>), dim3(groups), dim3(192), 0, s, a);
     else
-      hipLaunchKernelGGL((k_fxtp_det<AD_DET_SMALL_B, AD_DET_SMALL_NB>), dim3(groups), dim3(192), 0, s, a);
+      hipLaunchKernelGGL((k_fxtp_det<32, 14>), dim3(groups), dim3(192), 0, s, a);
   }
 }
 

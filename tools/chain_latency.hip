@@ -38,6 +38,64 @@ __global__ void k_env(double* out, const double* in, int iters, double a, double
   if (threadIdx.x == 0) *cyc = t1 - t0;
 }
 
+// env/d: the same map carried as dd = src_t - env_{t-1}:
+//   dd' = fma(-c2, |dd|, fma(k1, dd, src_{t+1} - src_t)), env_t = src_{t+1} - dd'
+// (V = 0: the differences formed in the loop; V = 1: precomputed outside it)
+// env/2s: two samples per step on the convex map (attack faster than release):
+//   env'' = max(A1 env + B1, A2 env + B2, A3 env + B3), the three composed lines'
+//   slopes constant, their intercepts from the two inputs (off the chain)
+template <int V>
+__global__ void k_envd(double* out, const double* in, int iters, double a, double r, long long* cyc) {
+#pragma clang fp contract(off)
+  double x[9];
+  for (int d = 0; d < 9; ++d) x[d] = fabs(in[d * 64 + threadIdx.x]);
+  const double b = 1.0 - r, c1 = 0.5 * (a + b), c2 = 0.5 * (a - b), k1 = 1.0 - c1;
+  double ds[8];
+  for (int d = 0; d < 8; ++d) ds[d] = x[d + 1] - x[d];
+  double dd = x[0], acc = 0.0;
+  const long long t0 = clock64();
+  for (int i = 0; i < iters; ++i) {
+#pragma unroll
+    for (int d = 0; d < 8; ++d) {
+      const double dl = V == 0 ? x[d + 1] - x[d] : ds[d];
+      dd = __builtin_fma(-c2, fabs(dd), __builtin_fma(k1, dd, dl));
+      acc += x[d + 1] - dd;
+    }
+  }
+  const long long t1 = clock64();
+  out[threadIdx.x] = acc + dd;
+  if (threadIdx.x == 0) *cyc = t1 - t0;
+}
+
+__global__ void k_env2s(double* out, const double* in, int iters, double a, double r, long long* cyc) {
+#pragma clang fp contract(off)
+  double x[8];
+  for (int d = 0; d < 8; ++d) x[d] = fabs(in[d * 64 + threadIdx.x]);
+  // one sample: L_a(e) = (1-a) e + a s, L_r(e) = r e + (1-r) s; convex when 1-a <= r
+  const double sa = 1.0 - a, sr = r;
+  double B1[4], B2[4], B3[4];
+  for (int p = 0; p < 4; ++p) {
+    const double s1 = x[2 * p], s2 = x[2 * p + 1];
+    B1[p] = sa * (a * s1) + a * s2;                                  // La2 o La1
+    B2[p] = fmax(sa * ((1 - r) * s1) + a * s2, sr * (a * s1) + (1 - r) * s2);  // La2 o Lr1, Lr2 o La1 (same slope)
+    B3[p] = sr * ((1 - r) * s1) + (1 - r) * s2;                      // Lr2 o Lr1
+  }
+  const double A1 = sa * sa, A2 = sa * sr, A3 = sr * sr;
+  double env = 0.0, acc = 0.0;
+  const long long t0 = clock64();
+  for (int i = 0; i < iters; ++i) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const double e1 = fmax(__builtin_fma(sa, env, a * x[2 * p]), __builtin_fma(sr, env, (1 - r) * x[2 * p]));
+      env = fmax(fmax(__builtin_fma(A1, env, B1[p]), __builtin_fma(A2, env, B2[p])), __builtin_fma(A3, env, B3[p]));
+      acc += e1 + env;
+    }
+  }
+  const long long t1 = clock64();
+  out[threadIdx.x] = acc + env;
+  if (threadIdx.x == 0) *cyc = t1 - t0;
+}
+
 __device__ __forceinline__ double flush_int(double v) {
   // |v| < 1e-23 -> +0 (v itself otherwise), from the bit pattern: the
   // magnitude bits compare like the magnitudes (non-negative, non-NaN)
@@ -90,6 +148,12 @@ int main() {
   report("env/ref");
   for (int r = 0; r < 2; ++r) hipLaunchKernelGGL(k_env<1>, dim3(1), dim3(64), 0, 0, d, in, iters, 0.002, 0.9998, cy);
   report("env/abs");
+  for (int r = 0; r < 2; ++r) hipLaunchKernelGGL(k_envd<0>, dim3(1), dim3(64), 0, 0, d, in, iters, 0.002, 0.9998, cy);
+  report("env/d");
+  for (int r = 0; r < 2; ++r) hipLaunchKernelGGL(k_envd<1>, dim3(1), dim3(64), 0, 0, d, in, iters, 0.002, 0.9998, cy);
+  report("env/d-pre");
+  for (int r = 0; r < 2; ++r) hipLaunchKernelGGL(k_env2s, dim3(1), dim3(64), 0, 0, d, in, iters, 0.002, 0.9998, cy);
+  report("env/2s");
   for (int r = 0; r < 2; ++r) hipLaunchKernelGGL(k_comb<0>, dim3(1), dim3(64), 0, 0, d, in, iters, 0.45, 0.55, cy);
   report("comb/ref");
   for (int r = 0; r < 2; ++r) hipLaunchKernelGGL(k_comb<1>, dim3(1), dim3(64), 0, 0, d, in, iters, 0.45, 0.55, cy);
