@@ -131,6 +131,20 @@ __global__ void k_comb(double* out, const double* in, int iters, double d1, doub
   if (threadIdx.x == 0) *cyc = t1 - t0;
 }
 
+// the shader clock against the constant wall clock (s_memrealtime, 100 MHz) over one
+// wave's dependent FP64 chain: the engine clock a lightly loaded chip runs at
+__global__ void k_clock(double* out, int iters, long long* cyc) {
+  double v = out[threadIdx.x];
+  const long long c0 = clock64(), w0 = wall_clock64();
+  for (int i = 0; i < iters; ++i) v = __builtin_fma(v, 0.999999, 1e-9);
+  const long long c1 = clock64(), w1 = wall_clock64();
+  out[threadIdx.x] = v;
+  if (threadIdx.x == 0) {
+    cyc[0] = c1 - c0;
+    cyc[1] = w1 - w0;
+  }
+}
+
 int main() {
   double *d, *in;
   long long* cy;
@@ -154,6 +168,19 @@ int main() {
   report("env/d-pre");
   for (int r = 0; r < 2; ++r) hipLaunchKernelGGL(k_env2s, dim3(1), dim3(64), 0, 0, d, in, iters, 0.002, 0.9998, cy);
   report("env/2s");
+  {
+    long long* cy2;
+    if (hipMalloc(&cy2, 16)) return 1;
+    int wrate = 0;
+    (void)hipDeviceGetAttribute(&wrate, hipDeviceAttributeWallClockRate, 0);  // kHz
+    for (int grid : {1, 8, 256, 2048}) {
+      for (int r = 0; r < 2; ++r) hipLaunchKernelGGL(k_clock, dim3(grid), dim3(64), 0, 0, d, 2000000, cy2);
+      long long h2[2];
+      if (hipMemcpy(h2, cy2, 16, hipMemcpyDeviceToHost)) return 1;
+      printf("clock    %4d waves: %lld shader cycles in %lld wall ticks (%d kHz) = %.0f MHz\n", grid, h2[0], h2[1], wrate,
+             (double)h2[0] / ((double)h2[1] / (wrate * 1e3)) / 1e6);
+    }
+  }
   for (int r = 0; r < 2; ++r) hipLaunchKernelGGL(k_comb<0>, dim3(1), dim3(64), 0, 0, d, in, iters, 0.45, 0.55, cy);
   report("comb/ref");
   for (int r = 0; r < 2; ++r) hipLaunchKernelGGL(k_comb<1>, dim3(1), dim3(64), 0, 0, d, in, iters, 0.45, 0.55, cy);
