@@ -405,9 +405,6 @@ void fx_run_staged(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hip
         double* out = k == ns - 1 ? (verb ? ac.inT : ac.vT) : h->secT[k][c & 1].p;
         e.part[e.nparts++] = FxEqPart{k, 1, 0, ac.len, in, out, nullptr};
       }
-      // the first launch with every section busy: {compute, barrier wait} of
-      // each part's section wave and I/O wave
-      if (li == ns - 1) e.prof = fx_prof_begin(h, kFxProfWords, s);
       launch_fx_eq_sec(e, s);
       if (cd < 0) continue;
       const FxStageArgs b = chunk_args(cd);

@@ -358,10 +358,7 @@ __global__ __launch_bounds__(64 * (kMaxSecPerPass + 2)) void k_fx_eq(FxStageArgs
 #define AD_SEC_P 32
 #endif
 constexpr int kSecP = AD_SEC_P;   // samples per step
-#ifndef AD_SEC_PF
-#define AD_SEC_PF 2
-#endif
-constexpr int kSecPF = AD_SEC_PF;   // I/O wave: steps of input loads in flight
+constexpr int kSecPF = 2;   // I/O wave: steps of input loads in flight
 __global__ __launch_bounds__(128) void k_fx_eq_sec(FxStageArgs a) {
 #pragma clang fp contract(off)
   __shared__ __attribute__((aligned(16))) double xr[2][kSecP][64];
@@ -385,9 +382,7 @@ __global__ __launch_bounds__(128) void k_fx_eq_sec(FxStageArgs a) {
     double d0 = st[0], d1 = st[1];
     __builtin_amdgcn_s_waitcnt(0);
     lds_barrier();  // step 0's rows are in xr[0]
-    unsigned long long tc = 0, tb = 0;  // per-wave clocks (ad_fx_chain_set_profiling)
     for (int64_t k = 0; k <= nst; ++k) {
-      const unsigned long long t0c = a.prof ? clock64() : 0;
       if (k < nst) {
         const int nreal = (int)min((int64_t)kSecP, len - k * kSecP);
         double x[kSecP], y[kSecP];
@@ -407,16 +402,7 @@ __global__ __launch_bounds__(128) void k_fx_eq_sec(FxStageArgs a) {
 #pragma unroll
         for (int d = 0; d < kSecP; ++d) yr[k & 1][d][l] = y[d];
       }
-      const unsigned long long t1c = a.prof ? clock64() : 0;
       lds_barrier();
-      if (a.prof) {
-        tc += t1c - t0c;
-        tb += clock64() - t1c;
-      }
-    }
-    if (a.prof && l == 0 && blockIdx.x == 0) {
-      a.prof[4 * blockIdx.y] = tc;
-      a.prof[4 * blockIdx.y + 1] = tb;
     }
     if (c < a.channels) {
       st[0] = d0;
@@ -461,29 +447,18 @@ __global__ __launch_bounds__(128) void k_fx_eq_sec(FxStageArgs a) {
     fetch(buf[0], kSecPF);
     lds_barrier();
     // step k: rows of step k + 1 into xr, loads of step k + 1 + PF, outputs of step k - 1
-    unsigned long long tc = 0, tb = 0;
     for (int64_t k = 0; k <= nst; k += kSecPF) {
 #pragma unroll
       for (int u = 0; u < kSecPF; ++u) {
         const int64_t kk = k + u;
         if (kk <= nst) {
-          const unsigned long long t0c = a.prof ? clock64() : 0;
           const int b = (u + 1) % kSecPF;
           if (kk + 1 < nst) put(buf[b], kk + 1);
           fetch(buf[b], kk + 1 + kSecPF);
           if (kk >= 1) flush(kk - 1);
-          const unsigned long long t1c = a.prof ? clock64() : 0;
           lds_barrier();
-          if (a.prof) {
-            tc += t1c - t0c;
-            tb += clock64() - t1c;
-          }
         }
       }
-    }
-    if (a.prof && l == 0 && blockIdx.x == 0) {
-      a.prof[4 * blockIdx.y + 2] = tc;
-      a.prof[4 * blockIdx.y + 3] = tb;
     }
   }
 }
