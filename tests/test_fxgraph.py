@@ -308,3 +308,41 @@ def test_reverb_conv_node_vs_oracle(gpu, with_dry):
     y = x.copy()
     assert ch2.Process(y)
     np.testing.assert_array_equal(y, x)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("field,value", [("ratio", 100.5), ("attack_ms", 0.05), ("release_ms", 5001.0),
+                                         ("rms_window_ms", 0.5), ("makeup_db", float("nan")),
+                                         ("sidechain_low_cut_hz", 30000.0)])
+def test_graph_compressor_node_rejects_setter_ranges(gpu, field, value):
+    """A COMPRESSOR node whose config a reference setter would reject
+    (compressor.go:16-23, core.go:131-198, 542-564) fails ad_fx_graph_create
+    with AD_ERR_INVALID_ARGUMENT, as the node's Configure would fail; the same
+    graph with an in-range config builds."""
+    import ctypes as C
+
+    from algodsp import _lib
+
+    def build(cfg):
+        nodes = (E._Node * 3)()
+        par = [(C.c_int32 * 1)(0), (C.c_int32 * 1)(1)]
+        ports = [(C.c_int32 * 1)(0), (C.c_int32 * 1)(0)]
+        nodes[0].type = 0  # AD_FXN_INPUT
+        nodes[1].type = 5  # AD_FXN_COMPRESSOR
+        nodes[1].n_parents, nodes[1].parents, nodes[1].parent_ports = 1, par[0], ports[0]
+        nodes[1].comp = C.pointer(cfg)
+        nodes[2].type = 1  # AD_FXN_OUTPUT
+        nodes[2].n_parents, nodes[2].parents, nodes[2].parent_ports = 1, par[1], ports[1]
+        h = C.c_void_p()
+        rc = _lib.lib().ad_fx_graph_create(C.cast(nodes, C.c_void_p), 3, 4, 0, C.byref(h))
+        if rc == _lib.AD_OK:
+            _lib.lib().ad_fx_graph_destroy(h)
+        return rc
+
+    good = _lib.CompressorConfig()
+    _lib.lib().ad_compressor_default_config(C.byref(good), FS)
+    assert build(good) == _lib.AD_OK
+    bad = _lib.CompressorConfig()
+    _lib.lib().ad_compressor_default_config(C.byref(bad), FS)
+    setattr(bad, field, value)
+    assert build(bad) == _lib.AD_ERR_INVALID_ARGUMENT

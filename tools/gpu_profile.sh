@@ -9,7 +9,7 @@ OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 # the N = 1 workload alone (no shard_per_gpu / host_io sub-measurements in the
 # kernel statistics or the PMC averages)
-BARGS=${BENCH_ARGS:---steps 5 --warmup 2 --no-cpu-baseline --host-io off --shard-sub off --fx-leg off --stream-leg off}
+BARGS=${BENCH_ARGS:---steps 5 --warmup 2 --no-cpu-baseline --host-io off --shard-sub off --fx-leg off --stream-leg off --corr-leg off}
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o bench -- python3 bench.py $BARGS > $OUT/bench_trace.log 2>&1
 rc=$?; echo "trace rc=$rc"; tail -3 $OUT/bench_trace.log
 if [ $rc -ne 0 ]; then exit $rc; fi
