@@ -180,3 +180,27 @@ def test_compressor_validation_low_must_be_below_high():
 @pytest.mark.parametrize("field,value", GOOD_COMPRESSOR_EDGES)
 def test_compressor_validation_accepts_range_edges(field, value):
     assert _lib.lib().ad_compressor_validate(C.byref(_comp_cfg(**{field: value}))) == _lib.AD_OK
+
+
+def test_integration_snippets_name_real_abi():
+    """Every C.ad_* function and C.AD_* constant INTEGRATION.md's Go snippets
+    call exists in include/algodsp.h, and every Go snippet that registers with
+    the reference names the reference line it matches."""
+    import re
+
+    root = pathlib.Path(__file__).resolve().parents[1]
+    doc = (root / "INTEGRATION.md").read_text()
+    header = (root / "include" / "algodsp.h").read_text()
+    funcs = set(re.findall(r"\bC\.(ad_[a-z0-9_]+)\(", doc))
+    consts = set(re.findall(r"\bC\.(AD_[A-Z0-9_]+)\b", doc))
+    types = set(re.findall(r"\bC\.(ad_[a-z0-9_]+)\b", doc)) - funcs
+    assert funcs and consts
+    missing = [f for f in funcs if not re.search(r"\b" + f + r"\s*\(", header)]
+    missing += [c for c in consts if not re.search(r"#define\s+" + c + r"\b", header)]
+    missing += [t for t in types if not re.search(r"\b" + t + r"\b", header)]
+    assert not missing, missing
+    # the registrations carry the reference's own types and line numbers
+    for needle in ("registry.OpEntry{", "ProcessBlock: processBlock", "registry.go:17",
+                   "func(ctx effectchain.Context) (effectchain.Runtime, error)", "registry.go:24",
+                   "conv.RegisterBackend", "convolution.go:35"):
+        assert needle in doc, needle
