@@ -154,6 +154,7 @@ struct ad_fx_chain {
   // EQ-only chains, one K_eq part per section (fx_run_staged): section k's
   // output rows of chunk c in secT[k][c & 1], read by section k + 1 one launch later
   DevBuf<double> secT[kMaxSecPerPass][2];
+  DevBuf<double> lane_dump;  // K_lanes: the stores outside the signal (kFxEqLaneDump doubles)
   // time-parallel engine (fx_tp.hip): K_eq segment states
   DevBuf<double> tp_zs, tp_carry;
   // K_carry's segment maps per (seg, nseg): M = A^seg and M^Q per section and
@@ -265,6 +266,17 @@ int fx_eq_split(const ad_fx_chain* h) {
 // Msamples/s at 4096 ch 39.4 / 38.2, 8192 ch 44.9 / 60.7, 16384 ch 47.9 / 85.2)
 #define AD_FX_EQ_PER_SECTION_MAXCH 4096
 #endif
+// EQ-only chains without Freeverb run K_lanes (fx_eq_lanes.hip): the sections
+// across the lanes of a DPP row, one launch over the whole call, in place on
+// the user buffer (no transposes, no chunks).
+#ifndef AD_FX_EQ_LANES  // tools/ A/B builds
+#define AD_FX_EQ_LANES 1
+#endif
+bool fx_eq_lanes(const ad_fx_chain* h) {
+  return AD_FX_EQ_LANES && h->engine != AD_FX_ENGINE_STAGED_NOSPLIT && !h->comp_on && !h->verb_on && h->nsec >= 1 &&
+         h->nsec <= kMaxSecPerPass;
+}
+
 bool fx_eq_per_section(const ad_fx_chain* h) {
   return AD_FX_EQ_PER_SECTION && h->engine != AD_FX_ENGINE_STAGED_NOSPLIT && !h->comp_on && h->nsec >= 2 &&
          h->nsec <= kMaxSecPerPass && h->cpad <= AD_FX_EQ_PER_SECTION_MAXCH;
@@ -301,6 +313,29 @@ void fx_grow_tmax(ad_fx_chain* h, int64_t t) {
 
 void fx_run_staged(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hipStream_t s) {
   const bool eq = h->nsec > 0, comp = h->comp_on, verb = h->verb_on;
+  if (fx_eq_lanes(h)) {
+    if (!h->lane_dump.p) h->lane_dump.alloc(kFxEqLaneDump);
+    FxEqLaneArgs a{};
+    a.buf = d_buf;
+    a.stride = stride;
+    a.n = n;
+    a.channels = h->channels;
+    a.eq.nsec = h->nsec;
+    a.eq.sec = h->sec_dev.p;
+    a.eq.sec_ch_stride = h->eq_uniform ? 0 : (int64_t)h->nsec * kSecStride;
+    a.eq.state = h->eq_state.p;
+    a.dump = h->lane_dump.p;
+    // g1: every section after the first has pre-gain 1.0 in every table, so
+    // the kernel multiplies only the input by section 0's pre-gain
+    bool g1 = true;
+    const size_t sets = h->sec_host.size() / ((size_t)h->nsec * kSecStride);
+    for (size_t t = 0; t < sets && g1; ++t)
+      for (int k = 1; k < h->nsec; ++k)
+        if (h->sec_host[(t * h->nsec + k) * kSecStride] != 1.0) g1 = false;
+    launch_fx_eq_lanes(a, g1, s);
+    AD_HIP(hipGetLastError());
+    return;
+  }
   const int64_t T = std::min(h->chunk > 0 ? h->chunk : kFxChunk, n);
   if (!h->st[0]) {
     for (auto& x : h->st) AD_HIP(lib_stream_create(&x));
@@ -881,7 +916,8 @@ void fx_run(ad_fx_chain* h, double* d_buf, int64_t stride, int64_t n, hipStream_
       h->last_engine = AD_FX_ENGINE_TIME_PARALLEL;
     } else {
       fx_run_staged(h, d_buf, stride, n, s);
-      h->last_engine = (fx_eq_split(h) || fx_eq_per_section(h)) ? AD_FX_ENGINE_STAGED : AD_FX_ENGINE_STAGED_NOSPLIT;
+      h->last_engine =
+          (fx_eq_lanes(h) || fx_eq_split(h) || fx_eq_per_section(h)) ? AD_FX_ENGINE_STAGED : AD_FX_ENGINE_STAGED_NOSPLIT;
     }
     AD_HIP(hipEventRecord(h->ev_last, s));
     return;

@@ -133,6 +133,18 @@ void launch_fx_eq_parts(const FxStageArgs& a, hipStream_t s);  // a.part[0 .. np
 // one section per part (part.s0, ns = 1, no detector), a workgroup each (EQ-only pipeline)
 void launch_fx_eq_sec(const FxStageArgs& a, hipStream_t s);
 void launch_fx_gain(const FxStageArgs& a, bool to_user, hipStream_t s);
+// EQ-only chains with the cascade's sections across lanes (fx_eq_lanes.hip):
+// the user buffer [channels][stride] filtered in place, state eq.state
+// [channels][nsec][2]; g1: every section after the first has pre-gain 1.0
+struct FxEqLaneArgs {
+  double* buf;
+  int64_t stride, n;
+  int channels;
+  EqArgs eq;
+  double* dump;  // kFxEqLaneDump doubles of scratch (stores outside the signal)
+};
+constexpr int kFxEqLaneDump = 256;
+void launch_fx_eq_lanes(const FxEqLaneArgs& a, bool g1, hipStream_t s);
 void launch_fx_transpose_in(const FxStageArgs& a, double* dstT, hipStream_t s);   // user -> dstT
 void launch_fx_transpose_out(const FxStageArgs& a, const double* srcT, hipStream_t s);  // srcT -> user
 void launch_fx_comb(const FxStageArgs& a, hipStream_t s);

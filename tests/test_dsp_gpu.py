@@ -780,13 +780,12 @@ def test_eq_only_per_section_pipeline_bit_exact(gpu):
 
 
 def test_eq_only_many_channels_whole_chain_bit_exact(gpu):
-    """Above 4096 channels an EQ-only chain runs the one-workgroup-per-channel-
-    group kernel again (the per-section pipeline's hand-offs cost more than
-    they gain once the groups fill the chip; AD_FX_EQ_PER_SECTION_MAXCH):
-    still bit-exact against the oracle's biquad.Chain.ProcessBlock
-    (chain.go:59-70) at 4160 channels (a partial last group), device buffers,
-    over a chunk boundary, on the first and last channels of the groups at
-    both ends."""
+    """Many channels: an EQ-only chain at 4160 channels (a partial last group
+    of every engine's channel grouping) runs K_lanes, bit-exact against the
+    oracle's biquad.Chain.ProcessBlock (chain.go:59-70) on device buffers, on
+    the first and last channels of the groups at both ends; the
+    one-workgroup-per-channel-group staged kernel (ENGINE_STAGED_NOSPLIT)
+    gives the same bits."""
     import torch
 
     fs = 48000.0
@@ -801,11 +800,109 @@ def test_eq_only_many_channels_whole_chain_bit_exact(gpu):
     s.synchronize()
     y = dx.cpu().numpy()
     engine, _ = fx.LastEngine()
-    # not the per-section pipeline (ENGINE_STAGED); the staged one-workgroup form or the fused kernels
-    assert engine in (P.EffectChain.ENGINE_STAGED_NOSPLIT, P.EffectChain.ENGINE_FUSED), engine
+    assert engine == P.EffectChain.ENGINE_STAGED, engine
     for c in (0, 63, 4097, 4159):
         v = x[c].copy()
         for co, g in eq:
             v, _ = O.biquad_chain_block(np.ravel(co), np.zeros(2 * len(co)), g, v)
         assert np.array_equal(y[c], v), (c, float(np.max(np.abs(y[c] - v))))
     fx.close()
+    fx = P.EffectChain(C, eq, None, None, fs)
+    fx.SetEngine(P.EffectChain.ENGINE_STAGED_NOSPLIT)
+    dx = torch.from_numpy(x).cuda()
+    fx.process_device(dx.data_ptr(), n, n, s.cuda_stream)
+    s.synchronize()
+    assert np.array_equal(dx.cpu().numpy(), y)
+    fx.close()
+
+
+def _lane_oracle(tab, x):
+    """The fx chain's section table [nsec][6] {pre_gain, b0, b1, b2, a1, a2}
+    through the oracle: each section a one-section biquad.Chain with gain
+    pre_gain (chain.go:59-70), states from zero."""
+    v = x.copy()
+    for row in np.asarray(tab):
+        v, _ = O.biquad_chain_block(np.ravel(row[1:]), np.zeros(2), row[0], v)
+    return v
+
+
+@pytest.mark.parametrize("nsec,gains,per_channel", [(1, "one", False), (2, "first", False), (5, "first", False),
+                                                   (8, "first", True), (3, "every", False), (7, "every", True)])
+def test_eq_lanes_bit_exact(gpu, nsec, gains, per_channel):
+    """K_lanes (fx_eq_lanes.hip): an EQ-only chain with its sections across the
+    lanes of a DPP row, one launch over the call, in place on the caller's
+    buffer.  Bit-exact against the oracle's biquad chain (section.go:47-53,
+    chain.go:59-70) for 1 to 8 sections, a pre-gain on the first section only
+    (the kernel's pre-gained input) or on every section (its per-lane
+    multiply), one table or one per channel, 1 to 9 channels (partial rows of
+    a wave), calls of 1, 31, 32, 33 and 5000 samples (shorter than the
+    section skew, block edges, several blocks) that carry the state, and
+    the EQ state read back afterwards (Chain.State, chain.go:119-128)."""
+    import ctypes as Cc
+
+    from algodsp._lib import lib
+    from algodsp.processors import section_table
+
+    rng = np.random.default_rng(77 + nsec)
+    for C in (1, 4, 9):
+        tabs = []
+        for c in range(C if per_channel else 1):
+            secs = stable_sections(nsec, 1000 * nsec + c)
+            t = section_table(secs, 0.75 if gains != "one" else 1.0)
+            if gains == "every":
+                t[1:, 0] = rng.uniform(0.5, 1.5, nsec - 1)
+            tabs.append(t)
+        tab = np.ascontiguousarray(np.stack(tabs) if per_channel else tabs[0])
+        fx = P.EffectChain(C, (), None, None, 48000.0)
+        assert lib().ad_fx_chain_set_eq(fx._h, tab.ctypes.data_as(Cc.POINTER(Cc.c_double)), nsec,
+                                        1 if per_channel else 0) == 0
+        lens = [1, 31, 32, 33, 5000]
+        x = np.stack([0.5 * signals.white_noise(sum(lens), 5100 + c) for c in range(C)])
+        parts, lo = [], 0
+        for L in lens:
+            b = x[:, lo:lo + L].copy()
+            fx.Process(b)
+            parts.append(b)
+            lo += L
+        y = np.concatenate(parts, axis=1)
+        assert fx.LastEngine()[0] == P.EffectChain.ENGINE_STAGED
+        for c in range(C):
+            want = _lane_oracle(tab[c] if per_channel else tab, x[c])
+            assert np.array_equal(y[c], want), (C, c, float(np.max(np.abs(y[c] - want))))
+        fx.close()
+
+
+def test_eq_lanes_device_stride_matches_staged(gpu):
+    """K_lanes on a device buffer whose row stride exceeds the call (the
+    samples past n stay untouched), at 256 channels x 70000 samples over two
+    calls, gives the staged one-workgroup kernel's bits (ENGINE_STAGED_NOSPLIT)
+    and its EQ state."""
+    import ctypes as Cc
+
+    import torch
+
+    from algodsp._lib import lib
+
+    fs = 48000.0
+    eq = design.config5_eq(fs)
+    C, n, stride = 256, 70000, 70013
+    x = np.zeros((C, stride))
+    x[:, :n] = np.stack([0.5 * signals.white_noise(n, 7000 + c) for c in range(C)])
+    x[:, n:] = 9.0
+    outs, states = [], []
+    for eng in (P.EffectChain.ENGINE_AUTO, P.EffectChain.ENGINE_STAGED_NOSPLIT):
+        fx = P.EffectChain(C, eq, None, None, fs)
+        fx.SetEngine(eng)
+        dx = torch.from_numpy(x.copy()).cuda()
+        s = torch.cuda.current_stream()
+        fx.process_device(dx.data_ptr(), stride, 40000, s.cuda_stream)
+        fx.process_device(dx.data_ptr() + 40000 * 8, stride, n - 40000, s.cuda_stream)
+        s.synchronize()
+        outs.append(dx.cpu().numpy())
+        st = np.zeros((C, len(eq), 2))
+        assert lib().ad_fx_chain_eq_state(fx._h, st.ctypes.data_as(Cc.POINTER(Cc.c_double)), st.size) == 0
+        states.append(st)
+        fx.close()
+    assert np.array_equal(outs[0], outs[1])
+    assert np.all(outs[0][:, n:] == 9.0)
+    assert np.array_equal(np.asarray(states[0]), np.asarray(states[1]))
