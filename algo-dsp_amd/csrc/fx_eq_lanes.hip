@@ -37,9 +37,9 @@
 // has a VGPR destination, so nothing can read a register whose load is still
 // in flight, and the vector-memory counter is counted here (hipcc drains it
 // to 0 before the first LDS read behind a DMA).  Per block the issue order is
-//   [wait DMA(b)] [DMA(b+1+D)] [steps] [stores(b)]
-// and vmcnt retires in issue order.  Every block issues exactly four DMAs and
-// two stores per lane (samples past the signal re-read its last one; outputs
+//   [stores(b-1)] [DMA(b+1+D)] [wait DMA(b+1)]   (steps 8, 16, kLnB - 16)
+// and vmcnt retires in issue order.  Every block issues exactly kLnDma DMAs
+// and kLnSt stores per lane (samples past the signal re-read its last one; outputs
 // outside [0, n) and the rows of a partial last wave go to a per-lane dump
 // slot), so the counts are exact.  In place: a sample's DMA is issued blocks
 // before its output is stored.
@@ -82,63 +82,42 @@ __device__ __forceinline__ void dma4(const void* g, unsigned lds) {
                : "memory");
 }
 __device__ __forceinline__ void gstore(double* p, double v) {
+#if defined(AD_LN_EXP) && (AD_LN_EXP & 4)
+  asm volatile("global_store_dwordx2 %0, %1, off nt" ::"v"(p), "v"(v) : "memory");
+#else
   asm volatile("global_store_dwordx2 %0, %1, off" ::"v"(p), "v"(v) : "memory");
+#endif
 }
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-// One block of kLnB steps.  The step is software-pipelined by hand: the
-// next step's input (the DPP of this step's output) and its three input
-// products are formed while this step's output runs down its chain
-// yy -> q4 yy -> (q2 v - q4 yy) -> + d1 -> d0, so that in the wave's in-order
-// issue the loop-carried path is that chain alone (4 dependent operations)
-// and everything else fills its latency.  sched_barrier pins the order (the
-// scheduler's model interleaved the steps less well: 96 clocks per step).
-#define AD_LN_SB __builtin_amdgcn_sched_barrier(0)
-template <bool MASK, bool G1>
+#ifndef AD_LN_EXP  // tools/ probe builds only: 1 no output stores, 2 no DMAs or waits (wrong results);
+#define AD_LN_EXP 0  // 4 nt stores, 8 s_setprio 3 on the compute wave, 16 stores after the DMA wait,
+                     // 32 every store to the dump slot, 64 output LDS reads without stores, 128 stores without reads,
+                     // 256 the compute wave stores its outputs (no LDS hand-over)
+#endif
+constexpr int kLnPre = 16;             // input read-ahead of the compute wave (steps)
+constexpr int kLnIBar = kLnB - kLnPre;  // the step at which the compute wave meets the barrier
+
+// One block of kLnB steps of the cascade (the operations of eq_section_step
+// in its order; the compiler's schedule interleaves consecutive steps).
+// side(i) runs at the start of step i (the input read-ahead, the barrier).
+template <bool MASK, bool G1, class Side>
 __device__ __forceinline__ void lane_steps(const double (&q)[kSecStride], double g0, double& d0, double& d1, double& y,
-                                           const double* xb, double* yl, int lane, int64_t tk, int64_t n) {
+                                           double (&xv)[kLnB], double (&yb)[kLnB], int64_t tk, int64_t n,
+                                           const Side& side) {
 #pragma clang fp contract(off)
-  double xv[kLnB];
-#pragma unroll
-  for (int i = 0; i < kLnB; ++i) xv[i] = xb[(i >> 3) * (kLnRows * 8) + (i & 7)];  // the row's input (broadcast read)
-  // lane 0 takes x * pre_gain (section 0; G1), lanes k > 0 the output of lane k - 1 one step ago
-  auto input = [&](double yprev, int i) {
-    double v = row_shr1(yprev, G1 ? xv[i] * g0 : xv[i]);
-    if (!G1) v = v * q[0];  // G1: x * 1.0 == x on the other sections
-    return v;
-  };
-  double v = input(y, 0);
-  double t1 = q[1] * v, t2 = q[2] * v, t3 = q[3] * v;
-  AD_LN_SB;
 #pragma unroll
   for (int i = 0; i < kLnB; ++i) {
-    const double yy = t1 + d0;  // y = b0 x + d0
-    AD_LN_SB;
-    const double t4 = q[4] * yy;
-    AD_LN_SB;
-    double vn = 0.0;
-    if (i + 1 < kLnB) vn = input(yy, i + 1);
-    AD_LN_SB;
-    const double t5 = q[5] * yy;
-    AD_LN_SB;
-    const double e = t2 - t4;
-    AD_LN_SB;
-    double t1n = 0.0, t2n = 0.0, t3n = 0.0;
-    if (i + 1 < kLnB) {
-      t1n = q[1] * vn;
-      t2n = q[2] * vn;
-      t3n = q[3] * vn;
-    }
-    AD_LN_SB;
-    const double n0 = e + d1;  // d0 = b1 x - a1 y + d1
-    AD_LN_SB;
-    const double n1 = t3 - t5;  // d1 = b2 x - a2 y
-    AD_LN_SB;
-    y = yy;
-    yl[i * 64 + lane] = yy;
+    side(i);
+    // lane 0 takes x * pre_gain (section 0; G1), lanes k > 0 the output of lane k - 1 one step ago
+    double v = row_shr1(y, G1 ? xv[i] * g0 : xv[i]);
+    if (!G1) v = v * q[0];  // G1: x * 1.0 == x on the other sections
+    const double yy = q[1] * v + d0;
+    const double n0 = q[2] * v - q[4] * yy + d1;
+    const double n1 = q[3] * v - q[5] * yy;
     if (MASK) {  // lane k at step s0 + i filters sample s0 + i - k (tk = s0 - k)
       const int64_t t = tk + i;
       const bool ok = t >= 0 && t < n;
@@ -148,26 +127,101 @@ __device__ __forceinline__ void lane_steps(const double (&q)[kSecStride], double
       d0 = n0;
       d1 = n1;
     }
-    t1 = t1n;
-    t2 = t2n;
-    t3 = t3n;
-    AD_LN_SB;
+    y = yy;
+    yb[i] = yy;  // the block's outputs stay in registers (the last section's lane hands them over)
   }
 }
-#undef AD_LN_SB
 
+__device__ __forceinline__ void lds_fence_barrier() {
+  // the LDS writes before it are visible to the other wave after it (LDS
+  // operations of a wave complete in order: a count <= 15 covers every write
+  // issued 16 or more LDS operations earlier; callers pass 0 where fewer)
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// Two waves per workgroup (four channels):
+//   wave 0 (compute) runs the cascade: its only memory operations are LDS
+//     reads of the inputs (kLnPre steps ahead, from the slot the I/O wave
+//     filled) and, once per block, the last section's kLnB outputs written to
+//     yo by that lane; one barrier per block, at step kLnIBar, before the
+//     first read of the next block's slot;
+//   wave 1 (I/O) moves the samples: between barrier(b) and barrier(b+1) it
+//     stores block b-1's outputs from yo, issues the DMAs of block b+D+1 and
+//     waits for those of block b+2.
+// tools/eq_lanes_ab.sh: the compute wave's own global stores cost ~20 clocks
+// per step (1400 per 64-step block) and its DMAs ~10, more than the steps'
+// LDS traffic; a wave alone on its SIMD hides nothing behind a stall.
 template <bool G1>
-__global__ __launch_bounds__(64) void k_fx_eq_lanes(FxEqLaneArgs a) {
+__global__ __launch_bounds__(128) void k_fx_eq_lanes(FxEqLaneArgs a) {
 #pragma clang fp contract(off)
   __shared__ __attribute__((aligned(16))) double xl[kLnSlots][kLnB * kLnRows];  // [slot][dma][row][8]
-  __shared__ double yl[kLnB * 64];
-  const int lane = threadIdx.x, r = lane >> 4, k = lane & 15;
+  __shared__ __attribute__((aligned(16))) double yo[2][kLnRows][kLnB];          // [block & 1][row][step]
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63, r = lane >> 4, k = lane & 15;
   const int c = blockIdx.x * kLnRows + r;
   const bool live = c < a.channels;
   const int cc = live ? c : a.channels - 1;
   const int ns = a.eq.nsec;
-  const bool sec = k < ns;
   const int64_t n = a.n;
+  const int64_t S = n + ns - 1, nb = (S + kLnB - 1) / kLnB;
+  const int tail = ns - 1;  // the last section's lane lags the input by tail samples
+  double* row = a.buf + (int64_t)cc * a.stride;
+  (void)row;
+  static_assert(kLnD == 2, "the wait counts below assume two blocks of DMAs ahead");
+  static_assert(kLnD * kLnDma <= 63, "vmcnt holds 6 bits");
+  if (wave == 1) {
+    // ---- I/O wave
+    double* dump = a.dump + lane * kLnSt;
+    const unsigned xl0 = lds_addr(&xl[0][0]);
+    // block m's input into slot m % kLnSlots: DMA h carries samples 8h .. 8h+7,
+    // lane (r, k) dword k & 1 of sample 8h + k / 2
+    auto dma_block = [&](int64_t m) {
+      if (AD_LN_EXP & 2) return;
+      const unsigned base = xl0 + (unsigned)(m % kLnSlots) * kLnSlotB;
+#pragma unroll
+      for (int h = 0; h < kLnDma; ++h) {
+        const int64_t t = min(m * kLnB + 8 * h + (k >> 1), n - 1);
+        dma4(reinterpret_cast<const char*>(row + t) + 4 * (k & 1), base + h * (kLnRows * 64));
+      }
+    };
+    // block m's outputs (samples m kLnB - tail + 16 h + k of row r)
+    auto store_outputs = [&](int64_t m) {
+      if (AD_LN_EXP & (1 | 256)) return;
+      double v[kLnSt];
+#pragma unroll
+      for (int h = 0; h < kLnSt; ++h) v[h] = (AD_LN_EXP & 128) ? 0.0 : yo[m & 1][r][16 * h + k];
+      if (AD_LN_EXP & 64) {
+#pragma unroll
+        for (int h = 0; h < kLnSt; ++h) asm volatile("" ::"v"(v[h]));
+        return;
+      }
+#pragma unroll
+      for (int h = 0; h < kLnSt; ++h) {
+        const int64_t t = m * kLnB - tail + 16 * h + k;
+        gstore((!(AD_LN_EXP & 32) && m >= 0 && live && t >= 0 && t < n) ? row + t : dump + h, v[h]);
+      }
+    };
+#pragma unroll
+    for (int m = 0; m <= kLnD; ++m) dma_block(m);
+    if (!(AD_LN_EXP & 2)) wait_vm<kLnD * kLnDma>();  // DMA(0)
+    lds_fence_barrier();                               // the compute wave reads slot 0
+    if (!(AD_LN_EXP & 2)) wait_vm<(kLnD - 1) * kLnDma>();  // DMA(1)
+    lds_fence_barrier();                                   // barrier(0): slot 1
+    for (int64_t b = 0; b < nb; ++b) {
+      if (!(AD_LN_EXP & 16)) store_outputs(b - 1);
+      dma_block(b + kLnD + 1);
+      // DMA(b + 2) was issued in phase b - 1 (the prologue for b = 0): the
+      // phase's stores and DMAs since
+      if (!(AD_LN_EXP & 2)) wait_vm<(AD_LN_EXP & 256) ? kLnDma : kLnSt + kLnDma>();
+      if (AD_LN_EXP & 16) store_outputs(b - 1);
+      lds_fence_barrier();  // barrier(b + 1)
+    }
+    store_outputs(nb - 1);
+    wait_vm<0>();
+    return;
+  }
+  // ---- compute wave
+  const bool sec = k < ns;
   const double* secp = a.eq.sec + (int64_t)cc * a.eq.sec_ch_stride;
   double q[kSecStride];
 #pragma unroll
@@ -175,57 +229,48 @@ __global__ __launch_bounds__(64) void k_fx_eq_lanes(FxEqLaneArgs a) {
   const double g0 = G1 ? secp[0] : 1.0;
   double* st = a.eq.state + ((int64_t)cc * ns + (sec ? k : 0)) * 2;
   double d0 = sec ? st[0] : 0.0, d1 = sec ? st[1] : 0.0;
-  __builtin_amdgcn_s_waitcnt(0);  // coefficients and state before the counted operations
   double y = 0.0;
-  double* row = a.buf + (int64_t)cc * a.stride;
-  double* dump = a.dump + lane * kLnSt;
-  const int64_t S = n + ns - 1, nb = (S + kLnB - 1) / kLnB;
-  const unsigned xl0 = lds_addr(&xl[0][0]);
-  // block m's input into slot m % kLnSlots: DMA h carries samples 8h .. 8h+7,
-  // lane (r, k) dword k & 1 of sample 8h + k / 2
-  auto dma_block = [&](int64_t m) {
-    const unsigned base = xl0 + (unsigned)(m % kLnSlots) * kLnSlotB;
-#pragma unroll
-    for (int h = 0; h < kLnDma; ++h) {
-      const int64_t t = min(m * kLnB + 8 * h + (k >> 1), n - 1);
-      dma4(reinterpret_cast<const char*>(row + t) + 4 * (k & 1), base + h * (kLnRows * 64));
-    }
+  auto slot_x = [&](int64_t m, int i) {  // the row's input of step i of block m (broadcast read)
+    return xl[m % kLnSlots][(i >> 3) * (kLnRows * 8) + r * 8 + (i & 7)];
   };
+  if (AD_LN_EXP & 8) __builtin_amdgcn_s_setprio(3);
+  lds_fence_barrier();  // slot 0 has landed
+  double xv[kLnB], yb[kLnB];
 #pragma unroll
-  for (int m = 0; m <= kLnD; ++m) dma_block(m);
-  const int tail = ns - 1;  // the last section's lane lags the input by tail samples
+  for (int i = 0; i < kLnPre; ++i) xv[i] = slot_x(0, i);
   for (int64_t b = 0; b < nb; ++b) {
-    // DMA(b) was issued at block b - 1 - D, or in the prologue; the operations
-    // issued after it (kLnDma DMAs and kLnSt stores per block):
-    // prologue blocks b <= D: kLnDma (D - b) + b (kLnDma + kLnSt); later: kLnSt + D (kLnDma + kLnSt)
-    static_assert(kLnD == 2, "the wait counts below cover prologue blocks b = 0 .. 2");
-    static_assert(kLnSt + kLnD * (kLnDma + kLnSt) <= 63, "vmcnt holds 6 bits");
-    if (b > kLnD)
-      wait_vm<kLnSt + kLnD * (kLnDma + kLnSt)>();
-    else if (b == 0)
-      wait_vm<kLnDma * kLnD>();
-    else if (b == 1)
-      wait_vm<kLnDma * (kLnD - 1) + (kLnDma + kLnSt)>();
-    else
-      wait_vm<2 * (kLnDma + kLnSt)>();
-    dma_block(b + 1 + kLnD);
+    const auto side = [&](int i) {
+      if (i == kLnIBar) {
+        // barrier(b): block b + 1's slot has landed; the outputs of block b - 1
+        // (written a block ago, followed by more than 15 LDS reads) reach the I/O wave
+        asm volatile("s_waitcnt lgkmcnt(15)\n\ts_barrier" ::: "memory");
+      }
+      const int j = i + kLnPre;  // the ring slot of step j (this block) or j - kLnB (the next)
+      if (j < kLnB)
+        xv[j] = slot_x(b, j);
+      else
+        xv[j - kLnB] = slot_x(b + 1, j - kLnB);
+    };
     const int64_t s0 = b * kLnB;
-    const double* xb = &xl[b % kLnSlots][r * 8];
     const bool full = s0 >= tail && s0 + kLnB - 1 <= n - 1;
     if (full)
-      lane_steps<false, G1>(q, g0, d0, d1, y, xb, yl, lane, s0 - k, n);
+      lane_steps<false, G1>(q, g0, d0, d1, y, xv, yb, s0 - k, n, side);
     else
-      lane_steps<true, G1>(q, g0, d0, d1, y, xb, yl, lane, s0 - k, n);
-    // the last section's outputs of this block: samples s0 - tail + i
+      lane_steps<true, G1>(q, g0, d0, d1, y, xv, yb, s0 - k, n, side);
+    if (AD_LN_EXP & 256) {  // probe: the last section's lane stores its outputs itself
+      if (k == tail) {
 #pragma unroll
-    for (int h = 0; h < kLnSt; ++h) {
-      const int i = 16 * h + k;
-      const double v = yl[i * 64 + 16 * r + tail];
-      const int64_t t = s0 - tail + i;
-      gstore((live && t >= 0 && t < n) ? row + t : dump + h, v);
+        for (int i = 0; i < kLnB; ++i) {
+          const int64_t t = s0 - tail + i;
+          if (live && t >= 0 && t < n) gstore(row + t, yb[i]);
+        }
+      }
+    } else if (k == tail) {  // the last section's outputs of block b
+#pragma unroll
+      for (int i = 0; i < kLnB; i += 2) *reinterpret_cast<double2*>(&yo[b & 1][r][i]) = make_double2(yb[i], yb[i + 1]);
     }
   }
-  wait_vm<0>();
+  lds_fence_barrier();  // barrier(nb): the last block's outputs
   if (live && sec) {
     st[0] = d0;
     st[1] = d1;
@@ -238,9 +283,9 @@ void launch_fx_eq_lanes(const FxEqLaneArgs& a, bool g1, hipStream_t s) {
   if (a.n <= 0 || a.channels <= 0 || a.eq.nsec <= 0) return;
   const dim3 grid((unsigned)((a.channels + kLnRows - 1) / kLnRows));
   if (g1)
-    hipLaunchKernelGGL(k_fx_eq_lanes<true>, grid, dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_fx_eq_lanes<true>, grid, dim3(128), 0, s, a);
   else
-    hipLaunchKernelGGL(k_fx_eq_lanes<false>, grid, dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_fx_eq_lanes<false>, grid, dim3(128), 0, s, a);
 }
 
 }  // namespace adsp
