@@ -272,9 +272,15 @@ int fx_eq_split(const ad_fx_chain* h) {
 #ifndef AD_FX_EQ_LANES  // tools/ A/B builds
 #define AD_FX_EQ_LANES 1
 #endif
+#ifndef AD_FX_EQ_LANES_MAXCH
+// above this many channels the one-workgroup-per-channel-group kernel fills
+// the chip and wins (tools/eq_lanes_bench.py: 8192 ch 69.6 / 60.2, 16384 ch
+// 79.1 / 84.8 Gsamples/s, lanes / one workgroup per group)
+#define AD_FX_EQ_LANES_MAXCH 8192
+#endif
 bool fx_eq_lanes(const ad_fx_chain* h) {
   return AD_FX_EQ_LANES && h->engine != AD_FX_ENGINE_STAGED_NOSPLIT && !h->comp_on && !h->verb_on && h->nsec >= 1 &&
-         h->nsec <= kMaxSecPerPass;
+         h->nsec <= kMaxSecPerPass && h->channels <= AD_FX_EQ_LANES_MAXCH;
 }
 
 bool fx_eq_per_section(const ad_fx_chain* h) {

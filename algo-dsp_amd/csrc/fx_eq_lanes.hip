@@ -23,26 +23,22 @@
 //     of step s - 1, moved by one DPP row shift (row_shr:1), and lane 0 of the
 //     row, which has no source lane in the shift, keeps the DPP's old operand,
 //     the input sample (read from LDS, where it was staged a block ahead);
-//   - every lane writes its output to an LDS row per step; once per block of
-//     kLnB steps the row's 16 lanes store the last section's kLnB outputs
-//     (two 128-B runs).
+//   - the block's outputs stay in registers (kLnB per lane) and are handed
+//     to an I/O wave through LDS once per block.
 // So the step has no barrier and no hand-over beyond one DPP pair, and the
 // loop-carried path is the section's own four-operation chain.  A wave holds
 // four channels; lanes are cheap here (the EQ of 256 channels is 64 waves on
 // a 1024-SIMD chip), latency is not.
 //
-// Memory: each block's input samples (kLnB per channel) are moved into an
-// LDS slot by LDS-DMA (global_load_lds_dword: four 64-B runs per channel),
-// kLnD blocks ahead, and the outputs stored with inline-asm stores; neither
-// has a VGPR destination, so nothing can read a register whose load is still
-// in flight, and the vector-memory counter is counted here (hipcc drains it
-// to 0 before the first LDS read behind a DMA).  Per block the issue order is
-//   [stores(b-1)] [DMA(b+1+D)] [wait DMA(b+1)]   (steps 8, 16, kLnB - 16)
-// and vmcnt retires in issue order.  Every block issues exactly kLnDma DMAs
-// and kLnSt stores per lane (samples past the signal re-read its last one; outputs
-// outside [0, n) and the rows of a partial last wave go to a per-lane dump
-// slot), so the counts are exact.  In place: a sample's DMA is issued blocks
-// before its output is stored.
+// Memory (the I/O wave, see k_fx_eq_lanes): each block's input samples
+// (kLnB per channel) are moved into an LDS slot by LDS-DMA
+// (global_load_lds_dword: kLnDma 64-B runs per channel), two blocks ahead;
+// the outputs are stored with inline-asm stores.  Neither has a VGPR
+// destination, and the wave drains its vector-memory counter once per block
+// (hipcc would drain it to 0 before the first LDS read behind a DMA anyway).
+// Samples past the signal re-read its last one; outputs outside [0, n) and
+// the rows of a partial last wave go to a per-lane dump slot.  In place: a
+// sample's DMA is issued blocks before its output is stored.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -82,23 +78,20 @@ __device__ __forceinline__ void dma4(const void* g, unsigned lds) {
                : "memory");
 }
 __device__ __forceinline__ void gstore(double* p, double v) {
-#if defined(AD_LN_EXP) && (AD_LN_EXP & 4)
-  asm volatile("global_store_dwordx2 %0, %1, off nt" ::"v"(p), "v"(v) : "memory");
-#else
   asm volatile("global_store_dwordx2 %0, %1, off" ::"v"(p), "v"(v) : "memory");
-#endif
 }
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-#ifndef AD_LN_EXP  // tools/ probe builds only: 1 no output stores, 2 no DMAs or waits (wrong results);
-#define AD_LN_EXP 0  // 4 nt stores, 8 s_setprio 3 on the compute wave, 16 stores after the DMA wait,
-                     // 32 every store to the dump slot, 64 output LDS reads without stores, 128 stores without reads,
-                     // 256 the compute wave stores its outputs (no LDS hand-over)
+#ifndef AD_LN_EXP  // tools/ probe builds only: 1 no output stores, 2 no DMAs (wrong results);
+#define AD_LN_EXP 0  // 16384 output writes by every lane (no exec mask)
 #endif
 constexpr int kLnPre = 16;             // input read-ahead of the compute wave (steps)
+// yo row stride: rows r and r + 1 (one half-wave of a 64-bit read) on disjoint banks
+constexpr int kLnYoS = kLnB + 16;
+constexpr int kLnYoN = 2;  // output buffers (block parity)
 constexpr int kLnIBar = kLnB - kLnPre;  // the step at which the compute wave meets the barrier
 
 // One block of kLnB steps of the cascade (the operations of eq_section_step
@@ -142,20 +135,24 @@ __device__ __forceinline__ void lds_fence_barrier() {
 // Two waves per workgroup (four channels):
 //   wave 0 (compute) runs the cascade: its only memory operations are LDS
 //     reads of the inputs (kLnPre steps ahead, from the slot the I/O wave
-//     filled) and, once per block, the last section's kLnB outputs written to
-//     yo by that lane; one barrier per block, at step kLnIBar, before the
-//     first read of the next block's slot;
+//     filled) and, once per block, the block's outputs written to LDS (the
+//     last section's lane into yo); one barrier per block, at step kLnIBar,
+//     before the first read of the next block's slot;
 //   wave 1 (I/O) moves the samples: between barrier(b) and barrier(b+1) it
-//     stores block b-1's outputs from yo, issues the DMAs of block b+D+1 and
-//     waits for those of block b+2.
-// tools/eq_lanes_ab.sh: the compute wave's own global stores cost ~20 clocks
-// per step (1400 per 64-step block) and its DMAs ~10, more than the steps'
-// LDS traffic; a wave alone on its SIMD hides nothing behind a stall.
+//     waits for its previous phase's operations (DMA(b+2) among them), stores
+//     block b-1's outputs from yo and issues the DMAs of block b+D+1.
+// Measured (tools/eq_lanes_ab.sh, tools/lane_probe.hip, 256 ch x 2^20): the
+// compute wave's own global stores cost ~100 clocks each (a one-wave form:
+// 184 clocks per step with them, 62 without), its DMAs ~10 clocks per step,
+// and the 32 output writes per block ~13 (76 clocks per step against 63 with
+// no hand-over; writes by every lane without an exec mask: 79).  A wave
+// alone on its SIMD hides nothing behind a stall.
 template <bool G1>
 __global__ __launch_bounds__(128) void k_fx_eq_lanes(FxEqLaneArgs a) {
 #pragma clang fp contract(off)
   __shared__ __attribute__((aligned(16))) double xl[kLnSlots][kLnB * kLnRows];  // [slot][dma][row][8]
-  __shared__ __attribute__((aligned(16))) double yo[2][kLnRows][kLnB];          // [block & 1][row][step]
+  __shared__ __attribute__((aligned(16))) double yo[kLnYoN][kLnRows][kLnYoS];    // [block % kLnYoN][row][step]
+  __shared__ __attribute__((aligned(16))) double junk[2 * 64 + kLnB];            // the other lanes' output writes
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63, r = lane >> 4, k = lane & 15;
   const int c = blockIdx.x * kLnRows + r;
@@ -166,9 +163,7 @@ __global__ __launch_bounds__(128) void k_fx_eq_lanes(FxEqLaneArgs a) {
   const int64_t S = n + ns - 1, nb = (S + kLnB - 1) / kLnB;
   const int tail = ns - 1;  // the last section's lane lags the input by tail samples
   double* row = a.buf + (int64_t)cc * a.stride;
-  (void)row;
   static_assert(kLnD == 2, "the wait counts below assume two blocks of DMAs ahead");
-  static_assert(kLnD * kLnDma <= 63, "vmcnt holds 6 bits");
   if (wave == 1) {
     // ---- I/O wave
     double* dump = a.dump + lane * kLnSt;
@@ -186,36 +181,28 @@ __global__ __launch_bounds__(128) void k_fx_eq_lanes(FxEqLaneArgs a) {
     };
     // block m's outputs (samples m kLnB - tail + 16 h + k of row r)
     auto store_outputs = [&](int64_t m) {
-      if (AD_LN_EXP & (1 | 256)) return;
+      if (AD_LN_EXP & 1) return;
       double v[kLnSt];
 #pragma unroll
-      for (int h = 0; h < kLnSt; ++h) v[h] = (AD_LN_EXP & 128) ? 0.0 : yo[m & 1][r][16 * h + k];
-      if (AD_LN_EXP & 64) {
-#pragma unroll
-        for (int h = 0; h < kLnSt; ++h) asm volatile("" ::"v"(v[h]));
-        return;
-      }
+      for (int h = 0; h < kLnSt; ++h) v[h] = yo[m % kLnYoN][r][16 * h + k];
 #pragma unroll
       for (int h = 0; h < kLnSt; ++h) {
         const int64_t t = m * kLnB - tail + 16 * h + k;
-        gstore((!(AD_LN_EXP & 32) && m >= 0 && live && t >= 0 && t < n) ? row + t : dump + h, v[h]);
+        gstore((m >= 0 && live && t >= 0 && t < n) ? row + t : dump + h, v[h]);
       }
     };
 #pragma unroll
     for (int m = 0; m <= kLnD; ++m) dma_block(m);
-    if (!(AD_LN_EXP & 2)) wait_vm<kLnD * kLnDma>();  // DMA(0)
-    lds_fence_barrier();                               // the compute wave reads slot 0
-    if (!(AD_LN_EXP & 2)) wait_vm<(kLnD - 1) * kLnDma>();  // DMA(1)
-    lds_fence_barrier();                                   // barrier(0): slot 1
+    wait_vm<0>();         // DMA(0 .. D)
+    lds_fence_barrier();  // the compute wave reads slot 0
+    lds_fence_barrier();  // barrier(0): slot 1
     for (int64_t b = 0; b < nb; ++b) {
-      if (!(AD_LN_EXP & 16)) store_outputs(b - 1);
+      wait_vm<0>();  // the previous phase's stores and DMA(b + 2), read after barrier(b + 1)
+      store_outputs(b - 1);
       dma_block(b + kLnD + 1);
-      // DMA(b + 2) was issued in phase b - 1 (the prologue for b = 0): the
-      // phase's stores and DMAs since
-      if (!(AD_LN_EXP & 2)) wait_vm<(AD_LN_EXP & 256) ? kLnDma : kLnSt + kLnDma>();
-      if (AD_LN_EXP & 16) store_outputs(b - 1);
       lds_fence_barrier();  // barrier(b + 1)
     }
+    wait_vm<0>();
     store_outputs(nb - 1);
     wait_vm<0>();
     return;
@@ -233,7 +220,6 @@ __global__ __launch_bounds__(128) void k_fx_eq_lanes(FxEqLaneArgs a) {
   auto slot_x = [&](int64_t m, int i) {  // the row's input of step i of block m (broadcast read)
     return xl[m % kLnSlots][(i >> 3) * (kLnRows * 8) + r * 8 + (i & 7)];
   };
-  if (AD_LN_EXP & 8) __builtin_amdgcn_s_setprio(3);
   lds_fence_barrier();  // slot 0 has landed
   double xv[kLnB], yb[kLnB];
 #pragma unroll
@@ -245,11 +231,21 @@ __global__ __launch_bounds__(128) void k_fx_eq_lanes(FxEqLaneArgs a) {
         // (written a block ago, followed by more than 15 LDS reads) reach the I/O wave
         asm volatile("s_waitcnt lgkmcnt(15)\n\ts_barrier" ::: "memory");
       }
-      const int j = i + kLnPre;  // the ring slot of step j (this block) or j - kLnB (the next)
-      if (j < kLnB)
-        xv[j] = slot_x(b, j);
-      else
-        xv[j - kLnB] = slot_x(b + 1, j - kLnB);
+      // every 8 steps, the inputs of the 8 steps kLnPre ahead (one 64-B run per
+      // row) in one group the scheduler may not move: it otherwise sinks the
+      // reads next to their use, where the LDS latency shows
+      if (i % 8 == 0) {
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int j = i + kLnPre + e;  // the ring slot of step j (this block) or j - kLnB (the next)
+          if (j < kLnB)
+            xv[j] = slot_x(b, j);
+          else
+            xv[j - kLnB] = slot_x(b + 1, j - kLnB);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
     };
     const int64_t s0 = b * kLnB;
     const bool full = s0 >= tail && s0 + kLnB - 1 <= n - 1;
@@ -257,17 +253,18 @@ __global__ __launch_bounds__(128) void k_fx_eq_lanes(FxEqLaneArgs a) {
       lane_steps<false, G1>(q, g0, d0, d1, y, xv, yb, s0 - k, n, side);
     else
       lane_steps<true, G1>(q, g0, d0, d1, y, xv, yb, s0 - k, n, side);
-    if (AD_LN_EXP & 256) {  // probe: the last section's lane stores its outputs itself
-      if (k == tail) {
+    if (AD_LN_EXP & 16384) {
+      // probe: every lane writes its outputs (no exec mask), the last section's
+      // lane into yo, the others each into a junk run of their own (distinct
+      // addresses within every instruction): 79 against 76 clocks per step
+      double2* wp = k == tail ? reinterpret_cast<double2*>(&yo[b % kLnYoN][r][0])
+                              : reinterpret_cast<double2*>(&junk[2 * lane]);
 #pragma unroll
-        for (int i = 0; i < kLnB; ++i) {
-          const int64_t t = s0 - tail + i;
-          if (live && t >= 0 && t < n) gstore(row + t, yb[i]);
-        }
-      }
+      for (int i = 0; i < kLnB; i += 2) wp[i / 2] = make_double2(yb[i], yb[i + 1]);
     } else if (k == tail) {  // the last section's outputs of block b
 #pragma unroll
-      for (int i = 0; i < kLnB; i += 2) *reinterpret_cast<double2*>(&yo[b & 1][r][i]) = make_double2(yb[i], yb[i + 1]);
+      for (int i = 0; i < kLnB; i += 2)
+        *reinterpret_cast<double2*>(&yo[b % kLnYoN][r][i]) = make_double2(yb[i], yb[i + 1]);
     }
   }
   lds_fence_barrier();  // barrier(nb): the last block's outputs

@@ -20,7 +20,7 @@ from algodsp import design, processors, signals
 fs = 48000.0
 eq = design.config5_eq(fs)
 P = processors.EffectChain
-for C_, n in [(256, 1 << 20), (1024, 1 << 18), (4096, 1 << 16), (16384, 1 << 15)]:
+for C_, n in [(256, 1 << 20), (1024, 1 << 18), (4096, 1 << 16), (8192, 1 << 15), (16384, 1 << 15)]:
     x0 = torch.from_numpy(0.5 * signals.white_noise(C_ * n, 3).reshape(C_, n)).cuda()
     res = {}
     outs = {}

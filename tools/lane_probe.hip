@@ -67,7 +67,28 @@ __global__ __launch_bounds__(64) void probe(double* out, const double* coef, int
       if constexpr (V == 2 || V == 4) return yp * 0.5 + xv[i];
       else return row_shr1(yp, xv[i] * g0);
     };
-    if constexpr (V == 3 || (V >= 6 && V <= 11)) {
+    if constexpr (V >= 12) {
+      double yb[B];
+#pragma unroll
+      for (int i = 0; i < B; ++i) {
+        const double v = input(y, i);
+        const double yy = q[1] * v + d0;
+        const double n0 = q[2] * v - q[4] * yy + d1;
+        const double n1 = q[3] * v - q[5] * yy;
+        d0 = n0;
+        d1 = n1;
+        y = yy;
+        yb[i] = yy;
+      }
+      constexpr int NW = V == 12 ? 0 : V == 13 ? 8 : V == 14 ? 16 : 32;
+      if constexpr (V == 16) {
+#pragma unroll
+        for (int i = 0; i < 32; ++i) *reinterpret_cast<double2*>(&yl[(2 * i) * 64 + 2 * lane]) = make_double2(yb[2 * i], yb[2 * i + 1]);
+      } else if ((lane & 15) == 4) {
+#pragma unroll
+        for (int i = 0; i < NW; ++i) *reinterpret_cast<double2*>(&yl[r * 80 + 2 * i]) = make_double2(yb[2 * i], yb[2 * i + 1]);
+      }
+    } else if constexpr (V == 3 || (V >= 6 && V <= 11)) {
 #pragma unroll
       for (int i = 0; i < B; ++i) {
         const double v = input(y, i);
@@ -189,18 +210,13 @@ void run(const char* name, int blocks) {
 
 int main() {
   for (int blocks : {64}) {
-    run<0>("full (pipelined, dpp, LDS write)", blocks);
-    run<1>("no LDS write", blocks);
-    run<2>("no dpp", blocks);
-    run<3>("unpipelined order", blocks);
     run<4>("chain only", blocks);
-    run<5>("pipelined, no sched barriers", blocks);
-    run<6>("unpipelined + per-block DMAs", blocks);
-    run<7>("unpipelined + per-block stores", blocks);
-    run<8>("unpipelined + DMAs + stores", blocks);
-    run<9>("unpipelined + stores (reads first)", blocks);
-    run<10>("unpipelined + DMAs, no vmcnt wait", blocks);
     run<3>("unpipelined order", blocks);
+    run<12>("V3, outputs in registers, no writes", blocks);
+    run<13>("  + 8 masked b128 writes per block", blocks);
+    run<14>("  + 16 masked b128 writes per block", blocks);
+    run<15>("  + 32 masked b128 writes per block", blocks);
+    run<16>("  + 32 unmasked b128 writes per block", blocks);
   }
   return 0;
 }
