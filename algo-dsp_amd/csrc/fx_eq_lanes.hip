@@ -145,7 +145,8 @@ __device__ __forceinline__ void lds_fence_barrier() {
 // compute wave's own global stores cost ~100 clocks each (a one-wave form:
 // 184 clocks per step with them, 62 without), its DMAs ~10 clocks per step,
 // and the 32 output writes per block ~13 (76 clocks per step against 63 with
-// no hand-over; writes by every lane without an exec mask: 79).  A wave
+// no hand-over; writes by every lane without an exec mask: 79; four bursts of
+// 8 inside the block: 80).  A wave
 // alone on its SIMD hides nothing behind a stall.
 template <bool G1>
 __global__ __launch_bounds__(128) void k_fx_eq_lanes(FxEqLaneArgs a) {
