@@ -86,7 +86,8 @@ __device__ __forceinline__ void wait_vm() {
 }
 
 #ifndef AD_LN_EXP  // tools/ probe builds only: 1 no output stores, 2 no DMAs (wrong results);
-#define AD_LN_EXP 0  // 16384 output writes by every lane (no exec mask)
+#define AD_LN_EXP 0  // 16384 output writes by every lane (no exec mask), 4096 no output writes,
+                     // 8192 16-B output writes
 #endif
 constexpr int kLnPre = 16;             // input read-ahead of the compute wave (steps)
 // yo row stride: rows r and r + 1 (one half-wave of a 64-bit read) on disjoint banks
@@ -144,8 +145,8 @@ __device__ __forceinline__ void lds_fence_barrier() {
 // Measured (tools/eq_lanes_ab.sh, tools/lane_probe.hip, 256 ch x 2^20): the
 // compute wave's own global stores cost ~100 clocks each (a one-wave form:
 // 184 clocks per step with them, 62 without), its DMAs ~10 clocks per step,
-// and the 32 output writes per block ~13 (76 clocks per step against 63 with
-// no hand-over; writes by every lane without an exec mask: 79; four bursts of
+// and the output writes per block ~11 (74 clocks per step against 63 with
+// no hand-over; 16-B writes 76; writes by every lane without an exec mask: 79; four bursts of
 // 8 inside the block: 80).  A wave
 // alone on its SIMD hides nothing behind a stall.
 template <bool G1>
@@ -262,10 +263,21 @@ __global__ __launch_bounds__(128) void k_fx_eq_lanes(FxEqLaneArgs a) {
                               : reinterpret_cast<double2*>(&junk[2 * lane]);
 #pragma unroll
       for (int i = 0; i < kLnB; i += 2) wp[i / 2] = make_double2(yb[i], yb[i + 1]);
-    } else if (k == tail) {  // the last section's outputs of block b
+    } else if (k == tail && (AD_LN_EXP & 8192)) {  // probe: the first build's 16-B writes (ds_write_b128)
 #pragma unroll
       for (int i = 0; i < kLnB; i += 2)
         *reinterpret_cast<double2*>(&yo[b % kLnYoN][r][i]) = make_double2(yb[i], yb[i + 1]);
+    } else if (k == tail && !(AD_LN_EXP & 4096)) {
+      // the last section's outputs of block b, one 8-B write each: the sched
+      // barriers keep them apart (merged into 16-B writes they measured 75.8
+      // against 74.1 clocks per step; an exec-masked ds_write_b128 occupies the
+      // LDS issue ~5x as long as a read, SQ_ACTIVE_INST_LDS)
+      double* yw = &yo[b % kLnYoN][r][0];
+#pragma unroll
+      for (int i = 0; i < kLnB; ++i) {
+        yw[i] = yb[i];
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
   }
   lds_fence_barrier();  // barrier(nb): the last block's outputs
