@@ -546,14 +546,14 @@ __global__ __launch_bounds__((PassShape<R>::BLOCK)) void k_fft_pass(FftPassArgs 
   const int64_t j = j0 + f;
   double2 v[V];
 #pragma unroll
-  for (int s = 0; s < V; ++s) v[s] = lds[lds_slot(pass0_index<R, V>(tid, s))];
+  for (int s = 0; s < V; ++s) v[s] = lds[pass0_slot<R, V>(tid, s)];
   if (a.Ns > 1)  // pre-twiddle W_{Ns R}^{(j mod Ns) r} = W_N^{(j mod Ns) r N/(Ns R)}
     pass_pretwiddle<R, V, FWD>(v, j, a.Ns, a.N, tid, a.tw_lo, a.tw_hi, a.S);
   __syncthreads();
   fft_run<R, V, FWD>(v, tid, lds, twr);
   __syncthreads();
 #pragma unroll
-  for (int s = 0; s < V; ++s) lds[lds_slot(last_pass_index<R, V>(tid, s))] = v[s];
+  for (int s = 0; s < V; ++s) lds[last_pass_slot<R, V>(tid, s)] = v[s];
   __syncthreads();
 
   // stage out: output rr of butterfly j goes to (j/Ns) Ns R + (j mod Ns) + rr Ns
@@ -788,13 +788,13 @@ __global__ __launch_bounds__((PfShape<R>::BLOCK)) __attribute__((amdgpu_waves_pe
     pass_lds_barrier();
     double2 v[V];
 #pragma unroll
-    for (int s = 0; s < V; ++s) v[s] = lds[lds_slot(pass0_index<R, V>(tid, s))];
+    for (int s = 0; s < V; ++s) v[s] = lds[pass0_slot<R, V>(tid, s)];
     if (Ns > 1) pretwiddle_apply<R, V>(v, twb, twc);
     pass_lds_barrier();
     fft_run_lb<R, V, FWD>(v, tid, lds, twr);
     pass_lds_barrier();
 #pragma unroll
-    for (int s = 0; s < V; ++s) lds[lds_slot(last_pass_index<R, V>(tid, s))] = v[s];
+    for (int s = 0; s < V; ++s) lds[last_pass_slot<R, V>(tid, s)] = v[s];
     pass_lds_barrier();
     // output rr of butterfly j0 + jj goes to (jo & ~(Ns-1)) R + (jo & (Ns-1)) + rr Ns:
     // Ns = 1: contiguous (o = j0 R + idx); Ns >= F: the tile sits in one Ns group, so
@@ -922,12 +922,12 @@ __global__ __launch_bounds__((FT * FftPlan<R, 8>::T)) void k_corr_split0(FftPass
   double2* lds = lds_all + f * MP;
   double2 v[V];
 #pragma unroll
-  for (int s = 0; s < V; ++s) v[s] = lds[lds_slot(pass0_index<R, V>(tid, s))];
+  for (int s = 0; s < V; ++s) v[s] = lds[pass0_slot<R, V>(tid, s)];
   __syncthreads();
   fft_run<R, V, true>(v, tid, lds, twr);
   __syncthreads();
 #pragma unroll
-  for (int s = 0; s < V; ++s) lds[lds_slot(last_pass_index<R, V>(tid, s))] = v[s];
+  for (int s = 0; s < V; ++s) lds[last_pass_slot<R, V>(tid, s)] = v[s];
   __syncthreads();
   // stage out (Ns = 1): slot k of column j0 + jj at (j0 + jj) R + k, contiguous
   auto split = [&](int fi, int k, int second) {  // DFT of FFT fi's re (second = 0) or im input at bin k
@@ -1058,11 +1058,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 512 ? 
   }
 #endif
   // 1. stage the forward butterflies' inputs: element r of slot b is in[fbut(b) + r nbF]
+  static_assert(NT % NBF == 0, "staging: b = tid mod NBF for every i");
+  const int sb1 = lds_slot((int)threadIdx.x / NBF);  // r = i NT / NBF + tid / NBF: disjoint bits
 #pragma unroll
   for (int i = 0; i < V; ++i) {
     const int idx = i * NT + (int)threadIdx.x;
     const int b = idx % NBF, r = idx / NBF;
-    lds_all[b * MP + lds_slot(r)] = a.in[fbut(b) + (int64_t)r * nbF];
+    lds_all[b * MP + lds_slot_split(sb1, i * (NT / NBF))] = a.in[fbut(b) + (int64_t)r * nbF];
   }
   __syncthreads();
   // 2. the forward last pass (k_fft_pass<R, true, ...> with Ns = nbF)
@@ -1070,7 +1072,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 512 ? 
   double2* lds = lds_all + fs * MP;
   double2 v[V];
 #pragma unroll
-  for (int s = 0; s < V; ++s) v[s] = lds[lds_slot(pass0_index<R, V>(tid, s))];
+  for (int s = 0; s < V; ++s) v[s] = lds[pass0_slot<R, V>(tid, s)];
 #if AD_CORR_TW_EARLY
   pretwiddle_apply<R, V>(v, c_mul(tl1, th1), c_mul(tl2, th2));
 #else
@@ -1080,7 +1082,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 512 ? 
   fft_run<R, V, true>(v, tid, lds, twr);
   __syncthreads();
 #pragma unroll
-  for (int s = 0; s < V; ++s) lds[lds_slot(last_pass_index<R, V>(tid, s))] = v[s];  // Z[fbut(fs) + nbF k]
+  for (int s = 0; s < V; ++s) lds[last_pass_slot<R, V>(tid, s)] = v[s];  // Z[fbut(fs) + nbF k]
   __syncthreads();
   // 3. z for the inverse pairs (k_fft_pass's PAIR form): element (jj, r) of
   //    tile A and (jj, R-1-r) of tile B; Z of slot b, output k:
@@ -1107,9 +1109,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 512 ? 
       vB[i] = half_in0(nbH / 2 + (int64_t)(R - 1 - r) * nbH);
     } else {
       const int odd = r & 1, k1 = r >> 1, k3 = (R - 1 - r) >> 1;
-      const double2 z1 = zs(odd * FP + jj, k1), z2 = zs(odd * FP + jj, k1 + R / 2);          // Z[g], Z[g + NH]
+      // k1, k3 < R / 2: the slots of k + R / 2 are one XOR away (lds_slot_split)
+      const int s1 = lds_slot(k1), s3 = lds_slot(k3);
+      const double2* z13 = lds_all + (odd * FP + jj) * MP;
+      const double2* z34 = lds_all + ((2 + odd) * FP + jj) * MP;
+      const double2 z1 = z13[s1], z2 = z13[lds_slot_split(s1, R / 2)];  // Z[g], Z[g + NH]
       // gs = (nbH - j) + (R-1-r) nbH: forward butterfly nbF - j (r even, set 2) or nbH - j (r odd, set 3)
-      const double2 z3 = zs((2 + odd) * FP + jj, k3), z4 = zs((2 + odd) * FP + jj, k3 + R / 2);  // Z[-(g + NH)], Z[-g]
+      const double2 z3 = z34[s3], z4 = z34[lds_slot_split(s3, R / 2)];  // Z[-(g + NH)], Z[-g]
 #if AD_CORR_TW_EARLY
       const double2 w = c_conj(c_mul(zl[i], zh[i]));  // W_N^-g, g = j + r nbH
 #else
@@ -1125,8 +1131,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 512 ? 
   for (int i = 0; i < NPAIR; ++i) {
     const int idx = i * NT + (int)threadIdx.x;
     const int jj = idx % FP, r = idx / FP;
-    lds_all[jj * MP + lds_slot(r)] = vA[i];
-    lds_all[(FP + jj) * MP + lds_slot(R - 1 - r)] = vB[i];
+    const int sr = lds_slot(r);  // R - 1 - r == r ^ (R - 1): one XOR away
+    lds_all[jj * MP + sr] = vA[i];
+    lds_all[(FP + jj) * MP + lds_slot_split(sr, R - 1)] = vB[i];
   }
   __syncthreads();
   // 4. the inverse first pass (Ns = 1: no pre-twiddle) on slots 0 .. 2 FP - 1:
@@ -1144,14 +1151,14 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 512 ? 
   double2 u[VI];
   if (act) {
 #pragma unroll
-    for (int s = 0; s < VI; ++s) u[s] = ldsi[lds_slot(pass0_index<R, VI>(ti, s))];
+    for (int s = 0; s < VI; ++s) u[s] = ldsi[pass0_slot<R, VI>(ti, s)];
   }
   __syncthreads();
   fft_run_active<R, VI, false>(u, ti, ldsi, twr, act);
   __syncthreads();
   if (act) {
 #pragma unroll
-    for (int s = 0; s < VI; ++s) ldsi[lds_slot(last_pass_index<R, VI>(ti, s))] = u[s];
+    for (int s = 0; s < VI; ++s) ldsi[last_pass_slot<R, VI>(ti, s)] = u[s];
   }
   __syncthreads();
   // 5. outputs: inverse butterfly jo's R values at jo R .. jo R + R - 1
@@ -1238,7 +1245,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
     double2* lds = lds_all + fs * MP;
     double2 v[V];
 #pragma unroll
-    for (int s = 0; s < V; ++s) v[s] = lds[lds_slot(pass0_index<R, V>(tid, s))];
+    for (int s = 0; s < V; ++s) v[s] = lds[pass0_slot<R, V>(tid, s)];
     pass_pretwiddle<R, V, true>(v, fbut(fs), nbF, N, tid, a.tw_lo, a.tw_hi, a.S);
     if constexpr (PF) {
       pass_lds_barrier();
@@ -1250,7 +1257,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
       __syncthreads();
     }
 #pragma unroll
-    for (int s = 0; s < V; ++s) lds[lds_slot(last_pass_index<R, V>(tid, s))] = v[s];  // Z[fbut(fs) + nbF k]
+    for (int s = 0; s < V; ++s) lds[last_pass_slot<R, V>(tid, s)] = v[s];  // Z[fbut(fs) + nbF k]
     if (AD_CORR_PF_AT == 1 && item + G < items) load_item(item + G, tx);  // v is dead: room for the next item
     if constexpr (PF) pass_lds_barrier(); else __syncthreads();
     // 3. z for the inverse pairs (k_fft_pass's PAIR form): element (jj, r) of
@@ -1312,7 +1319,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
     double2 u[VI];
     if (act) {
 #pragma unroll
-      for (int s = 0; s < VI; ++s) u[s] = ldsi[lds_slot(pass0_index<R, VI>(ti, s))];
+      for (int s = 0; s < VI; ++s) u[s] = ldsi[pass0_slot<R, VI>(ti, s)];
     }
     if constexpr (PF) {
       pass_lds_barrier();
@@ -1325,7 +1332,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void k_
     }
     if (act) {
 #pragma unroll
-      for (int s = 0; s < VI; ++s) ldsi[lds_slot(last_pass_index<R, VI>(ti, s))] = u[s];
+      for (int s = 0; s < VI; ++s) ldsi[last_pass_slot<R, VI>(ti, s)] = u[s];
     }
     if constexpr (PF) pass_lds_barrier(); else __syncthreads();
     // 5. outputs: inverse butterfly jo's R values at jo R .. jo R + R - 1

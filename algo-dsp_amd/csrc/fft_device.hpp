@@ -196,6 +196,14 @@ __device__ __forceinline__ int lds_slot(int i) {
   return i ^ ((q ^ ((q & 4) << 1)) & 15);
 #endif
 }
+// lds_slot is linear over GF(2) (x(t) is an XOR of per-bit constants; checked
+// for every t pair), so for a base and an offset with disjoint bits
+// lds_slot(base + off) == lds_slot(base) ^ lds_slot(off).  The Stockham indices
+// below are all of that form (base < the offset's lowest bit, or a multiple of
+// a power of two above its highest), with the offset known at compile time:
+// one swizzle per butterfly and one XOR per access instead of the shift / mask
+// chain per access.
+__device__ __forceinline__ int lds_slot_split(int swz_base, int off) { return swz_base ^ lds_slot(off); }
 // Twiddle-table slot: stride-8 reads (the NS = 64 pass at M = 4096) and
 // consecutive reads both spread over 16 slots.
 __device__ __forceinline__ int tw_slot(int i) { return i ^ ((i >> 3) & 7); }
@@ -293,9 +301,10 @@ __device__ __forceinline__ void pass_compute_store(double2* v, int tid, double2*
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
     const int jb = tid + b * Plan::T;
-    const int base = (jb / NS) * NS * R + (jb & (NS - 1));
+    const int base = (jb / NS) * NS * R + (jb & (NS - 1));  // bits disjoint from r * NS
+    const int sb = lds_slot(base);
 #pragma unroll
-    for (int r = 0; r < R; ++r) lds[lds_slot(base + r * NS)] = v[b * R + r];
+    for (int r = 0; r < R; ++r) lds[lds_slot_split(sb, r * NS)] = v[b * R + r];
   }
 }
 
@@ -307,9 +316,10 @@ __device__ __forceinline__ void pass_load(double2* v, int tid, const double2* ld
   constexpr int NB = V / R;
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
-    const int jb = tid + b * Plan::T;
+    const int jb = tid + b * Plan::T;  // < M / R: bits disjoint from r * (M / R)
+    const int sb = lds_slot(jb);
 #pragma unroll
-    for (int r = 0; r < R; ++r) v[b * R + r] = lds[lds_slot(jb + r * (M / R))];
+    for (int r = 0; r < R; ++r) v[b * R + r] = lds[lds_slot_split(sb, r * (M / R))];
   }
 }
 
@@ -320,6 +330,15 @@ __device__ __forceinline__ int pass0_index(int tid, int s) {
   constexpr int R = Plan::R0;
   const int b = s / R, r = s % R;
   return tid + b * Plan::T + r * (M / R);
+}
+
+// lds_slot(pass0_index(tid, s)): jb = tid + b T < M / R and r (M / R) have disjoint bits.
+template <int M, int V = 16>
+__device__ __forceinline__ int pass0_slot(int tid, int s) {
+  using Plan = FftPlan<M, V>;
+  constexpr int R = Plan::R0;
+  const int b = s / R, r = s % R;
+  return lds_slot_split(lds_slot(tid + b * Plan::T), r * (M / R));
 }
 
 // Runs passes [1, NPASS-1) (the middle passes) after pass 0 has been stored:
@@ -365,6 +384,19 @@ __device__ __forceinline__ int last_pass_index(int tid, int s) {
   const int b = s / R, r = s % R;
   const int jb = tid + b * Plan::T;
   return (jb / NS) * NS * R + (jb & (NS - 1)) + r * NS;
+}
+
+// lds_slot(last_pass_index(tid, s)): the base (jb / NS) NS R + (jb mod NS) and
+// r NS have disjoint bits.
+template <int M, int V = 16>
+__device__ __forceinline__ int last_pass_slot(int tid, int s) {
+  using Plan = FftPlan<M, V>;
+  constexpr int P = Plan::NPASS - 1;
+  constexpr int R = Plan::radix(P);
+  constexpr int NS = Plan::ns(P);
+  const int b = s / R, r = s % R;
+  const int jb = tid + b * Plan::T;
+  return lds_slot_split(lds_slot((jb / NS) * NS * R + (jb & (NS - 1))), r * NS);
 }
 
 // Full FFT of the thread's V pass-0 values (forward or inverse); the result
