@@ -872,6 +872,40 @@ def test_eq_lanes_bit_exact(gpu, nsec, gains, per_channel):
         fx.close()
 
 
+def test_eq_lanes_edge_values_bitwise(gpu):
+    """K_lanes on inputs with signed zeros, subnormals, silence runs and large
+    values: every output's bit pattern (including the sign of a zero result)
+    equals the oracle's biquad chain (section.go:47-53), the staged one-workgroup
+    kernel's and the fused kernel's; 5 sections, 6 channels, two calls."""
+    fs = 48000.0
+    eq = design.config5_eq(fs)
+    C, n = 6, 3000
+    rng = np.random.default_rng(11)
+    x = 0.5 * rng.standard_normal((C, n))
+    x[0, :] = -0.0                                  # negative-zero silence
+    x[1, 100:900] = 0.0                             # a silence run inside noise
+    x[2, ::7] = -0.0
+    x[3, :] = rng.standard_normal(n) * 1e-310       # subnormal input
+    x[4, :] *= 1e150                                # large values
+    x[5, 1500:] = 5e-324                            # the smallest subnormal
+    outs = {}
+    for name, eng in [("lanes", P.EffectChain.ENGINE_AUTO), ("nosplit", P.EffectChain.ENGINE_STAGED_NOSPLIT),
+                      ("fused", P.EffectChain.ENGINE_FUSED)]:
+        fx = P.EffectChain(C, eq, None, None, fs)
+        fx.SetEngine(eng)
+        a, b = x[:, :1234].copy(), x[:, 1234:].copy()
+        fx.Process(a)
+        fx.Process(b)
+        outs[name] = np.concatenate([a, b], axis=1)
+        fx.close()
+    for c in range(C):
+        v = x[c].copy()
+        for co, g in eq:
+            v, _ = O.biquad_chain_block(np.ravel(co), np.zeros(2 * len(co)), g, v)
+        for name, y in outs.items():
+            assert np.array_equal(y[c].view(np.uint64), v.view(np.uint64)), (name, c)
+
+
 def test_eq_lanes_device_stride_matches_staged(gpu):
     """K_lanes on a device buffer whose row stride exceeds the call (the
     samples past n stay untouched), at 256 channels x 70000 samples over two
