@@ -223,3 +223,116 @@ def test_find_peak_empty():
     assert conv.FindPeak([0.5, 3.0, 3.0, -7.0]) == (1, 3.0)
     assert conv.LagFromIndex(conv.IndexFromLag(-4, 9), 9) == -4
     assert not math.isnan(conv.SNR([1.0, 2.0], [1.0, 2.5]))
+
+
+# ------------------------------------------------ PartitionedConvolution
+def _impulse_kernel(n):
+    """makeImpulseKernel (partitioned_test.go:11-20): 0.99^k."""
+    k = np.empty(n)
+    k[0] = 1.0
+    for i in range(1, n):
+        k[i] = k[i - 1] * 0.99
+    return k
+
+
+def _test_signal(n):
+    """Stands in for makePartitionedTestSignal (partitioned_test.go:23-32, Go's
+    PCG(42, 0) uniforms in [-1, 1)): seeded uniforms of the same range; the
+    tests compare two paths on the same input, so the generator is free."""
+    return np.random.default_rng(42).uniform(-1.0, 1.0, n)
+
+
+def _partitioned_out(kernel, sig, lo, hi):
+    """convolveWithPartitioned (partitioned_test.go:78-101)."""
+    pc = conv.NewPartitionedConvolution(kernel, lo, hi)
+    lat = pc.Latency()
+    padded = np.concatenate([sig, np.zeros(lat)])
+    out = np.zeros(padded.size)
+    pc.ProcessBlock(padded, out)
+    return out[lat:]
+
+
+def _soa_out(kernel, sig, block):
+    """convolveWithSOA (partitioned_test.go:36-76): the last block zero padded."""
+    s = conv.NewStreamingOverlapAdd(kernel, block)
+    outs = []
+    for i in range(0, sig.size, block):
+        b = np.zeros(block)
+        b[:min(block, sig.size - i)] = sig[i:i + block]
+        outs.append(s.ProcessBlock(b))
+    return np.concatenate(outs)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("order", [4, 5, 6, 7])
+def test_partitioned_latency(order):
+    """TestPartitionedConvolutionLatency (partitioned_test.go:103-119)."""
+    assert conv.NewPartitionedConvolution(_impulse_kernel(64), order, order + 4).Latency() == 1 << order
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("klen, slen, lo, hi", [(64, 512, 4, 10), (256, 1024, 5, 12), (1024, 4096, 6, 13),
+                                                (8192, 16384, 6, 13)])
+def test_partitioned_matches_soa(klen, slen, lo, hi):
+    """TestPartitionedConvolutionMatchesSOA (partitioned_test.go:121-165), 1e-7."""
+    k, sig = _impulse_kernel(klen), _test_signal(slen)
+    pc = _partitioned_out(k, sig, lo, hi)
+    soa = _soa_out(k, sig, 1 << lo)
+    n = min(sig.size, pc.size, soa.size)
+    assert np.max(np.abs(pc[:n] - soa[:n])) <= 1e-7
+
+
+@pytest.mark.gpu
+def test_partitioned_reset():
+    """TestPartitionedConvolutionReset (partitioned_test.go:167-197); equal
+    bits here."""
+    sig = _test_signal(512)
+    pc = conv.NewPartitionedConvolution(_impulse_kernel(128), 6, 12)
+    o1, o2 = np.zeros(512), np.zeros(512)
+    pc.ProcessBlock(sig, o1)
+    pc.Reset()
+    pc.ProcessBlock(sig, o2)
+    assert np.array_equal(o1, o2)
+
+
+@pytest.mark.gpu
+def test_partitioned_errors():
+    """TestPartitionedConvolutionErrors (partitioned_test.go:199-235)."""
+    with pytest.raises(conv.ErrEmptyImpulseResponse):
+        conv.NewPartitionedConvolution([], 6, 12)
+    with pytest.raises(conv.ErrInvalidBlockOrder):
+        conv.NewPartitionedConvolution([1, 2, 3], 0, 12)
+    with pytest.raises(conv.ErrInvalidBlockOrder):
+        conv.NewPartitionedConvolution([1, 2, 3], 8, 5)
+    pc = conv.NewPartitionedConvolution([1, 2, 3, 4], 2, 10)
+    with pytest.raises(conv.ErrLengthMismatch):
+        pc.ProcessBlock(np.zeros(10), np.zeros(8))
+
+
+@pytest.mark.gpu
+def test_partitioned_stage_info_and_kernel_len():
+    """TestPartitionedConvolutionStageInfo (partitioned_test.go:237-277) and
+    TestPartitionedConvolutionKernelLen (:279-290)."""
+    pc = conv.NewPartitionedConvolution(_impulse_kernel(1024), 6, 13)
+    count = pc.StageCount()
+    assert count > 0
+    for bad in (-1, count):
+        with pytest.raises(conv.ErrStageIndexOutOfRange):
+            pc.StageInfo(bad)
+    for i in range(count):
+        part, blocks = pc.StageInfo(i)
+        assert part > 0 and blocks > 0
+    assert conv.NewPartitionedConvolution(_impulse_kernel(300), 6, 13).KernelLen() == 300
+
+
+@pytest.mark.gpu
+def test_partitioned_dirac_delta_reference_form():
+    """TestPartitionedConvolutionDiracDelta (partitioned_test.go:292-322): a
+    one-tap kernel delays the input by 2^minBlockOrder, 1e-9."""
+    sig = _test_signal(256)
+    lat = 1 << 4
+    pc = conv.NewPartitionedConvolution([1.0], 4, 12)
+    padded = np.concatenate([sig, np.zeros(lat)])
+    out = np.zeros(padded.size)
+    pc.ProcessBlock(padded, out)
+    assert np.max(np.abs(out[lat:lat + sig.size] - sig)) <= 1e-9
