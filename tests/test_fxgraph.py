@@ -346,3 +346,48 @@ def test_graph_compressor_node_rejects_setter_ranges(gpu, field, value):
     _lib.lib().ad_compressor_default_config(C.byref(bad), FS)
     setattr(bad, field, value)
     assert build(bad) == _lib.AD_ERR_INVALID_ARGUMENT
+
+
+# the reference's own integration graphs (integration_test.go), at its 44.1 kHz;
+# its "threshold" key is not one the dynamics runtime reads (runtime_dynamics.go:21
+# reads thresholdDB), so the default applies on both sides
+def _ref_graph_run(g, x, fs=44100.0, calls=(0, None)):
+    ch = E.Chain(fs, x.shape[0], designer=design.RBJDesigner())
+    ch.LoadGraph(g)
+    oracles = [O.FxGraph(ch.spec, fs) for _ in range(x.shape[0])]
+    y = x.copy()
+    assert ch.Process(y)
+    for c in range(x.shape[0]):
+        want = oracles[c].process(x[c])
+        assert np.all(np.isfinite(y[c]))
+        assert rms(y[c], want) < RMS_TOL
+        assert np.max(np.abs(y[c] - want)) < 1e-10
+    return y
+
+
+@pytest.mark.gpu
+def test_reference_integration_linear(gpu):
+    """TestChainIntegrationLinear (integration_test.go:153-193): _input ->
+    dyn-compressor (ratio 4, attack 10 ms, release 100 ms) -> _output on 512
+    samples of 0.8 sin(2 pi 1000 i / 44100): finite, and the oracle's."""
+    g = graph([{"id": "comp", "type": "dyn-compressor",
+                "params": {"threshold": -20.0, "ratio": 4.0, "attackMs": 10.0, "releaseMs": 100.0}}],
+              [("_input", "comp"), ("comp", "_output")])
+    i = np.arange(512)
+    _ref_graph_run(g, np.stack([0.8 * np.sin(2 * np.pi * 1000 * i / 44100.0)] * 2))
+
+
+@pytest.mark.gpu
+def test_reference_integration_split_freq(gpu):
+    """TestChainIntegrationSplitFreq (integration_test.go:196-248): a 1 kHz
+    split-freq, a compressor per band, summed: finite, and the oracle's."""
+    p = {"threshold": -10.0, "ratio": 2.0, "attackMs": 5.0, "releaseMs": 50.0}
+    g = graph([{"id": "xo", "type": "split-freq", "params": {"freqHz": 1000.0}},
+               {"id": "low_comp", "type": "dyn-compressor", "params": p},
+               {"id": "hi_comp", "type": "dyn-compressor", "params": p},
+               {"id": "sum", "type": "sum"}],
+              [("_input", "xo"), ("xo", "low_comp", 0), ("xo", "hi_comp", 1), ("low_comp", "sum"),
+               ("hi_comp", "sum"), ("sum", "_output")])
+    i = np.arange(512)
+    x = 0.5 * np.sin(2 * np.pi * 200 * i / 44100.0) + 0.3 * np.sin(2 * np.pi * 5000 * i / 44100.0)
+    _ref_graph_run(g, np.stack([x, x]))
