@@ -225,9 +225,18 @@ class Expander(Compressor):
         check(lib().ad_fx_chain_set_expander(self._h, C.byref(self.cfg), int(self.GATE), float(self.range_db),
                                              float(self.hold_ms)))
 
+    def _set_attr(self, name, value):
+        # a rejected value raises and leaves the stage as it was (like _set)
+        old = getattr(self, name)
+        setattr(self, name, value)
+        try:
+            self._apply()
+        except Exception:
+            setattr(self, name, old)
+            raise
+
     def SetRange(self, db):  # expander.go / gate.go SetRange
-        self.range_db = db
-        self._apply()
+        self._set_attr("range_db", db)
 
 
 class Gate(Expander):
@@ -237,8 +246,7 @@ class Gate(Expander):
     GATE = True
 
     def SetHold(self, ms):  # gate.go:196-223
-        self.hold_ms = ms
-        self._apply()
+        self._set_attr("hold_ms", ms)
 
 
 class Reverb(_FxChain):

@@ -264,3 +264,48 @@ def test_gate_negative_input(gpu):
     g = P.Gate(FS)
     g.Reset()
     assert one_sample_calls(g, [-0.5])[0] <= 0.0
+
+
+# ------------------------------------------------------------------ Expander
+def test_expander_parameter_validation(gpu):
+    """TestExpanderParameterValidation (expander_test.go:65-92): ratio 0.5,
+    knee 25, attack 0.05 ms, release 0.5 ms and range -121 dB are rejected."""
+    for field, value in (("ratio", 0.5), ("knee_db", 25.0), ("attack_ms", 0.05), ("release_ms", 0.5)):
+        e = P.Expander(FS)
+        with pytest.raises(Exception):
+            e._set(**{field: value})
+    e = P.Expander(FS)
+    with pytest.raises(Exception):
+        e.SetRange(-121.0)
+    assert e.range_db == -60.0  # the rejected value left the stage as it was
+
+
+def test_expander_gain_behavior(gpu):
+    """TestExpanderGainBehavior (expander_test.go:94-121): threshold -20 dB,
+    6:1, hard knee, range -80 dB: 1024 x 0.5 settle at >= 0.49; after Reset,
+    1024 x 0.02 are attenuated below 0.02.  Both against the oracle, 1e-12."""
+    cfg = dict(threshold_db=-20.0, ratio=6.0, knee_db=0.0, range_db=-80.0)
+    e = P.Expander(FS, **cfg)
+    hi = np.full(1024, 0.5)
+    e.ProcessInPlace(hi)
+    assert hi[-1] >= 0.49
+    e.Reset()
+    lo = np.full(1024, 0.02)
+    e.ProcessInPlace(lo)
+    assert lo[-1] < 0.02
+    o = O.Expander(FS, **cfg)
+    assert float(np.max(np.abs(hi - o.process_in_place(np.full(1024, 0.5))))) <= 1e-12
+    o.reset()
+    assert float(np.max(np.abs(lo - o.process_in_place(np.full(1024, 0.02))))) <= 1e-12
+
+
+def test_expander_topology_changes_output(gpu):
+    """TestExpanderTopologyDetectorAndSidechain (expander_test.go:123-150):
+    RMS detector, 20 ms window, threshold -25 dB, 4:1; 512 x 0.05 give a
+    different last output in feedback and feed-forward topology."""
+    base = dict(threshold_db=-25.0, ratio=4.0, detector_mode=1, rms_window_ms=20.0)
+    fb = np.full(512, 0.05)
+    P.Expander(FS, topology=1, **base).ProcessInPlace(fb)
+    ff = np.full(512, 0.05)
+    P.Expander(FS, topology=0, **base).ProcessInPlace(ff)
+    assert fb[-1] != ff[-1]
