@@ -215,6 +215,11 @@ __global__ __launch_bounds__(256) void k_absmax2(const double* __restrict__ a, i
 #ifndef AD_FFT_FWX
 #define AD_FFT_FWX 2
 #endif
+#ifndef AD_FFT_FWX_RO
+#define AD_FFT_FWX_RO 1  // the real-output (last inverse) pass: one FftPlan tile (CorrelateFFT 2 x 2^23,
+                         // profiles/r06_corr_ro_tile_ab.txt:
+                         // 0.4947 -> 0.4900 ms per call, same box)
+#endif
 #ifndef AD_FFT_PAIR
 #define AD_FFT_PAIR 1  // mirror-paired tiles in the half inverse's first pass
 #endif
@@ -423,11 +428,11 @@ __device__ __forceinline__ void realout_store(const FftPassArgs& a, const double
   }
 }
 
-template <int R>
+template <int R, bool RO = false>
 struct PassShape {
   static constexpr int V = AD_FFT_V;
   static constexpr int T = FftPlan<R, V>::T;
-  static constexpr int F = FftPlan<R, V>::F * AD_FFT_FWX;
+  static constexpr int F = FftPlan<R, V>::F * (RO ? AD_FFT_FWX_RO : AD_FFT_FWX);
   static constexpr int BLOCK = F * T;
 };
 // HALF: the first inverse pass of the spectral row's half-length inverse
@@ -437,8 +442,8 @@ struct PassShape {
 // tile {nb - j}: the four Z values a lane loads (Z[g], Z[g + NF/2] and their
 // mirrors) give one element of each tile, so Z is read once instead of twice.
 template <int R, bool FWD, bool REALIN, bool REALOUT, int HALF = 0, bool PAIR = false>
-__global__ __launch_bounds__((PassShape<R>::BLOCK)) void k_fft_pass(FftPassArgs a) {
-  using Sh = PassShape<R>;
+__global__ __launch_bounds__((PassShape<R, REALOUT>::BLOCK)) void k_fft_pass(FftPassArgs a) {
+  using Sh = PassShape<R, REALOUT>;
   using Plan = FftPlan<R, Sh::V>;
   // per-butterfly LDS stride: odd when a 16-lane group stays inside one
   // transform (T >= 16), so the jj-fastest staging accesses spread over the banks
@@ -1396,7 +1401,7 @@ double2* upload(const std::vector<double2>& v) {
 
 template <int R, bool FWD, bool RI, bool RO>
 void go_pass(const FftPassArgs& a, int batch, hipStream_t s) {
-  using Sh = PassShape<R>;
+  using Sh = PassShape<R, RO>;
   const dim3 grid((unsigned)((a.N / R + Sh::F - 1) / Sh::F), (unsigned)batch);
   if constexpr (!FWD && !RI) {
     if (a.half) {
