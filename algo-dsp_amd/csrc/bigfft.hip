@@ -215,10 +215,16 @@ __global__ __launch_bounds__(256) void k_absmax2(const double* __restrict__ a, i
 #ifndef AD_FFT_FWX
 #define AD_FFT_FWX 2
 #endif
+// The real-output last pass at radix <= 256 (PassShape::SMALL_RO): 4 values per
+// thread, two FftPlan tiles per workgroup (R = 128: 16 butterflies, 512 threads,
+// 33 KiB of LDS).  CorrelateFFT 2 x 2^23, same box (profiles/r06_corr_ro_tile_ab.txt):
+// V 8 / 2 tiles 0.4947, V 8 / 1 tile 0.4900-0.4914, V 4 / 2 tiles 0.4842-0.4854 ms
+// per call; V 16 0.517-0.522.
+#ifndef AD_FFT_V_RO
+#define AD_FFT_V_RO 4
+#endif
 #ifndef AD_FFT_FWX_RO
-#define AD_FFT_FWX_RO 1  // the real-output (last inverse) pass: one FftPlan tile (CorrelateFFT 2 x 2^23,
-                         // profiles/r06_corr_ro_tile_ab.txt:
-                         // 0.4947 -> 0.4900 ms per call, same box)
+#define AD_FFT_FWX_RO 2
 #endif
 #ifndef AD_FFT_PAIR
 #define AD_FFT_PAIR 1  // mirror-paired tiles in the half inverse's first pass
@@ -430,9 +436,11 @@ __device__ __forceinline__ void realout_store(const FftPassArgs& a, const double
 
 template <int R, bool RO = false>
 struct PassShape {
-  static constexpr int V = AD_FFT_V;
+  // the real-output last pass of a multi-pass plan (radix <= 256) has its own shape
+  static constexpr bool SMALL_RO = RO && R <= 256;
+  static constexpr int V = SMALL_RO ? AD_FFT_V_RO : AD_FFT_V;
   static constexpr int T = FftPlan<R, V>::T;
-  static constexpr int F = FftPlan<R, V>::F * (RO ? AD_FFT_FWX_RO : AD_FFT_FWX);
+  static constexpr int F = FftPlan<R, V>::F * (SMALL_RO ? AD_FFT_FWX_RO : AD_FFT_FWX);
   static constexpr int BLOCK = F * T;
 };
 // HALF: the first inverse pass of the spectral row's half-length inverse
